@@ -1,0 +1,120 @@
+"""ctypes binding of libmim.so (include/mim.h).  Loading fails loudly: there is no CPU path."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+SO_PATH = os.path.join(_HERE, "lib", "libmim.so")
+
+MIM_OK, MIM_EINVAL, MIM_ENOMODEL, MIM_EDEVICE, MIM_ENOMEM, MIM_ERANGE = range(6)
+STATUS_NAMES = {0: "accepted", 1: "few_good", 2: "empty_H", 3: "few_inliers", 4: "bad_det"}
+
+# every symbol include/mim.h declares (checked by tests/test_abi.py)
+EXPORTS = [
+    "mim_version", "mim_default_params", "mim_ctx_create", "mim_ctx_destroy", "mim_last_error",
+    "mim_ctx_set_stream", "mim_synchronize", "mim_set_create", "mim_sets_clear", "mim_knn2_l2",
+    "mim_ratio_filter", "mim_find_homography", "mim_batch_run", "mim_batch_results",
+    "mim_batch_results_dev", "mim_batch_problem_detail", "mim_knn2_sets_dev", "mim_last_kernel_ms",
+    "mim_set_timing",
+]
+
+
+class MimError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"mim status {code}: {msg}")
+        self.code = code
+
+
+class Params(C.Structure):
+    _fields_ = [("ratio", C.c_float), ("min_good", C.c_int32), ("min_inliers", C.c_int32),
+                ("ransac_thresh", C.c_double), ("max_iters", C.c_int32), ("confidence", C.c_double),
+                ("det_lo", C.c_double), ("det_hi", C.c_double)]
+
+
+class Result(C.Structure):
+    _fields_ = [("n_good", C.c_int32), ("n_inl", C.c_int32), ("status", C.c_int32),
+                ("iters", C.c_int32), ("H", C.c_double * 9), ("det", C.c_double)]
+
+
+class Problem(C.Structure):
+    _fields_ = [("query_set", C.c_int32), ("train_set", C.c_int32)]
+
+
+RESULT_DTYPE = np.dtype([("n_good", np.int32), ("n_inl", np.int32), ("status", np.int32),
+                         ("iters", np.int32), ("H", np.float64, 9), ("det", np.float64)])
+assert RESULT_DTYPE.itemsize == C.sizeof(Result)
+
+_lib = None
+
+
+class _Lazy:
+    """Attribute setter that tolerates symbols a partial build does not export yet."""
+
+    def __init__(self, cdll):
+        object.__setattr__(self, "_cdll", cdll)
+
+    def __getattr__(self, name):
+        cd = object.__getattribute__(self, "_cdll")
+        if hasattr(cd, name):
+            return getattr(cd, name)
+        return _Missing(name)
+
+
+class _Missing:
+    def __init__(self, name):
+        self.__dict__["name"] = name
+
+    def __setattr__(self, k, v):
+        pass
+
+    def __call__(self, *a, **k):
+        raise MimError(-1, f"{self.name} is not exported by this libmim.so build")
+
+
+def load():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(SO_PATH):
+        raise ImportError(f"{SO_PATH} is missing: run `python -m computervision_objectdetection_featurematching_amd.build`"
+                          " (there is no CPU fallback)")
+    L = _Lazy(C.CDLL(SO_PATH))
+    vp, i32, f32p, f64p, u8p, i32p = C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p
+    L.mim_version.restype = C.c_char_p
+    L.mim_default_params.argtypes = [C.POINTER(Params)]
+    L.mim_ctx_create.argtypes = [C.c_int, C.POINTER(vp)]
+    L.mim_ctx_destroy.argtypes = [vp]
+    L.mim_last_error.argtypes = [vp]
+    L.mim_last_error.restype = C.c_char_p
+    L.mim_ctx_set_stream.argtypes = [vp, vp]
+    L.mim_synchronize.argtypes = [vp]
+    L.mim_set_create.argtypes = [vp, f32p, f32p, i32, i32, i32, C.POINTER(C.c_int32)]
+    L.mim_sets_clear.argtypes = [vp]
+    L.mim_knn2_l2.argtypes = [vp, f32p, i32, f32p, i32, i32, i32p, f32p]
+    L.mim_ratio_filter.argtypes = [vp, i32p, f32p, i32, C.c_float, i32p, i32p, C.POINTER(C.c_int32)]
+    L.mim_find_homography.argtypes = [vp, f32p, f32p, i32, C.c_double, i32, C.c_double, f64p, u8p]
+    L.mim_batch_run.argtypes = [vp, C.POINTER(Problem), i32, C.POINTER(Params)]
+    L.mim_batch_results.argtypes = [vp, vp]
+    L.mim_batch_results_dev.argtypes = [vp]
+    L.mim_batch_results_dev.restype = vp
+    L.mim_batch_problem_detail.argtypes = [vp, i32, i32p, i32p, u8p]
+    L.mim_knn2_sets_dev.argtypes = [vp, i32, i32, vp, vp]
+    L.mim_last_kernel_ms.argtypes = [vp, C.c_char_p]
+    L.mim_last_kernel_ms.restype = C.c_double
+    L.mim_set_timing.argtypes = [vp, i32]
+    for name in ("mim_ctx_create", "mim_ctx_set_stream", "mim_synchronize", "mim_set_create", "mim_sets_clear",
+                 "mim_knn2_l2", "mim_ratio_filter", "mim_find_homography", "mim_batch_run", "mim_batch_results",
+                 "mim_batch_problem_detail", "mim_knn2_sets_dev", "mim_set_timing"):
+        getattr(L, name).restype = C.c_int32
+    _lib = L
+    return L
+
+
+def ptr(a) -> int:
+    """Address of a numpy array or a torch tensor."""
+    if hasattr(a, "data_ptr"):
+        return a.data_ptr()
+    return a.ctypes.data

@@ -1,0 +1,487 @@
+// api.cpp — the C ABI of include/mim.h: context, descriptor sets, batch orchestration.
+//
+// Host side of the drop-in boundary for TestsDetector.cpp:58-95.  Everything numeric runs in the
+// HIP kernels of knn.hip / ransac.hip; this file only allocates, builds problem tables and
+// enqueues launches on the ctx stream.  There is no CPU compute path: a missing device or a
+// failed launch is reported as MIM_EDEVICE.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cfloat>
+#include <climits>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/mim.h"
+#include "mim_internal.h"
+
+namespace mim {
+void launch_prep_set(const float* src, int n, uint16_t* frag, float* norm, int* flags, hipStream_t st);
+void launch_knn(const ProbDev* probs, const KnnWork* works, int n_works, Top2* parts, hipStream_t st);
+void launch_ratio(const ProbDev* probs, int n_probs, const Top2* parts, float ratio, int32_t* good_q,
+                  int32_t* good_t, float4* pts, int* n_good, int32_t* knn_idx, float* knn_dist,
+                  hipStream_t st);
+struct RansacWs;
+void ransac_enqueue(const RansacParams& prm, int n_probs, const ProbDev* probs_dev, const float4* pts,
+                    const int* n_good, RansacWs& ws, mim_result* results, uint8_t* masks,
+                    hipStream_t st, const std::vector<std::pair<std::string, hipEvent_t>>* evs);
+}  // namespace mim
+
+using namespace mim;
+
+namespace {
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t bytes) {
+        if (bytes <= cap) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t want = std::max(bytes, (size_t)4096);
+        hipError_t e = hipMalloc(&p, want);
+        if (e == hipSuccess) cap = want;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+    template <class T> T* as() const { return static_cast<T*>(p); }
+};
+
+// Bump arena for per-set device storage; mim_sets_clear() rewinds it without freeing.
+struct Arena {
+    std::vector<std::pair<char*, size_t>> chunks;
+    size_t chunk_i = 0, off = 0;
+    hipError_t alloc(size_t bytes, void** out) {
+        bytes = (bytes + 255) & ~size_t(255);
+        while (chunk_i < chunks.size() && off + bytes > chunks[chunk_i].second) {
+            ++chunk_i;
+            off = 0;
+        }
+        if (chunk_i == chunks.size()) {
+            size_t sz = std::max(bytes, (size_t)256 << 20);
+            char* p = nullptr;
+            hipError_t e = hipMalloc(&p, sz);
+            if (e != hipSuccess) return e;
+            chunks.push_back({p, sz});
+            off = 0;
+        }
+        *out = chunks[chunk_i].first + off;
+        off += bytes;
+        return hipSuccess;
+    }
+    void rewind() { chunk_i = 0; off = 0; }
+    void release() {
+        for (auto& c : chunks) (void)hipFree(c.first);
+        chunks.clear();
+        rewind();
+    }
+};
+
+struct SetRec {
+    SetDev d;
+};
+
+}  // namespace
+
+namespace mim {
+// RANSAC workspace (definition shared with ransac.hip through this layout)
+struct RansacWs {
+    DevBuf state, samples, hyp, counts, stream, scratch;
+    long long stream_len = 0;
+    int timing = 0;
+};
+}  // namespace mim
+
+struct mim_ctx {
+    int device = 0;
+    hipStream_t own = nullptr, stream = nullptr;
+    std::mutex mu;
+    std::string err;
+    Arena arena;
+    std::vector<SetRec> sets;
+    // batch workspace
+    DevBuf probs, works, parts, good_q, good_t, pts, n_good, results, masks, knn_idx, knn_dist;
+    RansacWs rws;
+    std::vector<ProbDev> h_probs;
+    std::vector<KnnWork> h_works;
+    int n_works = 0;
+    std::vector<long long> h_good_off;
+    int last_n = 0;
+    // timing
+    bool timing = false;
+    std::vector<std::pair<std::string, hipEvent_t>> evs;
+    std::map<std::string, double> last_ms;
+};
+
+static mim_status fail(mim_ctx* c, mim_status code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    if (c) c->err = buf;
+    return code;
+}
+
+#define HIPCHK(c, expr)                                                                          \
+    do {                                                                                         \
+        hipError_t e_ = (expr);                                                                  \
+        if (e_ != hipSuccess)                                                                    \
+            return fail((c), e_ == hipErrorOutOfMemory ? MIM_ENOMEM : MIM_EDEVICE, "%s: %s (%s:%d)", \
+                        #expr, hipGetErrorString(e_), __FILE__, __LINE__);                       \
+    } while (0)
+
+extern "C" {
+
+const char* mim_version(void) { return "mim 0.1.0 (gfx950)"; }
+
+void mim_default_params(mim_params* p) {
+    p->ratio = 0.9f;          // TestsDetector.cpp:21
+    p->min_good = 4;          // :22, :74
+    p->min_inliers = 4;       // :22, :81
+    p->ransac_thresh = 5.0;   // :23
+    p->max_iters = 2000;      // findHomography default
+    p->confidence = 0.995;    // findHomography default
+    p->det_lo = (double)0.1f; // :24 (constexpr float)
+    p->det_hi = (double)10.0f;  // :25
+}
+
+mim_status mim_ctx_create(int device, mim_ctx** out) {
+    if (!out) return MIM_EINVAL;
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return MIM_EDEVICE;
+    if (device < 0 || device >= ndev) return MIM_EINVAL;
+    if (hipSetDevice(device) != hipSuccess) return MIM_EDEVICE;
+    mim_ctx* c = new mim_ctx();
+    c->device = device;
+    if (hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return MIM_EDEVICE;
+    }
+    c->stream = c->own;
+    *out = c;
+    return MIM_OK;
+}
+
+void mim_ctx_destroy(mim_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    for (auto& e : c->evs) (void)hipEventDestroy(e.second);
+    c->arena.release();
+    for (DevBuf* b : {&c->probs, &c->works, &c->parts, &c->good_q, &c->good_t, &c->pts, &c->n_good,
+                      &c->results, &c->masks, &c->knn_idx, &c->knn_dist, &c->rws.state, &c->rws.samples,
+                      &c->rws.hyp, &c->rws.counts, &c->rws.stream, &c->rws.scratch})
+        b->release();
+    if (c->own) (void)hipStreamDestroy(c->own);
+    delete c;
+}
+
+const char* mim_last_error(const mim_ctx* c) { return c ? c->err.c_str() : "null ctx"; }
+
+mim_status mim_ctx_set_stream(mim_ctx* c, void* stream) {
+    if (!c) return MIM_EINVAL;
+    std::lock_guard<std::mutex> lk(c->mu);
+    c->stream = stream ? (hipStream_t)stream : c->own;
+    return MIM_OK;
+}
+
+mim_status mim_synchronize(mim_ctx* c) {
+    if (!c) return MIM_EINVAL;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return MIM_OK;
+}
+
+mim_status mim_set_timing(mim_ctx* c, int32_t enable) {
+    if (!c) return MIM_EINVAL;
+    c->timing = enable != 0;
+    return MIM_OK;
+}
+
+double mim_last_kernel_ms(mim_ctx* c, const char* name) {
+    if (!c || !name) return -1;
+    auto it = c->last_ms.find(name);
+    return it == c->last_ms.end() ? -1 : it->second;
+}
+
+static mim_status set_create_locked(mim_ctx* c, const float* desc, const float* kp, int32_t n, int32_t dim,
+                                    int32_t on_device, int32_t* set_id) {
+    if (!set_id || n < 0 || (n > 0 && (!desc || !kp))) return fail(c, MIM_EINVAL, "set_create: bad arguments");
+    if (dim != kDim) return fail(c, MIM_EINVAL, "set_create: dim must be %d (got %d)", kDim, dim);
+    if (n >= (1 << 18))  // BFMatcher::knnMatchImpl asserts trainDescCollection rows < 1<<18 (IMGIDX_SHIFT)
+        return fail(c, MIM_EINVAL, "set_create: n=%d exceeds OpenCV's 2^18 train-row limit", n);
+    HIPCHK(c, hipSetDevice(c->device));
+    SetRec r{};
+    r.d.n = n;
+    r.d.n_tiles = (n + 63) / 64;
+    const size_t tiles = (size_t)std::max(r.d.n_tiles, 1);
+    void *frag, *norm, *flags;
+    HIPCHK(c, c->arena.alloc(tiles * kTileBytes, &frag));
+    HIPCHK(c, c->arena.alloc(tiles * 64 * sizeof(float), &norm));
+    HIPCHK(c, c->arena.alloc(sizeof(int) * 4, &flags));
+    HIPCHK(c, hipMemsetAsync(flags, 0, sizeof(int) * 4, c->stream));
+    const float* f32 = desc;
+    const float* kpd = kp;
+    if (!on_device && n > 0) {
+        void *df, *dk;
+        HIPCHK(c, c->arena.alloc((size_t)n * kDim * sizeof(float), &df));
+        HIPCHK(c, c->arena.alloc((size_t)n * 2 * sizeof(float), &dk));
+        HIPCHK(c, hipMemcpyAsync(df, desc, (size_t)n * kDim * sizeof(float), hipMemcpyHostToDevice, c->stream));
+        HIPCHK(c, hipMemcpyAsync(dk, kp, (size_t)n * 2 * sizeof(float), hipMemcpyHostToDevice, c->stream));
+        f32 = (const float*)df;
+        kpd = (const float*)dk;
+    }
+    r.d.frag = (const uint16_t*)frag;
+    r.d.norm = (const float*)norm;
+    r.d.f32 = f32;
+    r.d.kp = (const float2*)kpd;
+    r.d.flags = (int*)flags;
+    launch_prep_set(f32, n, (uint16_t*)frag, (float*)norm, (int*)flags, c->stream);
+    HIPCHK(c, hipGetLastError());
+    if (!on_device) HIPCHK(c, hipStreamSynchronize(c->stream));  // host buffers may go away
+    *set_id = (int32_t)c->sets.size();
+    c->sets.push_back(r);
+    return MIM_OK;
+}
+
+mim_status mim_set_create(mim_ctx* c, const float* desc, const float* kp, int32_t n, int32_t dim,
+                          int32_t on_device, int32_t* set_id) {
+    if (!c) return MIM_EINVAL;
+    std::lock_guard<std::mutex> lk(c->mu);
+    return set_create_locked(c, desc, kp, n, dim, on_device, set_id);
+}
+
+mim_status mim_sets_clear(mim_ctx* c) {
+    if (!c) return MIM_EINVAL;
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->sets.clear();
+    c->arena.rewind();
+    return MIM_OK;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------------------------
+// Problem table + distance work list.  Work items of one problem are placed at block indices
+// with equal (index % 8) so they share one XCD's L2 under round-robin dispatch (speed only).
+// ---------------------------------------------------------------------------------------------
+static mim_status build_tables(mim_ctx* c, const mim_problem* problems, int n, int max_iters) {
+    HIPCHK(c, hipStreamSynchronize(c->stream));  // previous batch done with the tables
+    c->h_probs.assign(n, ProbDev{});
+    long long part = 0, good = 0, it = 0;
+    int total_qblocks = 0;
+    for (int i = 0; i < n; ++i) {
+        const int qs = problems[i].query_set, ts = problems[i].train_set;
+        if (qs < 0 || qs >= (int)c->sets.size() || ts < 0 || ts >= (int)c->sets.size())
+            return fail(c, MIM_EINVAL, "problem %d: bad set id (%d, %d)", i, qs, ts);
+        total_qblocks += (c->sets[qs].d.n + 255) / 256;
+    }
+    // split the train side until the grid has ~2 blocks per CU
+    const int target = 512;
+    std::vector<std::vector<KnnWork>> per_prob(n);
+    for (int i = 0; i < n; ++i) {
+        ProbDev& P = c->h_probs[i];
+        P.q = c->sets[problems[i].query_set].d;
+        P.t = c->sets[problems[i].train_set].d;
+        const int qb = (P.q.n + 255) / 256;
+        int nsplit = total_qblocks > 0 ? (target + total_qblocks - 1) / total_qblocks : 1;
+        nsplit = std::max(1, std::min(nsplit, std::max(P.t.n_tiles, 1)));
+        P.nsplit = nsplit;
+        P.q_pad = qb * 256;
+        P.part_off = part;
+        part += (long long)nsplit * P.q_pad;
+        P.good_off = good;
+        good += std::max(P.q.n, 1);
+        P.it_off = it;
+        it += std::max(max_iters, 1);
+        for (int qb_i = 0; qb_i < qb; ++qb_i)
+            for (int s = 0; s < nsplit; ++s) {
+                const int t0 = (int)((long long)P.t.n_tiles * s / nsplit);
+                const int t1 = (int)((long long)P.t.n_tiles * (s + 1) / nsplit);
+                per_prob[i].push_back(KnnWork{i, qb_i * 256, t0, t1, s});
+            }
+    }
+    // XCD-aware order: bucket problems over 8 lanes of the grid
+    std::vector<std::vector<KnnWork>> xcd(8);
+    for (int i = 0; i < n; ++i)
+        for (auto& w : per_prob[i]) xcd[i % 8].push_back(w);
+    std::vector<KnnWork> works;
+    size_t longest = 0;
+    for (auto& v : xcd) longest = std::max(longest, v.size());
+    for (size_t k = 0; k < longest; ++k)
+        for (int x = 0; x < 8; ++x)
+            if (k < xcd[x].size()) works.push_back(xcd[x][k]);
+    HIPCHK(c, c->probs.ensure(sizeof(ProbDev) * std::max(n, 1)));
+    HIPCHK(c, c->works.ensure(sizeof(KnnWork) * std::max<size_t>(works.size(), 1)));
+    HIPCHK(c, c->parts.ensure(sizeof(Top2) * std::max<long long>(part, 1)));
+    HIPCHK(c, c->good_q.ensure(sizeof(int32_t) * good));
+    HIPCHK(c, c->good_t.ensure(sizeof(int32_t) * good));
+    HIPCHK(c, c->pts.ensure(sizeof(float4) * good));
+    HIPCHK(c, c->n_good.ensure(sizeof(int) * std::max(n, 1)));
+    HIPCHK(c, c->masks.ensure(good));
+    HIPCHK(c, hipMemcpyAsync(c->probs.p, c->h_probs.data(), sizeof(ProbDev) * n, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->works.p, works.data(), sizeof(KnnWork) * works.size(), hipMemcpyHostToDevice,
+                             c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));  // pageable sources: copy complete before reuse
+    c->h_good_off.resize(n);
+    for (int i = 0; i < n; ++i) c->h_good_off[i] = c->h_probs[i].good_off;
+    c->last_n = n;
+    c->h_works.swap(works);  // source of the async copy stays alive in the ctx
+    c->n_works = (int)c->h_works.size();
+    return MIM_OK;
+}
+
+static void ev_mark(mim_ctx* c, const char* name) {
+    if (!c->timing) return;
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) return;
+    (void)hipEventRecord(e, c->stream);
+    c->evs.push_back({name, e});
+}
+
+static void ev_collect(mim_ctx* c) {
+    if (c->evs.empty()) return;
+    (void)hipEventSynchronize(c->evs.back().second);
+    c->last_ms.clear();
+    for (size_t i = 1; i < c->evs.size(); ++i) {
+        float ms = 0;
+        (void)hipEventElapsedTime(&ms, c->evs[i - 1].second, c->evs[i].second);
+        c->last_ms[c->evs[i].first] += ms;
+    }
+    for (auto& e : c->evs) (void)hipEventDestroy(e.second);
+    c->evs.clear();
+}
+
+static mim_status knn_ratio_locked(mim_ctx* c, int n, float ratio, bool emit_knn) {
+    Top2* parts = c->parts.as<Top2>();
+    ev_mark(c, "begin");
+    launch_knn(c->probs.as<ProbDev>(), c->works.as<KnnWork>(), c->n_works, parts, c->stream);
+    HIPCHK(c, hipGetLastError());
+    ev_mark(c, "knn");
+    launch_ratio(c->probs.as<ProbDev>(), n, parts, ratio, c->good_q.as<int32_t>(), c->good_t.as<int32_t>(),
+                 c->pts.as<float4>(), c->n_good.as<int>(), emit_knn ? c->knn_idx.as<int32_t>() : nullptr,
+                 emit_knn ? c->knn_dist.as<float>() : nullptr, c->stream);
+    HIPCHK(c, hipGetLastError());
+    ev_mark(c, "ratio");
+    return MIM_OK;
+}
+
+extern "C" {
+
+mim_status mim_knn2_l2(mim_ctx* c, const float* q, int32_t nq, const float* t, int32_t nt, int32_t dim,
+                       int32_t* idx, float* dist) {
+    if (!c) return MIM_EINVAL;
+    if (nq < 0 || nt < 0 || (nq > 0 && (!q || !idx || !dist)) || (nt > 0 && !t))
+        return fail(c, MIM_EINVAL, "knn2_l2: bad arguments");
+    if (dim != kDim) return fail(c, MIM_EINVAL, "knn2_l2: dim must be %d", kDim);
+    if (nq == 0) return MIM_OK;  // knnMatch on an empty query returns no rows
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIPCHK(c, hipSetDevice(c->device));
+    // private sets appended after the user's sets, removed afterwards
+    const size_t base = c->sets.size();
+    std::vector<float> kp0((size_t)std::max(nq, nt) * 2, 0.f);
+    int32_t sq, st;
+    mim_status s = set_create_locked(c, q, kp0.data(), nq, dim, 0, &sq);
+    if (s != MIM_OK) return s;
+    s = set_create_locked(c, t ? t : kp0.data(), kp0.data(), nt, dim, 0, &st);
+    if (s != MIM_OK) return s;
+    mim_problem pr{sq, st};
+    s = build_tables(c, &pr, 1, 1);
+    if (s != MIM_OK) return s;
+    HIPCHK(c, c->knn_idx.ensure(sizeof(int32_t) * 2 * nq));
+    HIPCHK(c, c->knn_dist.ensure(sizeof(float) * 2 * nq));
+    s = knn_ratio_locked(c, 1, 0.9f, true);
+    if (s != MIM_OK) return s;
+    HIPCHK(c, hipMemcpyAsync(idx, c->knn_idx.p, sizeof(int32_t) * 2 * nq, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(dist, c->knn_dist.p, sizeof(float) * 2 * nq, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    ev_collect(c);
+    c->sets.resize(base);  // arena space is reclaimed at the next mim_sets_clear
+    return MIM_OK;
+}
+
+mim_status mim_ratio_filter(mim_ctx* c, const int32_t* idx, const float* dist, int32_t nq, float ratio,
+                            int32_t* q_out, int32_t* t_out, int32_t* n_good) {
+    if (!c) return MIM_EINVAL;
+    if (nq < 0 || !n_good || (nq > 0 && (!idx || !dist))) return fail(c, MIM_EINVAL, "ratio_filter: bad arguments");
+    *n_good = 0;
+    if (nq == 0) return MIM_OK;
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    // knnMatch rows -> one train split of Top2 partials, then the device ratio/compaction kernel
+    int max_t = 0;
+    std::vector<Top2> parts(nq);
+    for (int i = 0; i < nq; ++i) {
+        const int a = idx[2 * i], b = idx[2 * i + 1];
+        parts[i] = Top2{a < 0 ? FLT_MAX : dist[2 * i], a < 0 ? INT_MAX : a, b < 0 ? FLT_MAX : dist[2 * i + 1],
+                        b < 0 ? INT_MAX : b};
+        max_t = std::max(max_t, std::max(a, b));
+    }
+    const int q_pad = (nq + 255) / 256 * 256;
+    const size_t nkp = (size_t)std::max(nq, max_t + 1);
+    HIPCHK(c, c->parts.ensure(sizeof(Top2) * q_pad));
+    HIPCHK(c, c->rws.scratch.ensure(sizeof(float2) * nkp));
+    HIPCHK(c, c->good_q.ensure(sizeof(int32_t) * nq));
+    HIPCHK(c, c->good_t.ensure(sizeof(int32_t) * nq));
+    HIPCHK(c, c->pts.ensure(sizeof(float4) * nq));
+    HIPCHK(c, c->n_good.ensure(sizeof(int)));
+    HIPCHK(c, c->probs.ensure(sizeof(ProbDev)));
+    HIPCHK(c, hipMemsetAsync(c->rws.scratch.p, 0, sizeof(float2) * nkp, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->parts.p, parts.data(), sizeof(Top2) * nq, hipMemcpyHostToDevice, c->stream));
+    ProbDev P{};
+    P.q.n = nq;
+    P.q.kp = c->rws.scratch.as<float2>();
+    P.t.kp = c->rws.scratch.as<float2>();
+    P.nsplit = 1;
+    P.q_pad = q_pad;
+    HIPCHK(c, hipMemcpyAsync(c->probs.p, &P, sizeof P, hipMemcpyHostToDevice, c->stream));
+    launch_ratio(c->probs.as<ProbDev>(), 1, c->parts.as<Top2>(), ratio, c->good_q.as<int32_t>(),
+                 c->good_t.as<int32_t>(), c->pts.as<float4>(), c->n_good.as<int>(), nullptr, nullptr, c->stream);
+    HIPCHK(c, hipGetLastError());
+    int ng = 0;
+    HIPCHK(c, hipMemcpyAsync(&ng, c->n_good.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (ng > 0) {
+        if (q_out) HIPCHK(c, hipMemcpy(q_out, c->good_q.p, sizeof(int32_t) * ng, hipMemcpyDeviceToHost));
+        if (t_out) HIPCHK(c, hipMemcpy(t_out, c->good_t.p, sizeof(int32_t) * ng, hipMemcpyDeviceToHost));
+    }
+    *n_good = ng;
+    c->last_n = 0;
+    return MIM_OK;
+}
+
+mim_status mim_knn2_sets_dev(mim_ctx* c, int32_t query_set, int32_t train_set, int32_t* idx_dev,
+                             float* dist_dev) {
+    if (!c || !idx_dev || !dist_dev) return MIM_EINVAL;
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIPCHK(c, hipSetDevice(c->device));
+    mim_problem pr{query_set, train_set};
+    mim_status s = build_tables(c, &pr, 1, 1);
+    if (s != MIM_OK) return s;
+    ev_mark(c, "begin");
+    launch_knn(c->probs.as<ProbDev>(), c->works.as<KnnWork>(), c->n_works, c->parts.as<Top2>(), c->stream);
+    HIPCHK(c, hipGetLastError());
+    ev_mark(c, "knn");
+    launch_ratio(c->probs.as<ProbDev>(), 1, c->parts.as<Top2>(), 0.9f, c->good_q.as<int32_t>(),
+                 c->good_t.as<int32_t>(), c->pts.as<float4>(), c->n_good.as<int>(), idx_dev, dist_dev, c->stream);
+    HIPCHK(c, hipGetLastError());
+    ev_mark(c, "ratio");
+    return MIM_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,409 @@
+// knn.hip — brute-force NORM_L2 k=2 matching + Lowe ratio test on gfx950.
+//
+// Replaces BFMatcher(NORM_L2).knnMatch(view, scene, m, 2) and the ratio-test loop of
+// /root/reference/src/TestsDetector.cpp:36,60,66-72 (OpenCV: matchers.cpp knnMatchImpl ->
+// batch_distance.cpp batchDistance(K=2) -> normL2Sqr_).
+//
+// Exact path (SIFT rows: integers in [0,255]): D[i][j] = |t_i|^2 - 2 q_j.t_i on the bf16 MFMA
+// (v_mfma_f32_32x32x16_bf16, fp32 accumulate).  Every operand (0..255, -2q in -510..0) is exact in
+// bf16 and every partial sum is an integer of magnitude < 2^24, so D is exact in any order and
+// d = sqrtf(D + |q_j|^2) is bit-identical to OpenCV's sqrt(normL2Sqr_).
+// Top-2 selection keys on the float distance (ties -> lower train index), computed without a sqrt
+// per pair: a candidate beats the running 2nd best iff its integer d^2 is below the smallest
+// integer whose sqrtf equals the 2nd-best key.
+//
+// Generic path (any other float rows): per-pair fp32 arithmetic in OpenCV's SSE normL2Sqr_ order
+// (4 accumulators x 4 lanes, no FMA), bit-identical to oracle/mim_oracle.c l2sqr_sse_order.
+#include "mim_internal.h"
+#include <float.h>
+#include <limits.h>
+
+namespace mim {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+
+// ------------------------------------------------------------------------------------------------
+// prep: fp32 rows -> bf16 fragment-major tiles + squared norms + integrality flag.
+// Fragment-major: a tile of 64 rows is [u 0..1][kstep s 0..7][lane 0..63][j 0..7] with
+// row = 32u + (lane & 31), col = 16s + 8(lane >> 5) + j — exactly the per-lane operand of
+// v_mfma_f32_32x32x16_bf16, so one 1 KiB wave load = one fragment, fully coalesced.
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void prep_set_kernel(const float* __restrict__ src, int n,
+                                                       uint16_t* __restrict__ frag,
+                                                       float* __restrict__ norm,
+                                                       int* __restrict__ flags) {
+    const int tile = blockIdx.x, tid = threadIdx.x;
+    int bad = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int ci = k * 256 + tid;  // output chunk (16 B) within the tile
+        const int u = ci >> 9, s = (ci >> 6) & 7, lane = ci & 63;
+        const int row = tile * 64 + 32 * u + (lane & 31);
+        const int col = 16 * s + 8 * (lane >> 5);
+        uint16_t o[8];
+        if (row < n) {
+            const float4* p = reinterpret_cast<const float4*>(src + (size_t)row * kDim + col);
+            float4 a = p[0], b = p[1];
+            float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                bad |= !(v[j] >= 0.f && v[j] <= 255.f && v[j] == rintf(v[j]));
+                __bf16 hb = (__bf16)v[j];
+                o[j] = __builtin_bit_cast(uint16_t, hb);
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) o[j] = 0;
+        }
+        uint4 w;
+        w.x = o[0] | (uint32_t(o[1]) << 16);
+        w.y = o[2] | (uint32_t(o[3]) << 16);
+        w.z = o[4] | (uint32_t(o[5]) << 16);
+        w.w = o[6] | (uint32_t(o[7]) << 16);
+        reinterpret_cast<uint4*>(frag)[(size_t)tile * 1024 + ci] = w;
+    }
+    if (tid < 64) {
+        const int row = tile * 64 + tid;
+        float s = 0.f;
+        if (row < n) {
+            const float* p = src + (size_t)row * kDim;
+            for (int c = 0; c < kDim; ++c) s += p[c] * p[c];
+        }
+        norm[row] = s;
+    }
+    if (__any(bad) && (tid & 63) == 0) atomicOr(flags, 1);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Running top-2 of one query inside one lane.  Candidates arrive in increasing train index, so an
+// equal key never displaces an earlier one (OpenCV's strict `d < dist[K-1]` / `dist[k] > d`).
+// ------------------------------------------------------------------------------------------------
+struct LaneTop2 {
+    float k1, k2;    // keys (distances), FLT_MAX = absent
+    int i1, i2;      // train indices, INT_MAX = absent
+    float d1, d2;    // exact squared distances of the two entries
+    float T;         // candidate test: D < T  <=>  sqrtf(D + qn) < k2
+};
+
+__device__ __forceinline__ void top2_init(LaneTop2& s) {
+    s.k1 = s.k2 = FLT_MAX;
+    s.i1 = s.i2 = INT_MAX;
+    s.d1 = s.d2 = 0.f;
+    s.T = FLT_MAX;
+}
+
+// smallest integer m with sqrtf(m) == key (key = sqrtf(d2), d2 an exact integer < 2^24)
+__device__ __forceinline__ float sqrt_class_floor(float d2, float key) {
+    float lo = d2;
+    while (lo >= 1.f && sqrtf(lo - 1.f) == key) lo -= 1.f;
+    return lo;
+}
+
+__device__ __forceinline__ void top2_insert_exact(LaneTop2& s, float D, float qn, int idx) {
+    const float d2 = D + qn;  // exact: integers < 2^24
+    const float key = sqrtf(d2);
+    if (key < s.k1) {
+        s.k2 = s.k1; s.i2 = s.i1; s.d2 = s.d1;
+        s.k1 = key;  s.i1 = idx;  s.d1 = d2;
+    } else {
+        s.k2 = key; s.i2 = idx; s.d2 = d2;
+    }
+    s.T = (s.i2 == INT_MAX) ? FLT_MAX : sqrt_class_floor(s.d2, s.k2) - qn;
+}
+
+__device__ __forceinline__ bool key_less(float ka, int ia, float kb, int ib) {
+    return ka < kb || (ka == kb && ia < ib);
+}
+
+__device__ __forceinline__ void top2_merge(float& k1, int& i1, float& k2, int& i2, float k, int i) {
+    if (key_less(k, i, k1, i1)) {
+        k2 = k1; i2 = i1; k1 = k; i1 = i;
+    } else if (key_less(k, i, k2, i2)) {
+        k2 = k; i2 = i;
+    }
+}
+
+// D values of one 32x32 MFMA tile for this lane's query: rows (g&3) + 8(g>>2) + 4h, g ascending.
+__device__ __forceinline__ void epilogue(const f32x16& acc, LaneTop2& s, float qn, int row0) {
+    float m = acc[0];
+#pragma unroll
+    for (int g = 1; g < 16; ++g) m = fminf(m, acc[g]);
+    if (m < s.T) {
+#pragma unroll
+        for (int g = 0; g < 16; ++g) {
+            if (acc[g] < s.T) top2_insert_exact(s, acc[g], qn, row0 + (g & 3) + 8 * (g >> 2));
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Exact distance kernel.  Block = 4 waves = 256 queries (each wave: two 32-query MFMA column
+// tiles, their -2q fragments held in VGPRs for the whole sweep).  Train tiles of 64 rows stream
+// HBM -> registers -> LDS (double buffer, one barrier per tile); each wave reads the 16 KiB tile
+// as 16 conflict-free ds_read_b128 and issues 32 MFMAs per tile.
+// ------------------------------------------------------------------------------------------------
+constexpr int kLdsTile = kTileBytes + 256;  // fragments + 64 norms
+
+__global__ __launch_bounds__(256, 2) void knn2_bf16_kernel(const ProbDev* __restrict__ probs,
+                                                          const KnnWork* __restrict__ works,
+                                                          Top2* __restrict__ parts) {
+    __shared__ __attribute__((aligned(16))) unsigned char smem[2 * kLdsTile];
+    const KnnWork w = works[blockIdx.x];
+    const ProbDev* P = probs + w.problem;
+    if (*P->q.flags | *P->t.flags) return;  // not integer-valued: generic kernel handles it
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, h = lane >> 5, r = lane & 31;
+    const int nq = P->q.n, nt = P->t.n;
+    const uint4* __restrict__ tsrc = reinterpret_cast<const uint4*>(P->t.frag);
+    const float* __restrict__ tnorm = P->t.norm;
+
+    // ---- query fragments: B[k][j] = -2 q_j[k] (exact in bf16) ----
+    const int qtile = (w.q0 >> 6) + wave;
+    const bool qvalid = qtile < P->q.n_tiles;
+    bf16x8 B[2][8];
+    float qn[2] = {0.f, 0.f};
+    {
+        const uint4* qsrc = reinterpret_cast<const uint4*>(P->q.frag) + (size_t)(qvalid ? qtile : 0) * 1024;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+#pragma unroll
+            for (int s = 0; s < 8; ++s) {
+                uint4 v = qvalid ? qsrc[(u * 8 + s) * 64 + lane] : make_uint4(0, 0, 0, 0);
+                bf16x8 b = __builtin_bit_cast(bf16x8, v);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) b[j] = (__bf16)(-2.f * (float)b[j]);
+                B[u][s] = b;
+            }
+            qn[u] = qvalid ? P->q.norm[qtile * 64 + 32 * u + r] : 0.f;
+        }
+    }
+    LaneTop2 st[2];
+    top2_init(st[0]);
+    top2_init(st[1]);
+
+    // ---- train tile staging ----
+    uint4 stg[4];
+    float stgn = FLT_MAX;
+    auto gload = [&](int tile) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) stg[k] = tsrc[(size_t)tile * 1024 + k * 256 + tid];
+        if (tid < 64) {
+            const int row = tile * 64 + tid;
+            stgn = row < nt ? tnorm[row] : FLT_MAX;  // padded rows never win
+        }
+    };
+    auto lstore = [&](int buf) {
+        uint4* dst = reinterpret_cast<uint4*>(smem + buf * kLdsTile);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) dst[k * 256 + tid] = stg[k];
+        if (tid < 64) reinterpret_cast<float*>(smem + buf * kLdsTile + kTileBytes)[tid] = stgn;
+    };
+
+    if (w.tile0 < w.tile1) {
+        gload(w.tile0);
+        lstore(0);
+    }
+    __syncthreads();
+    for (int tile = w.tile0; tile < w.tile1; ++tile) {
+        const int buf = (tile - w.tile0) & 1;
+        const bool more = tile + 1 < w.tile1;
+        if (more) gload(tile + 1);
+        const bf16x8* A = reinterpret_cast<const bf16x8*>(smem + buf * kLdsTile);
+        const float* tn = reinterpret_cast<const float*>(smem + buf * kLdsTile + kTileBytes);
+#pragma unroll
+        for (int u2 = 0; u2 < 2; ++u2) {
+            f32x16 c;
+#pragma unroll
+            for (int gg = 0; gg < 4; ++gg) {
+                float4 v = *reinterpret_cast<const float4*>(tn + 32 * u2 + 8 * gg + 4 * h);
+                c[4 * gg + 0] = v.x; c[4 * gg + 1] = v.y; c[4 * gg + 2] = v.z; c[4 * gg + 3] = v.w;
+            }
+            f32x16 acc0 = c, acc1 = c;
+#pragma unroll
+            for (int s = 0; s < 8; ++s) {
+                const bf16x8 a = A[(u2 * 8 + s) * 64 + lane];
+                acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, B[0][s], acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, B[1][s], acc1, 0, 0, 0);
+            }
+            const int row0 = tile * 64 + 32 * u2 + 4 * h;
+            epilogue(acc0, st[0], qn[0], row0);
+            epilogue(acc1, st[1], qn[1], row0);
+        }
+        if (more) lstore(buf ^ 1);
+        __syncthreads();
+    }
+
+    // ---- merge the two lane halves (h = 0/1 hold disjoint train rows of the same query) ----
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        float k1 = st[u].k1, k2 = st[u].k2;
+        int i1 = st[u].i1, i2 = st[u].i2;
+        const float ok1 = __shfl_xor(k1, 32), ok2 = __shfl_xor(k2, 32);
+        const int oi1 = __shfl_xor(i1, 32), oi2 = __shfl_xor(i2, 32);
+        top2_merge(k1, i1, k2, i2, ok1, oi1);
+        top2_merge(k1, i1, k2, i2, ok2, oi2);
+        const int q = qtile * 64 + 32 * u + r;
+        if (h == 0 && qvalid && q < nq) {
+            Top2 o{k1, i1, k2, i2};
+            parts[P->part_off + (long long)w.split * P->q_pad + q] = o;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Generic fp32 path: one thread per query, train rows broadcast from LDS, OpenCV SSE summation
+// order (core/src/norm.cpp normL2Sqr_: 4 accumulators x 4 lanes, v_reduce_sum (a0+a2)+(a1+a3)).
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ float l2sqr_sse_order(const float* q, const float* t) {
+    float acc[4][4];
+#pragma unroll
+    for (int v = 0; v < 4; ++v)
+#pragma unroll
+        for (int l = 0; l < 4; ++l) acc[v][l] = 0.f;
+#pragma unroll
+    for (int j = 0; j < kDim; j += 16) {
+#pragma unroll
+        for (int v = 0; v < 4; ++v)
+#pragma unroll
+            for (int l = 0; l < 4; ++l) {
+                const float d = q[j + 4 * v + l] - t[j + 4 * v + l];
+                acc[v][l] = __fadd_rn(__fmul_rn(d, d), acc[v][l]);
+            }
+    }
+    float s[4];
+#pragma unroll
+    for (int l = 0; l < 4; ++l) s[l] = ((acc[0][l] + acc[1][l]) + acc[2][l]) + acc[3][l];
+    return (s[0] + s[2]) + (s[1] + s[3]);
+}
+
+__global__ __launch_bounds__(256) void knn2_f32_kernel(const ProbDev* __restrict__ probs,
+                                                       const KnnWork* __restrict__ works,
+                                                       Top2* __restrict__ parts) {
+    __shared__ __attribute__((aligned(16))) float tl[kTileRows * kDim];
+    const KnnWork w = works[blockIdx.x];
+    const ProbDev* P = probs + w.problem;
+    if (!(*P->q.flags | *P->t.flags)) return;  // integer-valued: exact MFMA kernel handles it
+    const int tid = threadIdx.x;
+    const int nq = P->q.n, nt = P->t.n;
+    const int q = w.q0 + tid;
+    float qv[kDim];
+    const bool qvalid = q < nq;
+#pragma unroll
+    for (int c = 0; c < kDim; c += 4) {
+        float4 v = qvalid ? *reinterpret_cast<const float4*>(P->q.f32 + (size_t)q * kDim + c)
+                          : make_float4(0.f, 0.f, 0.f, 0.f);
+        qv[c] = v.x; qv[c + 1] = v.y; qv[c + 2] = v.z; qv[c + 3] = v.w;
+    }
+    float k1 = FLT_MAX, k2 = FLT_MAX;
+    int i1 = INT_MAX, i2 = INT_MAX;
+    for (int tile = w.tile0; tile < w.tile1; ++tile) {
+        __syncthreads();
+        for (int e = tid; e < kTileRows * kDim / 4; e += 256) {
+            const int row = tile * 64 + e / (kDim / 4);
+            float4 v = row < nt ? reinterpret_cast<const float4*>(P->t.f32)[(size_t)tile * 64 * (kDim / 4) + e]
+                                : make_float4(0.f, 0.f, 0.f, 0.f);
+            reinterpret_cast<float4*>(tl)[e] = v;
+        }
+        __syncthreads();
+        const int rows = min(64, nt - tile * 64);
+        for (int rr = 0; rr < rows; ++rr) {
+            const float d = sqrtf(l2sqr_sse_order(qv, tl + rr * kDim));
+            // OpenCV compares the bit patterns as int: for non-negative floats that is float order;
+            // NaN (> FLT_MAX bits) and values >= FLT_MAX are never inserted.
+            if (d < k2) {
+                const int j = tile * 64 + rr;
+                if (d < k1) { k2 = k1; i2 = i1; k1 = d; i1 = j; }
+                else { k2 = d; i2 = j; }
+            }
+        }
+    }
+    if (qvalid) parts[P->part_off + (long long)w.split * P->q_pad + q] = Top2{k1, i1, k2, i2};
+}
+
+// ------------------------------------------------------------------------------------------------
+// Merge train splits, emit knnMatch rows, Lowe ratio test and ordered compaction
+// (TestsDetector.cpp:62-72): survivors keep ascending query order — the order findHomography's
+// point lists and inlier mask are indexed by.  One 1024-thread block per problem.
+// Output pts[k] = (objPt.x, objPt.y, scenePt.x, scenePt.y) of the k-th good match.
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(1024) void ratio_compact_kernel(const ProbDev* __restrict__ probs,
+                                                            const Top2* __restrict__ parts, float ratio,
+                                                            int32_t* __restrict__ good_q,
+                                                            int32_t* __restrict__ good_t,
+                                                            float4* __restrict__ pts,
+                                                            int* __restrict__ n_good,
+                                                            int32_t* __restrict__ knn_idx,
+                                                            float* __restrict__ knn_dist) {
+    __shared__ int wsum[16];
+    __shared__ int wbase[17];
+    const ProbDev* P = probs + blockIdx.x;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int nq = P->q.n;
+    int running = 0;
+    for (int base = 0; base < nq; base += 1024) {
+        const int q = base + tid;
+        float k1 = FLT_MAX, k2 = FLT_MAX;
+        int i1 = INT_MAX, i2 = INT_MAX;
+        if (q < nq) {
+            for (int sp = 0; sp < P->nsplit; ++sp) {
+                const Top2 t = parts[P->part_off + (long long)sp * P->q_pad + q];
+                top2_merge(k1, i1, k2, i2, t.k1, t.i1);
+                top2_merge(k1, i1, k2, i2, t.k2, t.i2);
+            }
+            if (knn_idx) {
+                knn_idx[2 * q] = i1 == INT_MAX ? -1 : i1;
+                knn_idx[2 * q + 1] = i2 == INT_MAX ? -1 : i2;
+                knn_dist[2 * q] = k1;
+                knn_dist[2 * q + 1] = k2;
+            }
+        }
+        const bool good = q < nq && i1 != INT_MAX && i2 != INT_MAX && k1 < ratio * k2;
+        const unsigned long long bal = __ballot(good);
+        const int within = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0));
+        if (lane == 0) wsum[wave] = __popcll(bal);
+        __syncthreads();
+        if (tid == 0) {
+            int acc = 0;
+            for (int i = 0; i < 16; ++i) { wbase[i] = acc; acc += wsum[i]; }
+            wbase[16] = acc;
+        }
+        __syncthreads();
+        if (good) {
+            const long long o = P->good_off + running + wbase[wave] + within;
+            good_q[o] = q;
+            good_t[o] = i1;
+            const float2 a = P->q.kp[q], b = P->t.kp[i1];
+            pts[o] = make_float4(a.x, a.y, b.x, b.y);
+        }
+        running += wbase[16];
+        __syncthreads();
+    }
+    if (tid == 0) n_good[blockIdx.x] = running;
+}
+
+// ------------------------------------------------------------------------------------------------
+// host-side launchers (called from api.cpp)
+// ------------------------------------------------------------------------------------------------
+void launch_prep_set(const float* src, int n, uint16_t* frag, float* norm, int* flags, hipStream_t st) {
+    const int tiles = (n + 63) / 64;
+    if (tiles > 0) prep_set_kernel<<<tiles, 256, 0, st>>>(src, n, frag, norm, flags);
+}
+
+// Both kernels are enqueued; each block reads its problem's integrality flags (set by prep on the
+// device) and only the matching kernel does the work, so no host round trip is needed.
+void launch_knn(const ProbDev* probs, const KnnWork* works, int n_works, Top2* parts, hipStream_t st) {
+    if (n_works <= 0) return;
+    knn2_bf16_kernel<<<n_works, 256, 0, st>>>(probs, works, parts);
+    knn2_f32_kernel<<<n_works, 256, 0, st>>>(probs, works, parts);
+}
+
+void launch_ratio(const ProbDev* probs, int n_probs, const Top2* parts, float ratio, int32_t* good_q,
+                  int32_t* good_t, float4* pts, int* n_good, int32_t* knn_idx, float* knn_dist,
+                  hipStream_t st) {
+    if (n_probs > 0)
+        ratio_compact_kernel<<<n_probs, 1024, 0, st>>>(probs, parts, ratio, good_q, good_t, pts, n_good,
+                                                       knn_idx, knn_dist);
+}
+
+}  // namespace mim

@@ -1,0 +1,74 @@
+// mim_internal.h — device-side data layout shared by the HIP kernels and the host launcher.
+// See DESIGN.md "Data layout in HBM".  gfx950 only (wave64, bf16 MFMA 32x32x16).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mim {
+
+constexpr int kDim = 128;          // SIFT descriptor length (TestsDetector.cpp:60 operands)
+constexpr int kTileRows = 64;      // descriptor rows per staged tile
+constexpr int kTileBytes = kTileRows * kDim * 2;  // 16 KiB of bf16 per tile
+constexpr int kWave = 64;
+
+// One descriptor set = one ObjectModel view (objectModel.hpp:11-16) or one scaled scene
+// (TestsDetector.cpp:104-106), resident in HBM.
+struct SetDev {
+    const uint16_t* frag;  // bf16 bits, "fragment-major" tiles: [tile][u 0..1][kstep 0..7][lane 0..63][8]
+    const float* norm;     // |d|^2 per row (exact integer for integer rows), n_pad entries
+    const float* f32;      // row-major n x 128 fp32 (the caller's CV_32F rows)
+    const float2* kp;      // KeyPoint::pt per row
+    int n;
+    int n_tiles;           // ceil(n / 64)
+    int* flags;            // bit0: a value is not an integer in [0,255]
+};
+
+struct Top2 {  // partial top-2 of one query over one train split; key = distance (float)
+    float k1; int i1; float k2; int i2;
+};
+
+// Per-problem device record (knn + ratio + RANSAC).  Built by the host launcher.
+struct ProbDev {
+    SetDev q, t;
+    int nsplit;          // train splits for the distance kernel
+    int q_pad;           // nq rounded up to 256
+    long long part_off;  // into Top2 partials: [split][q_pad]
+    long long good_off;  // into good arrays (capacity nq)
+    long long it_off;    // into per-iteration arrays (capacity max_iters)
+};
+
+// Work item of the distance kernel: 256 queries x a train tile range of one problem.
+struct KnnWork {
+    int problem;
+    int q0;        // first query row (multiple of 256)
+    int tile0;     // train tiles [tile0, tile1)
+    int tile1;
+    int split;
+};
+
+// RANSAC state per problem (RANSACPointSetRegistrator::run locals, ptsetreg.cpp).
+struct RansacState {
+    long long stream_pos;  // RNG draws consumed so far (all calls see RNG((uint64)-1))
+    int produced;          // samples produced (iterations whose getSubset succeeded)
+    int fail_iter;         // iteration whose getSubset failed after 10000 attempts (-1: none)
+    int fail_run;          // consecutive failed subset attempts carried across sampler rounds
+    int niters;            // current iteration bound (RANSACUpdateNumIters)
+    int max_good;          // maxGoodCount
+    int best_iter;         // iteration of bestModel
+    int next_iter;         // first iteration not yet replayed by the select kernel
+    int done;              // loop finished (iter >= niters or getSubset failure)
+    int n;                 // point count (= n_good)
+    int active;            // problem takes the RANSAC path (n_good > 4)
+    int pad_;
+};
+
+struct RansacParams {
+    double thresh;   // reprojection threshold (5.0)
+    double conf;     // 0.995
+    int max_iters;   // 2000 (reference) / 50000 (BASELINE C3/C4)
+    float ratio;
+    int min_good, min_inliers;
+    double det_lo, det_hi;
+};
+
+}  // namespace mim

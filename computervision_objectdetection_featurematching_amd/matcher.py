@@ -1,0 +1,176 @@
+"""Python mirror of the reference's hot-path interface, running on the HIP kernels of libmim.so.
+
+Reference call sites (/root/reference/src/TestsDetector.cpp):
+  :36,60   BFMatcher(NORM_L2).knnMatch(view_desc, scene_desc, knn, 2)  -> Matcher.knn_match
+  :66-72   ratio test `m[0].distance < 0.9f * m[1].distance`           -> Matcher.ratio_filter
+  :78      findHomography(objPts, scenePts, RANSAC, 5.0, inlierMask)   -> Matcher.find_homography
+  :58-95   the per-view loop with its gates (:74, :79, :81, :84)       -> Matcher.match_batch
+Argument meaning and error behaviour follow OpenCV: an empty query gives no rows, n < 4 points
+raise (CV_Error StsVecLengthErr), a failed RANSAC returns an empty H (None) and a zero mask.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib
+from ._lib import MimError, Params, Problem, RESULT_DTYPE
+
+DIM = 128
+
+
+def default_params(**kw) -> Params:
+    p = Params()
+    _lib.load().mim_default_params(C.byref(p))
+    for k, v in kw.items():
+        setattr(p, k, v)
+    return p
+
+
+@dataclass
+class DMatch:  # cv::DMatch
+    queryIdx: int
+    trainIdx: int
+    imgIdx: int
+    distance: float
+
+
+class Matcher:
+    """One GPU context (device + HIP stream).  Not a CPU object: construction fails without a GPU."""
+
+    def __init__(self, device: int = 0):
+        self.L = _lib.load()
+        self._ctx = C.c_void_p()
+        st = self.L.mim_ctx_create(device, C.byref(self._ctx))
+        if st != _lib.MIM_OK:
+            raise MimError(st, f"mim_ctx_create(device={device}) failed (no HIP device?)")
+        self.device = device
+
+    def close(self):
+        if self._ctx:
+            self.L.mim_ctx_destroy(self._ctx)
+            self._ctx = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, st: int):
+        if st != _lib.MIM_OK:
+            raise MimError(st, self.L.mim_last_error(self._ctx).decode())
+
+    @property
+    def ctx(self):
+        return self._ctx
+
+    def set_stream(self, stream_handle: int | None):
+        self._check(self.L.mim_ctx_set_stream(self._ctx, C.c_void_p(stream_handle or 0)))
+
+    def synchronize(self):
+        self._check(self.L.mim_synchronize(self._ctx))
+
+    # ---- descriptor sets ------------------------------------------------------------------
+    def add_set(self, desc, kp) -> int:
+        """Register one ObjectModel view / scene scale.  numpy (host) or torch (device) arrays."""
+        on_dev = int(hasattr(desc, "is_cuda") and desc.is_cuda)
+        if not on_dev:
+            desc = np.ascontiguousarray(desc, np.float32).reshape(-1, DIM)
+            kp = np.ascontiguousarray(kp, np.float32).reshape(-1, 2)
+        n = int(desc.shape[0])
+        sid = C.c_int32()
+        self._check(self.L.mim_set_create(self._ctx, C.c_void_p(_lib.ptr(desc)), C.c_void_p(_lib.ptr(kp)), n,
+                                          int(desc.shape[1]), on_dev, C.byref(sid)))
+        return sid.value
+
+    def clear_sets(self):
+        self._check(self.L.mim_sets_clear(self._ctx))
+
+    # ---- primitives -----------------------------------------------------------------------
+    def knn_match_arrays(self, query, train):
+        """knnMatch(query, train, k=2) as arrays: idx (nq,2) int32 (-1 absent), dist (nq,2) float32."""
+        q = np.ascontiguousarray(query, np.float32).reshape(-1, DIM)
+        t = np.ascontiguousarray(train, np.float32).reshape(-1, DIM)
+        nq = q.shape[0]
+        idx = np.full((max(nq, 1), 2), -1, np.int32)
+        dist = np.zeros((max(nq, 1), 2), np.float32)
+        self._check(self.L.mim_knn2_l2(self._ctx, C.c_void_p(q.ctypes.data), nq, C.c_void_p(t.ctypes.data),
+                                       t.shape[0], DIM, C.c_void_p(idx.ctypes.data), C.c_void_p(dist.ctypes.data)))
+        return idx[:nq], dist[:nq]
+
+    def knn_match(self, query, train, k: int = 2):
+        """BFMatcher(NORM_L2).knnMatch(query, train, matches, k=2) -> list of lists of DMatch."""
+        if k != 2:
+            raise ValueError("only k=2 is on the hot path (TestsDetector.cpp:60)")
+        idx, dist = self.knn_match_arrays(query, train)
+        return [[DMatch(i, int(idx[i, j]), 0, float(dist[i, j])) for j in range(2) if idx[i, j] >= 0]
+                for i in range(idx.shape[0])]
+
+    def ratio_filter(self, idx, dist, ratio: float = 0.9):
+        idx = np.ascontiguousarray(idx, np.int32)
+        dist = np.ascontiguousarray(dist, np.float32)
+        nq = idx.shape[0]
+        qo = np.zeros(max(nq, 1), np.int32)
+        to = np.zeros(max(nq, 1), np.int32)
+        ng = C.c_int32()
+        self._check(self.L.mim_ratio_filter(self._ctx, C.c_void_p(idx.ctypes.data), C.c_void_p(dist.ctypes.data),
+                                            nq, ratio, C.c_void_p(qo.ctypes.data), C.c_void_p(to.ctypes.data),
+                                            C.byref(ng)))
+        return qo[:ng.value], to[:ng.value]
+
+    def find_homography(self, src, dst, thresh: float = 5.0, max_iters: int = 2000, confidence: float = 0.995):
+        """cv::findHomography(src, dst, RANSAC, thresh, mask, max_iters, confidence) -> (H or None, mask)."""
+        src = np.ascontiguousarray(src, np.float32).reshape(-1, 2)
+        dst = np.ascontiguousarray(dst, np.float32).reshape(-1, 2)
+        n = src.shape[0]
+        if n < 4 or dst.shape[0] != n:
+            raise ValueError("The input arrays should have at least 4 corresponding point sets to calculate Homography")
+        H = np.zeros(9, np.float64)
+        mask = np.zeros(n, np.uint8)
+        st = self.L.mim_find_homography(self._ctx, C.c_void_p(src.ctypes.data), C.c_void_p(dst.ctypes.data), n,
+                                        thresh, max_iters, confidence, C.c_void_p(H.ctypes.data),
+                                        C.c_void_p(mask.ctypes.data))
+        if st == _lib.MIM_ENOMODEL:
+            return None, mask
+        self._check(st)
+        return H.reshape(3, 3), mask
+
+    # ---- fused batch ----------------------------------------------------------------------
+    def match_batch_async(self, problems, params: Params | None = None):
+        params = params or default_params()
+        arr = (Problem * len(problems))(*[Problem(int(a), int(b)) for a, b in problems])
+        self._check(self.L.mim_batch_run(self._ctx, arr, len(problems), C.byref(params)))
+        return len(problems)
+
+    def batch_results(self, n: int) -> np.ndarray:
+        out = np.zeros(n, RESULT_DTYPE)
+        self._check(self.L.mim_batch_results(self._ctx, C.c_void_p(out.ctypes.data)))
+        return out
+
+    def batch_results_dev_ptr(self) -> int:
+        return int(self.L.mim_batch_results_dev(self._ctx) or 0)
+
+    def problem_detail(self, i: int, n_good: int):
+        q = np.zeros(max(n_good, 1), np.int32)
+        t = np.zeros(max(n_good, 1), np.int32)
+        m = np.zeros(max(n_good, 1), np.uint8)
+        self._check(self.L.mim_batch_problem_detail(self._ctx, i, C.c_void_p(q.ctypes.data), C.c_void_p(t.ctypes.data),
+                                                    C.c_void_p(m.ctypes.data)))
+        return q[:n_good], t[:n_good], m[:n_good]
+
+    def match_batch(self, problems, params: Params | None = None) -> np.ndarray:
+        n = self.match_batch_async(problems, params)
+        return self.batch_results(n)
+
+    def knn_sets_dev(self, qset: int, tset: int, idx_dev, dist_dev):
+        self._check(self.L.mim_knn2_sets_dev(self._ctx, qset, tset, C.c_void_p(_lib.ptr(idx_dev)),
+                                             C.c_void_p(_lib.ptr(dist_dev))))
+
+    def set_timing(self, on: bool):
+        self._check(self.L.mim_set_timing(self._ctx, int(on)))
+
+    def kernel_ms(self, name: str) -> float:
+        return float(self.L.mim_last_kernel_ms(self._ctx, name.encode()))

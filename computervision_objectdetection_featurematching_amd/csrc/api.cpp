@@ -26,10 +26,9 @@ void launch_knn(const ProbDev* probs, const KnnWork* works, int n_works, Top2* p
 void launch_ratio(const ProbDev* probs, int n_probs, const Top2* parts, float ratio, int32_t* good_q,
                   int32_t* good_t, float4* pts, int* n_good, int32_t* knn_idx, float* knn_dist,
                   hipStream_t st);
-struct RansacWs;
-void ransac_enqueue(const RansacParams& prm, int n_probs, const ProbDev* probs_dev, const float4* pts,
-                    const int* n_good, RansacWs& ws, mim_result* results, uint8_t* masks,
-                    hipStream_t st, const std::vector<std::pair<std::string, hipEvent_t>>* evs);
+void ransac_enqueue(const RansacParams& prm, int n_probs, const ProbDev* probs, const float4* pts,
+                    const int* n_good, const RansacBufs& b, uint8_t* masks, mim_result* results, int raw,
+                    hipStream_t s, void (*mark)(void*, const char*), void* mark_ctx);
 }  // namespace mim
 
 using namespace mim;
@@ -96,9 +95,8 @@ struct SetRec {
 namespace mim {
 // RANSAC workspace (definition shared with ransac.hip through this layout)
 struct RansacWs {
-    DevBuf state, samples, hyp, counts, stream, scratch;
+    DevBuf state, samples, hyp, counts, stream, scratch, inl, err;
     long long stream_len = 0;
-    int timing = 0;
 };
 }  // namespace mim
 
@@ -182,7 +180,7 @@ void mim_ctx_destroy(mim_ctx* c) {
     c->arena.release();
     for (DevBuf* b : {&c->probs, &c->works, &c->parts, &c->good_q, &c->good_t, &c->pts, &c->n_good,
                       &c->results, &c->masks, &c->knn_idx, &c->knn_dist, &c->rws.state, &c->rws.samples,
-                      &c->rws.hyp, &c->rws.counts, &c->rws.stream, &c->rws.scratch})
+                      &c->rws.hyp, &c->rws.counts, &c->rws.stream, &c->rws.scratch, &c->rws.inl, &c->rws.err})
         b->release();
     if (c->own) (void)hipStreamDestroy(c->own);
     delete c;
@@ -481,6 +479,184 @@ mim_status mim_knn2_sets_dev(mim_ctx* c, int32_t query_set, int32_t train_set, i
                  c->good_t.as<int32_t>(), c->pts.as<float4>(), c->n_good.as<int>(), idx_dev, dist_dev, c->stream);
     HIPCHK(c, hipGetLastError());
     ev_mark(c, "ratio");
+    return MIM_OK;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------------------------
+// RANSAC: RNG stream, workspace, batch entry points
+// ---------------------------------------------------------------------------------------------
+static void mark_cb(void* vc, const char* name) { ev_mark((mim_ctx*)vc, name); }
+
+// cv::RNG((uint64)-1).next() stream (core/include/opencv2/core/operations.hpp). Every
+// findHomography call re-seeds, so one stream serves all problems; generated once per ctx.
+static mim_status ensure_stream(mim_ctx* c, long long need) {
+    if (c->rws.stream_len >= need) return MIM_OK;
+    long long len = std::max<long long>(need, 1LL << 23);
+    if (len > (1LL << 28)) return fail(c, MIM_ERANGE, "RNG stream of %lld draws exceeds the 2^28 cap", len);
+    std::vector<uint32_t> h((size_t)len);
+    uint64_t st = 0xffffffffffffffffULL;
+    for (long long i = 0; i < len; ++i) {
+        st = (uint64_t)(uint32_t)st * 4164903690U + (uint32_t)(st >> 32);
+        h[(size_t)i] = (uint32_t)st;
+    }
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, c->rws.stream.ensure(sizeof(uint32_t) * len));
+    HIPCHK(c, hipMemcpy(c->rws.stream.p, h.data(), sizeof(uint32_t) * len, hipMemcpyHostToDevice));
+    c->rws.stream_len = len;
+    return MIM_OK;
+}
+
+static mim_status ransac_locked(mim_ctx* c, int n, const mim_params* prm, int raw) {
+    const int max_iters = std::max(prm->max_iters, 1);
+    mim_status s = ensure_stream(c, (long long)max_iters * 64 + 40000 * 4);
+    if (s != MIM_OK) return s;
+    long long it_total = 0, good_total = 0;
+    for (int i = 0; i < n; ++i) {
+        it_total = std::max(it_total, c->h_probs[i].it_off + max_iters);
+        good_total = std::max(good_total, c->h_probs[i].good_off + std::max(c->h_probs[i].q.n, 1));
+    }
+    HIPCHK(c, c->rws.state.ensure(sizeof(RansacState) * std::max(n, 1)));
+    HIPCHK(c, c->rws.samples.ensure(sizeof(int4) * it_total));
+    HIPCHK(c, c->rws.hyp.ensure(sizeof(float) * 8 * it_total));
+    HIPCHK(c, c->rws.counts.ensure(sizeof(int) * it_total));
+    HIPCHK(c, c->rws.inl.ensure(sizeof(float4) * good_total));
+    HIPCHK(c, c->rws.err.ensure(sizeof(int) * 4));
+    HIPCHK(c, c->results.ensure(sizeof(mim_result) * std::max(n, 1)));
+    HIPCHK(c, c->masks.ensure(good_total));
+    HIPCHK(c, hipMemsetAsync(c->rws.err.p, 0, sizeof(int) * 4, c->stream));
+    RansacBufs b{};
+    b.state = c->rws.state.as<RansacState>();
+    b.samples = c->rws.samples.as<int4>();
+    b.hyp = c->rws.hyp.as<float>();
+    b.counts = c->rws.counts.as<int>();
+    b.stream = c->rws.stream.as<uint32_t>();
+    b.stream_len = c->rws.stream_len;
+    b.inl = c->rws.inl.as<float4>();
+    b.err = c->rws.err.as<int>();
+    RansacParams rp{};
+    rp.thresh = prm->ransac_thresh > 0 ? prm->ransac_thresh : 3.0;  // findHomography: thresh <= 0 -> 3
+    rp.conf = prm->confidence;
+    rp.max_iters = max_iters;
+    rp.ratio = prm->ratio;
+    rp.min_good = prm->min_good;
+    rp.min_inliers = prm->min_inliers;
+    rp.det_lo = prm->det_lo;
+    rp.det_hi = prm->det_hi;
+    ransac_enqueue(rp, n, c->probs.as<ProbDev>(), c->pts.as<float4>(), c->n_good.as<int>(), b, c->masks.as<uint8_t>(),
+                   c->results.as<mim_result>(), raw, c->stream, mark_cb, c);
+    HIPCHK(c, hipGetLastError());
+    return MIM_OK;
+}
+
+static mim_status check_params(mim_ctx* c, const mim_params* p) {
+    if (!p) return fail(c, MIM_EINVAL, "null params");
+    if (!(p->confidence > 0 && p->confidence < 1)) return fail(c, MIM_EINVAL, "confidence must be in (0,1)");
+    if (p->max_iters > 10000000) return fail(c, MIM_EINVAL, "max_iters too large");
+    return MIM_OK;
+}
+
+extern "C" {
+
+mim_status mim_batch_run(mim_ctx* c, const mim_problem* problems, int32_t n, const mim_params* params) {
+    if (!c) return MIM_EINVAL;
+    if (n < 0 || (n > 0 && !problems)) return fail(c, MIM_EINVAL, "batch_run: bad arguments");
+    mim_status s = check_params(c, params);
+    if (s != MIM_OK) return s;
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIPCHK(c, hipSetDevice(c->device));
+    if (n == 0) { c->last_n = 0; return MIM_OK; }
+    s = build_tables(c, problems, n, std::max(params->max_iters, 1));
+    if (s != MIM_OK) return s;
+    s = knn_ratio_locked(c, n, params->ratio, false);
+    if (s != MIM_OK) return s;
+    return ransac_locked(c, n, params, 0);
+}
+
+mim_status mim_batch_results(mim_ctx* c, mim_result* out) {
+    if (!c) return MIM_EINVAL;
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    ev_collect(c);
+    if (c->last_n > 0 && out)
+        HIPCHK(c, hipMemcpy(out, c->results.p, sizeof(mim_result) * c->last_n, hipMemcpyDeviceToHost));
+    int err = 0;
+    if (c->rws.err.p) HIPCHK(c, hipMemcpy(&err, c->rws.err.p, sizeof(int), hipMemcpyDeviceToHost));
+    if (err & 1) return fail(c, MIM_ERANGE, "RANSAC consumed the whole RNG stream (%lld draws)", c->rws.stream_len);
+    return MIM_OK;
+}
+
+const mim_result* mim_batch_results_dev(mim_ctx* c) { return c ? c->results.as<mim_result>() : nullptr; }
+
+mim_status mim_batch_problem_detail(mim_ctx* c, int32_t i, int32_t* q_idx, int32_t* t_idx, uint8_t* mask) {
+    if (!c) return MIM_EINVAL;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (i < 0 || i >= c->last_n) return fail(c, MIM_EINVAL, "problem %d out of range", i);
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    int ng = 0;
+    HIPCHK(c, hipMemcpy(&ng, c->n_good.as<int>() + i, sizeof(int), hipMemcpyDeviceToHost));
+    const long long o = c->h_good_off[i];
+    if (ng > 0) {
+        if (q_idx) HIPCHK(c, hipMemcpy(q_idx, c->good_q.as<int32_t>() + o, sizeof(int32_t) * ng, hipMemcpyDeviceToHost));
+        if (t_idx) HIPCHK(c, hipMemcpy(t_idx, c->good_t.as<int32_t>() + o, sizeof(int32_t) * ng, hipMemcpyDeviceToHost));
+        if (mask) HIPCHK(c, hipMemcpy(mask, c->masks.as<uint8_t>() + o, ng, hipMemcpyDeviceToHost));
+    }
+    return MIM_OK;
+}
+
+mim_status mim_find_homography(mim_ctx* c, const float* src, const float* dst, int32_t n, double thresh,
+                               int32_t max_iters, double conf, double H[9], uint8_t* mask) {
+    if (!c) return MIM_EINVAL;
+    if (!src || !dst || !H || !mask) return fail(c, MIM_EINVAL, "find_homography: null pointer");
+    if (n < 4)  // CV_Error(StsVecLengthErr) in cv::findHomography
+        return fail(c, MIM_EINVAL, "The input arrays should have at least 4 corresponding point sets");
+    mim_params prm;
+    mim_default_params(&prm);
+    prm.ransac_thresh = thresh;
+    prm.max_iters = max_iters;
+    prm.confidence = conf;
+    prm.min_good = 4;
+    prm.min_inliers = 0;
+    mim_status s = check_params(c, &prm);
+    if (s != MIM_OK) return s;
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    std::vector<float4> pts(n);
+    for (int i = 0; i < n; ++i) pts[i] = make_float4(src[2 * i], src[2 * i + 1], dst[2 * i], dst[2 * i + 1]);
+    HIPCHK(c, c->pts.ensure(sizeof(float4) * n));
+    HIPCHK(c, c->n_good.ensure(sizeof(int)));
+    HIPCHK(c, c->probs.ensure(sizeof(ProbDev)));
+    HIPCHK(c, hipMemcpy(c->pts.p, pts.data(), sizeof(float4) * n, hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(c->n_good.p, &n, sizeof(int), hipMemcpyHostToDevice));
+    ProbDev P{};
+    P.q.n = n;
+    P.good_off = 0;
+    P.it_off = 0;
+    HIPCHK(c, hipMemcpy(c->probs.p, &P, sizeof P, hipMemcpyHostToDevice));
+    c->h_probs.assign(1, P);
+    c->h_good_off.assign(1, 0);
+    c->last_n = 1;
+    ev_mark(c, "begin");
+    s = ransac_locked(c, 1, &prm, 1);
+    if (s != MIM_OK) return s;
+    mim_result r;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    ev_collect(c);
+    HIPCHK(c, hipMemcpy(&r, c->results.p, sizeof r, hipMemcpyDeviceToHost));
+    HIPCHK(c, hipMemcpy(mask, c->masks.p, n, hipMemcpyDeviceToHost));
+    int err = 0;
+    HIPCHK(c, hipMemcpy(&err, c->rws.err.p, sizeof(int), hipMemcpyDeviceToHost));
+    if (err & 1) return fail(c, MIM_ERANGE, "RANSAC consumed the whole RNG stream");
+    if (r.status == MIM_EMPTY_H) {
+        for (int i = 0; i < 9; ++i) H[i] = 0;
+        memset(mask, 0, n);
+        return MIM_ENOMODEL;
+    }
+    for (int i = 0; i < 9; ++i) H[i] = r.H[i];
     return MIM_OK;
 }
 

@@ -72,3 +72,17 @@ struct RansacParams {
 };
 
 }  // namespace mim
+
+namespace mim {
+// Device buffers of one RANSAC batch (owned by the ctx in api.cpp).
+struct RansacBufs {
+    RansacState* state;       // [n_probs]
+    int4* samples;            // [it_off + iter]  4 point indices of the minimal sample
+    float* hyp;               // [(it_off + iter) * 8]  (float)H[0..7] of the minimal-sample model
+    int* counts;              // [it_off + iter]  inlier count, -1 when runKernel returned 0
+    const uint32_t* stream;   // raw cv::RNG((uint64)-1).next() stream shared by every problem
+    long long stream_len;
+    float4* inl;              // [good_off + k] compressed inliers for the refit (scratch)
+    int* err;                 // device error word (bit0: RNG stream exhausted)
+};
+}  // namespace mim

@@ -17,7 +17,7 @@ EXPORTS = [
     "mim_version", "mim_default_params", "mim_ctx_create", "mim_ctx_destroy", "mim_last_error",
     "mim_ctx_set_stream", "mim_synchronize", "mim_set_create", "mim_sets_clear", "mim_knn2_l2",
     "mim_ratio_filter", "mim_find_homography", "mim_batch_run", "mim_batch_results",
-    "mim_batch_results_dev", "mim_batch_problem_detail", "mim_knn2_sets_dev", "mim_last_kernel_ms",
+    "mim_batch_results_dev", "mim_batch_results_copy", "mim_batch_problem_detail", "mim_knn2_sets_dev", "mim_last_kernel_ms",
     "mim_set_timing",
 ]
 
@@ -100,6 +100,8 @@ def load():
     L.mim_batch_results.argtypes = [vp, vp]
     L.mim_batch_results_dev.argtypes = [vp]
     L.mim_batch_results_dev.restype = vp
+    L.mim_batch_results_copy.argtypes = [vp, vp, i32]
+    L.mim_batch_results_copy.restype = C.c_int32
     L.mim_batch_problem_detail.argtypes = [vp, i32, i32p, i32p, u8p]
     L.mim_knn2_sets_dev.argtypes = [vp, i32, i32, vp, vp]
     L.mim_last_kernel_ms.argtypes = [vp, C.c_char_p]

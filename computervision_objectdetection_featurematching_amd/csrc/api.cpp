@@ -590,6 +590,16 @@ mim_status mim_batch_results(mim_ctx* c, mim_result* out) {
 
 const mim_result* mim_batch_results_dev(mim_ctx* c) { return c ? c->results.as<mim_result>() : nullptr; }
 
+mim_status mim_batch_results_copy(mim_ctx* c, void* dst, int32_t dst_on_device) {
+    if (!c || !dst) return MIM_EINVAL;
+    if (!dst_on_device) return mim_batch_results(c, (mim_result*)dst);
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIPCHK(c, hipSetDevice(c->device));
+    if (c->last_n > 0)
+        HIPCHK(c, hipMemcpyAsync(dst, c->results.p, sizeof(mim_result) * c->last_n, hipMemcpyDeviceToDevice, c->stream));
+    return MIM_OK;
+}
+
 mim_status mim_batch_problem_detail(mim_ctx* c, int32_t i, int32_t* q_idx, int32_t* t_idx, uint8_t* mask) {
     if (!c) return MIM_EINVAL;
     std::lock_guard<std::mutex> lk(c->mu);

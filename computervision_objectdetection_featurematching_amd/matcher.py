@@ -150,6 +150,10 @@ class Matcher:
         self._check(self.L.mim_batch_results(self._ctx, C.c_void_p(out.ctypes.data)))
         return out
 
+    def batch_results_copy_to(self, dst_dev):
+        """Async device-to-device copy of the last batch's records (for an RCCL gather)."""
+        self._check(self.L.mim_batch_results_copy(self._ctx, C.c_void_p(_lib.ptr(dst_dev)), 1))
+
     def batch_results_dev_ptr(self) -> int:
         return int(self.L.mim_batch_results_dev(self._ctx) or 0)
 

@@ -115,6 +115,9 @@ mim_status mim_batch_run(struct mim_ctx* ctx, const mim_problem* problems, int32
 mim_status mim_batch_results(struct mim_ctx* ctx, mim_result* out);
 /* Device pointer to the n mim_result records of the last batch (valid until the next batch). */
 const mim_result* mim_batch_results_dev(struct mim_ctx* ctx);
+/* Copies the n records of the last batch into dst (device memory when dst_on_device != 0: async on
+ * the ctx stream, for an RCCL gather; host memory otherwise: synchronous). */
+mim_status mim_batch_results_copy(struct mim_ctx* ctx, void* dst, int32_t dst_on_device);
 /* Waits, then copies problem i's good matches (n_good query/train indices, ascending query order)
  * and its RANSAC inlier mask (n_good bytes).  Any output may be NULL. */
 mim_status mim_batch_problem_detail(struct mim_ctx* ctx, int32_t i, int32_t* q_idx, int32_t* t_idx,

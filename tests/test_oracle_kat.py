@@ -1,0 +1,135 @@
+"""Known-answer tests that pin the CPU restatement (oracle/) without OpenCV.
+
+The reference ships no tests/fixtures for the path, so these analytic facts are the
+pin: MWC RNG sequence, RANSACUpdateNumIters table, exact homography recovery, planted nearest
+neighbours, ratio/tie boundaries, Jacobi eigen-decomposition, checkSubset geometry.
+"""
+import numpy as np
+import pytest
+
+from computervision_objectdetection_featurematching_amd.synthetic import apply_h, random_homography, sift_like
+
+
+def test_rng_kat(oracle):
+    # cv::RNG((uint64)-1).next(): state = (u32)state * 4164903690 + (state >> 32)
+    s = oracle.rng_stream(8)
+    assert list(s) == [130063605, 3133359004, 2578348940, 925327173, 1080261831, 2946015512, 94037301, 2298661280]
+    assert [int(v) % 2000 for v in s] == [1605, 1004, 940, 1173, 1831, 1512, 1301, 1280]
+    # python reference recurrence for a longer prefix
+    st, ref = (1 << 64) - 1, []
+    for _ in range(1000):
+        st = ((st & 0xFFFFFFFF) * 4164903690 + (st >> 32)) & ((1 << 64) - 1)
+        ref.append(st & 0xFFFFFFFF)
+    assert list(oracle.rng_stream(1000)) == ref
+
+
+@pytest.mark.parametrize("w,mi,expect", [(0.1014, 50000, 50000), (0.1015, 50000, 49917), (0.12, 50000, 25549),
+                                         (0.2, 50000, 3309), (0.5, 50000, 82), (0.5, 2000, 82), (0.2, 2000, 2000),
+                                         (1.0, 2000, 0), (0.0, 2000, 2000)])
+def test_update_num_iters_kat(oracle, w, mi, expect):
+    assert oracle.update_num_iters(0.995, 1 - w, 4, mi) == expect
+
+
+def test_update_num_iters_formula(oracle):
+    for w in np.linspace(0.11, 0.95, 40):
+        num, den = np.log(1 - 0.995), np.log(1 - w ** 4)
+        exp = 50000 if -num >= 50000 * -den else int(np.rint(num / den))
+        assert oracle.update_num_iters(0.995, 1 - w, 4, 50000) == exp
+
+
+def test_jacobi_eigen(oracle):
+    rng = np.random.default_rng(0)
+    for n in (3, 8, 9):
+        A = rng.normal(size=(n, n))
+        A = A @ A.T
+        W, V = oracle.jacobi(A)
+        assert np.all(np.diff(W) <= 0)                          # descending
+        np.testing.assert_allclose(V @ A @ V.T, np.diag(W), atol=1e-9 * np.abs(W).max())
+        np.testing.assert_allclose(np.sort(W), np.sort(np.linalg.eigvalsh(A)), rtol=1e-10, atol=1e-10)
+
+
+def test_run_kernel_exact_recovery(oracle):
+    rng = np.random.default_rng(1)
+    for _ in range(20):
+        H = random_homography(rng)
+        src = np.c_[rng.uniform(0, 640, 4), rng.uniform(0, 480, 4)].astype(np.float32)
+        dst = apply_h(H, src)
+        ok, Hk = oracle.run_kernel(src, dst)
+        assert ok == 1
+        # the DLT solution maps the 4 points exactly (up to float rounding of dst)
+        p = np.c_[src.astype(np.float64), np.ones(4)] @ Hk.T
+        np.testing.assert_allclose(p[:, :2] / p[:, 2:], dst, atol=2e-3)
+        assert Hk[2, 2] == pytest.approx(1.0, abs=1e-12)
+
+
+def test_run_kernel_degenerate(oracle):
+    src = np.tile(np.array([[3.0, 4.0]], np.float32), (4, 1))
+    ok, _ = oracle.run_kernel(src, src)
+    assert ok == 0
+
+
+def test_check_subset(oracle):
+    sq = np.array([[0, 0], [10, 0], [10, 10], [0, 10]], np.float32)
+    assert oracle.check_subset(sq, sq + 5)
+    assert not oracle.check_subset(sq, sq[[0, 1, 3, 2]])            # orientation flips on some triplets
+    coll = np.array([[0, 0], [1, 1], [2, 2], [5, 0]], np.float32)
+    coll2 = np.array([[0, 0], [5, 1], [2, 7], [3, 3]], np.float32)
+    coll2[3] = coll2[0] + 0.5 * (coll2[1] - coll2[0])               # point 3 on the line 0-1
+    assert not oracle.check_subset(coll2, sq)
+    assert oracle.check_subset(sq, sq[[1, 2, 3, 0]])               # a rotation keeps every orientation
+
+
+def test_find_homography_noiseless(oracle):
+    rng = np.random.default_rng(3)
+    H = random_homography(rng)
+    src = np.c_[rng.uniform(0, 640, 60), rng.uniform(0, 480, 60)].astype(np.float32)
+    dst = apply_h(H, src)
+    ok, Hr, mask = oracle.find_homography(src, dst)
+    assert ok and mask.all()
+    np.testing.assert_allclose(Hr, H / H[2, 2], rtol=1e-4, atol=1e-6)
+
+
+def test_knn_planted_neighbours_and_ties(oracle):
+    rng = np.random.default_rng(4)
+    t = sift_like(rng, 500)
+    t[300] = t[10]
+    q = np.stack([t[10], t[77], t[499]])
+    idx, dist = oracle.knn2(q, t, 2)
+    assert list(idx[0]) == [10, 300] and list(dist[0]) == [0.0, 0.0]   # tie -> lower index first
+    assert idx[1, 0] == 77 and idx[2, 0] == 499
+    # brute force float64 reference for integer descriptors: exact squared distances
+    d2 = ((q[:, None, :].astype(np.float64) - t[None].astype(np.float64)) ** 2).sum(-1)
+    order = np.lexsort((np.arange(500)[None].repeat(3, 0), np.sqrt(d2).astype(np.float32)), axis=1)
+    np.testing.assert_array_equal(idx, order[:, :2])
+    np.testing.assert_array_equal(dist, np.sqrt(d2.astype(np.float32))[np.arange(3)[:, None], order[:, :2]])
+
+
+def test_knn_fewer_than_two_train(oracle):
+    rng = np.random.default_rng(5)
+    q = sift_like(rng, 4)
+    idx, dist = oracle.knn2(q, q[:1], 1)
+    assert (idx[:, 0] == 0).all() and (idx[:, 1] == -1).all()
+    assert oracle.ratio_filter(idx, dist)[0].size == 0     # m.size() == 2 required
+
+
+def test_ratio_strict(oracle):
+    d1 = np.float32(10.0)
+    idx = np.array([[0, 1], [2, 3]], np.int32)
+    dist = np.array([[np.float32(0.9) * d1, d1], [np.nextafter(np.float32(0.9) * d1, 0), d1]], np.float32)
+    q, t = oracle.ratio_filter(idx, dist, 0.9)
+    assert list(q) == [1] and list(t) == [2]
+
+
+def test_golden_fixture_regenerates(oracle):
+    # the committed goldens equal what the restatement computes today
+    import os
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "golden_v1.npz"))
+    idx, dist = oracle.knn2(g["knn_q"], g["knn_t"], 1)
+    np.testing.assert_array_equal(idx, g["knn_idx"])
+    np.testing.assert_array_equal(dist, g["knn_dist"])
+    for name in "abc":
+        r = oracle.ransac(g[f"rs_{name}_src"], g[f"rs_{name}_dst"], 5.0, 0.995, int(g[f"rs_{name}_iters_max"]))
+        np.testing.assert_array_equal(r["mask"], g[f"rs_{name}_mask"])
+        assert r["iters"] == int(g[f"rs_{name}_iters"])
+        assert np.array_equal(r["H"], g[f"rs_{name}_Hbest"])
+    assert list(g["rng_first8"]) == list(oracle.rng_stream(8))

@@ -72,7 +72,7 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
 
-    from computervision_objectdetection_featurematching_amd import Matcher, build, default_params
+    from computervision_objectdetection_featurematching_amd import Matcher, build, default_params, shard
     from computervision_objectdetection_featurematching_amd._lib import RESULT_DTYPE
     from computervision_objectdetection_featurematching_amd.synthetic import CONFIGS, SEED_BASE, make_dataset
 
@@ -92,8 +92,8 @@ def main():
     stream = torch.cuda.current_stream(dev)
     m.set_stream(stream.cuda_stream)
     prm = default_params(max_iters=cfg["max_iters"])
-    gathered = torch.empty((world, n_probs * RESULT_DTYPE.itemsize), dtype=torch.uint8, device=dev)
     mine = torch.empty(n_probs * RESULT_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+    gathered = [None]
 
     def step():
         m.clear_sets()
@@ -101,8 +101,7 @@ def main():
         t_ids = [m.add_set(d, k) for d, k in zip(sdesc, skp)]
         m.match_batch_async([(q_ids[a], t_ids[b]) for a, b in ds.problems], prm)
         m.batch_results_copy_to(mine)
-        if world > 1:
-            dist.all_gather_into_tensor(gathered, mine)
+        gathered[0] = shard.gather_results(mine, world)  # RCCL all-gather of the result records
 
     m.set_timing(False)
     for _ in range(args.warmup):

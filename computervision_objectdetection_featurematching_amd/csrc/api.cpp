@@ -11,6 +11,7 @@
 #include <climits>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -28,7 +29,7 @@ void launch_ratio(const ProbDev* probs, int n_probs, const Top2* parts, float ra
                   hipStream_t st);
 void ransac_enqueue(const RansacParams& prm, int n_probs, const ProbDev* probs, const float4* pts,
                     const int* n_good, const RansacBufs& b, uint8_t* masks, mim_result* results, int raw,
-                    hipStream_t s, void (*mark)(void*, const char*), void* mark_ctx);
+                    hipStream_t s, void (*mark)(void*, const char*), void* mark_ctx, int exact_all);
 }  // namespace mim
 
 using namespace mim;
@@ -95,7 +96,7 @@ struct SetRec {
 namespace mim {
 // RANSAC workspace (definition shared with ransac.hip through this layout)
 struct RansacWs {
-    DevBuf state, samples, hyp, counts, stream, scratch, inl, err;
+    DevBuf state, samples, hyp, counts, bounds, stream, scratch, inl, err;
     long long stream_len = 0;
 };
 }  // namespace mim
@@ -115,6 +116,8 @@ struct mim_ctx {
     int n_works = 0;
     std::vector<long long> h_good_off;
     int last_n = 0;
+    // MIM_RANSAC_EXACT=1: evaluate every hypothesis exactly (reference mode for cross-checks)
+    int exact_all = 0;
     // timing
     bool timing = false;
     std::vector<std::pair<std::string, hipEvent_t>> evs;
@@ -168,6 +171,8 @@ mim_status mim_ctx_create(int device, mim_ctx** out) {
         return MIM_EDEVICE;
     }
     c->stream = c->own;
+    const char* ex = getenv("MIM_RANSAC_EXACT");
+    c->exact_all = (ex && ex[0] == '1') ? 1 : 0;
     *out = c;
     return MIM_OK;
 }
@@ -180,7 +185,7 @@ void mim_ctx_destroy(mim_ctx* c) {
     c->arena.release();
     for (DevBuf* b : {&c->probs, &c->works, &c->parts, &c->good_q, &c->good_t, &c->pts, &c->n_good,
                       &c->results, &c->masks, &c->knn_idx, &c->knn_dist, &c->rws.state, &c->rws.samples,
-                      &c->rws.hyp, &c->rws.counts, &c->rws.stream, &c->rws.scratch, &c->rws.inl, &c->rws.err})
+                      &c->rws.hyp, &c->rws.counts, &c->rws.bounds, &c->rws.stream, &c->rws.scratch, &c->rws.inl, &c->rws.err})
         b->release();
     if (c->own) (void)hipStreamDestroy(c->own);
     delete c;
@@ -521,6 +526,7 @@ static mim_status ransac_locked(mim_ctx* c, int n, const mim_params* prm, int ra
     HIPCHK(c, c->rws.samples.ensure(sizeof(int4) * it_total));
     HIPCHK(c, c->rws.hyp.ensure(sizeof(float) * 8 * it_total));
     HIPCHK(c, c->rws.counts.ensure(sizeof(int) * it_total));
+    HIPCHK(c, c->rws.bounds.ensure(sizeof(int2) * it_total));
     HIPCHK(c, c->rws.inl.ensure(sizeof(float4) * good_total));
     HIPCHK(c, c->rws.err.ensure(sizeof(int) * 4));
     HIPCHK(c, c->results.ensure(sizeof(mim_result) * std::max(n, 1)));
@@ -531,6 +537,7 @@ static mim_status ransac_locked(mim_ctx* c, int n, const mim_params* prm, int ra
     b.samples = c->rws.samples.as<int4>();
     b.hyp = c->rws.hyp.as<float>();
     b.counts = c->rws.counts.as<int>();
+    b.bounds = c->rws.bounds.as<int2>();
     b.stream = c->rws.stream.as<uint32_t>();
     b.stream_len = c->rws.stream_len;
     b.inl = c->rws.inl.as<float4>();
@@ -545,7 +552,7 @@ static mim_status ransac_locked(mim_ctx* c, int n, const mim_params* prm, int ra
     rp.det_lo = prm->det_lo;
     rp.det_hi = prm->det_hi;
     ransac_enqueue(rp, n, c->probs.as<ProbDev>(), c->pts.as<float4>(), c->n_good.as<int>(), b, c->masks.as<uint8_t>(),
-                   c->results.as<mim_result>(), raw, c->stream, mark_cb, c);
+                   c->results.as<mim_result>(), raw, c->stream, mark_cb, c, c->exact_all);
     HIPCHK(c, hipGetLastError());
     return MIM_OK;
 }

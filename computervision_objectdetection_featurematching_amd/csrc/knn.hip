@@ -100,15 +100,23 @@ __device__ __forceinline__ float sqrt_class_floor(float d2, float key) {
     return lo;
 }
 
+// Candidate insertion inside one MFMA tile: d^2 = D + |q|^2 (exact), key = sqrtf(d^2).  Inside a
+// lane candidates come in increasing train index, so `key < k2` (strict) is OpenCV's rule; the
+// threshold T is refreshed once per tile (it only tightens, so the tile-start T is a valid filter).
 __device__ __forceinline__ void top2_insert_exact(LaneTop2& s, float D, float qn, int idx) {
     const float d2 = D + qn;  // exact: integers < 2^24
     const float key = sqrtf(d2);
-    if (key < s.k1) {
-        s.k2 = s.k1; s.i2 = s.i1; s.d2 = s.d1;
-        s.k1 = key;  s.i1 = idx;  s.d1 = d2;
-    } else {
-        s.k2 = key; s.i2 = idx; s.d2 = d2;
+    if (key < s.k2) {
+        if (key < s.k1) {
+            s.k2 = s.k1; s.i2 = s.i1; s.d2 = s.d1;
+            s.k1 = key;  s.i1 = idx;  s.d1 = d2;
+        } else {
+            s.k2 = key; s.i2 = idx; s.d2 = d2;
+        }
     }
+}
+
+__device__ __forceinline__ void top2_refresh(LaneTop2& s, float qn) {
     s.T = (s.i2 == INT_MAX) ? FLT_MAX : sqrt_class_floor(s.d2, s.k2) - qn;
 }
 
@@ -116,12 +124,19 @@ __device__ __forceinline__ bool key_less(float ka, int ia, float kb, int ib) {
     return ka < kb || (ka == kb && ia < ib);
 }
 
-__device__ __forceinline__ void top2_merge(float& k1, int& i1, float& k2, int& i2, float k, int i) {
-    if (key_less(k, i, k1, i1)) {
-        k2 = k1; i2 = i1; k1 = k; i1 = i;
-    } else if (key_less(k, i, k2, i2)) {
-        k2 = k; i2 = i;
-    }
+struct T2 {
+    float k1; int i1; float k2; int i2;
+};
+
+__device__ __forceinline__ T2 top2_merge(T2 a, float k, int i) {
+    const bool l1 = key_less(k, i, a.k1, a.i1);
+    const bool l2 = key_less(k, i, a.k2, a.i2);
+    T2 r;
+    r.k1 = l1 ? k : a.k1;
+    r.i1 = l1 ? i : a.i1;
+    r.k2 = l1 ? a.k1 : (l2 ? k : a.k2);
+    r.i2 = l1 ? a.i1 : (l2 ? i : a.i2);
+    return r;
 }
 
 // D values of one 32x32 MFMA tile for this lane's query: rows (g&3) + 8(g>>2) + 4h, g ascending.
@@ -130,10 +145,12 @@ __device__ __forceinline__ void epilogue(const f32x16& acc, LaneTop2& s, float q
 #pragma unroll
     for (int g = 1; g < 16; ++g) m = fminf(m, acc[g]);
     if (m < s.T) {
+        const float T = s.T;
 #pragma unroll
         for (int g = 0; g < 16; ++g) {
-            if (acc[g] < s.T) top2_insert_exact(s, acc[g], qn, row0 + (g & 3) + 8 * (g >> 2));
+            if (acc[g] < T) top2_insert_exact(s, acc[g], qn, row0 + (g & 3) + 8 * (g >> 2));
         }
+        top2_refresh(s, qn);
     }
 }
 
@@ -181,33 +198,39 @@ __global__ __launch_bounds__(256, 2) void knn2_bf16_kernel(const ProbDev* __rest
     top2_init(st[0]);
     top2_init(st[1]);
 
-    // ---- train tile staging ----
-    uint4 stg[4];
-    float stgn = FLT_MAX;
-    auto gload = [&](int tile) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) stg[k] = tsrc[(size_t)tile * 1024 + k * 256 + tid];
-        if (tid < 64) {
-            const int row = tile * 64 + tid;
-            stgn = row < nt ? tnorm[row] : FLT_MAX;  // padded rows never win
-        }
-    };
-    auto lstore = [&](int buf) {
-        uint4* dst = reinterpret_cast<uint4*>(smem + buf * kLdsTile);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) dst[k * 256 + tid] = stg[k];
-        if (tid < 64) reinterpret_cast<float*>(smem + buf * kLdsTile + kTileBytes)[tid] = stgn;
-    };
+    // ---- train tile staging (HBM -> registers -> LDS, double buffered) ----
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    typedef const __attribute__((address_space(1))) u32x4 gu4;
+    typedef const __attribute__((address_space(1))) float gf;
+    gu4* tg = (gu4*)tsrc;
+    gf* tng = (gf*)tnorm;
+    u32x4 s0, s1, s2, s3;
+    float sn = FLT_MAX;
+#define GLOAD(tile)                                                     \
+    do {                                                                \
+        const size_t b_ = (size_t)(tile) * 1024 + tid;                  \
+        s0 = tg[b_]; s1 = tg[b_ + 256]; s2 = tg[b_ + 512]; s3 = tg[b_ + 768]; \
+        if (tid < 64) {                                                 \
+            const int row_ = (tile) * 64 + tid;                         \
+            sn = row_ < nt ? tng[row_] : FLT_MAX; /* padded rows never win */ \
+        }                                                               \
+    } while (0)
+#define LSTORE(buf)                                                     \
+    do {                                                                \
+        u32x4* d_ = reinterpret_cast<u32x4*>(smem + (buf) * kLdsTile);  \
+        d_[tid] = s0; d_[tid + 256] = s1; d_[tid + 512] = s2; d_[tid + 768] = s3; \
+        if (tid < 64) reinterpret_cast<float*>(smem + (buf) * kLdsTile + kTileBytes)[tid] = sn; \
+    } while (0)
 
     if (w.tile0 < w.tile1) {
-        gload(w.tile0);
-        lstore(0);
+        GLOAD(w.tile0);
+        LSTORE(0);
     }
     __syncthreads();
     for (int tile = w.tile0; tile < w.tile1; ++tile) {
         const int buf = (tile - w.tile0) & 1;
         const bool more = tile + 1 < w.tile1;
-        if (more) gload(tile + 1);
+        if (more) GLOAD(tile + 1);
         const bf16x8* A = reinterpret_cast<const bf16x8*>(smem + buf * kLdsTile);
         const float* tn = reinterpret_cast<const float*>(smem + buf * kLdsTile + kTileBytes);
 #pragma unroll
@@ -229,22 +252,23 @@ __global__ __launch_bounds__(256, 2) void knn2_bf16_kernel(const ProbDev* __rest
             epilogue(acc0, st[0], qn[0], row0);
             epilogue(acc1, st[1], qn[1], row0);
         }
-        if (more) lstore(buf ^ 1);
+        if (more) LSTORE(buf ^ 1);
         __syncthreads();
     }
+#undef GLOAD
+#undef LSTORE
 
     // ---- merge the two lane halves (h = 0/1 hold disjoint train rows of the same query) ----
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-        float k1 = st[u].k1, k2 = st[u].k2;
-        int i1 = st[u].i1, i2 = st[u].i2;
-        const float ok1 = __shfl_xor(k1, 32), ok2 = __shfl_xor(k2, 32);
-        const int oi1 = __shfl_xor(i1, 32), oi2 = __shfl_xor(i2, 32);
-        top2_merge(k1, i1, k2, i2, ok1, oi1);
-        top2_merge(k1, i1, k2, i2, ok2, oi2);
+        T2 t{st[u].k1, st[u].i1, st[u].k2, st[u].i2};
+        const float ok1 = __shfl_xor(t.k1, 32), ok2 = __shfl_xor(t.k2, 32);
+        const int oi1 = __shfl_xor(t.i1, 32), oi2 = __shfl_xor(t.i2, 32);
+        t = top2_merge(t, ok1, oi1);
+        t = top2_merge(t, ok2, oi2);
         const int q = qtile * 64 + 32 * u + r;
         if (h == 0 && qvalid && q < nq) {
-            Top2 o{k1, i1, k2, i2};
+            Top2 o{t.k1, t.i1, t.k2, t.i2};
             parts[P->part_off + (long long)w.split * P->q_pad + q] = o;
         }
     }
@@ -342,14 +366,17 @@ __global__ __launch_bounds__(1024) void ratio_compact_kernel(const ProbDev* __re
     int running = 0;
     for (int base = 0; base < nq; base += 1024) {
         const int q = base + tid;
-        float k1 = FLT_MAX, k2 = FLT_MAX;
-        int i1 = INT_MAX, i2 = INT_MAX;
+        T2 m{FLT_MAX, INT_MAX, FLT_MAX, INT_MAX};
         if (q < nq) {
             for (int sp = 0; sp < P->nsplit; ++sp) {
                 const Top2 t = parts[P->part_off + (long long)sp * P->q_pad + q];
-                top2_merge(k1, i1, k2, i2, t.k1, t.i1);
-                top2_merge(k1, i1, k2, i2, t.k2, t.i2);
+                m = top2_merge(m, t.k1, t.i1);
+                m = top2_merge(m, t.k2, t.i2);
             }
+        }
+        const float k1 = m.k1, k2 = m.k2;
+        const int i1 = m.i1, i2 = m.i2;
+        if (q < nq) {
             if (knn_idx) {
                 knn_idx[2 * q] = i1 == INT_MAX ? -1 : i1;
                 knn_idx[2 * q + 1] = i2 == INT_MAX ? -1 : i2;

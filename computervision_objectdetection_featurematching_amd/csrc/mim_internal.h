@@ -59,7 +59,7 @@ struct RansacState {
     int done;              // loop finished (iter >= niters or getSubset failure)
     int n;                 // point count (= n_good)
     int active;            // problem takes the RANSAC path (n_good > 4)
-    int pad_;
+    int lo_max;            // max lower-bound count seen (filtered path: lower bound of maxGoodCount)
 };
 
 struct RansacParams {
@@ -80,6 +80,7 @@ struct RansacBufs {
     int4* samples;            // [it_off + iter]  4 point indices of the minimal sample
     float* hyp;               // [(it_off + iter) * 8]  (float)H[0..7] of the minimal-sample model
     int* counts;              // [it_off + iter]  inlier count, -1 when runKernel returned 0
+    int2* bounds;             // [it_off + iter]  (lower, upper) bound of the count (filtered path)
     const uint32_t* stream;   // raw cv::RNG((uint64)-1).next() stream shared by every problem
     long long stream_len;
     float4* inl;              // [good_off + k] compressed inliers for the refit (scratch)

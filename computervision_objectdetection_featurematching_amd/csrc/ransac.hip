@@ -21,6 +21,7 @@
 #include <float.h>
 
 #include <algorithm>
+#include <climits>
 
 #include "../../include/mim.h"
 #include "mim_internal.h"
@@ -30,131 +31,191 @@ namespace mim {
 // ------------------------------------------------------------------------------------------------
 // shared fp64 helpers (core/src/lapack.cpp)
 // ------------------------------------------------------------------------------------------------
+// hypot<double> of core/src/lapack.cpp in select form (same operations, no divergent branches):
+//   a > b ? a*sqrt(1+(b/a)^2) : (b > 0 ? b*sqrt(1+(a/b)^2) : 0)
 __device__ __forceinline__ double d_hypot(double a, double b) {
     a = fabs(a);
     b = fabs(b);
-    if (a > b) {
-        b /= a;
-        return a * sqrt(1 + b * b);
-    }
-    if (b > 0) {
-        a /= b;
-        return b * sqrt(1 + a * a);
-    }
-    return 0;
+    const bool ab = a > b;
+    const double big = ab ? a : b, sm = ab ? b : a;
+    const double r = sm / big;
+    const double res = big * sqrt(1 + r * r);
+    return (ab || b > 0) ? res : 0.0;
 }
 
 // packed upper-triangle index of (i, j), i < j, for an n x n symmetric matrix
-template <int n> __device__ __forceinline__ int pk(int i, int j) { return (i * (2 * n - i - 1)) / 2 + (j - i - 1); }
+template <int n> __device__ __forceinline__ int pk(int i, int j) {
+    return (int)(__umul24((unsigned)i, (unsigned)(2 * n - i - 1)) >> 1) + (j - i - 1);
+}
 
-// JacobiImpl_<double> (core/src/lapack.cpp) on strided storage: element e of an array lives at
-// base[e * S] (S = 64 in the per-lane hypothesis kernel, 1 for single-thread use).
-//   A: packed strict upper triangle; W: diagonal on entry, eigenvalues (descending) on exit;
-//   V: n x n, eigenvectors in rows; ind: indR[0..n) then indC[0..n).
+template <int n> __device__ __forceinline__ int pk_any(int a, int b) {  // (min, max) of two distinct indices
+    const int i = min(a, b), j = max(a, b);
+    return pk<n>(i, j);
+}
+
+// JacobiImpl_<double> (core/src/lapack.cpp), bit-identical arithmetic, restructured for a GPU lane:
+// the matrix lives in LDS with element e at base[e * S] (S = 64: one lane's private column in an
+// [element][lane] interleave, conflict-free for any per-lane index; S = 1 for single-thread use),
+// indR/indC live in registers, and every loop has static bounds so all loads of a phase issue
+// back to back (two LDS round trips per rotation instead of one per element).  OpenCV's cached
+// row/column maxima are refreshed only for rows k and l, exactly like the reference.
+//   A: packed strict upper triangle; W: diagonal on entry (unsorted eigenvalues on exit);
+//   V: n x n rows = eigenvectors (unsorted).  Outputs Ws = eigenvalues in OpenCV's descending
+//   selection-sort order and perm[i] = row of V holding the i-th sorted eigenvector.
 template <int n, int S>
-__device__ void jacobi_strided(double* __restrict__ A, double* __restrict__ W, double* __restrict__ V,
-                               int* __restrict__ ind) {
+__device__ void jacobi_fast(double* __restrict__ A, double* __restrict__ W, double* __restrict__ V,
+                            double (&Ws)[n], int (&perm)[n]) {
 #define AU(i, j) A[pk<n>((i), (j)) * S]
-#define WW(k) W[(k) * S]
-#define VV(r, c) V[((r) * n + (c)) * S]
-#define IR(k) ind[(k) * S]
-#define IC(k) ind[(n + (k)) * S]
+    // spare slot after the matrix state (A | W | V | trash) absorbing predicated-off stores
+    const int trash = n * (n - 1) / 2 + n + n * n;
     const double eps = DBL_EPSILON;
-    int i, j, k, m;
-    double mv;
-    for (i = 0; i < n; i++)
-        for (j = 0; j < n; j++) VV(i, j) = i == j ? 1.0 : 0.0;
-    for (k = 0; k < n; k++) {
+#pragma unroll
+    for (int i = 0; i < n; i++)
+#pragma unroll
+        for (int j = 0; j < n; j++) V[(i * n + j) * S] = i == j ? 1.0 : 0.0;
+    int indR[n], indC[n];
+#pragma unroll
+    for (int k = 0; k < n; k++) {
+        indR[k] = 0;
+        indC[k] = 0;
         if (k < n - 1) {
-            for (m = k + 1, mv = fabs(AU(k, m)), i = k + 2; i < n; i++) {
+            int m = k + 1;
+            double mv = fabs(AU(k, k + 1));
+#pragma unroll
+            for (int i = k + 2; i < n; i++) {
                 const double val = fabs(AU(k, i));
                 if (mv < val) mv = val, m = i;
             }
-            IR(k) = m;
+            indR[k] = m;
         }
         if (k > 0) {
-            for (m = 0, mv = fabs(AU(0, k)), i = 1; i < k; i++) {
+            int m = 0;
+            double mv = fabs(AU(0, k));
+#pragma unroll
+            for (int i = 1; i < k; i++) {
                 const double val = fabs(AU(i, k));
                 if (mv < val) mv = val, m = i;
             }
-            IC(k) = m;
+            indC[k] = m;
         }
     }
     for (int iters = 0; iters < n * n * 30; iters++) {
-        for (k = 0, mv = fabs(AU(0, IR(0))), i = 1; i < n - 1; i++) {
-            const double val = fabs(AU(i, IR(i)));
-            if (mv < val) mv = val, k = i;
+        double vr[n], vc[n];
+#pragma unroll
+        for (int i = 0; i < n - 1; i++) vr[i] = A[(pk<n>(i, i + 1) + indR[i] - i - 1) * S];
+#pragma unroll
+        for (int i = 1; i < n; i++) vc[i] = A[pk_any<n>(indC[i], i) * S];
+        int k = 0, l = indR[0];
+        double mv = fabs(vr[0]), p = vr[0];
+#pragma unroll
+        for (int i = 1; i < n - 1; i++) {  // select form of `if (mv < val) mv = val, k = i`
+            const double val = fabs(vr[i]);
+            const bool u = mv < val;
+            mv = u ? val : mv;
+            k = u ? i : k;
+            l = u ? indR[i] : l;
+            p = u ? vr[i] : p;
         }
-        int l = IR(k);
-        for (i = 1; i < n; i++) {
-            const int ci = IC(i);
-            const double val = fabs(AU(ci, i));
-            if (mv < val) mv = val, k = ci, l = i;
+#pragma unroll
+        for (int i = 1; i < n; i++) {
+            const double val = fabs(vc[i]);
+            const bool u = mv < val;
+            mv = u ? val : mv;
+            k = u ? indC[i] : k;
+            l = u ? i : l;
+            p = u ? vc[i] : p;
         }
-        const double p = AU(k, l);
         if (fabs(p) <= eps) break;
-        double y = (WW(l) - WW(k)) * 0.5;
+        // issue every load of this rotation before the dependent arithmetic
+        const double wk = W[k * S], wl = W[l * S];
+        double a0[n], b0[n], vk[n], vl[n];
+#pragma unroll
+        for (int i = 0; i < n; i++) {
+            const bool vi = i != k && i != l;
+            a0[i] = A[(vi ? pk_any<n>(i, k) : 0) * S];
+            b0[i] = A[(vi ? pk_any<n>(i, l) : 0) * S];
+            vk[i] = V[(k * n + i) * S];
+            vl[i] = V[(l * n + i) * S];
+        }
+        const double y = (wl - wk) * 0.5;
         double t = fabs(y) + d_hypot(p, y);
         double s = d_hypot(p, t);
         const double c = t / s;
         s = p / s;
         t = (p / t) * p;
-        if (y < 0) s = -s, t = -t;
+        s = y < 0 ? -s : s;
+        t = y < 0 ? -t : t;
         AU(k, l) = 0;
-        WW(k) -= t;
-        WW(l) += t;
-        double a0, b0;
-#define ROT(v0, v1) a0 = v0, b0 = v1, v0 = a0 * c - b0 * s, v1 = a0 * s + b0 * c
-        for (i = 0; i < k; i++) ROT(AU(i, k), AU(i, l));
-        for (i = k + 1; i < l; i++) ROT(AU(k, i), AU(i, l));
-        for (i = l + 1; i < n; i++) ROT(AU(k, i), AU(l, i));
-        for (i = 0; i < n; i++) ROT(VV(k, i), VV(l, i));
-#undef ROT
-        for (j = 0; j < 2; j++) {
-            const int idx = j == 0 ? k : l;
-            if (idx < n - 1) {
-                for (m = idx + 1, mv = fabs(AU(idx, m)), i = idx + 2; i < n; i++) {
-                    const double val = fabs(AU(idx, i));
-                    if (mv < val) mv = val, m = i;
-                }
-                IR(idx) = m;
-            }
-            if (idx > 0) {
-                for (m = 0, mv = fabs(AU(0, idx)), i = 1; i < idx; i++) {
-                    const double val = fabs(AU(i, idx));
-                    if (mv < val) mv = val, m = i;
-                }
-                IC(idx) = m;
-            }
+        W[k * S] = wk - t;
+        W[l * S] = wl + t;
+        double rk[n], rl[n];  // rows k and l after the rotation (column entries by symmetry)
+#pragma unroll
+        for (int i = 0; i < n; i++) {
+            const bool vi = i != k && i != l;
+            const double na = a0[i] * c - b0[i] * s;
+            const double nb = a0[i] * s + b0[i] * c;
+            // unconditional stores (a dropped pair goes to the spare slot `trash`): no branches
+            A[(vi ? pk_any<n>(i, k) : trash) * S] = na;
+            A[(vi ? pk_any<n>(i, l) : trash) * S] = nb;
+            rk[i] = vi ? na : 0.0;
+            rl[i] = vi ? nb : 0.0;
+            V[(k * n + i) * S] = vk[i] * c - vl[i] * s;
+            V[(l * n + i) * S] = vk[i] * s + vl[i] * c;
+        }
+        // refresh the cached maxima of rows/columns k and l (the only ones OpenCV refreshes)
+        int rkR = -1, rkC = -1, rlR = -1, rlC = -1;
+        double bkR = 0, bkC = 0, blR = 0, blC = 0;
+#pragma unroll
+        for (int m = 0; m < n; m++) {
+            const double ak = fabs(rk[m]), al = fabs(rl[m]);
+            const bool u1 = m > k && (rkR < 0 || bkR < ak);
+            const bool u2 = m < k && (rkC < 0 || bkC < ak);
+            const bool u3 = m > l && (rlR < 0 || blR < al);
+            const bool u4 = m < l && (rlC < 0 || blC < al);
+            bkR = u1 ? ak : bkR; rkR = u1 ? m : rkR;
+            bkC = u2 ? ak : bkC; rkC = u2 ? m : rkC;
+            blR = u3 ? al : blR; rlR = u3 ? m : rlR;
+            blC = u4 ? al : blC; rlC = u4 ? m : rlC;
+        }
+#pragma unroll
+        for (int i = 0; i < n; i++) {
+            indR[i] = (i == k && i < n - 1) ? rkR : ((i == l && i < n - 1) ? rlR : indR[i]);
+            indC[i] = (i == k && i > 0) ? rkC : ((i == l && i > 0) ? rlC : indC[i]);
         }
     }
-    for (k = 0; k < n - 1; k++) {
-        m = k;
-        for (i = k + 1; i < n; i++)
-            if (WW(m) < WW(i)) m = i;
-        if (k != m) {
-            double tmp = WW(m);
-            WW(m) = WW(k);
-            WW(k) = tmp;
-            for (i = 0; i < n; i++) {
-                tmp = VV(m, i);
-                VV(m, i) = VV(k, i);
-                VV(k, i) = tmp;
+    // selection sort to descending order (OpenCV swaps V rows; here the permutation is tracked)
+#pragma unroll
+    for (int i = 0; i < n; i++) {
+        Ws[i] = W[i * S];
+        perm[i] = i;
+    }
+#pragma unroll
+    for (int k = 0; k < n - 1; k++) {
+        int m = k;
+        double wm = Ws[k];
+#pragma unroll
+        for (int i = k + 1; i < n; i++)
+            if (wm < Ws[i]) wm = Ws[i], m = i;
+        const double wk = Ws[k];
+        const int pkk = perm[k];
+        int pm = perm[k];
+#pragma unroll
+        for (int i = k + 1; i < n; i++) pm = i == m ? perm[i] : pm;
+#pragma unroll
+        for (int i = k + 1; i < n; i++) {
+            if (i == m) {
+                Ws[i] = wk;
+                perm[i] = pkk;
             }
         }
+        Ws[k] = wm;
+        perm[k] = pm;
     }
 #undef AU
-#undef WW
-#undef VV
-#undef IR
-#undef IC
 }
 
-// storage footprint of jacobi_strided<9>: 36 + 9 + 81 doubles, 18 ints
-constexpr int kJ9D = 36 + 9 + 81;
-constexpr int kJ9I = 18;
-constexpr int kJ8D = 28 + 8 + 64;
-constexpr int kJ8I = 16;
+// storage footprint of jacobi_fast<9>: 36 + 9 + 81 doubles
+constexpr int kJ9D = 36 + 9 + 81 + 1;  // + the trash slot
 
 __device__ __forceinline__ void mat3_mul(const double* a, const double* b, double* c) {
 #pragma unroll
@@ -167,29 +228,35 @@ __device__ __forceinline__ void mat3_mul(const double* a, const double* b, doubl
 // Eigen-decompose LtL (upper incl. diagonal in lt[45], row-major (j,k>=j) order) and build H from
 // the smallest eigenvector: HomographyEstimatorCallback::runKernel after completeSymm.
 template <int S>
-__device__ void dlt_finish(const double* lt, double* D, int* I, const double* invHnorm, const double* Hnorm2,
-                           double* H) {
+__device__ void dlt_finish(const double* lt, double* D, const double* invHnorm, const double* Hnorm2, double* H) {
     double* A = D;
     double* W = D + 36 * S;
     double* V = D + 45 * S;
     int e = 0;
+#pragma unroll
     for (int j = 0; j < 9; ++j)
+#pragma unroll
         for (int k = j; k < 9; ++k, ++e) {
             if (k == j) W[j * S] = lt[e];
             else A[pk<9>(j, k) * S] = lt[e];
         }
-    jacobi_strided<9, S>(A, W, V, I);
+    double Ws[9];
+    int perm[9];
+    jacobi_fast<9, S>(A, W, V, Ws, perm);
     double H0[9], Ht[9];
-    for (int i = 0; i < 9; ++i) H0[i] = V[(8 * 9 + i) * S];
+    const int r = perm[8];  // eigenvector of the smallest eigenvalue (V[8] after OpenCV's sort)
+#pragma unroll
+    for (int i = 0; i < 9; ++i) H0[i] = V[(r * 9 + i) * S];
     mat3_mul(invHnorm, H0, Ht);
     mat3_mul(Ht, Hnorm2, H0);
     const double sc = 1. / H0[8];  // _H0.convertTo(_model, type, 1./H0(2,2))
+#pragma unroll
     for (int i = 0; i < 9; ++i) H[i] = H0[i] * sc;
 }
 
 // runKernel on the 4 points of a minimal sample (M = object, m = scene), one lane.
 template <int S>
-__device__ int run_kernel4(const float* M, const float* m, double* D, int* I, double* H) {
+__device__ int run_kernel4(const float* M, const float* m, double* D, double* H) {
     const int count = 4;
     double cMx = 0, cMy = 0, cmx = 0, cmy = 0, sMx = 0, sMy = 0, smx = 0, smy = 0;
 #pragma unroll
@@ -225,7 +292,7 @@ __device__ int run_kernel4(const float* M, const float* m, double* D, int* I, do
 #pragma unroll
             for (int k = j; k < 9; k++, ++e) lt[e] += Lx[j] * Lx[k] + Ly[j] * Ly[k];
     }
-    dlt_finish<S>(lt, D, I, invHnorm, Hnorm2, H);
+    dlt_finish<S>(lt, D, invHnorm, Hnorm2, H);
     return 1;
 }
 
@@ -418,7 +485,6 @@ __global__ __launch_bounds__(64) void ransac_hypo_kernel(const RansacState* __re
                                                          float* __restrict__ hyp, int* __restrict__ counts, int c0,
                                                          int c1, int bpp) {
     __shared__ double sd[kJ9D * 64];
-    __shared__ int si[kJ9I * 64];
     const int p = blockIdx.x / bpp, lane = threadIdx.x;
     const int it = c0 + (blockIdx.x % bpp) * 64 + lane;
     const RansacState S = st[p];
@@ -431,7 +497,7 @@ __global__ __launch_bounds__(64) void ransac_hypo_kernel(const RansacState* __re
     const float M[8] = {a.x, a.y, b.x, b.y, c.x, c.y, d.x, d.y};
     const float m[8] = {a.z, a.w, b.z, b.w, c.z, c.w, d.z, d.w};
     double H[9];
-    const int ok = run_kernel4<64>(M, m, sd + lane, si + lane, H);
+    const int ok = run_kernel4<64>(M, m, sd + lane, H);
     counts[o] = ok ? 0 : -1;
     if (ok) {
         float4* h = reinterpret_cast<float4*>(hyp + o * 8);
@@ -479,6 +545,217 @@ __global__ __launch_bounds__(256) void ransac_score_kernel(const RansacState* __
         cnt += reproj_err(Hf, q.x, q.y, q.z, q.w) <= thr2;
     }
     counts[o] = cnt;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Filtered path (default).  Deciding the RANSAC trajectory only needs, per iteration, whether the
+// exact inlier count beats max(best, 3).  `bound` brackets every count from a closed-form fp64
+// homography through the same 4 correspondences (Heckbert's square->quad maps), with a per-point
+// margin on the reprojection error that is orders of magnitude above the disagreement between that
+// solution and OpenCV's normalized-DLT/Jacobi one for any sample that passes the conditioning
+// screen; samples that fail the screen get [0, N].  `select_filtered` then evaluates exactly —
+// OpenCV's runKernel + computeError, bit for bit — only the iterations whose upper bound can
+// exceed the running best, and replays them in order.  tests/test_ransac_gpu.py checks the
+// filtered and the all-exact paths produce identical results.
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ void square_to_quad(const double* x, const double* y, double* Q) {
+    const double sx = x[0] - x[1] + x[2] - x[3], sy = y[0] - y[1] + y[2] - y[3];
+    const double dx1 = x[1] - x[2], dx2 = x[3] - x[2], dy1 = y[1] - y[2], dy2 = y[3] - y[2];
+    const double den = dx1 * dy2 - dx2 * dy1;
+    const double g = (sx * dy2 - sy * dx2) / den, h = (dx1 * sy - dy1 * sx) / den;
+    Q[0] = x[1] - x[0] + g * x[1]; Q[1] = x[3] - x[0] + h * x[3]; Q[2] = x[0];
+    Q[3] = y[1] - y[0] + g * y[1]; Q[4] = y[3] - y[0] + h * y[3]; Q[5] = y[0];
+    Q[6] = g; Q[7] = h; Q[8] = 1.0;
+}
+
+// min over the 4 triangles of |2*area| / bbox_diag^2 (conditioning of a 4-point configuration)
+__device__ __forceinline__ double min_rel_area(const double* x, const double* y) {
+    const double mnx = fmin(fmin(x[0], x[1]), fmin(x[2], x[3])), mxx = fmax(fmax(x[0], x[1]), fmax(x[2], x[3]));
+    const double mny = fmin(fmin(y[0], y[1]), fmin(y[2], y[3])), mxy = fmax(fmax(y[0], y[1]), fmax(y[2], y[3]));
+    const double d2 = (mxx - mnx) * (mxx - mnx) + (mxy - mny) * (mxy - mny);
+    const int tt[4][3] = {{0, 1, 2}, {1, 2, 3}, {0, 2, 3}, {0, 1, 3}};
+    double m = 1e300;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int a = tt[i][0], b = tt[i][1], c = tt[i][2];
+        m = fmin(m, fabs((x[b] - x[a]) * (y[c] - y[a]) - (x[c] - x[a]) * (y[b] - y[a])));
+    }
+    return d2 > 0 ? m / d2 : 0.0;
+}
+
+constexpr double kScreenArea = 1e-5;  // samples less conditioned than this are evaluated exactly
+
+__global__ __launch_bounds__(256) void ransac_bound_kernel(const RansacState* __restrict__ st,
+                                                           const ProbDev* __restrict__ probs,
+                                                           const float4* __restrict__ pts,
+                                                           const int4* __restrict__ samples,
+                                                           int2* __restrict__ bounds, int c0, int c1, int bpp,
+                                                           float thr2) {
+    const int p = blockIdx.x / bpp;
+    const int it = c0 + (blockIdx.x % bpp) * 256 + threadIdx.x;
+    const RansacState S = st[p];
+    if (!S.active || S.done) return;
+    if (it >= c1 || it >= S.produced) return;
+    const long long o = probs[p].it_off + it;
+    const float4* __restrict__ P = pts + probs[p].good_off;
+    const int4 s4 = samples[o];
+    const float4 q0 = P[s4.x], q1 = P[s4.y], q2 = P[s4.z], q3 = P[s4.w];
+    // runKernel's own degeneracy test (exact, cheap): spread < DBL_EPSILON -> no model
+    {
+        const float M[8] = {q0.x, q0.y, q1.x, q1.y, q2.x, q2.y, q3.x, q3.y};
+        const float m[8] = {q0.z, q0.w, q1.z, q1.w, q2.z, q2.w, q3.z, q3.w};
+        double cMx = 0, cMy = 0, cmx = 0, cmy = 0, sMx = 0, sMy = 0, smx = 0, smy = 0;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            cmx += m[2 * i]; cmy += m[2 * i + 1];
+            cMx += M[2 * i]; cMy += M[2 * i + 1];
+        }
+        cmx /= 4; cmy /= 4; cMx /= 4; cMy /= 4;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            smx += fabs(m[2 * i] - cmx); smy += fabs(m[2 * i + 1] - cmy);
+            sMx += fabs(M[2 * i] - cMx); sMy += fabs(M[2 * i + 1] - cMy);
+        }
+        if (fabs(smx) < DBL_EPSILON || fabs(smy) < DBL_EPSILON || fabs(sMx) < DBL_EPSILON ||
+            fabs(sMy) < DBL_EPSILON) {
+            bounds[o] = make_int2(-1, -1);
+            return;
+        }
+    }
+    const double sx[4] = {q0.x, q1.x, q2.x, q3.x}, sy[4] = {q0.y, q1.y, q2.y, q3.y};
+    const double dx[4] = {q0.z, q1.z, q2.z, q3.z}, dy[4] = {q0.w, q1.w, q2.w, q3.w};
+    bool uncertain = min_rel_area(sx, sy) < kScreenArea || min_rel_area(dx, dy) < kScreenArea;
+    double Qs[9], Qd[9], Ai[9], H[9];
+    square_to_quad(sx, sy, Qs);
+    square_to_quad(dx, dy, Qd);
+    // adjugate of Qs (inverse up to scale)
+    Ai[0] = Qs[4] * Qs[8] - Qs[5] * Qs[7]; Ai[1] = Qs[2] * Qs[7] - Qs[1] * Qs[8]; Ai[2] = Qs[1] * Qs[5] - Qs[2] * Qs[4];
+    Ai[3] = Qs[5] * Qs[6] - Qs[3] * Qs[8]; Ai[4] = Qs[0] * Qs[8] - Qs[2] * Qs[6]; Ai[5] = Qs[2] * Qs[3] - Qs[0] * Qs[5];
+    Ai[6] = Qs[3] * Qs[7] - Qs[4] * Qs[6]; Ai[7] = Qs[1] * Qs[6] - Qs[0] * Qs[7]; Ai[8] = Qs[0] * Qs[4] - Qs[1] * Qs[3];
+    mat3_mul(Qd, Ai, H);
+    double hmax = 0;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) hmax = fmax(hmax, fabs(H[i]));
+    uncertain |= !(fabs(H[8]) > 1e-9 * hmax);  // also catches NaN
+    const double inv = 1.0 / H[8];
+    float Hf[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) Hf[i] = (float)(H[i] * inv);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) uncertain |= !isfinite(Hf[i]);
+    const int n = S.n;
+    if (uncertain) {
+        bounds[o] = make_int2(0, n);
+        return;
+    }
+    int lo = 0, hi = 0;
+#pragma unroll 4
+    for (int i = 0; i < n; ++i) {
+        const float4 q = P[i];
+        const float W = fmaf(Hf[6], q.x, fmaf(Hf[7], q.y, 1.f));
+        const float ww = __builtin_amdgcn_rcpf(W);
+        const float X = fmaf(Hf[0], q.x, fmaf(Hf[1], q.y, Hf[2]));
+        const float Y = fmaf(Hf[3], q.x, fmaf(Hf[4], q.y, Hf[5]));
+        const float ex = fmaf(X, ww, -q.z), ey = fmaf(Y, ww, -q.w);
+        const float e = fmaf(ex, ex, ey * ey);
+        const float sc = fabsf(q.x) + fabsf(q.y) + fabsf(q.z) + fabsf(q.w);
+        const float d = fmaf(1e-7f * sc, sc, 2.0f);  // margin (px^2) on the reprojection error
+        lo += e < thr2 - d;
+        hi += e <= thr2 + d;
+    }
+    bounds[o] = make_int2(lo, hi);
+}
+
+// exact count of one hypothesis (runKernel + computeError + findInliers, bit-exact)
+__device__ int exact_count(const float4* __restrict__ P, int n, int4 s4, double* D, float thr2) {
+    const float4 a = P[s4.x], b = P[s4.y], c = P[s4.z], d = P[s4.w];
+    const float M[8] = {a.x, a.y, b.x, b.y, c.x, c.y, d.x, d.y};
+    const float m[8] = {a.z, a.w, b.z, b.w, c.z, c.w, d.z, d.w};
+    double H[9];
+    if (!run_kernel4<64>(M, m, D, H)) return -1;
+    float Hf[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) Hf[i] = (float)H[i];
+    int cnt = 0;
+    for (int i = 0; i < n; ++i) {
+        const float4 q = P[i];
+        cnt += reproj_err(Hf, q.x, q.y, q.z, q.w) <= thr2;
+    }
+    return cnt;
+}
+
+__device__ __forceinline__ int wave_excl_prefix_max(int v) {
+    const int lane = threadIdx.x & 63;
+    int incl = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int o = __shfl_up(incl, off);
+        if (lane >= off) incl = max(incl, o);
+    }
+    const int ex = __shfl_up(incl, 1);
+    return lane == 0 ? INT_MIN : ex;
+}
+
+__global__ __launch_bounds__(64) void ransac_select_filtered_kernel(RansacState* __restrict__ st,
+                                                                    const ProbDev* __restrict__ probs,
+                                                                    const float4* __restrict__ pts,
+                                                                    const int4* __restrict__ samples,
+                                                                    const int2* __restrict__ bounds, int c1,
+                                                                    double conf, float thr2) {
+    __shared__ double sd[kJ9D * 64];
+    __shared__ int cand[64];
+    const int p = blockIdx.x, lane = threadIdx.x;
+    RansacState S = st[p];
+    if (!S.active || S.done) return;
+    const int2* Bd = bounds + probs[p].it_off;
+    const int4* Sm = samples + probs[p].it_off;
+    const float4* __restrict__ P = pts + probs[p].good_off;
+    const int end = min(c1, S.produced);
+    const int N = S.n;
+    int ncand = 0;
+    // exact evaluation of the queued candidates, then their replay in iteration order
+    auto flush = [&]() {
+        if (ncand == 0) return;
+        const int t = lane < ncand ? cand[lane] : INT_MAX;
+        int ex = -1;
+        if (lane < ncand && t < S.niters) ex = exact_count(P, N, Sm[t], sd + lane, thr2);
+        for (;;) {
+            const int thr = max(S.max_good, 3);
+            const unsigned long long m = __ballot(t < S.niters && ex > thr);
+            if (!m) break;
+            const int f = __ffsll((long long)m) - 1;
+            const int cf = __shfl(ex, f);
+            S.max_good = cf;
+            S.best_iter = __shfl(t, f);
+            S.niters = update_num_iters(conf, (double)(N - cf) / N, 4, S.niters);
+        }
+        ncand = 0;
+        __syncthreads();
+    };
+    for (int base = S.next_iter; base < end && base < S.niters; base += 64) {
+        const int t = base + lane;
+        const bool valid = t < end;
+        const int2 b = valid ? Bd[t] : make_int2(-1, -1);
+        const int lb = max(max(3, max(S.max_good, S.lo_max)), wave_excl_prefix_max(b.x));
+        const bool c = valid && t < S.niters && b.y > lb;
+        int wmax = b.x;
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) wmax = max(wmax, __shfl_xor(wmax, off));
+        S.lo_max = max(S.lo_max, wmax);
+        const unsigned long long cm = __ballot(c);
+        const int nc = __popcll(cm);
+        if (nc == 0) continue;
+        if (ncand + nc > 64) flush();
+        const int pos = __builtin_amdgcn_mbcnt_hi((uint32_t)(cm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)cm, 0));
+        if (c) cand[ncand + pos] = t;
+        ncand += nc;
+        __syncthreads();
+    }
+    flush();
+    S.next_iter = end;
+    const bool failed = S.fail_iter != -1 && S.produced <= end;
+    if (S.niters <= end || failed) S.done = 1;
+    if (lane == 0) st[p] = S;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -612,8 +889,9 @@ __device__ double lm_cost(const float4* __restrict__ X, int n, const double* h, 
     return acc[0];
 }
 
-// Jacobi of an 8x8 symmetric matrix (single thread, stride-1 scratch)
-__device__ void eig8(const double* Ain, double* J, int* JI, double* w, double* V) {
+// Jacobi of an 8x8 symmetric matrix (single thread, stride-1 scratch); w sorted descending,
+// V rows in the matching order (OpenCV's sorted layout)
+__device__ void eig8(const double* Ain, double* J, double* w, double* V) {
     double* A = J;
     double* W = J + 28;
     double* VV = J + 36;
@@ -621,15 +899,19 @@ __device__ void eig8(const double* Ain, double* J, int* JI, double* w, double* V
         W[i] = Ain[9 * i];
         for (int j = i + 1; j < 8; ++j) A[pk<8>(i, j)] = Ain[8 * i + j];
     }
-    jacobi_strided<8, 1>(A, W, VV, JI);
-    for (int i = 0; i < 8; ++i) w[i] = W[i];
-    for (int i = 0; i < 64; ++i) V[i] = VV[i];
+    double Ws[8];
+    int perm[8];
+    jacobi_fast<8, 1>(A, W, VV, Ws, perm);
+    for (int i = 0; i < 8; ++i) {
+        w[i] = Ws[i];
+        for (int j = 0; j < 8; ++j) V[8 * i + j] = VV[perm[i] * 8 + j];
+    }
 }
 
 // solve(Ap, v, d, DECOMP_EIG) = Jacobi + SVBkSb(eps = 2 DBL_EPSILON)
-__device__ void solve_eig8(const double* Ap, const double* b, double* x, double* J, int* JI) {
+__device__ void solve_eig8(const double* Ap, const double* b, double* x, double* J) {
     double w[8], V[64];
-    eig8(Ap, J, JI, w, V);
+    eig8(Ap, J, w, V);
     double threshold = 0;
     for (int i = 0; i < 8; i++) threshold += w[i];
     threshold *= DBL_EPSILON * 2;
@@ -645,9 +927,9 @@ __device__ void solve_eig8(const double* Ap, const double* b, double* x, double*
     }
 }
 
-__device__ double inv_diag_max8(const double* A, double* J, int* JI) {
+__device__ double inv_diag_max8(const double* A, double* J) {
     double w[8], V[64];
-    eig8(A, J, JI, w, V);
+    eig8(A, J, w, V);
     double threshold = 0;
     for (int i = 0; i < 8; i++) threshold += w[i];
     threshold *= DBL_EPSILON * 2;
@@ -671,7 +953,6 @@ struct RefineShared {
     double A[64], v[8], D[8], x[8], xd[8], d[8];
     double S, Sd, rinf, dinf, lambda, lc;
     double J9[kJ9D];
-    int J9I[kJ9I];
     int flag, n_inl, proceed, accept;
     int wcnt[4];
 };
@@ -708,7 +989,7 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                 const float4 q = P[i];
                 M[2 * i] = q.x; M[2 * i + 1] = q.y; m[2 * i] = q.z; m[2 * i + 1] = q.w;
             }
-            sh.flag = run_kernel4<1>(M, m, sh.J9, sh.J9I, sh.H);
+            sh.flag = run_kernel4<1>(M, m, sh.J9, sh.H);
         }
         __syncthreads();
         ok = sh.flag;
@@ -725,7 +1006,7 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                 const float4 a = P[s4.x], b = P[s4.y], c = P[s4.z], d = P[s4.w];
                 const float M[8] = {a.x, a.y, b.x, b.y, c.x, c.y, d.x, d.y};
                 const float m[8] = {a.z, a.w, b.z, b.w, c.z, c.w, d.z, d.w};
-                run_kernel4<1>(M, m, sh.J9, sh.J9I, sh.Hb);
+                run_kernel4<1>(M, m, sh.J9, sh.Hb);
             }
             __syncthreads();
             float Hf[8];
@@ -795,7 +1076,7 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                     if (tid == 0) {
                         const double invHnorm[9] = {1. / smx, 0, cmx, 0, 1. / smy, cmy, 0, 0, 1};
                         const double Hnorm2[9] = {sMx, 0, -cMx * sMx, 0, sMy, -cMy * sMy, 0, 0, 1};
-                        dlt_finish<1>(lt, sh.J9, sh.J9I, invHnorm, Hnorm2, sh.H);
+                        dlt_finish<1>(lt, sh.J9, invHnorm, Hnorm2, sh.H);
                     }
                 } else if (tid == 0) {
                     for (int i = 0; i < 9; ++i) sh.H[i] = sh.Hb[i];  // runKernel returned 0: H kept
@@ -820,7 +1101,7 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                         double Ap[64];
                         for (int i = 0; i < 64; ++i) Ap[i] = sh.A[i];
                         for (int i = 0; i < 8; ++i) Ap[9 * i] += sh.lambda * sh.D[i];
-                        solve_eig8(Ap, sh.v, sh.d, sh.J9, sh.J9I);
+                        solve_eig8(Ap, sh.v, sh.d, sh.J9);
                         double dinf = 0;
                         for (int i = 0; i < 8; ++i) {
                             sh.xd[i] = sh.x[i] - sh.d[i];
@@ -852,7 +1133,7 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                             double nu = (Sd - sh.S) / (fabs(t) > DBL_EPSILON ? t : 1) + 2;
                             nu = fmin(fmax(nu, 2.), 10.);
                             if (sh.lambda == 0) {
-                                const double maxval = inv_diag_max8(sh.A, sh.J9, sh.J9I);
+                                const double maxval = inv_diag_max8(sh.A, sh.J9);
                                 sh.lambda = sh.lc = 1. / maxval;
                                 nu *= 0.5;
                             }
@@ -920,28 +1201,37 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
 // ------------------------------------------------------------------------------------------------
 void ransac_enqueue(const RansacParams& prm, int n_probs, const ProbDev* probs, const float4* pts,
                     const int* n_good, const RansacBufs& b, uint8_t* masks, mim_result* results, int raw,
-                    hipStream_t s, void (*mark)(void*, const char*), void* mark_ctx) {
+                    hipStream_t s, void (*mark)(void*, const char*), void* mark_ctx, int exact_all) {
     if (n_probs <= 0) return;
     ransac_init_kernel<<<(n_probs + 255) / 256, 256, 0, s>>>(b.state, n_good, n_probs, prm.max_iters, prm.min_good);
     const int max_iters = prm.max_iters > 1 ? prm.max_iters : 1;
-    int c0 = 0, chunk = 512;
+    int c0 = 0, chunk = 1024;
     const float thr2 = (float)(prm.thresh * prm.thresh);
     while (c0 < max_iters) {
         const int c1 = (int)std::min<long long>((long long)c0 + chunk, max_iters);
         ransac_sample_kernel<<<n_probs, 64, 0, s>>>(b.state, probs, pts, b.stream, b.stream_len, b.samples, c1, b.err);
         mark(mark_ctx, "sample");
-        const int bpp64 = (c1 - c0 + 63) / 64;
-        ransac_hypo_kernel<<<n_probs * bpp64, 64, 0, s>>>(b.state, probs, pts, b.samples, b.hyp, b.counts, c0, c1,
-                                                         bpp64);
-        mark(mark_ctx, "hypo");
         const int bpp256 = (c1 - c0 + 255) / 256;
-        ransac_score_kernel<<<n_probs * bpp256, 256, 0, s>>>(b.state, probs, pts, b.hyp, b.counts, c0, c1, bpp256,
-                                                            thr2);
-        mark(mark_ctx, "score");
-        ransac_select_kernel<<<n_probs, 64, 0, s>>>(b.state, probs, b.counts, c1, prm.conf);
-        mark(mark_ctx, "select");
+        if (exact_all) {  // reference mode: every hypothesis through runKernel + computeError
+            const int bpp64 = (c1 - c0 + 63) / 64;
+            ransac_hypo_kernel<<<n_probs * bpp64, 64, 0, s>>>(b.state, probs, pts, b.samples, b.hyp, b.counts, c0, c1,
+                                                             bpp64);
+            mark(mark_ctx, "hypo");
+            ransac_score_kernel<<<n_probs * bpp256, 256, 0, s>>>(b.state, probs, pts, b.hyp, b.counts, c0, c1,
+                                                                bpp256, thr2);
+            mark(mark_ctx, "score");
+            ransac_select_kernel<<<n_probs, 64, 0, s>>>(b.state, probs, b.counts, c1, prm.conf);
+            mark(mark_ctx, "select");
+        } else {
+            ransac_bound_kernel<<<n_probs * bpp256, 256, 0, s>>>(b.state, probs, pts, b.samples, b.bounds, c0, c1,
+                                                                bpp256, thr2);
+            mark(mark_ctx, "score");
+            ransac_select_filtered_kernel<<<n_probs, 64, 0, s>>>(b.state, probs, pts, b.samples, b.bounds, c1,
+                                                                prm.conf, thr2);
+            mark(mark_ctx, "select");
+        }
         c0 = c1;
-        chunk = chunk < (1 << 16) ? chunk * 4 : chunk;
+        chunk = chunk < (1 << 15) ? chunk * 8 : chunk;
     }
     ransac_refine_kernel<<<n_probs, kRT, 0, s>>>(b.state, probs, pts, n_good, b.samples, b.inl, masks, results, prm,
                                                  raw);

@@ -1,0 +1,92 @@
+// C++ host-layer test: mim::Detector (include/mim.hpp) vs the CPU restatement running the reference's
+// view loop (TestsDetector.cpp:58-95) — identical allUnfilteredScenePts, element for element.
+#include <cmath>
+#include <cstdio>
+#include <random>
+#include <vector>
+
+#include "../../include/mim.hpp"
+#include "../../oracle/mim_oracle.h"
+
+static std::vector<float> sift_like(std::mt19937& g, int n) {
+    std::gamma_distribution<double> gam(0.5, 1.0);
+    std::vector<float> d((size_t)n * 128);
+    for (int i = 0; i < n; ++i) {
+        double v[128], nrm = 0;
+        for (int k = 0; k < 128; ++k) { v[k] = gam(g); nrm += v[k] * v[k]; }
+        nrm = std::sqrt(nrm);
+        double n2 = 0;
+        for (int k = 0; k < 128; ++k) { v[k] = std::min(v[k] / nrm, 0.2); n2 += v[k] * v[k]; }
+        n2 = std::sqrt(n2);
+        for (int k = 0; k < 128; ++k) d[(size_t)i * 128 + k] = (float)std::min(255.0, std::rint(v[k] * 512 / n2));
+    }
+    return d;
+}
+
+int main() {
+    std::mt19937 g(7);
+    std::uniform_real_distribution<float> ux(0, 640), uy(0, 480), un(-0.4f, 0.4f);
+    // scene (two scales = two descriptor sets), one model with 3 views planted in both
+    const int nt = 1500, nq = 400, plant = 150;
+    mim::ModelViews model{"004_sugar_box", {}};
+    std::vector<std::vector<mim::Point2f>> skp(2);
+    std::vector<std::vector<float>> sdesc(2);
+    for (int s = 0; s < 2; ++s) {
+        sdesc[s] = sift_like(g, nt);
+        for (int i = 0; i < nt; ++i) skp[s].push_back({ux(g), uy(g)});
+    }
+    for (int v = 0; v < 3; ++v) {
+        mim::View view;
+        view.descriptors = sift_like(g, nq);
+        for (int i = 0; i < nq; ++i) view.keypoints.push_back({ux(g), uy(g)});
+        for (int s = 0; s < 2; ++s) {
+            const float sc = s == 0 ? 0.85f : 1.0f, tx = 20.f * (v + 1), ty = -10.f * s;
+            for (int i = 0; i < plant; ++i) {
+                const int row = 100 + v * plant + i;  // disjoint rows per view
+                for (int k = 0; k < 128; ++k) sdesc[s][(size_t)row * 128 + k] = view.descriptors[(size_t)i * 128 + k];
+                sdesc[s][(size_t)row * 128 + (i % 128)] = std::min(255.f, sdesc[s][(size_t)row * 128 + (i % 128)] + 1.f);
+                if (i % 2 == 0) skp[s][row] = {view.keypoints[i].x * sc + tx + un(g), view.keypoints[i].y * sc + ty + un(g)};
+            }
+        }
+        model.views.push_back(std::move(view));
+    }
+    const float scales[2] = {0.85f, 1.0f};
+    mim::Detector det(0);
+    det.params().max_iters = 2000;
+    std::vector<std::vector<mim::Point2f>> out;
+    det.detect_scene({&model}, {{&skp[0], &sdesc[0], scales[0]}, {&skp[1], &sdesc[1], scales[1]}}, out);
+
+    // reference loop on the CPU restatement
+    orc_params prm;
+    orc_default_params(&prm);
+    prm.max_iters = 2000;
+    std::vector<mim::Point2f> ref;
+    for (int s = 0; s < 2; ++s)
+        for (int v = 0; v < 3; ++v) {
+            orc_result r;
+            std::vector<uint8_t> mask(nq);
+            std::vector<int32_t> gq(nq), gt(nq);
+            orc_match_problem(model.views[v].descriptors.data(), &model.views[v].keypoints[0].x, nq, sdesc[s].data(),
+                              &skp[s][0].x, nt, 128, &prm, 1, &r, mask.data(), gq.data(), gt.data());
+            if (r.status != 0) continue;
+            for (int j = 0; j < r.n_good; ++j)
+                if (mask[j]) {
+                    mim::Point2f p = skp[s][gt[j]];
+                    if (scales[s] != 1.0f) { p.x /= scales[s]; p.y /= scales[s]; }
+                    ref.push_back(p);
+                }
+        }
+    if (out.size() != 1 || out[0].size() != ref.size()) {
+        std::printf("FAIL size %zu vs %zu\n", out.empty() ? 0 : out[0].size(), ref.size());
+        return 1;
+    }
+    for (size_t i = 0; i < ref.size(); ++i)
+        if (out[0][i].x != ref[i].x || out[0][i].y != ref[i].y) {
+            std::printf("FAIL at %zu\n", i);
+            return 1;
+        }
+    std::printf("OK %zu inlier points, statuses:", ref.size());
+    for (auto& r : det.last_results()) std::printf(" %d/%d/%d", r.n_good, r.n_inl, r.status);
+    std::printf("\n");
+    return ref.empty() ? 1 : 0;
+}

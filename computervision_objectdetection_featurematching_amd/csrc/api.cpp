@@ -96,7 +96,7 @@ struct SetRec {
 namespace mim {
 // RANSAC workspace (definition shared with ransac.hip through this layout)
 struct RansacWs {
-    DevBuf state, samples, hyp, counts, bounds, stream, scratch, inl, err;
+    DevBuf state, samples, hyp, counts, bounds, flags, stream, scratch, inl, err;
     long long stream_len = 0;
 };
 }  // namespace mim
@@ -185,7 +185,7 @@ void mim_ctx_destroy(mim_ctx* c) {
     c->arena.release();
     for (DevBuf* b : {&c->probs, &c->works, &c->parts, &c->good_q, &c->good_t, &c->pts, &c->n_good,
                       &c->results, &c->masks, &c->knn_idx, &c->knn_dist, &c->rws.state, &c->rws.samples,
-                      &c->rws.hyp, &c->rws.counts, &c->rws.bounds, &c->rws.stream, &c->rws.scratch, &c->rws.inl, &c->rws.err})
+                      &c->rws.hyp, &c->rws.counts, &c->rws.bounds, &c->rws.flags, &c->rws.stream, &c->rws.scratch, &c->rws.inl, &c->rws.err})
         b->release();
     if (c->own) (void)hipStreamDestroy(c->own);
     delete c;
@@ -527,6 +527,10 @@ static mim_status ransac_locked(mim_ctx* c, int n, const mim_params* prm, int ra
     HIPCHK(c, c->rws.hyp.ensure(sizeof(float) * 8 * it_total));
     HIPCHK(c, c->rws.counts.ensure(sizeof(int) * it_total));
     HIPCHK(c, c->rws.bounds.ensure(sizeof(int2) * it_total));
+    // attempt-outcome windows: largest chunk x 28 draws per problem (chunks <= 32768 + tail)
+    const long long chunk_max = std::min<long long>(max_iters, 1 << 18);
+    const long long flag_cap = (long long)std::max(n, 1) * (chunk_max * 28 + 4096);
+    HIPCHK(c, c->rws.flags.ensure((size_t)flag_cap));
     HIPCHK(c, c->rws.inl.ensure(sizeof(float4) * good_total));
     HIPCHK(c, c->rws.err.ensure(sizeof(int) * 4));
     HIPCHK(c, c->results.ensure(sizeof(mim_result) * std::max(n, 1)));
@@ -538,6 +542,8 @@ static mim_status ransac_locked(mim_ctx* c, int n, const mim_params* prm, int ra
     b.hyp = c->rws.hyp.as<float>();
     b.counts = c->rws.counts.as<int>();
     b.bounds = c->rws.bounds.as<int2>();
+    b.flags = c->rws.flags.as<uint8_t>();
+    b.flag_cap = flag_cap;
     b.stream = c->rws.stream.as<uint32_t>();
     b.stream_len = c->rws.stream_len;
     b.inl = c->rws.inl.as<float4>();

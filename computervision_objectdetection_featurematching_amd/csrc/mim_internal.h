@@ -60,6 +60,7 @@ struct RansacState {
     int n;                 // point count (= n_good)
     int active;            // problem takes the RANSAC path (n_good > 4)
     int lo_max;            // max lower-bound count seen (filtered path: lower bound of maxGoodCount)
+    unsigned long long modM;  // Lemire fast-modulo constant for % n (RNG::uniform(0, n))
 };
 
 struct RansacParams {
@@ -81,6 +82,8 @@ struct RansacBufs {
     float* hyp;               // [(it_off + iter) * 8]  (float)H[0..7] of the minimal-sample model
     int* counts;              // [it_off + iter]  inlier count, -1 when runKernel returned 0
     int2* bounds;             // [it_off + iter]  (lower, upper) bound of the count (filtered path)
+    uint8_t* flags;           // [problem][window] getSubset attempt outcomes ahead of stream_pos
+    long long flag_cap;       // bytes of `flags`
     const uint32_t* stream;   // raw cv::RNG((uint64)-1).next() stream shared by every problem
     long long stream_len;
     float4* inl;              // [good_off + k] compressed inliers for the refit (scratch)

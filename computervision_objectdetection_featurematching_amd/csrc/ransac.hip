@@ -354,6 +354,59 @@ __device__ int update_num_iters(double p, double ep, int model_points, int max_i
 }
 
 // ------------------------------------------------------------------------------------------------
+// RNG::uniform(0, n) = next() % n via Lemire's exact fast modulo (M = 2^64 / n + 1)
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ unsigned fastmod(unsigned a, unsigned long long M, unsigned d) {
+    return (unsigned)__umul64hi(M * (unsigned long long)a, (unsigned long long)d);
+}
+
+// getSubset's draw loop for one attempt starting at stream position q: redraw while an index
+// repeats.  Returns the number of draws consumed (0 if the stream ends first).
+__device__ __forceinline__ int resolve_at(long long q, const uint32_t* __restrict__ stream, long long slen,
+                                          unsigned N, unsigned long long M, int (&idx)[4]) {
+    unsigned buf[8];
+    long long bq = q, r = q;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) buf[k] = q + k < slen ? stream[q + k] : 0u;
+    for (int i = 0; i < 4; ++i) {
+        for (;;) {
+            if (r >= slen) return 0;
+            if (r >= bq + 8) {
+#pragma unroll
+                for (int k = 0; k < 8; ++k) buf[k] = r + k < slen ? stream[r + k] : 0u;
+                bq = r;
+            }
+            unsigned raw = buf[0];
+#pragma unroll
+            for (int k = 1; k < 8; ++k) raw = (r - bq) == k ? buf[k] : raw;
+            ++r;
+            const int v = (int)fastmod(raw, M, N);
+            bool dup = false;
+            for (int j = 0; j < i; ++j) dup |= idx[j] == v;
+            if (!dup) {
+                idx[i] = v;
+                break;
+            }
+        }
+    }
+    return (int)(r - q);
+}
+
+// A sample is stored as (q, -1, 0, 0) when its 4 draws are stream[q..q+3] (no repeat), as
+// (q, -2, 0, 0) when getSubset redrew repeated indices starting at q, or as the 4 indices.
+__device__ __forceinline__ int4 decode_sample(int4 s, const uint32_t* __restrict__ stream, unsigned N,
+                                              unsigned long long M) {
+    if (s.y >= 0) return s;
+    const long long q = s.x;
+    if (s.y == -1)
+        return make_int4((int)fastmod(stream[q], M, N), (int)fastmod(stream[q + 1], M, N),
+                         (int)fastmod(stream[q + 2], M, N), (int)fastmod(stream[q + 3], M, N));
+    int idx[4] = {0, 0, 0, 0};
+    resolve_at(q, stream, 1LL << 62, N, M, idx);  // the walker already checked the stream bound
+    return make_int4(idx[0], idx[1], idx[2], idx[3]);
+}
+
+// ------------------------------------------------------------------------------------------------
 // init: per-problem RANSAC state from the ratio-test survivors
 // ------------------------------------------------------------------------------------------------
 __global__ void ransac_init_kernel(RansacState* __restrict__ st, const int* __restrict__ n_good, int n_probs,
@@ -362,6 +415,7 @@ __global__ void ransac_init_kernel(RansacState* __restrict__ st, const int* __re
     if (p >= n_probs) return;
     RansacState S{};
     S.n = n_good[p];
+    S.modM = S.n > 0 ? (~0ull / (unsigned long long)S.n + 1) : 0;
     S.active = (S.n >= min_good && S.n > 4) ? 1 : 0;  // n == 4: direct runKernel, no RANSAC
     S.niters = max(max_iters, 1);
     S.fail_iter = -1;
@@ -370,102 +424,202 @@ __global__ void ransac_init_kernel(RansacState* __restrict__ st, const int* __re
 }
 
 // ------------------------------------------------------------------------------------------------
-// sample: getSubset replay, one wave per problem
+// attempt: the outcome of a getSubset attempt that starts at stream position q, for every q of a
+// window ahead of each problem's current position — fully parallel over the GPU.  The sampler
+// below then only walks the chain of attempt start positions.  flag: 0 checkSubset fails,
+// 1 passes, 2 an index repeats (resolved serially by the walker), 3 beyond the RNG stream.
+// attempts precomputed ahead of the walker: the expected draws of the remaining iterations of the
+// chunk (draws per iteration measured so far, 28 before any) + 25 % + 4096, capped by the buffer
+__device__ __forceinline__ int window_len(const RansacState& S, int c1, int wcap) {
+    const int need = min(c1, S.niters) - S.produced;
+    const double rate = S.produced > 0 ? (double)S.stream_pos / S.produced : 28.0;
+    const long long w = (long long)((double)need * rate * 1.25) + 4096;
+    return (int)min((long long)wcap, w);
+}
+
+// Outcome of the getSubset attempt whose draws start at q, as one byte: bit 0 = checkSubset
+// passes, bits 1..6 = draws consumed - 4 (repeated indices redrawn); 0xFF = the walker must resolve
+// it itself (RNG stream end, or > 67 draws).
+constexpr int kAttemptSerial = 0xFF;
+__device__ __forceinline__ int attempt_flag(long long q, const uint32_t* __restrict__ stream, long long slen,
+                                            unsigned N, unsigned long long M, const float4* __restrict__ P) {
+    if (q + 4 > slen) return kAttemptSerial;
+    int idx[4] = {(int)fastmod(stream[q], M, N), (int)fastmod(stream[q + 1], M, N),
+                  (int)fastmod(stream[q + 2], M, N), (int)fastmod(stream[q + 3], M, N)};
+    int len = 4;
+    if (idx[1] == idx[0] || idx[2] == idx[0] || idx[2] == idx[1] || idx[3] == idx[0] || idx[3] == idx[1] ||
+        idx[3] == idx[2]) {
+        len = resolve_at(q, stream, slen, N, M, idx);
+        if (len == 0 || len > 67) return kAttemptSerial;
+    }
+    const float4 a = P[idx[0]], b = P[idx[1]], c = P[idx[2]], d = P[idx[3]];
+    const float s4[8] = {a.x, a.y, b.x, b.y, c.x, c.y, d.x, d.y};
+    const float t4[8] = {a.z, a.w, b.z, b.w, c.z, c.w, d.z, d.w};
+    return ((len - 4) << 1) | (check_subset(s4, t4) ? 1 : 0);
+}
+
+__global__ __launch_bounds__(256) void ransac_attempt_kernel(const RansacState* __restrict__ st,
+                                                             const ProbDev* __restrict__ probs,
+                                                             const float4* __restrict__ pts,
+                                                             const uint32_t* __restrict__ stream, long long slen,
+                                                             uint8_t* __restrict__ flags, int wcap, int bpp, int c1) {
+    const int p = blockIdx.x / bpp;
+    const int off = (blockIdx.x % bpp) * 256 + threadIdx.x;
+    const RansacState S = st[p];
+    if (!S.active || S.done || S.fail_iter != -1 || S.produced >= min(c1, S.niters)) return;
+    if (off >= window_len(S, c1, wcap)) return;
+    flags[(long long)p * wcap + off] =
+        (uint8_t)attempt_flag(S.stream_pos + off, stream, slen, (unsigned)S.n, S.modM, pts + probs[p].good_off);
+}
+
+__device__ __forceinline__ int wave_excl_prefix_sum(int v) {
+    const int lane = threadIdx.x & 63;
+    int incl = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int o = __shfl_up(incl, off);
+        if (lane >= off) incl += o;
+    }
+    return incl - v;
+}
+
+__device__ __forceinline__ int wave_min(int v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v = min(v, __shfl_xor(v, off));
+    return v;
+}
+
+__device__ __forceinline__ int wave_max(int v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v = max(v, __shfl_xor(v, off));
+    return v;
+}
+
+// ------------------------------------------------------------------------------------------------
+// sample: walk the chain of getSubset attempts, 256 per round (4 per lane, in order), with the
+// outcomes precomputed by ransac_attempt_kernel; reproduces getSubset's redraw-on-repeat, the
+// checkSubset rejections and the 10000-attempt failure exactly (ptsetreg.cpp).
 // ------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(64) void ransac_sample_kernel(RansacState* __restrict__ st,
                                                            const ProbDev* __restrict__ probs,
                                                            const float4* __restrict__ pts,
                                                            const uint32_t* __restrict__ stream, long long slen,
                                                            int4* __restrict__ samples, int c1,
-                                                           int* __restrict__ err) {
+                                                           int* __restrict__ err, const uint8_t* __restrict__ flags,
+                                                           int wcap) {
+    constexpr int BIG = 1 << 30;
     const int p = blockIdx.x, lane = threadIdx.x;
     RansacState S = st[p];
     if (!S.active || S.done || S.fail_iter != -1) return;
     const int target = min(c1, S.niters);
     if (S.produced >= target) return;
+    const long long wbase = S.stream_pos;
+    const int wlen = window_len(S, c1, wcap);
+    const uint8_t* F = flags + (long long)p * wcap;
     const unsigned N = (unsigned)S.n;
+    const unsigned long long M = S.modM;
     const float4* P = pts + probs[p].good_off;
     int4* out = samples + probs[p].it_off;
     long long pos = S.stream_pos;
     int produced = S.produced, fail_run = S.fail_run;
-    bool stopped = false;
-    while (produced < target && !stopped) {
-        const long long p0 = pos + 4LL * lane;
-        int i0 = 0, i1 = 0, i2 = 0, i3 = 0;
-        bool coll = true;
-        if (p0 + 4 <= slen) {
-            i0 = (int)(stream[p0] % N);
-            i1 = (int)(stream[p0 + 1] % N);
-            i2 = (int)(stream[p0 + 2] % N);
-            i3 = (int)(stream[p0 + 3] % N);
-            coll = i1 == i0 || i2 == i0 || i2 == i1 || i3 == i0 || i3 == i1 || i3 == i2;
+    while (produced < target) {
+        int f[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const long long q = pos + 4LL * (4 * lane + i);
+            const long long rel = q - wbase;
+            f[i] = rel < wlen ? (int)F[rel] : attempt_flag(q, stream, slen, N, M, P);
         }
-        const unsigned long long cm = __ballot(coll);
-        const int fc = cm ? __ffsll((long long)cm) - 1 : 64;  // first attempt with a repeated draw
-        long long end = p0 + 4;
-        bool oob = false;
-        if (lane == fc) {  // resolve serially: redraw while the index repeats (getSubset inner loop)
-            long long q = p0;
-            int idx[4];
-            for (int i = 0; i < 4 && !oob; ++i) {
-                for (;;) {
-                    if (q >= slen) { oob = true; break; }
-                    const int v = (int)(stream[q++] % N);
-                    bool dup = false;
-                    for (int j = 0; j < i; ++j) dup |= idx[j] == v;
-                    if (!dup) { idx[i] = v; break; }
+        // first attempt whose length is not 4 draws: later lanes' start positions are wrong
+        int lc = 4;
+#pragma unroll
+        for (int i = 3; i >= 0; --i) lc = (f[i] == kAttemptSerial || (f[i] >> 1) != 0) ? i : lc;
+        const unsigned long long cm = __ballot(lc < 4);
+        const int L = cm ? __ffsll((long long)cm) - 1 : 64;
+        const int afc = L < 64 ? 4 * L + __shfl(lc, L) : 256;
+        long long endfc = 0;
+        int fcpass = 0, fcres = 0;  // fcres: the attempt redrew repeated indices
+        int oob = 0;
+        if (afc < 256) {
+            const int ffc = __shfl(f[0], L);
+            int fsel = ffc;
+#pragma unroll
+            for (int i = 1; i < 4; ++i) {
+                const int fi = __shfl(f[i], L);
+                fsel = (afc - 4 * L) == i ? fi : fsel;
+            }
+            const long long qfc = pos + 4LL * afc;
+            if (fsel != kAttemptSerial) {
+                endfc = qfc + 4 + (fsel >> 1);
+                fcpass = fsel & 1;
+                fcres = 1;
+            } else {  // resolve here (stream end or a very long redraw run)
+                int idx[4] = {0, 0, 0, 0};
+                const int len = resolve_at(qfc, stream, slen, N, M, idx);
+                if (len == 0) {
+                    oob = 1;
+                } else {
+                    const float4 a = P[idx[0]], b = P[idx[1]], c = P[idx[2]], d = P[idx[3]];
+                    const float s4[8] = {a.x, a.y, b.x, b.y, c.x, c.y, d.x, d.y};
+                    const float t4[8] = {a.z, a.w, b.z, b.w, c.z, c.w, d.z, d.w};
+                    fcpass = check_subset(s4, t4) ? 1 : 0;
+                    fcres = len != 4;
+                    endfc = qfc + len;
                 }
             }
-            i0 = idx[0]; i1 = idx[1]; i2 = idx[2]; i3 = idx[3];
-            end = q;
         }
-        if (__any(oob)) {  // RNG stream exhausted: report, never guess
+        if (oob) {  // RNG stream exhausted: report, never guess
             if (lane == 0) atomicOr(err, 1);
             S.fail_iter = -2;
-            stopped = true;
             break;
         }
-        const bool valid = lane <= fc;
-        bool pass = false;
-        if (valid) {
-            const float4 a = P[i0], b = P[i1], c = P[i2], d = P[i3];
-            const float s[8] = {a.x, a.y, b.x, b.y, c.x, c.y, d.x, d.y};
-            const float t[8] = {a.z, a.w, b.z, b.w, c.z, c.w, d.z, d.w};
-            pass = check_subset(s, t);
+        unsigned bits = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int a = 4 * lane + i;
+            const bool ps = (a < afc && f[i] == 1) || (a == afc && fcpass);
+            bits |= ps ? (1u << i) : 0u;
         }
-        const unsigned long long pm = __ballot(pass);
-        const int last_valid = fc < 64 ? fc : 63;
-        const unsigned long long vmask = last_valid == 63 ? ~0ull : ((1ull << (last_valid + 1)) - 1);
-        // lane at which the target-th sample is produced
+        const int nvalid = afc < 256 ? afc + 1 : 256;
+        const int c = __popc(bits);
+        const int E = wave_excl_prefix_sum(c);
+        const int tot = __shfl(E + c, 63);
+        const int a_p = wave_min(bits ? 4 * lane + __ffs(bits) - 1 : BIG);        // first pass
+        const int a_lp = wave_max(bits ? 4 * lane + 31 - __clz(bits) : -1);      // last pass
         const int need = target - produced;
-        const unsigned long long below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-        const int rank = __popcll(pm & below);  // passes before this lane
-        const bool is_target = pass && rank == need - 1;
-        const unsigned long long tm = __ballot(is_target);
-        // consecutive failures reaching getSubset's maxAttempts = 10000
-        const unsigned long long pb = pm & below;
-        const int run = pb ? (lane - (63 - __clzll((long long)pb))) : (fail_run + lane + 1);
-        const bool is_fail = valid && !pass && run >= 10000;
-        const unsigned long long fm = __ballot(is_fail);
-        int stop_lane = last_valid;
-        bool hit_target = false, hit_fail = false;
-        const int tl = tm ? __ffsll((long long)tm) - 1 : 64;
-        const int fl = fm ? __ffsll((long long)fm) - 1 : 64;
-        if (tl < 64 && tl <= fl) { stop_lane = tl; hit_target = true; }
-        else if (fl < 64) { stop_lane = fl; hit_fail = true; }
-        // emit samples of passing lanes up to the stop lane
-        if (pass && lane <= stop_lane) out[produced + rank] = make_int4(i0, i1, i2, i3);
-        const unsigned long long upto = stop_lane == 63 ? ~0ull : ((1ull << (stop_lane + 1)) - 1);
-        const unsigned long long pu = pm & upto & vmask;
-        produced += __popcll(pu);
-        if (pu) fail_run = stop_lane - (63 - __clzll((long long)pu));
-        else fail_run += stop_lane + 1;
-        pos = __shfl(end, stop_lane);
-        if (hit_fail) {
-            S.fail_iter = produced;  // getSubset returned false in this iteration
-            stopped = true;
+        int at = BIG;
+        if (E < need && need <= E + c) {
+            int k = need - E;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                if ((bits >> i) & 1) {
+                    if (--k == 0 && at == BIG) at = 4 * lane + i;
+                }
+            }
         }
-        if (hit_target) break;
+        at = wave_min(at);
+        const int fails_before = a_p < BIG ? a_p : nvalid;
+        const int af = fail_run + fails_before >= 10000 ? 10000 - fail_run - 1 : BIG;  // 10000th failure
+        int stop = nvalid - 1, got = tot;
+        bool hit_t = false, hit_f = false;
+        if (at < BIG && at < af) { stop = at; hit_t = true; got = need; }
+        else if (af < BIG) { stop = af; hit_f = true; got = 0; }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int a = 4 * lane + i;
+            if (((bits >> i) & 1) && a <= stop) {
+                const int rank = E + __popc(bits & ((1u << i) - 1));
+                out[produced + rank] = make_int4((int)(pos + 4LL * a), (a == afc && fcres) ? -2 : -1, 0, 0);
+            }
+        }
+        produced += got;
+        fail_run = hit_t ? 0 : (hit_f ? 10000 : (tot > 0 ? stop - a_lp : fail_run + nvalid));
+        pos = stop == afc ? endfc : pos + 4LL * (stop + 1);
+        if (hit_f) {
+            S.fail_iter = produced;  // getSubset returned false in this iteration
+            break;
+        }
+        if (hit_t) break;
     }
     if (lane == 0) {
         S.stream_pos = pos;
@@ -482,6 +636,7 @@ __global__ __launch_bounds__(64) void ransac_hypo_kernel(const RansacState* __re
                                                          const ProbDev* __restrict__ probs,
                                                          const float4* __restrict__ pts,
                                                          const int4* __restrict__ samples,
+                                                         const uint32_t* __restrict__ stream,
                                                          float* __restrict__ hyp, int* __restrict__ counts, int c0,
                                                          int c1, int bpp) {
     __shared__ double sd[kJ9D * 64];
@@ -492,7 +647,7 @@ __global__ __launch_bounds__(64) void ransac_hypo_kernel(const RansacState* __re
     if (it >= c1 || it >= S.produced) return;
     const long long o = probs[p].it_off + it;
     const float4* P = pts + probs[p].good_off;
-    const int4 s4 = samples[o];
+    const int4 s4 = decode_sample(samples[o], stream, (unsigned)S.n, S.modM);
     const float4 a = P[s4.x], b = P[s4.y], c = P[s4.z], d = P[s4.w];
     const float M[8] = {a.x, a.y, b.x, b.y, c.x, c.y, d.x, d.y};
     const float m[8] = {a.z, a.w, b.z, b.w, c.z, c.w, d.z, d.w};
@@ -585,23 +740,32 @@ __device__ __forceinline__ double min_rel_area(const double* x, const double* y)
 
 constexpr double kScreenArea = 1e-5;  // samples less conditioned than this are evaluated exactly
 
+constexpr int kBoundTile = 1024;  // points per LDS tile of the bound kernel (16 KiB + 8 KiB)
+
 __global__ __launch_bounds__(256) void ransac_bound_kernel(const RansacState* __restrict__ st,
                                                            const ProbDev* __restrict__ probs,
                                                            const float4* __restrict__ pts,
                                                            const int4* __restrict__ samples,
+                                                           const uint32_t* __restrict__ stream,
                                                            int2* __restrict__ bounds, int c0, int c1, int bpp,
                                                            float thr2) {
+    __shared__ float4 tp[kBoundTile];
+    __shared__ float2 tt[kBoundTile];
     const int p = blockIdx.x / bpp;
     const int it = c0 + (blockIdx.x % bpp) * 256 + threadIdx.x;
     const RansacState S = st[p];
-    if (!S.active || S.done) return;
-    if (it >= c1 || it >= S.produced) return;
+    if (!S.active || S.done) return;  // uniform over the block
+    if (c0 + (blockIdx.x % bpp) * 256 >= min(c1, S.produced)) return;  // whole block idle
+    const bool act = it < c1 && it < S.produced;
     const long long o = probs[p].it_off + it;
     const float4* __restrict__ P = pts + probs[p].good_off;
-    const int4 s4 = samples[o];
-    const float4 q0 = P[s4.x], q1 = P[s4.y], q2 = P[s4.z], q3 = P[s4.w];
-    // runKernel's own degeneracy test (exact, cheap): spread < DBL_EPSILON -> no model
-    {
+    const int n = S.n;
+    bool uncertain = false, invalid = false;
+    float Hf[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (act) {
+        const int4 s4 = decode_sample(samples[o], stream, (unsigned)n, S.modM);
+        const float4 q0 = P[s4.x], q1 = P[s4.y], q2 = P[s4.z], q3 = P[s4.w];
+        // runKernel's own degeneracy test (exact, cheap): spread < DBL_EPSILON -> no model
         const float M[8] = {q0.x, q0.y, q1.x, q1.y, q2.x, q2.y, q3.x, q3.y};
         const float m[8] = {q0.z, q0.w, q1.z, q1.w, q2.z, q2.w, q3.z, q3.w};
         double cMx = 0, cMy = 0, cmx = 0, cmy = 0, sMx = 0, sMy = 0, smx = 0, smy = 0;
@@ -616,54 +780,61 @@ __global__ __launch_bounds__(256) void ransac_bound_kernel(const RansacState* __
             smx += fabs(m[2 * i] - cmx); smy += fabs(m[2 * i + 1] - cmy);
             sMx += fabs(M[2 * i] - cMx); sMy += fabs(M[2 * i + 1] - cMy);
         }
-        if (fabs(smx) < DBL_EPSILON || fabs(smy) < DBL_EPSILON || fabs(sMx) < DBL_EPSILON ||
-            fabs(sMy) < DBL_EPSILON) {
-            bounds[o] = make_int2(-1, -1);
-            return;
+        invalid = fabs(smx) < DBL_EPSILON || fabs(smy) < DBL_EPSILON || fabs(sMx) < DBL_EPSILON ||
+                  fabs(sMy) < DBL_EPSILON;
+        const double sx[4] = {q0.x, q1.x, q2.x, q3.x}, sy[4] = {q0.y, q1.y, q2.y, q3.y};
+        const double dx[4] = {q0.z, q1.z, q2.z, q3.z}, dy[4] = {q0.w, q1.w, q2.w, q3.w};
+        uncertain = min_rel_area(sx, sy) < kScreenArea || min_rel_area(dx, dy) < kScreenArea;
+        double Qs[9], Qd[9], Ai[9], H[9];
+        square_to_quad(sx, sy, Qs);
+        square_to_quad(dx, dy, Qd);
+        // adjugate of Qs (inverse up to scale)
+        Ai[0] = Qs[4] * Qs[8] - Qs[5] * Qs[7]; Ai[1] = Qs[2] * Qs[7] - Qs[1] * Qs[8]; Ai[2] = Qs[1] * Qs[5] - Qs[2] * Qs[4];
+        Ai[3] = Qs[5] * Qs[6] - Qs[3] * Qs[8]; Ai[4] = Qs[0] * Qs[8] - Qs[2] * Qs[6]; Ai[5] = Qs[2] * Qs[3] - Qs[0] * Qs[5];
+        Ai[6] = Qs[3] * Qs[7] - Qs[4] * Qs[6]; Ai[7] = Qs[1] * Qs[6] - Qs[0] * Qs[7]; Ai[8] = Qs[0] * Qs[4] - Qs[1] * Qs[3];
+        mat3_mul(Qd, Ai, H);
+        double hmax = 0;
+#pragma unroll
+        for (int i = 0; i < 9; ++i) hmax = fmax(hmax, fabs(H[i]));
+        uncertain |= !(fabs(H[8]) > 1e-9 * hmax);  // also catches NaN
+        const double inv = 1.0 / H[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) Hf[i] = (float)(H[i] * inv);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) uncertain |= !isfinite(Hf[i]);
+    }
+    const bool count = act && !invalid && !uncertain;
+    // points stream through LDS tiles (broadcast reads); per-point margins computed at staging:
+    // err bound 2 px^2 + 1e-7 (|x|+|y|+|u|+|v|)^2 around the squared threshold
+    int lo = 0, hi = 0;
+    for (int b0 = 0; b0 < n; b0 += kBoundTile) {
+        const int tn = min(kBoundTile, n - b0);
+        __syncthreads();
+        for (int i = threadIdx.x; i < tn; i += 256) {
+            const float4 q = P[b0 + i];
+            const float sc = fabsf(q.x) + fabsf(q.y) + fabsf(q.z) + fabsf(q.w);
+            const float d = fmaf(1e-7f * sc, sc, 2.0f);
+            tp[i] = q;
+            tt[i] = make_float2(thr2 - d, thr2 + d);
+        }
+        __syncthreads();
+        if (count) {
+#pragma unroll 4
+            for (int i = 0; i < tn; ++i) {
+                const float4 q = tp[i];
+                const float2 th = tt[i];
+                const float W = fmaf(Hf[6], q.x, fmaf(Hf[7], q.y, 1.f));
+                const float ww = __builtin_amdgcn_rcpf(W);
+                const float X = fmaf(Hf[0], q.x, fmaf(Hf[1], q.y, Hf[2]));
+                const float Y = fmaf(Hf[3], q.x, fmaf(Hf[4], q.y, Hf[5]));
+                const float ex = fmaf(X, ww, -q.z), ey = fmaf(Y, ww, -q.w);
+                const float e = fmaf(ex, ex, ey * ey);
+                lo += e < th.x;
+                hi += e <= th.y;
+            }
         }
     }
-    const double sx[4] = {q0.x, q1.x, q2.x, q3.x}, sy[4] = {q0.y, q1.y, q2.y, q3.y};
-    const double dx[4] = {q0.z, q1.z, q2.z, q3.z}, dy[4] = {q0.w, q1.w, q2.w, q3.w};
-    bool uncertain = min_rel_area(sx, sy) < kScreenArea || min_rel_area(dx, dy) < kScreenArea;
-    double Qs[9], Qd[9], Ai[9], H[9];
-    square_to_quad(sx, sy, Qs);
-    square_to_quad(dx, dy, Qd);
-    // adjugate of Qs (inverse up to scale)
-    Ai[0] = Qs[4] * Qs[8] - Qs[5] * Qs[7]; Ai[1] = Qs[2] * Qs[7] - Qs[1] * Qs[8]; Ai[2] = Qs[1] * Qs[5] - Qs[2] * Qs[4];
-    Ai[3] = Qs[5] * Qs[6] - Qs[3] * Qs[8]; Ai[4] = Qs[0] * Qs[8] - Qs[2] * Qs[6]; Ai[5] = Qs[2] * Qs[3] - Qs[0] * Qs[5];
-    Ai[6] = Qs[3] * Qs[7] - Qs[4] * Qs[6]; Ai[7] = Qs[1] * Qs[6] - Qs[0] * Qs[7]; Ai[8] = Qs[0] * Qs[4] - Qs[1] * Qs[3];
-    mat3_mul(Qd, Ai, H);
-    double hmax = 0;
-#pragma unroll
-    for (int i = 0; i < 9; ++i) hmax = fmax(hmax, fabs(H[i]));
-    uncertain |= !(fabs(H[8]) > 1e-9 * hmax);  // also catches NaN
-    const double inv = 1.0 / H[8];
-    float Hf[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) Hf[i] = (float)(H[i] * inv);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) uncertain |= !isfinite(Hf[i]);
-    const int n = S.n;
-    if (uncertain) {
-        bounds[o] = make_int2(0, n);
-        return;
-    }
-    int lo = 0, hi = 0;
-#pragma unroll 4
-    for (int i = 0; i < n; ++i) {
-        const float4 q = P[i];
-        const float W = fmaf(Hf[6], q.x, fmaf(Hf[7], q.y, 1.f));
-        const float ww = __builtin_amdgcn_rcpf(W);
-        const float X = fmaf(Hf[0], q.x, fmaf(Hf[1], q.y, Hf[2]));
-        const float Y = fmaf(Hf[3], q.x, fmaf(Hf[4], q.y, Hf[5]));
-        const float ex = fmaf(X, ww, -q.z), ey = fmaf(Y, ww, -q.w);
-        const float e = fmaf(ex, ex, ey * ey);
-        const float sc = fabsf(q.x) + fabsf(q.y) + fabsf(q.z) + fabsf(q.w);
-        const float d = fmaf(1e-7f * sc, sc, 2.0f);  // margin (px^2) on the reprojection error
-        lo += e < thr2 - d;
-        hi += e <= thr2 + d;
-    }
-    bounds[o] = make_int2(lo, hi);
+    if (act) bounds[o] = invalid ? make_int2(-1, -1) : (uncertain ? make_int2(0, n) : make_int2(lo, hi));
 }
 
 // exact count of one hypothesis (runKernel + computeError + findInliers, bit-exact)
@@ -700,6 +871,7 @@ __global__ __launch_bounds__(64) void ransac_select_filtered_kernel(RansacState*
                                                                     const ProbDev* __restrict__ probs,
                                                                     const float4* __restrict__ pts,
                                                                     const int4* __restrict__ samples,
+                                                                    const uint32_t* __restrict__ stream,
                                                                     const int2* __restrict__ bounds, int c1,
                                                                     double conf, float thr2) {
     __shared__ double sd[kJ9D * 64];
@@ -718,7 +890,8 @@ __global__ __launch_bounds__(64) void ransac_select_filtered_kernel(RansacState*
         if (ncand == 0) return;
         const int t = lane < ncand ? cand[lane] : INT_MAX;
         int ex = -1;
-        if (lane < ncand && t < S.niters) ex = exact_count(P, N, Sm[t], sd + lane, thr2);
+        if (lane < ncand && t < S.niters)
+            ex = exact_count(P, N, decode_sample(Sm[t], stream, (unsigned)N, S.modM), sd + lane, thr2);
         for (;;) {
             const int thr = max(S.max_good, 3);
             const unsigned long long m = __ballot(t < S.niters && ex > thr);
@@ -962,6 +1135,7 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                                                             const float4* __restrict__ pts,
                                                             const int* __restrict__ n_good_arr,
                                                             const int4* __restrict__ samples,
+                                                            const uint32_t* __restrict__ stream,
                                                             float4* __restrict__ inl, uint8_t* __restrict__ masks,
                                                             mim_result* __restrict__ results, RansacParams prm,
                                                             int raw) {
@@ -1002,7 +1176,7 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
         if (ok) {
             // bestModel = runKernel(sample[best_iter]) (bit-identical to the hypo kernel's)
             if (tid == 0) {
-                const int4 s4 = samples[probs[p].it_off + S.best_iter];
+                const int4 s4 = decode_sample(samples[probs[p].it_off + S.best_iter], stream, (unsigned)S.n, S.modM);
                 const float4 a = P[s4.x], b = P[s4.y], c = P[s4.z], d = P[s4.w];
                 const float M[8] = {a.x, a.y, b.x, b.y, c.x, c.y, d.x, d.y};
                 const float m[8] = {a.z, a.w, b.z, b.w, c.z, c.w, d.z, d.w};
@@ -1209,12 +1383,20 @@ void ransac_enqueue(const RansacParams& prm, int n_probs, const ProbDev* probs, 
     const float thr2 = (float)(prm.thresh * prm.thresh);
     while (c0 < max_iters) {
         const int c1 = (int)std::min<long long>((long long)c0 + chunk, max_iters);
-        ransac_sample_kernel<<<n_probs, 64, 0, s>>>(b.state, probs, pts, b.stream, b.stream_len, b.samples, c1, b.err);
+        // attempt outcomes for a window of ~28 draws per wanted iteration (pass rate ~1/5), the walk
+        // falls back to inline evaluation past the window
+        const int wcap = (int)std::min<long long>((long long)(c1 - c0) * 28 + 4096, b.flag_cap / std::max(n_probs, 1));
+        const int bppw = (wcap + 255) / 256;
+        ransac_attempt_kernel<<<n_probs * bppw, 256, 0, s>>>(b.state, probs, pts, b.stream, b.stream_len, b.flags, wcap,
+                                                            bppw, c1);
+        mark(mark_ctx, "attempt");
+        ransac_sample_kernel<<<n_probs, 64, 0, s>>>(b.state, probs, pts, b.stream, b.stream_len, b.samples, c1, b.err,
+                                                    b.flags, wcap);
         mark(mark_ctx, "sample");
         const int bpp256 = (c1 - c0 + 255) / 256;
         if (exact_all) {  // reference mode: every hypothesis through runKernel + computeError
             const int bpp64 = (c1 - c0 + 63) / 64;
-            ransac_hypo_kernel<<<n_probs * bpp64, 64, 0, s>>>(b.state, probs, pts, b.samples, b.hyp, b.counts, c0, c1,
+            ransac_hypo_kernel<<<n_probs * bpp64, 64, 0, s>>>(b.state, probs, pts, b.samples, b.stream, b.hyp, b.counts, c0, c1,
                                                              bpp64);
             mark(mark_ctx, "hypo");
             ransac_score_kernel<<<n_probs * bpp256, 256, 0, s>>>(b.state, probs, pts, b.hyp, b.counts, c0, c1,
@@ -1223,17 +1405,17 @@ void ransac_enqueue(const RansacParams& prm, int n_probs, const ProbDev* probs, 
             ransac_select_kernel<<<n_probs, 64, 0, s>>>(b.state, probs, b.counts, c1, prm.conf);
             mark(mark_ctx, "select");
         } else {
-            ransac_bound_kernel<<<n_probs * bpp256, 256, 0, s>>>(b.state, probs, pts, b.samples, b.bounds, c0, c1,
+            ransac_bound_kernel<<<n_probs * bpp256, 256, 0, s>>>(b.state, probs, pts, b.samples, b.stream, b.bounds, c0, c1,
                                                                 bpp256, thr2);
             mark(mark_ctx, "score");
-            ransac_select_filtered_kernel<<<n_probs, 64, 0, s>>>(b.state, probs, pts, b.samples, b.bounds, c1,
+            ransac_select_filtered_kernel<<<n_probs, 64, 0, s>>>(b.state, probs, pts, b.samples, b.stream, b.bounds, c1,
                                                                 prm.conf, thr2);
             mark(mark_ctx, "select");
         }
         c0 = c1;
         chunk = chunk < (1 << 15) ? chunk * 8 : chunk;
     }
-    ransac_refine_kernel<<<n_probs, kRT, 0, s>>>(b.state, probs, pts, n_good, b.samples, b.inl, masks, results, prm,
+    ransac_refine_kernel<<<n_probs, kRT, 0, s>>>(b.state, probs, pts, n_good, b.samples, b.stream, b.inl, masks, results, prm,
                                                  raw);
     mark(mark_ctx, "refine");
 }

@@ -30,7 +30,7 @@ def _cmp_h(Hg, Ho):
     assert np.max(np.abs(Hg - Ho) / (np.abs(Ho) + 1e-3)) < H_RTOL, (Hg, Ho)
 
 
-@pytest.mark.parametrize("n,w,iters", [(5, 1.0, 2000), (12, 0.8, 2000), (60, 0.5, 2000), (200, 0.3, 2000),
+@pytest.mark.parametrize("n,w,iters", [(5, 1.0, 2000), (6, 0.5, 2000), (7, 0.3, 3000), (9, 0.5, 2000), (12, 0.8, 2000), (60, 0.5, 2000), (200, 0.3, 2000),
                                        (500, 0.15, 2000), (1000, 0.08, 5000), (3000, 0.25, 2000)])
 def test_find_homography_matches_oracle(matcher, oracle, n, w, iters):
     src, dst, _ = _points(n, w, seed=n * 31 + iters)
@@ -204,3 +204,16 @@ def test_filtered_equals_exact_all(oracle):
     for (ha, ma), (hb, mb) in zip(f0, f1):
         np.testing.assert_array_equal(ma, mb)
         assert (ha is None) == (hb is None) and (ha is None or np.array_equal(ha, hb))
+
+
+def test_mostly_degenerate_points(matcher, oracle):
+    """Most 4-subsets collinear: long runs of rejected getSubset attempts, many redraws."""
+    rng = np.random.default_rng(17)
+    src = np.c_[np.arange(40, dtype=np.float32) * 7, np.full(40, 100, np.float32)]   # all on one line
+    src[-3:] = rng.uniform(0, 400, size=(3, 2))                                          # 3 off-line points
+    dst = src * np.float32(1.1) + np.float32(3)
+    for iters in (50, 2000):
+        Hg, mg = matcher.find_homography(src, dst, 5.0, iters, 0.995)
+        ok, Ho, mo = oracle.find_homography(src, dst, 5.0, iters, 0.995)
+        assert (Hg is not None) == bool(ok)
+        np.testing.assert_array_equal(mg, mo)

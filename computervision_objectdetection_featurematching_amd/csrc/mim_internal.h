@@ -82,6 +82,7 @@ struct RansacBufs {
     float* hyp;               // [(it_off + iter) * 8]  (float)H[0..7] of the minimal-sample model
     int* counts;              // [it_off + iter]  inlier count, -1 when runKernel returned 0
     int2* bounds;             // [it_off + iter]  (lower, upper) bound of the count (filtered path)
+    double* best_h;           // [problem][9] bestModel of the filtered select (double H of the best sample)
     uint8_t* flags;           // [problem][window] getSubset attempt outcomes ahead of stream_pos
     long long flag_cap;       // bytes of `flags`
     const uint32_t* stream;   // raw cv::RNG((uint64)-1).next() stream shared by every problem

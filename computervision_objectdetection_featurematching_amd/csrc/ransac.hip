@@ -838,11 +838,10 @@ __global__ __launch_bounds__(256) void ransac_bound_kernel(const RansacState* __
 }
 
 // exact count of one hypothesis (runKernel + computeError + findInliers, bit-exact)
-__device__ int exact_count(const float4* __restrict__ P, int n, int4 s4, double* D, float thr2) {
+__device__ int exact_count(const float4* __restrict__ P, int n, int4 s4, double* D, float thr2, double (&H)[9]) {
     const float4 a = P[s4.x], b = P[s4.y], c = P[s4.z], d = P[s4.w];
     const float M[8] = {a.x, a.y, b.x, b.y, c.x, c.y, d.x, d.y};
     const float m[8] = {a.z, a.w, b.z, b.w, c.z, c.w, d.z, d.w};
-    double H[9];
     if (!run_kernel4<64>(M, m, D, H)) return -1;
     float Hf[8];
 #pragma unroll
@@ -873,7 +872,8 @@ __global__ __launch_bounds__(64) void ransac_select_filtered_kernel(RansacState*
                                                                     const int4* __restrict__ samples,
                                                                     const uint32_t* __restrict__ stream,
                                                                     const int2* __restrict__ bounds, int c1,
-                                                                    double conf, float thr2) {
+                                                                    double conf, float thr2,
+                                                                    double* __restrict__ best_h) {
     __shared__ double sd[kJ9D * 64];
     __shared__ int cand[64];
     const int p = blockIdx.x, lane = threadIdx.x;
@@ -890,8 +890,10 @@ __global__ __launch_bounds__(64) void ransac_select_filtered_kernel(RansacState*
         if (ncand == 0) return;
         const int t = lane < ncand ? cand[lane] : INT_MAX;
         int ex = -1;
+        double H[9];
         if (lane < ncand && t < S.niters)
-            ex = exact_count(P, N, decode_sample(Sm[t], stream, (unsigned)N, S.modM), sd + lane, thr2);
+            ex = exact_count(P, N, decode_sample(Sm[t], stream, (unsigned)N, S.modM), sd + lane, thr2, H);
+        int fbest = -1;
         for (;;) {
             const int thr = max(S.max_good, 3);
             const unsigned long long m = __ballot(t < S.niters && ex > thr);
@@ -901,6 +903,11 @@ __global__ __launch_bounds__(64) void ransac_select_filtered_kernel(RansacState*
             S.max_good = cf;
             S.best_iter = __shfl(t, f);
             S.niters = update_num_iters(conf, (double)(N - cf) / N, 4, S.niters);
+            fbest = f;
+        }
+        if (fbest >= 0 && lane == fbest) {  // keep bestModel: the refine kernel starts from it
+#pragma unroll
+            for (int i = 0; i < 9; ++i) best_h[(long long)p * 9 + i] = H[i];
         }
         ncand = 0;
         __syncthreads();
@@ -1100,6 +1107,49 @@ __device__ void solve_eig8(const double* Ap, const double* b, double* x, double*
     }
 }
 
+// LM step solve.  cv::solve(DECOMP_EIG) applies the pseudo-inverse with eigenvalues below
+// 2*DBL_EPSILON*trace dropped; for the positive-definite systems of a refit on >= 4 points in
+// general position no eigenvalue is dropped and the solution equals the Cholesky one to rounding
+// (the LM contract is |dH| <= 1e-4).  Ill-conditioned systems fall back to the Jacobi path.
+__device__ bool solve_chol8(const double* A, const double* b, double* x) {
+    double L[8][8];
+    double dmax = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) dmax = fmax(dmax, fabs(A[9 * i]));
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        double sjj = A[9 * j];
+#pragma unroll
+        for (int k = 0; k < j; ++k) sjj -= L[j][k] * L[j][k];
+        if (!(sjj > 1e-12 * dmax)) return false;
+        const double ljj = sqrt(sjj);
+        L[j][j] = ljj;
+#pragma unroll
+        for (int i = j + 1; i < 8; ++i) {
+            double sij = A[8 * i + j];
+#pragma unroll
+            for (int k = 0; k < j; ++k) sij -= L[i][k] * L[j][k];
+            L[i][j] = sij / ljj;
+        }
+    }
+    double y[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        double si = b[i];
+#pragma unroll
+        for (int k = 0; k < i; ++k) si -= L[i][k] * y[k];
+        y[i] = si / L[i][i];
+    }
+#pragma unroll
+    for (int i = 7; i >= 0; --i) {
+        double si = y[i];
+#pragma unroll
+        for (int k = i + 1; k < 8; ++k) si -= L[k][i] * x[k];
+        x[i] = si / L[i][i];
+    }
+    return true;
+}
+
 __device__ double inv_diag_max8(const double* A, double* J) {
     double w[8], V[64];
     eig8(A, J, w, V);
@@ -1138,7 +1188,7 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                                                             const uint32_t* __restrict__ stream,
                                                             float4* __restrict__ inl, uint8_t* __restrict__ masks,
                                                             mim_result* __restrict__ results, RansacParams prm,
-                                                            int raw) {
+                                                            int raw, const double* __restrict__ best_h, int exact_all) {
     __shared__ RefineShared sh;
     const int p = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const RansacState S = st[p];
@@ -1175,7 +1225,9 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
         res.iters = (S.fail_iter >= 0 && S.fail_iter < S.niters) ? S.fail_iter : S.niters;
         if (ok) {
             // bestModel = runKernel(sample[best_iter]) (bit-identical to the hypo kernel's)
-            if (tid == 0) {
+            if (tid == 0 && !exact_all) {
+                for (int i = 0; i < 9; ++i) sh.Hb[i] = best_h[(long long)p * 9 + i];  // from the select kernel
+            } else if (tid == 0) {
                 const int4 s4 = decode_sample(samples[probs[p].it_off + S.best_iter], stream, (unsigned)S.n, S.modM);
                 const float4 a = P[s4.x], b = P[s4.y], c = P[s4.z], d = P[s4.w];
                 const float M[8] = {a.x, a.y, b.x, b.y, c.x, c.y, d.x, d.y};
@@ -1275,7 +1327,7 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                         double Ap[64];
                         for (int i = 0; i < 64; ++i) Ap[i] = sh.A[i];
                         for (int i = 0; i < 8; ++i) Ap[9 * i] += sh.lambda * sh.D[i];
-                        solve_eig8(Ap, sh.v, sh.d, sh.J9);
+                        if (!solve_chol8(Ap, sh.v, sh.d)) solve_eig8(Ap, sh.v, sh.d, sh.J9);
                         double dinf = 0;
                         for (int i = 0; i < 8; ++i) {
                             sh.xd[i] = sh.x[i] - sh.d[i];
@@ -1379,7 +1431,7 @@ void ransac_enqueue(const RansacParams& prm, int n_probs, const ProbDev* probs, 
     if (n_probs <= 0) return;
     ransac_init_kernel<<<(n_probs + 255) / 256, 256, 0, s>>>(b.state, n_good, n_probs, prm.max_iters, prm.min_good);
     const int max_iters = prm.max_iters > 1 ? prm.max_iters : 1;
-    int c0 = 0, chunk = 1024;
+    int c0 = 0, chunk = 2048;
     const float thr2 = (float)(prm.thresh * prm.thresh);
     while (c0 < max_iters) {
         const int c1 = (int)std::min<long long>((long long)c0 + chunk, max_iters);
@@ -1409,14 +1461,14 @@ void ransac_enqueue(const RansacParams& prm, int n_probs, const ProbDev* probs, 
                                                                 bpp256, thr2);
             mark(mark_ctx, "score");
             ransac_select_filtered_kernel<<<n_probs, 64, 0, s>>>(b.state, probs, pts, b.samples, b.stream, b.bounds, c1,
-                                                                prm.conf, thr2);
+                                                                prm.conf, thr2, b.best_h);
             mark(mark_ctx, "select");
         }
         c0 = c1;
-        chunk = chunk < (1 << 15) ? chunk * 8 : chunk;
+        chunk = chunk < (1 << 15) ? chunk * 16 : chunk;
     }
     ransac_refine_kernel<<<n_probs, kRT, 0, s>>>(b.state, probs, pts, n_good, b.samples, b.stream, b.inl, masks, results, prm,
-                                                 raw);
+                                                 raw, b.best_h, exact_all);
     mark(mark_ctx, "refine");
 }
 

@@ -96,7 +96,7 @@ struct SetRec {
 namespace mim {
 // RANSAC workspace (definition shared with ransac.hip through this layout)
 struct RansacWs {
-    DevBuf state, samples, hyp, counts, bounds, flags, best_h, stream, scratch, inl, err;
+    DevBuf state, samples, hyp, counts, bounds, flags, best_h, cand, ncand, cex, cH, stream, scratch, inl, err;
     long long stream_len = 0;
 };
 }  // namespace mim
@@ -185,7 +185,7 @@ void mim_ctx_destroy(mim_ctx* c) {
     c->arena.release();
     for (DevBuf* b : {&c->probs, &c->works, &c->parts, &c->good_q, &c->good_t, &c->pts, &c->n_good,
                       &c->results, &c->masks, &c->knn_idx, &c->knn_dist, &c->rws.state, &c->rws.samples,
-                      &c->rws.hyp, &c->rws.counts, &c->rws.bounds, &c->rws.flags, &c->rws.best_h, &c->rws.stream, &c->rws.scratch, &c->rws.inl, &c->rws.err})
+                      &c->rws.hyp, &c->rws.counts, &c->rws.bounds, &c->rws.flags, &c->rws.best_h, &c->rws.cand, &c->rws.ncand, &c->rws.cex, &c->rws.cH, &c->rws.stream, &c->rws.scratch, &c->rws.inl, &c->rws.err})
         b->release();
     if (c->own) (void)hipStreamDestroy(c->own);
     delete c;
@@ -532,6 +532,11 @@ static mim_status ransac_locked(mim_ctx* c, int n, const mim_params* prm, int ra
     const long long flag_cap = (long long)std::max(n, 1) * (chunk_max * 28 + 4096);
     HIPCHK(c, c->rws.flags.ensure((size_t)flag_cap));
     HIPCHK(c, c->rws.best_h.ensure(sizeof(double) * 9 * std::max(n, 1)));
+    const size_t cap = (size_t)std::max(n, 1) * 1024;  // kCandCap per problem
+    HIPCHK(c, c->rws.cand.ensure(sizeof(int) * cap));
+    HIPCHK(c, c->rws.ncand.ensure(sizeof(int) * std::max(n, 1)));
+    HIPCHK(c, c->rws.cex.ensure(sizeof(int) * cap));
+    HIPCHK(c, c->rws.cH.ensure(sizeof(double) * 9 * cap));
     HIPCHK(c, c->rws.inl.ensure(sizeof(float4) * good_total));
     HIPCHK(c, c->rws.err.ensure(sizeof(int) * 4));
     HIPCHK(c, c->results.ensure(sizeof(mim_result) * std::max(n, 1)));
@@ -545,6 +550,10 @@ static mim_status ransac_locked(mim_ctx* c, int n, const mim_params* prm, int ra
     b.bounds = c->rws.bounds.as<int2>();
     b.flags = c->rws.flags.as<uint8_t>();
     b.best_h = c->rws.best_h.as<double>();
+    b.cand = c->rws.cand.as<int>();
+    b.ncand = c->rws.ncand.as<int>();
+    b.cex = c->rws.cex.as<int>();
+    b.cH = c->rws.cH.as<double>();
     b.flag_cap = flag_cap;
     b.stream = c->rws.stream.as<uint32_t>();
     b.stream_len = c->rws.stream_len;

@@ -83,6 +83,10 @@ struct RansacBufs {
     int* counts;              // [it_off + iter]  inlier count, -1 when runKernel returned 0
     int2* bounds;             // [it_off + iter]  (lower, upper) bound of the count (filtered path)
     double* best_h;           // [problem][9] bestModel of the filtered select (double H of the best sample)
+    int* cand;                // [problem][kCandCap] candidate iterations of the current chunk
+    int* ncand;               // [problem] candidates listed (may exceed the capacity)
+    int* cex;                 // [problem][kCandCap] their exact inlier counts
+    double* cH;               // [problem][kCandCap][9] their exact models
     uint8_t* flags;           // [problem][window] getSubset attempt outcomes ahead of stream_pos
     long long flag_cap;       // bytes of `flags`
     const uint32_t* stream;   // raw cv::RNG((uint64)-1).next() stream shared by every problem

@@ -22,6 +22,9 @@
 
 #include <algorithm>
 #include <climits>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
 
 #include "../../include/mim.h"
 #include "mim_internal.h"
@@ -866,6 +869,148 @@ __device__ __forceinline__ int wave_excl_prefix_max(int v) {
     return lane == 0 ? INT_MIN : ex;
 }
 
+// Split form of the filtered select (default): candidates of every problem are listed first,
+// evaluated exactly by a GPU-wide grid (one lane each), then replayed in order per problem.
+constexpr int kCandWaves = 16;                 // exact-evaluation waves per problem and chunk
+constexpr int kCandCap = kCandWaves * 64;      // listed candidates per problem and chunk
+
+__global__ __launch_bounds__(64) void ransac_cand_kernel(RansacState* __restrict__ st,
+                                                         const ProbDev* __restrict__ probs,
+                                                         const int2* __restrict__ bounds, int c1,
+                                                         int* __restrict__ cand, int* __restrict__ ncand) {
+    const int p = blockIdx.x, lane = threadIdx.x;
+    RansacState S = st[p];
+    int nc_total = 0;
+    if (S.active && !S.done) {
+        const int2* Bd = bounds + probs[p].it_off;
+        const int end = min(c1, S.produced);
+        int* C = cand + (long long)p * kCandCap;
+        for (int base = S.next_iter; base < end && base < S.niters; base += 64) {
+            const int t = base + lane;
+            const bool valid = t < end;
+            const int2 b = valid ? Bd[t] : make_int2(-1, -1);
+            const int lb = max(max(3, max(S.max_good, S.lo_max)), wave_excl_prefix_max(b.x));
+            const bool c = valid && t < S.niters && b.y > lb;
+            S.lo_max = max(S.lo_max, wave_max(b.x));
+            const unsigned long long cm = __ballot(c);
+            const int pos = __builtin_amdgcn_mbcnt_hi((uint32_t)(cm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)cm, 0));
+            if (c) {
+                // beyond the list capacity the replay kernel evaluates inline (marked by -t-1)
+                if (nc_total + pos < kCandCap) C[nc_total + pos] = t;
+            }
+            nc_total += __popcll(cm);
+        }
+    }
+    if (lane == 0) {
+        ncand[p] = nc_total;
+        st[p].lo_max = S.lo_max;
+    }
+}
+
+__global__ __launch_bounds__(64) void ransac_exact_kernel(const RansacState* __restrict__ st,
+                                                          const ProbDev* __restrict__ probs,
+                                                          const float4* __restrict__ pts,
+                                                          const int4* __restrict__ samples,
+                                                          const uint32_t* __restrict__ stream,
+                                                          const int* __restrict__ cand, const int* __restrict__ ncand,
+                                                          int* __restrict__ cex, double* __restrict__ cH, float thr2) {
+    __shared__ double sd[kJ9D * 64];
+    // problem-minor block order: the first (and usually only) busy wave of every problem comes
+    // first and lands on all 8 XCDs (blocks b and b+8 share an XCD under round-robin dispatch)
+    const int np = gridDim.x / kCandWaves;
+    const int p = blockIdx.x % np, w = blockIdx.x / np, lane = threadIdx.x;
+    const RansacState S = st[p];
+    if (!S.active || S.done) return;
+    const int nc = min(ncand[p], kCandCap);
+    const int k = w * 64 + lane;
+    if (w * 64 >= nc) return;
+    if (k >= nc) return;
+    const int t = cand[(long long)p * kCandCap + k];
+    double H[9];
+    const int ex = exact_count(pts + probs[p].good_off, S.n,
+                               decode_sample(samples[probs[p].it_off + t], stream, (unsigned)S.n, S.modM), sd + lane,
+                               thr2, H);
+    const long long o = (long long)p * kCandCap + k;
+    cex[o] = ex;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) cH[o * 9 + i] = H[i];
+}
+
+__global__ __launch_bounds__(64) void ransac_replay_kernel(RansacState* __restrict__ st,
+                                                           const ProbDev* __restrict__ probs,
+                                                           const float4* __restrict__ pts,
+                                                           const int4* __restrict__ samples,
+                                                           const uint32_t* __restrict__ stream,
+                                                           const int2* __restrict__ bounds, const int* __restrict__ cand,
+                                                           const int* __restrict__ ncand, const int* __restrict__ cex,
+                                                           const double* __restrict__ cH, int c1, double conf,
+                                                           float thr2, double* __restrict__ best_h) {
+    __shared__ double sd[kJ9D * 64];
+    const int p = blockIdx.x, lane = threadIdx.x;
+    RansacState S = st[p];
+    if (!S.active || S.done) return;
+    const int end = min(c1, S.produced);
+    const int N = S.n;
+    const int nc = ncand[p];
+    const int* C = cand + (long long)p * kCandCap;
+    const int* E = cex + (long long)p * kCandCap;
+    const double* HH = cH + (long long)p * kCandCap * 9;
+    int best_k = -1;  // candidate index whose H becomes bestModel (listed part)
+    for (int k0 = 0; k0 < min(nc, kCandCap); k0 += 64) {
+        const int k = k0 + lane;
+        const bool in = k < min(nc, kCandCap);
+        const int t = in ? C[k] : INT_MAX;
+        const int ex = in ? E[k] : -1;
+        for (;;) {
+            const int thr = max(S.max_good, 3);
+            const unsigned long long m = __ballot(t < S.niters && ex > thr);
+            if (!m) break;
+            const int f = __ffsll((long long)m) - 1;
+            S.max_good = __shfl(ex, f);
+            S.best_iter = __shfl(t, f);
+            S.niters = update_num_iters(conf, (double)(N - S.max_good) / N, 4, S.niters);
+            best_k = k0 + f;
+        }
+    }
+    if (best_k >= 0 && lane < 9) best_h[(long long)p * 9 + lane] = HH[(long long)best_k * 9 + lane];
+    if (nc > kCandCap) {
+        // overflow (very many candidates): rescan the iterations after the last listed one and
+        // evaluate their candidates here, 64 at a time, with the running exact best
+        const int2* Bd = bounds + probs[p].it_off;
+        const float4* __restrict__ P = pts + probs[p].good_off;
+        const int4* Sm = samples + probs[p].it_off;
+        const int start = C[kCandCap - 1] + 1;
+        for (int base = start; base < end && base < S.niters; base += 64) {
+            const int t = base + lane;
+            const bool valid = t < end;
+            const int2 b = valid ? Bd[t] : make_int2(-1, -1);
+            const bool c = valid && t < S.niters && b.y > max(S.max_good, 3);
+            int ex = -1;
+            double H[9];
+            if (__any(c)) {
+                if (c) ex = exact_count(P, N, decode_sample(Sm[t], stream, (unsigned)N, S.modM), sd + lane, thr2, H);
+            }
+            int fbest = -1;
+            for (;;) {
+                const int thr = max(S.max_good, 3);
+                const unsigned long long m = __ballot(c && t < S.niters && ex > thr);
+                if (!m) break;
+                const int f = __ffsll((long long)m) - 1;
+                S.max_good = __shfl(ex, f);
+                S.best_iter = __shfl(t, f);
+                S.niters = update_num_iters(conf, (double)(N - S.max_good) / N, 4, S.niters);
+                fbest = f;
+            }
+            if (fbest >= 0 && lane == fbest)
+                for (int i = 0; i < 9; ++i) best_h[(long long)p * 9 + i] = H[i];
+        }
+    }
+    S.next_iter = end;
+    const bool failed = S.fail_iter != -1 && S.produced <= end;
+    if (S.niters <= end || failed) S.done = 1;
+    if (lane == 0) st[p] = S;
+}
+
 __global__ __launch_bounds__(64) void ransac_select_filtered_kernel(RansacState* __restrict__ st,
                                                                     const ProbDev* __restrict__ probs,
                                                                     const float4* __restrict__ pts,
@@ -1112,21 +1257,25 @@ __device__ void solve_eig8(const double* Ap, const double* b, double* x, double*
 // general position no eigenvalue is dropped and the solution equals the Cholesky one to rounding
 // (the LM contract is |dH| <= 1e-4).  Ill-conditioned systems fall back to the Jacobi path.
 __device__ bool solve_chol8(const double* A, const double* b, double* x) {
-    double L[8][8];
-    double dmax = 0;
+    // symmetric diagonal scaling first (unit diagonal): J^T J of a homography spans ~1e13
+    double sc[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) dmax = fmax(dmax, fabs(A[9 * i]));
+    for (int i = 0; i < 8; ++i) {
+        if (!(A[9 * i] > 0)) return false;
+        sc[i] = 1.0 / sqrt(A[9 * i]);
+    }
+    double L[8][8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-        double sjj = A[9 * j];
+        double sjj = 1.0;
 #pragma unroll
         for (int k = 0; k < j; ++k) sjj -= L[j][k] * L[j][k];
-        if (!(sjj > 1e-12 * dmax)) return false;
+        if (!(sjj > 1e-10)) return false;
         const double ljj = sqrt(sjj);
         L[j][j] = ljj;
 #pragma unroll
         for (int i = j + 1; i < 8; ++i) {
-            double sij = A[8 * i + j];
+            double sij = A[8 * i + j] * sc[i] * sc[j];
 #pragma unroll
             for (int k = 0; k < j; ++k) sij -= L[i][k] * L[j][k];
             L[i][j] = sij / ljj;
@@ -1135,18 +1284,21 @@ __device__ bool solve_chol8(const double* A, const double* b, double* x) {
     double y[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-        double si = b[i];
+        double si = b[i] * sc[i];
 #pragma unroll
         for (int k = 0; k < i; ++k) si -= L[i][k] * y[k];
         y[i] = si / L[i][i];
     }
+    double z[8];
 #pragma unroll
     for (int i = 7; i >= 0; --i) {
         double si = y[i];
 #pragma unroll
-        for (int k = i + 1; k < 8; ++k) si -= L[k][i] * x[k];
-        x[i] = si / L[i][i];
+        for (int k = i + 1; k < 8; ++k) si -= L[k][i] * z[k];
+        z[i] = si / L[i][i];
     }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) x[i] = z[i] * sc[i];
     return true;
 }
 
@@ -1460,8 +1612,21 @@ void ransac_enqueue(const RansacParams& prm, int n_probs, const ProbDev* probs, 
             ransac_bound_kernel<<<n_probs * bpp256, 256, 0, s>>>(b.state, probs, pts, b.samples, b.stream, b.bounds, c0, c1,
                                                                 bpp256, thr2);
             mark(mark_ctx, "score");
-            ransac_select_filtered_kernel<<<n_probs, 64, 0, s>>>(b.state, probs, pts, b.samples, b.stream, b.bounds, c1,
-                                                                prm.conf, thr2, b.best_h);
+            ransac_cand_kernel<<<n_probs, 64, 0, s>>>(b.state, probs, b.bounds, c1, b.cand, b.ncand);
+            mark(mark_ctx, "cand");
+            if (getenv("MIM_DEBUG_NCAND")) {
+                std::vector<int> h(n_probs);
+                (void)hipMemcpyAsync(h.data(), b.ncand, sizeof(int) * n_probs, hipMemcpyDeviceToHost, s);
+                (void)hipStreamSynchronize(s);
+                long long sum = 0; int mx = 0;
+                for (int v : h) { sum += v; mx = std::max(mx, v); }
+                fprintf(stderr, "[mim] chunk [%d,%d): candidates mean %.1f max %d\n", c0, c1, (double)sum / n_probs, mx);
+            }
+            ransac_exact_kernel<<<n_probs * kCandWaves, 64, 0, s>>>(b.state, probs, pts, b.samples, b.stream, b.cand,
+                                                                   b.ncand, b.cex, b.cH, thr2);
+            mark(mark_ctx, "exact");
+            ransac_replay_kernel<<<n_probs, 64, 0, s>>>(b.state, probs, pts, b.samples, b.stream, b.bounds, b.cand,
+                                                        b.ncand, b.cex, b.cH, c1, prm.conf, thr2, b.best_h);
             mark(mark_ctx, "select");
         }
         c0 = c1;

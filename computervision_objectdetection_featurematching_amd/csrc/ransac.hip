@@ -413,7 +413,7 @@ __device__ __forceinline__ int4 decode_sample(int4 s, const uint32_t* __restrict
 // init: per-problem RANSAC state from the ratio-test survivors
 // ------------------------------------------------------------------------------------------------
 __global__ void ransac_init_kernel(RansacState* __restrict__ st, const int* __restrict__ n_good, int n_probs,
-                                   int max_iters, int min_good) {
+                                   int max_iters, int min_good, double* __restrict__ best_h) {
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= n_probs) return;
     RansacState S{};
@@ -424,6 +424,7 @@ __global__ void ransac_init_kernel(RansacState* __restrict__ st, const int* __re
     S.fail_iter = -1;
     S.best_iter = -1;
     st[p] = S;
+    best_h[(long long)p * 9 + 8] = 0.0;  // "not computed" until an exact pass stores bestModel
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -741,9 +742,26 @@ __device__ __forceinline__ double min_rel_area(const double* x, const double* y)
     return d2 > 0 ? m / d2 : 0.0;
 }
 
-constexpr double kScreenArea = 1e-5;  // samples less conditioned than this are evaluated exactly
+// Conditioning screen of the closed-form bound (rho = min relative triangle area of the sample).
+// Model of the disagreement between the closed form and OpenCV's normalized-DLT eigenvector:
+// eta ~ eps * kappa^2 with kappa ~ 1/rho (normal equations), taken ~100x larger: eta = 1e-14/rho^2.
+// A relative model error eta moves a reprojection error e <= 25.5 px^2 by <= 10.2*eta*s + (eta*s)^2
+// (s = |x|+|y|+|u|+|v| of the point).  The base margin 0.5 + 1e-7 s^2 (which also absorbs the fp32
+// rounding of both error evaluations) dominates 10.2*eta*s for every s once eta <= 4.4e-5, i.e.
+//   rho >= 2e-5        base margin only
+//   1e-7 <= rho < 2e-5 margin widened by 10.2*eta*s + (eta*s)^2 (rare: ~6e-4 of random samples)
+//   rho < 1e-7         no bound: [0, N] (the iteration is evaluated exactly)
+constexpr double kScreenArea = 1e-7;
+constexpr double kScreenTight = 2e-5;
 
-constexpr int kBoundTile = 1024;  // points per LDS tile of the bound kernel (16 KiB + 8 KiB)
+constexpr int kBoundTile = 1024;  // points per LDS tile of the bound kernel (24 KiB: 6 blocks per CU)
+
+// The bound kernel evaluates two points per lane and instruction with packed fp32 (v_pk_fma_f32,
+// v_pk_mul_f32): points are staged in LDS as pairs {x0,x1,y0,y1} {-u0,-u1,-v0,-v1} {lo0,lo1,hi0,hi1}.
+// The reprojection test runs division-free: |(X,Y) - W (u,v)|^2 against thr * W^2.
+typedef float f2v __attribute__((ext_vector_type(2)));
+typedef float f4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ f2v pk_fma(f2v a, f2v b, f2v c) { return __builtin_elementwise_fma(a, b, c); }
 
 __global__ __launch_bounds__(256) void ransac_bound_kernel(const RansacState* __restrict__ st,
                                                            const ProbDev* __restrict__ probs,
@@ -752,8 +770,7 @@ __global__ __launch_bounds__(256) void ransac_bound_kernel(const RansacState* __
                                                            const uint32_t* __restrict__ stream,
                                                            int2* __restrict__ bounds, int c0, int c1, int bpp,
                                                            float thr2) {
-    __shared__ float4 tp[kBoundTile];
-    __shared__ float2 tt[kBoundTile];
+    __shared__ f4v tp[3 * (kBoundTile / 2)];
     const int p = blockIdx.x / bpp;
     const int it = c0 + (blockIdx.x % bpp) * 256 + threadIdx.x;
     const RansacState S = st[p];
@@ -764,6 +781,7 @@ __global__ __launch_bounds__(256) void ransac_bound_kernel(const RansacState* __
     const float4* __restrict__ P = pts + probs[p].good_off;
     const int n = S.n;
     bool uncertain = false, invalid = false;
+    float eta = 0.f;  // widened-margin coefficient for poorly conditioned samples
     float Hf[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (act) {
         const int4 s4 = decode_sample(samples[o], stream, (unsigned)n, S.modM);
@@ -787,7 +805,9 @@ __global__ __launch_bounds__(256) void ransac_bound_kernel(const RansacState* __
                   fabs(sMy) < DBL_EPSILON;
         const double sx[4] = {q0.x, q1.x, q2.x, q3.x}, sy[4] = {q0.y, q1.y, q2.y, q3.y};
         const double dx[4] = {q0.z, q1.z, q2.z, q3.z}, dy[4] = {q0.w, q1.w, q2.w, q3.w};
-        uncertain = min_rel_area(sx, sy) < kScreenArea || min_rel_area(dx, dy) < kScreenArea;
+        const double rho = fmin(min_rel_area(sx, sy), min_rel_area(dx, dy));
+        uncertain = !(rho >= kScreenArea);
+        if (rho < kScreenTight) eta = (float)(1e-14 / (rho * rho));
         double Qs[9], Qd[9], Ai[9], H[9];
         square_to_quad(sx, sy, Qs);
         square_to_quad(dx, dy, Qd);
@@ -807,33 +827,59 @@ __global__ __launch_bounds__(256) void ransac_bound_kernel(const RansacState* __
         for (int i = 0; i < 8; ++i) uncertain |= !isfinite(Hf[i]);
     }
     const bool count = act && !invalid && !uncertain;
-    // points stream through LDS tiles (broadcast reads); per-point margins computed at staging:
-    // err bound 2 px^2 + 1e-7 (|x|+|y|+|u|+|v|)^2 around the squared threshold
+    // per-point margins computed at staging: err bound 0.5 px^2 + 1e-7 (|x|+|y|+|u|+|v|)^2 around the
+    // squared threshold (+ the widening for poorly conditioned samples)
+    const float k1 = 10.2f * eta, k2 = eta * eta;
+    const bool widen = __any(eta > 0.f);  // rare (~4e-2 of waves): the wave takes the widened loop
+    const f2v h0 = Hf[0], h1 = Hf[1], h2 = Hf[2], h3 = Hf[3], h4 = Hf[4], h5 = Hf[5], h6 = Hf[6], h7 = Hf[7];
     int lo = 0, hi = 0;
     for (int b0 = 0; b0 < n; b0 += kBoundTile) {
         const int tn = min(kBoundTile, n - b0);
+        const int tpairs = (tn + 1) >> 1;
         __syncthreads();
-        for (int i = threadIdx.x; i < tn; i += 256) {
-            const float4 q = P[b0 + i];
-            const float sc = fabsf(q.x) + fabsf(q.y) + fabsf(q.z) + fabsf(q.w);
-            const float d = fmaf(1e-7f * sc, sc, 2.0f);
-            tp[i] = q;
-            tt[i] = make_float2(thr2 - d, thr2 + d);
+        for (int i = threadIdx.x; i < tpairs; i += 256) {
+            const float4 q0 = P[b0 + 2 * i];
+            // odd tail: a point at the origin with negative thresholds never counts
+            const bool has1 = 2 * i + 1 < tn;
+            const float4 q1 = has1 ? P[b0 + 2 * i + 1] : make_float4(0.f, 0.f, 0.f, 0.f);
+            const float s0 = fabsf(q0.x) + fabsf(q0.y) + fabsf(q0.z) + fabsf(q0.w);
+            const float s1 = fabsf(q1.x) + fabsf(q1.y) + fabsf(q1.z) + fabsf(q1.w);
+            const float d0 = fmaf(1e-7f * s0, s0, 0.5f), d1 = fmaf(1e-7f * s1, s1, 0.5f);
+            tp[3 * i] = f4v{q0.x, q1.x, q0.y, q1.y};
+            tp[3 * i + 1] = f4v{-q0.z, -q1.z, -q0.w, -q1.w};
+            tp[3 * i + 2] = has1 ? f4v{thr2 - d0, thr2 - d1, thr2 + d0, thr2 + d1}
+                                 : f4v{thr2 - d0, -1.f, thr2 + d0, -1.f};
         }
         __syncthreads();
-        if (count) {
+        if (count && !widen) {
 #pragma unroll 4
-            for (int i = 0; i < tn; ++i) {
-                const float4 q = tp[i];
-                const float2 th = tt[i];
-                const float W = fmaf(Hf[6], q.x, fmaf(Hf[7], q.y, 1.f));
-                const float ww = __builtin_amdgcn_rcpf(W);
-                const float X = fmaf(Hf[0], q.x, fmaf(Hf[1], q.y, Hf[2]));
-                const float Y = fmaf(Hf[3], q.x, fmaf(Hf[4], q.y, Hf[5]));
-                const float ex = fmaf(X, ww, -q.z), ey = fmaf(Y, ww, -q.w);
-                const float e = fmaf(ex, ex, ey * ey);
-                lo += e < th.x;
-                hi += e <= th.y;
+            for (int i = 0; i < tpairs; ++i) {
+                const f4v a = tp[3 * i], m = tp[3 * i + 1], t = tp[3 * i + 2];
+                const f2v x = a.xy, y = a.zw;
+                const f2v W = pk_fma(h6, x, pk_fma(h7, y, f2v(1.f)));
+                const f2v ex = pk_fma(m.xy, W, pk_fma(h0, x, pk_fma(h1, y, h2)));
+                const f2v ey = pk_fma(m.zw, W, pk_fma(h3, x, pk_fma(h4, y, h5)));
+                const f2v e = pk_fma(ex, ex, ey * ey);
+                const f2v W2 = W * W;
+                const f2v L = t.xy * W2, U = t.zw * W2;
+                lo += (e.x < L.x) + (e.y < L.y);
+                hi += (e.x <= U.x) + (e.y <= U.y);
+            }
+        } else if (count) {
+            for (int i = 0; i < tpairs; ++i) {
+                const f4v a = tp[3 * i], m = tp[3 * i + 1], t = tp[3 * i + 2];
+                const f2v x = a.xy, y = a.zw;
+                const f2v W = pk_fma(h6, x, pk_fma(h7, y, f2v(1.f)));
+                const f2v ex = pk_fma(m.xy, W, pk_fma(h0, x, pk_fma(h1, y, h2)));
+                const f2v ey = pk_fma(m.zw, W, pk_fma(h3, x, pk_fma(h4, y, h5)));
+                const f2v e = pk_fma(ex, ex, ey * ey);
+                const f2v W2 = W * W;
+                const f2v sc = {fabsf(a.x) + fabsf(a.z) + fabsf(m.x) + fabsf(m.z),
+                                fabsf(a.y) + fabsf(a.w) + fabsf(m.y) + fabsf(m.w)};
+                const f2v wid = sc * pk_fma(f2v(k2), sc, f2v(k1));
+                const f2v L = (t.xy - wid) * W2, U = (t.zw + wid) * W2;
+                lo += (e.x < L.x) + (e.y < L.y);
+                hi += (e.x <= U.x) + (e.y <= U.y);
             }
         }
     }
@@ -913,6 +959,7 @@ __global__ __launch_bounds__(64) void ransac_exact_kernel(const RansacState* __r
                                                           const int4* __restrict__ samples,
                                                           const uint32_t* __restrict__ stream,
                                                           const int* __restrict__ cand, const int* __restrict__ ncand,
+                                                          const int2* __restrict__ bounds,
                                                           int* __restrict__ cex, double* __restrict__ cH, float thr2) {
     __shared__ double sd[kJ9D * 64];
     // problem-minor block order: the first (and usually only) busy wave of every problem comes
@@ -926,11 +973,17 @@ __global__ __launch_bounds__(64) void ransac_exact_kernel(const RansacState* __r
     if (w * 64 >= nc) return;
     if (k >= nc) return;
     const int t = cand[(long long)p * kCandCap + k];
+    const long long o = (long long)p * kCandCap + k;
+    const int2 b = bounds[probs[p].it_off + t];
+    if (b.x == b.y) {  // lo == hi pins the exact count: no eigensolve needed
+        cex[o] = b.x;
+        cH[o * 9 + 8] = 0.0;  // H not computed (H22 of a computed model is never 0)
+        return;
+    }
     double H[9];
     const int ex = exact_count(pts + probs[p].good_off, S.n,
                                decode_sample(samples[probs[p].it_off + t], stream, (unsigned)S.n, S.modM), sd + lane,
                                thr2, H);
-    const long long o = (long long)p * kCandCap + k;
     cex[o] = ex;
 #pragma unroll
     for (int i = 0; i < 9; ++i) cH[o * 9 + i] = H[i];
@@ -1377,9 +1430,9 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
         res.iters = (S.fail_iter >= 0 && S.fail_iter < S.niters) ? S.fail_iter : S.niters;
         if (ok) {
             // bestModel = runKernel(sample[best_iter]) (bit-identical to the hypo kernel's)
-            if (tid == 0 && !exact_all) {
-                for (int i = 0; i < 9; ++i) sh.Hb[i] = best_h[(long long)p * 9 + i];  // from the select kernel
-            } else if (tid == 0) {
+            if (tid == 0 && !exact_all && best_h[(long long)p * 9 + 8] != 0.0) {
+                for (int i = 0; i < 9; ++i) sh.Hb[i] = best_h[(long long)p * 9 + i];  // from the exact pass
+            } else if (tid == 0) {  // bestModel = runKernel(sample[best_iter]), bit-identical
                 const int4 s4 = decode_sample(samples[probs[p].it_off + S.best_iter], stream, (unsigned)S.n, S.modM);
                 const float4 a = P[s4.x], b = P[s4.y], c = P[s4.z], d = P[s4.w];
                 const float M[8] = {a.x, a.y, b.x, b.y, c.x, c.y, d.x, d.y};
@@ -1581,9 +1634,10 @@ void ransac_enqueue(const RansacParams& prm, int n_probs, const ProbDev* probs, 
                     const int* n_good, const RansacBufs& b, uint8_t* masks, mim_result* results, int raw,
                     hipStream_t s, void (*mark)(void*, const char*), void* mark_ctx, int exact_all) {
     if (n_probs <= 0) return;
-    ransac_init_kernel<<<(n_probs + 255) / 256, 256, 0, s>>>(b.state, n_good, n_probs, prm.max_iters, prm.min_good);
+    ransac_init_kernel<<<(n_probs + 255) / 256, 256, 0, s>>>(b.state, n_good, n_probs, prm.max_iters, prm.min_good,
+                                                             b.best_h);
     const int max_iters = prm.max_iters > 1 ? prm.max_iters : 1;
-    int c0 = 0, chunk = 2048;
+    int c0 = 0, chunk = 4096;
     const float thr2 = (float)(prm.thresh * prm.thresh);
     while (c0 < max_iters) {
         const int c1 = (int)std::min<long long>((long long)c0 + chunk, max_iters);
@@ -1623,14 +1677,14 @@ void ransac_enqueue(const RansacParams& prm, int n_probs, const ProbDev* probs, 
                 fprintf(stderr, "[mim] chunk [%d,%d): candidates mean %.1f max %d\n", c0, c1, (double)sum / n_probs, mx);
             }
             ransac_exact_kernel<<<n_probs * kCandWaves, 64, 0, s>>>(b.state, probs, pts, b.samples, b.stream, b.cand,
-                                                                   b.ncand, b.cex, b.cH, thr2);
+                                                                   b.ncand, b.bounds, b.cex, b.cH, thr2);
             mark(mark_ctx, "exact");
             ransac_replay_kernel<<<n_probs, 64, 0, s>>>(b.state, probs, pts, b.samples, b.stream, b.bounds, b.cand,
                                                         b.ncand, b.cex, b.cH, c1, prm.conf, thr2, b.best_h);
             mark(mark_ctx, "select");
         }
         c0 = c1;
-        chunk = chunk < (1 << 15) ? chunk * 16 : chunk;
+        chunk = 1 << 30;  // one chunk after the first: every chunk costs a latency-bound exact pass
     }
     ransac_refine_kernel<<<n_probs, kRT, 0, s>>>(b.state, probs, pts, n_good, b.samples, b.stream, b.inl, masks, results, prm,
                                                  raw, b.best_h, exact_all);

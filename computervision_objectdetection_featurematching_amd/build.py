@@ -15,6 +15,8 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 # x86-64 build has no FMA), see DESIGN.md "Floating-point contract".
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-Wall",
          "-Wno-unused-result", "-Wno-unused-function"]
+# extra defines for diagnostic builds (e.g. MIM_EXTRA_FLAGS=-DMIM_SAMPLER_PROF)
+FLAGS += os.environ.get("MIM_EXTRA_FLAGS", "").split()
 
 
 def sources():

@@ -96,7 +96,8 @@ struct SetRec {
 namespace mim {
 // RANSAC workspace (definition shared with ransac.hip through this layout)
 struct RansacWs {
-    DevBuf state, samples, hyp, counts, bounds, flags, best_h, cand, ncand, cex, cH, stream, scratch, inl, err;
+    DevBuf state, samples, hyp, counts, bounds, flags, irr, irr_cnt, pass_bits, best_h, cand, ncand, cex, cH, stream,
+        scratch, inl, err;
     long long stream_len = 0;
 };
 }  // namespace mim
@@ -118,9 +119,26 @@ struct mim_ctx {
     int last_n = 0;
     // MIM_RANSAC_EXACT=1: evaluate every hypothesis exactly (reference mode for cross-checks)
     int exact_all = 0;
-    // timing
+    // Pipelined batches: mim_batch_run splits the problems into groups, each on its own stream,
+    // so the latency-bound RANSAC kernels of one group overlap the GPU-filling distance and bound
+    // kernels of the next (DESIGN.md "Batch pipeline").  Group 0 runs on `stream`, the others
+    // fork from and join back into it; the distance kernels run one group after another (ev_knn
+    // chain).  A process has 4 hardware queues (GPU_MAX_HW_QUEUES): the caller's stream, `own`
+    // and two group streams fit, more groups would share a queue and serialise.
+    static constexpr int kMaxGroups = 3;
+    hipStream_t sub[kMaxGroups] = {};
+    hipEvent_t ev_fork = nullptr, ev_knn[kMaxGroups] = {}, ev_join[kMaxGroups] = {};
+    int n_groups = 1;
+    int grp_p0[kMaxGroups + 1] = {}, grp_w0[kMaxGroups + 1] = {};
+    hipStream_t cur = nullptr;  // stream the enqueue helpers launch on
+    // timing: events per stream, durations summed per kernel name over the streams
     bool timing = false;
-    std::vector<std::pair<std::string, hipEvent_t>> evs;
+    struct Ev {
+        std::string name;
+        hipStream_t s;
+        hipEvent_t e;
+    };
+    std::vector<Ev> evs;
     std::map<std::string, double> last_ms;
 };
 
@@ -171,6 +189,7 @@ mim_status mim_ctx_create(int device, mim_ctx** out) {
         return MIM_EDEVICE;
     }
     c->stream = c->own;
+    c->cur = c->own;
     const char* ex = getenv("MIM_RANSAC_EXACT");
     c->exact_all = (ex && ex[0] == '1') ? 1 : 0;
     *out = c;
@@ -181,11 +200,17 @@ void mim_ctx_destroy(mim_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
-    for (auto& e : c->evs) (void)hipEventDestroy(e.second);
+    for (auto& e : c->evs) (void)hipEventDestroy(e.e);
+    for (int g = 0; g < mim_ctx::kMaxGroups; ++g) {
+        if (c->sub[g]) (void)hipStreamDestroy(c->sub[g]);
+        if (c->ev_knn[g]) (void)hipEventDestroy(c->ev_knn[g]);
+        if (c->ev_join[g]) (void)hipEventDestroy(c->ev_join[g]);
+    }
+    if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
     c->arena.release();
     for (DevBuf* b : {&c->probs, &c->works, &c->parts, &c->good_q, &c->good_t, &c->pts, &c->n_good,
                       &c->results, &c->masks, &c->knn_idx, &c->knn_dist, &c->rws.state, &c->rws.samples,
-                      &c->rws.hyp, &c->rws.counts, &c->rws.bounds, &c->rws.flags, &c->rws.best_h, &c->rws.cand, &c->rws.ncand, &c->rws.cex, &c->rws.cH, &c->rws.stream, &c->rws.scratch, &c->rws.inl, &c->rws.err})
+                      &c->rws.hyp, &c->rws.counts, &c->rws.bounds, &c->rws.flags, &c->rws.irr, &c->rws.irr_cnt, &c->rws.pass_bits, &c->rws.best_h, &c->rws.cand, &c->rws.ncand, &c->rws.cex, &c->rws.cH, &c->rws.stream, &c->rws.scratch, &c->rws.inl, &c->rws.err})
         b->release();
     if (c->own) (void)hipStreamDestroy(c->own);
     delete c;
@@ -282,7 +307,14 @@ mim_status mim_sets_clear(mim_ctx* c) {
 // Problem table + distance work list.  Work items of one problem are placed at block indices
 // with equal (index % 8) so they share one XCD's L2 under round-robin dispatch (speed only).
 // ---------------------------------------------------------------------------------------------
-static mim_status build_tables(mim_ctx* c, const mim_problem* problems, int n, int max_iters) {
+static int pick_groups(int n) {
+    const char* e = getenv("MIM_GROUPS");
+    int g = e ? atoi(e) : 1;  // measured: no gain on C3 while the exact/refine chains dominate
+    g = std::max(1, std::min(g, mim_ctx::kMaxGroups));
+    return std::min(g, std::max(n, 1));
+}
+
+static mim_status build_tables(mim_ctx* c, const mim_problem* problems, int n, int max_iters, int groups = 1) {
     HIPCHK(c, hipStreamSynchronize(c->stream));  // previous batch done with the tables
     c->h_probs.assign(n, ProbDev{});
     long long part = 0, good = 0, it = 0;
@@ -318,16 +350,25 @@ static mim_status build_tables(mim_ctx* c, const mim_problem* problems, int n, i
                 per_prob[i].push_back(KnnWork{i, qb_i * 256, t0, t1, s});
             }
     }
-    // XCD-aware order: bucket problems over 8 lanes of the grid
-    std::vector<std::vector<KnnWork>> xcd(8);
-    for (int i = 0; i < n; ++i)
-        for (auto& w : per_prob[i]) xcd[i % 8].push_back(w);
+    // problem groups (contiguous ranges), each with its own contiguous slice of the work list;
+    // inside a group, XCD-aware order: bucket problems over 8 lanes of the grid
+    c->n_groups = groups;
     std::vector<KnnWork> works;
-    size_t longest = 0;
-    for (auto& v : xcd) longest = std::max(longest, v.size());
-    for (size_t k = 0; k < longest; ++k)
-        for (int x = 0; x < 8; ++x)
-            if (k < xcd[x].size()) works.push_back(xcd[x][k]);
+    for (int g = 0; g < groups; ++g) {
+        const int p0 = (int)((long long)n * g / groups), p1 = (int)((long long)n * (g + 1) / groups);
+        c->grp_p0[g] = p0;
+        c->grp_w0[g] = (int)works.size();
+        std::vector<std::vector<KnnWork>> xcd(8);
+        for (int i = p0; i < p1; ++i)
+            for (auto& w : per_prob[i]) xcd[i % 8].push_back(w);
+        size_t longest = 0;
+        for (auto& v : xcd) longest = std::max(longest, v.size());
+        for (size_t k = 0; k < longest; ++k)
+            for (int x = 0; x < 8; ++x)
+                if (k < xcd[x].size()) works.push_back(xcd[x][k]);
+    }
+    c->grp_p0[groups] = n;
+    c->grp_w0[groups] = (int)works.size();
     HIPCHK(c, c->probs.ensure(sizeof(ProbDev) * std::max(n, 1)));
     HIPCHK(c, c->works.ensure(sizeof(KnnWork) * std::max<size_t>(works.size(), 1)));
     HIPCHK(c, c->parts.ensure(sizeof(Top2) * std::max<long long>(part, 1)));
@@ -348,39 +389,55 @@ static mim_status build_tables(mim_ctx* c, const mim_problem* problems, int n, i
     return MIM_OK;
 }
 
+// Kernel timing: an event after every launch on the stream it ran on; a kernel's time is the gap to
+// the previous event of the same stream (with pipelined groups these are the kernels' own spans,
+// overlap with other groups included).
 static void ev_mark(mim_ctx* c, const char* name) {
     if (!c->timing) return;
     hipEvent_t e;
     if (hipEventCreate(&e) != hipSuccess) return;
-    (void)hipEventRecord(e, c->stream);
-    c->evs.push_back({name, e});
+    (void)hipEventRecord(e, c->cur);
+    c->evs.push_back({name, c->cur, e});
 }
 
 static void ev_collect(mim_ctx* c) {
     if (c->evs.empty()) return;
-    (void)hipEventSynchronize(c->evs.back().second);
+    for (auto& e : c->evs) (void)hipEventSynchronize(e.e);
     c->last_ms.clear();
-    for (size_t i = 1; i < c->evs.size(); ++i) {
-        float ms = 0;
-        (void)hipEventElapsedTime(&ms, c->evs[i - 1].second, c->evs[i].second);
-        c->last_ms[c->evs[i].first] += ms;
+    std::map<hipStream_t, hipEvent_t> prev;
+    for (auto& e : c->evs) {
+        auto it = prev.find(e.s);
+        if (it != prev.end()) {
+            float ms = 0;
+            (void)hipEventElapsedTime(&ms, it->second, e.e);
+            c->last_ms[e.name] += ms;
+        }
+        prev[e.s] = e.e;
     }
-    for (auto& e : c->evs) (void)hipEventDestroy(e.second);
+    for (auto& e : c->evs) (void)hipEventDestroy(e.e);
     c->evs.clear();
 }
 
-static mim_status knn_ratio_locked(mim_ctx* c, int n, float ratio, bool emit_knn) {
+// distance + ratio kernels for problems [p0, p0 + np) whose work items are works[w0, w0 + nw)
+static mim_status knn_ratio_enqueue(mim_ctx* c, int p0, int np, int w0, int nw, float ratio, bool emit_knn,
+                                    hipEvent_t after_knn = nullptr) {
     Top2* parts = c->parts.as<Top2>();
     ev_mark(c, "begin");
-    launch_knn(c->probs.as<ProbDev>(), c->works.as<KnnWork>(), c->n_works, parts, c->stream);
+    launch_knn(c->probs.as<ProbDev>(), c->works.as<KnnWork>() + w0, nw, parts, c->cur);
     HIPCHK(c, hipGetLastError());
     ev_mark(c, "knn");
-    launch_ratio(c->probs.as<ProbDev>(), n, parts, ratio, c->good_q.as<int32_t>(), c->good_t.as<int32_t>(),
-                 c->pts.as<float4>(), c->n_good.as<int>(), emit_knn ? c->knn_idx.as<int32_t>() : nullptr,
-                 emit_knn ? c->knn_dist.as<float>() : nullptr, c->stream);
+    if (after_knn) HIPCHK(c, hipEventRecord(after_knn, c->cur));
+    launch_ratio(c->probs.as<ProbDev>() + p0, np, parts, ratio, c->good_q.as<int32_t>(), c->good_t.as<int32_t>(),
+                 c->pts.as<float4>(), c->n_good.as<int>() + p0, emit_knn ? c->knn_idx.as<int32_t>() : nullptr,
+                 emit_knn ? c->knn_dist.as<float>() : nullptr, c->cur);
     HIPCHK(c, hipGetLastError());
     ev_mark(c, "ratio");
     return MIM_OK;
+}
+
+static mim_status knn_ratio_locked(mim_ctx* c, int n, float ratio, bool emit_knn) {
+    c->cur = c->stream;
+    return knn_ratio_enqueue(c, 0, n, 0, c->n_works, ratio, emit_knn);
 }
 
 extern "C" {
@@ -476,6 +533,7 @@ mim_status mim_knn2_sets_dev(mim_ctx* c, int32_t query_set, int32_t train_set, i
     mim_problem pr{query_set, train_set};
     mim_status s = build_tables(c, &pr, 1, 1);
     if (s != MIM_OK) return s;
+    c->cur = c->stream;
     ev_mark(c, "begin");
     launch_knn(c->probs.as<ProbDev>(), c->works.as<KnnWork>(), c->n_works, c->parts.as<Top2>(), c->stream);
     HIPCHK(c, hipGetLastError());
@@ -513,7 +571,10 @@ static mim_status ensure_stream(mim_ctx* c, long long need) {
     return MIM_OK;
 }
 
-static mim_status ransac_locked(mim_ctx* c, int n, const mim_params* prm, int raw) {
+// Buffers and parameters of one RANSAC batch over n problems (allocation only: call before any
+// launch of the batch, a reallocation synchronises the device).
+static mim_status ransac_prepare(mim_ctx* c, int n, const mim_params* prm, RansacBufs& b, RansacParams& rp,
+                                 long long& flag_per) {
     const int max_iters = std::max(prm->max_iters, 1);
     mim_status s = ensure_stream(c, (long long)max_iters * 64 + 40000 * 4);
     if (s != MIM_OK) return s;
@@ -527,12 +588,17 @@ static mim_status ransac_locked(mim_ctx* c, int n, const mim_params* prm, int ra
     HIPCHK(c, c->rws.hyp.ensure(sizeof(float) * 8 * it_total));
     HIPCHK(c, c->rws.counts.ensure(sizeof(int) * it_total));
     HIPCHK(c, c->rws.bounds.ensure(sizeof(int2) * it_total));
-    // attempt-outcome windows: largest chunk x 28 draws per problem (chunks <= 32768 + tail)
+    // attempt-outcome windows: largest chunk x 28 draws per problem, 64-byte granular per problem
     const long long chunk_max = std::min<long long>(max_iters, 1 << 18);
-    const long long flag_cap = (long long)std::max(n, 1) * (chunk_max * 28 + 4096);
+    flag_per = (chunk_max * 28 + 4096 + 63) & ~63LL;
+    const long long flag_cap = (long long)std::max(n, 1) * flag_per;
     HIPCHK(c, c->rws.flags.ensure((size_t)flag_cap));
+    const int irr_blocks = (int)((flag_per + kIrrBlock - 1) / kIrrBlock);
+    HIPCHK(c, c->rws.irr.ensure(sizeof(int) * (size_t)std::max(n, 1) * irr_blocks * kIrrCap));
+    HIPCHK(c, c->rws.irr_cnt.ensure(sizeof(int) * (size_t)std::max(n, 1) * irr_blocks));
+    HIPCHK(c, c->rws.pass_bits.ensure((size_t)flag_cap / 8));
     HIPCHK(c, c->rws.best_h.ensure(sizeof(double) * 9 * std::max(n, 1)));
-    const size_t cap = (size_t)std::max(n, 1) * 1024;  // kCandCap per problem
+    const size_t cap = (size_t)std::max(n, 1) * kCandPerProblem;
     HIPCHK(c, c->rws.cand.ensure(sizeof(int) * cap));
     HIPCHK(c, c->rws.ncand.ensure(sizeof(int) * std::max(n, 1)));
     HIPCHK(c, c->rws.cex.ensure(sizeof(int) * cap));
@@ -542,7 +608,7 @@ static mim_status ransac_locked(mim_ctx* c, int n, const mim_params* prm, int ra
     HIPCHK(c, c->results.ensure(sizeof(mim_result) * std::max(n, 1)));
     HIPCHK(c, c->masks.ensure(good_total));
     HIPCHK(c, hipMemsetAsync(c->rws.err.p, 0, sizeof(int) * 4, c->stream));
-    RansacBufs b{};
+    b = RansacBufs{};
     b.state = c->rws.state.as<RansacState>();
     b.samples = c->rws.samples.as<int4>();
     b.hyp = c->rws.hyp.as<float>();
@@ -555,11 +621,15 @@ static mim_status ransac_locked(mim_ctx* c, int n, const mim_params* prm, int ra
     b.cex = c->rws.cex.as<int>();
     b.cH = c->rws.cH.as<double>();
     b.flag_cap = flag_cap;
+    b.irr = c->rws.irr.as<int>();
+    b.irr_cnt = c->rws.irr_cnt.as<int>();
+    b.pass_bits = c->rws.pass_bits.as<uint32_t>();
+    b.irr_blocks = irr_blocks;
     b.stream = c->rws.stream.as<uint32_t>();
     b.stream_len = c->rws.stream_len;
     b.inl = c->rws.inl.as<float4>();
     b.err = c->rws.err.as<int>();
-    RansacParams rp{};
+    rp = RansacParams{};
     rp.thresh = prm->ransac_thresh > 0 ? prm->ransac_thresh : 3.0;  // findHomography: thresh <= 0 -> 3
     rp.conf = prm->confidence;
     rp.max_iters = max_iters;
@@ -568,9 +638,48 @@ static mim_status ransac_locked(mim_ctx* c, int n, const mim_params* prm, int ra
     rp.min_inliers = prm->min_inliers;
     rp.det_lo = prm->det_lo;
     rp.det_hi = prm->det_hi;
-    ransac_enqueue(rp, n, c->probs.as<ProbDev>(), c->pts.as<float4>(), c->n_good.as<int>(), b, c->masks.as<uint8_t>(),
-                   c->results.as<mim_result>(), raw, c->stream, mark_cb, c, c->exact_all);
+    return MIM_OK;
+}
+
+// RANSAC kernels for problems [p0, p0 + np) on c->cur: per-problem buffers are offset to the range
+// (problem-indexed ones by p0, the iteration/point-indexed ones use the global it_off/good_off).
+static mim_status ransac_enqueue_range(mim_ctx* c, int p0, int np, const RansacBufs& b, const RansacParams& rp,
+                                       long long flag_per, int raw) {
+    RansacBufs g = b;
+    g.state += p0;
+    g.flags += (long long)p0 * flag_per;
+    g.flag_cap = (long long)np * flag_per;
+    g.irr += (long long)p0 * b.irr_blocks * kIrrCap;
+    g.irr_cnt += (long long)p0 * b.irr_blocks;
+    g.pass_bits += (long long)p0 * flag_per / 32;
+    g.best_h += 9LL * p0;
+    g.cand += (long long)p0 * kCandPerProblem;
+    g.ncand += p0;
+    g.cex += (long long)p0 * kCandPerProblem;
+    g.cH += 9LL * p0 * kCandPerProblem;
+    ransac_enqueue(rp, np, c->probs.as<ProbDev>() + p0, c->pts.as<float4>(), c->n_good.as<int>() + p0, g,
+                   c->masks.as<uint8_t>(), c->results.as<mim_result>() + p0, raw, c->cur, mark_cb, c, c->exact_all);
     HIPCHK(c, hipGetLastError());
+    return MIM_OK;
+}
+
+static mim_status ransac_locked(mim_ctx* c, int n, const mim_params* prm, int raw) {
+    RansacBufs b;
+    RansacParams rp;
+    long long flag_per = 0;
+    mim_status s = ransac_prepare(c, n, prm, b, rp, flag_per);
+    if (s != MIM_OK) return s;
+    c->cur = c->stream;
+    return ransac_enqueue_range(c, 0, n, b, rp, flag_per, raw);
+}
+
+static mim_status ensure_groups(mim_ctx* c) {
+    if (!c->ev_fork) HIPCHK(c, hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
+    for (int g = 0; g < c->n_groups; ++g) {
+        if (g > 0 && !c->sub[g]) HIPCHK(c, hipStreamCreateWithFlags(&c->sub[g], hipStreamNonBlocking));
+        if (!c->ev_knn[g]) HIPCHK(c, hipEventCreateWithFlags(&c->ev_knn[g], hipEventDisableTiming));
+        if (!c->ev_join[g]) HIPCHK(c, hipEventCreateWithFlags(&c->ev_join[g], hipEventDisableTiming));
+    }
     return MIM_OK;
 }
 
@@ -591,11 +700,44 @@ mim_status mim_batch_run(mim_ctx* c, const mim_problem* problems, int32_t n, con
     std::lock_guard<std::mutex> lk(c->mu);
     HIPCHK(c, hipSetDevice(c->device));
     if (n == 0) { c->last_n = 0; return MIM_OK; }
-    s = build_tables(c, problems, n, std::max(params->max_iters, 1));
+    s = build_tables(c, problems, n, std::max(params->max_iters, 1), pick_groups(n));
     if (s != MIM_OK) return s;
-    s = knn_ratio_locked(c, n, params->ratio, false);
+    RansacBufs b;
+    RansacParams rp;
+    long long flag_per = 0;
+    s = ransac_prepare(c, n, params, b, rp, flag_per);
     if (s != MIM_OK) return s;
-    return ransac_locked(c, n, params, 0);
+    if (c->n_groups == 1) {
+        s = knn_ratio_locked(c, n, params->ratio, false);
+        if (s != MIM_OK) return s;
+        return ransac_enqueue_range(c, 0, n, b, rp, flag_per, 0);
+    }
+    // pipelined groups: fork from the caller's stream, distance kernels one group after another,
+    // each group's RANSAC right behind its own distance + ratio kernels, join back
+    s = ensure_groups(c);
+    if (s != MIM_OK) return s;
+    HIPCHK(c, hipEventRecord(c->ev_fork, c->stream));
+    for (int g = 0; g < c->n_groups; ++g) {
+        c->cur = g ? c->sub[g] : c->stream;
+        if (g > 0) HIPCHK(c, hipStreamWaitEvent(c->cur, c->ev_fork, 0));
+        if (g > 0) HIPCHK(c, hipStreamWaitEvent(c->cur, c->ev_knn[g - 1], 0));
+        const int p0 = c->grp_p0[g], w0 = c->grp_w0[g];
+        s = knn_ratio_enqueue(c, p0, c->grp_p0[g + 1] - p0, w0, c->grp_w0[g + 1] - w0, params->ratio, false,
+                              c->ev_knn[g]);
+        if (s != MIM_OK) return s;
+    }
+    for (int g = 0; g < c->n_groups; ++g) {
+        c->cur = g ? c->sub[g] : c->stream;
+        const int p0 = c->grp_p0[g];
+        s = ransac_enqueue_range(c, p0, c->grp_p0[g + 1] - p0, b, rp, flag_per, 0);
+        if (s != MIM_OK) return s;
+    }
+    for (int g = 1; g < c->n_groups; ++g) {
+        HIPCHK(c, hipEventRecord(c->ev_join[g], c->sub[g]));
+        HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_join[g], 0));
+    }
+    c->cur = c->stream;
+    return MIM_OK;
 }
 
 mim_status mim_batch_results(mim_ctx* c, mim_result* out) {
@@ -674,6 +816,7 @@ mim_status mim_find_homography(mim_ctx* c, const float* src, const float* dst, i
     c->h_probs.assign(1, P);
     c->h_good_off.assign(1, 0);
     c->last_n = 1;
+    c->cur = c->stream;
     ev_mark(c, "begin");
     s = ransac_locked(c, 1, &prm, 1);
     if (s != MIM_OK) return s;

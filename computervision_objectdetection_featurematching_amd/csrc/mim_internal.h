@@ -61,6 +61,8 @@ struct RansacState {
     int active;            // problem takes the RANSAC path (n_good > 4)
     int lo_max;            // max lower-bound count seen (filtered path: lower bound of maxGoodCount)
     unsigned long long modM;  // Lemire fast-modulo constant for % n (RNG::uniform(0, n))
+    long long win_base;    // stream position of flags[0] of the current chunk's attempt window
+    int win_len;           // attempts precomputed in that window
 };
 
 struct RansacParams {
@@ -75,6 +77,10 @@ struct RansacParams {
 }  // namespace mim
 
 namespace mim {
+constexpr int kCandPerProblem = 1024;  // listed exact-evaluation candidates per problem and chunk
+constexpr int kIrrBlock = 16384;       // attempt positions per irregular-list block
+constexpr int kIrrCap = 512;           // listed irregular attempts per block
+
 // Device buffers of one RANSAC batch (owned by the ctx in api.cpp).
 struct RansacBufs {
     RansacState* state;       // [n_probs]
@@ -83,12 +89,16 @@ struct RansacBufs {
     int* counts;              // [it_off + iter]  inlier count, -1 when runKernel returned 0
     int2* bounds;             // [it_off + iter]  (lower, upper) bound of the count (filtered path)
     double* best_h;           // [problem][9] bestModel of the filtered select (double H of the best sample)
-    int* cand;                // [problem][kCandCap] candidate iterations of the current chunk
+    int* cand;                // [problem][kCandPerProblem] candidate iterations of the current chunk
     int* ncand;               // [problem] candidates listed (may exceed the capacity)
-    int* cex;                 // [problem][kCandCap] their exact inlier counts
-    double* cH;               // [problem][kCandCap][9] their exact models
+    int* cex;                 // [problem][kCandPerProblem] their exact inlier counts
+    double* cH;               // [problem][kCandPerProblem][9] their exact models
     uint8_t* flags;           // [problem][window] getSubset attempt outcomes ahead of stream_pos
     long long flag_cap;       // bytes of `flags`
+    int* irr;                 // [problem][block][kIrrCap] positions of irregular attempts (chain sampler)
+    int* irr_cnt;             // [problem][block] their count (-1: more than kIrrCap)
+    uint32_t* pass_bits;      // [problem][window / 32] bit per position: a regular attempt that passes
+    int irr_blocks;           // list blocks per problem
     const uint32_t* stream;   // raw cv::RNG((uint64)-1).next() stream shared by every problem
     long long stream_len;
     float4* inl;              // [good_off + k] compressed inliers for the refit (scratch)

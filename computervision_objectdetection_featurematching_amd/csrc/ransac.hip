@@ -438,7 +438,7 @@ __device__ __forceinline__ int window_len(const RansacState& S, int c1, int wcap
     const int need = min(c1, S.niters) - S.produced;
     const double rate = S.produced > 0 ? (double)S.stream_pos / S.produced : 28.0;
     const long long w = (long long)((double)need * rate * 1.25) + 4096;
-    return (int)min((long long)wcap, w);
+    return (int)min((long long)wcap, w) & ~63;  // whole 16-byte flag vectors and 32-bit pass words
 }
 
 // Outcome of the getSubset attempt whose draws start at q, as one byte: bit 0 = checkSubset
@@ -499,20 +499,216 @@ __device__ __forceinline__ int wave_max(int v) {
     return v;
 }
 
+constexpr int kFlagWin = 16384;       // LDS window of attempt flags (bytes)
+constexpr int kFlagUnknown = 0xFE;    // past the precomputed window: evaluate inline
+
+__device__ __forceinline__ int ctz64(unsigned long long m) { return __builtin_ctzll(m); }
+// wave-uniform values: keep them in SGPRs so the walk's control flow stays scalar
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ long long uni64(long long v) {
+    const int lo = __builtin_amdgcn_readfirstlane((int)(unsigned)v);
+    const int hi = __builtin_amdgcn_readfirstlane((int)(v >> 32));
+    return (long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ int clz64(unsigned long long m) { return __builtin_clzll(m); }
+__device__ __forceinline__ int mbcnt64(unsigned long long m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+}
+
 // ------------------------------------------------------------------------------------------------
-// sample: walk the chain of getSubset attempts, 256 per round (4 per lane, in order), with the
-// outcomes precomputed by ransac_attempt_kernel; reproduces getSubset's redraw-on-repeat, the
-// checkSubset rejections and the 10000-attempt failure exactly (ptsetreg.cpp).
+// chain sampler.  getSubset attempts start 4 draws apart until one redraws a repeated index (an
+// "irregular" attempt, ~0.3 % of them at n = 2000), so the chain of attempt start positions is a
+// few arithmetic runs joined at irregular attempts.  ransac_irr_kernel lists the irregular
+// positions of the window (parallel), ransac_chain_kernel walks only those (one wave, LDS) and
+// then counts, ranks and writes the passing attempts of the runs in parallel from a pass bitmask.
+// Whatever it cannot settle (list overflow, RNG stream end, window end) it leaves to the
+// attempt-by-attempt walker (ransac_sample_kernel), which resumes from the state it stores.
 // ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(64) void ransac_sample_kernel(RansacState* __restrict__ st,
-                                                           const ProbDev* __restrict__ probs,
-                                                           const float4* __restrict__ pts,
-                                                           const uint32_t* __restrict__ stream, long long slen,
-                                                           int4* __restrict__ samples, int c1,
-                                                           int* __restrict__ err, const uint8_t* __restrict__ flags,
-                                                           int wcap) {
-    constexpr int BIG = 1 << 30;
-    const int p = blockIdx.x, lane = threadIdx.x;
+__global__ __launch_bounds__(256) void ransac_irr_kernel(const RansacState* __restrict__ st,
+                                                         const uint8_t* __restrict__ flags, int wcap, int bpp,
+                                                         int c1, int* __restrict__ irr, int* __restrict__ irr_cnt,
+                                                         uint32_t* __restrict__ pass_bits, int irr_blocks) {
+    __shared__ int wsum[4];
+    const int p = blockIdx.x / bpp, b = blockIdx.x % bpp, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const RansacState S = st[p];
+    if (!S.active || S.done || S.fail_iter != -1 || S.produced >= min(c1, S.niters)) return;
+    const int wlen = window_len(S, c1, wcap);
+    const int b0 = b * kIrrBlock;
+    if (b0 >= wlen) return;
+    const uint8_t* F = flags + (long long)p * wcap;
+    const int r0 = b0 + tid * 64;  // 64 positions per thread
+    uint32_t wd[16];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (r0 + 16 * k + 16 <= wlen) v = *reinterpret_cast<const uint4*>(F + r0 + 16 * k);
+        wd[4 * k] = v.x; wd[4 * k + 1] = v.y; wd[4 * k + 2] = v.z; wd[4 * k + 3] = v.w;
+    }
+    // positions past wlen (a partial last vector) read as 0 = regular, failing: the chain kernel never
+    // walks past wlen
+    uint64_t irrm = 0, pass = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t f = (wd[k] >> (8 * j)) & 0xFF;
+            const int bit = 4 * k + j;
+            irrm |= (uint64_t)(f >= 2) << bit;
+            pass |= (uint64_t)(f == 1) << bit;
+        }
+    if (r0 < wlen) {
+        uint32_t* PB = pass_bits + (long long)p * (wcap / 32) + r0 / 32;
+        PB[0] = (uint32_t)pass;
+        PB[1] = (uint32_t)(pass >> 32);
+    }
+    const int c = __popcll(irrm);
+    int incl = c;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int o = __shfl_up(incl, off);
+        if (lane >= off) incl += o;
+    }
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    int base = incl - c, total = 0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        base += w < wave ? wsum[w] : 0;
+        total += wsum[w];
+    }
+    const long long slot = (long long)p * irr_blocks + b;
+    if (tid == 0) irr_cnt[slot] = total <= kIrrCap ? total : -1;
+    if (total > kIrrCap) return;
+    int* L = irr + slot * kIrrCap;
+    while (irrm) {
+        const int bit = __builtin_ctzll(irrm);
+        irrm &= irrm - 1;
+        L[base++] = r0 + bit;
+    }
+}
+
+constexpr int kChainThreads = 1024;
+constexpr int kChainEntries = 8192;  // irregular attempts staged in LDS
+constexpr int kChainSegs = 4 * kChainThreads - 2;  // runs (segments) walked per chunk
+constexpr int kNoEvent = INT_MAX;
+
+struct ChainShared {
+    int q[kChainEntries];
+    uint8_t f[kChainEntries];
+    int seg_s[kChainSegs + 1];
+    int seg_q[kChainSegs];
+    uint8_t seg_f[kChainSegs];
+    int A[kChainSegs + 2];      // first attempt index of each segment (+ tail, + end)
+    int boff[kIrrCap + 1];      // list block -> first entry (exclusive scan of the counts)
+    int wred[kChainThreads / 64];
+    int wred2[kChainThreads / 64];
+    int n_entries, limit, nseg, s_end, tail;
+    int t_need, pos_need, len_need;
+};
+
+__device__ __forceinline__ int block_excl_sum(int v, int* wred, int& total) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    int incl = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int o = __shfl_up(incl, off);
+        if (lane >= off) incl += o;
+    }
+    __syncthreads();
+    if (lane == 63) wred[wave] = incl;
+    __syncthreads();
+    int base = incl - v;
+    total = 0;
+    for (int w = 0; w < nw; ++w) {
+        base += w < wave ? wred[w] : 0;
+        total += wred[w];
+    }
+    return base;
+}
+
+__device__ __forceinline__ int block_excl_max(int v, int init, int* wred, int& all) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    int incl = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int o = __shfl_up(incl, off);
+        if (lane >= off) incl = max(incl, o);
+    }
+    int ex = __shfl_up(incl, 1);
+    if (lane == 0) ex = INT_MIN;
+    __syncthreads();
+    if (lane == 63) wred[wave] = incl;
+    __syncthreads();
+    int r = max(init, ex);
+    all = init;
+    for (int w = 0; w < nw; ++w) {
+        if (w < wave) r = max(r, wred[w]);
+        all = max(all, wred[w]);
+    }
+    return r;
+}
+
+__device__ __forceinline__ int block_min(int v, int* wred) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    v = wave_min(v);
+    __syncthreads();
+    if (lane == 0) wred[wave] = v;
+    __syncthreads();
+    int r = INT_MAX;
+    for (int w = 0; w < nw; ++w) r = min(r, wred[w]);
+    return r;
+}
+
+// Visit the passing attempts with chain index in [t0, t1), in order: fn(t, rel_pos, irregular).
+template <class Fn>
+__device__ __forceinline__ void chain_visit(const ChainShared& sh, const uint32_t* __restrict__ PB, int t0, int t1,
+                                            Fn&& fn) {
+    if (t0 >= t1) return;
+    int lo = 0, hi = sh.nseg;  // segment j (tail = nseg) with A[j] <= t0 < A[j+1]
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (sh.A[mid] <= t0) lo = mid; else hi = mid - 1;
+    }
+    int j = lo, t = t0;
+    while (t < t1) {
+        const bool tail = j == sh.nseg;
+        const int Aj = sh.A[j], sj = sh.seg_s[j];
+        const int reg_end = tail ? sh.A[j + 1] : sh.A[j + 1] - 1;  // attempts before the irregular one
+        const int rb = min(t1, reg_end);
+        if (t < rb) {
+            const int P0 = sj + 4 * (t - Aj), P1 = sj + 4 * (rb - Aj);
+            const uint32_t res = 0x11111111u << (sj & 3);
+            for (int w = P0 >> 5; w <= (P1 - 1) >> 5; ++w) {
+                const int lo_b = max(P0 - 32 * w, 0), hi_b = min(P1 - 32 * w, 32);
+                const uint32_t rm = (hi_b == 32 ? 0xFFFFFFFFu : ((1u << hi_b) - 1)) & ~((1u << lo_b) - 1);
+                uint32_t bits = PB[w] & res & rm;
+                while (bits) {
+                    const int bit = __builtin_ctz(bits);
+                    bits &= bits - 1;
+                    const int pos = 32 * w + bit;
+                    fn(Aj + ((pos - sj) >> 2), pos, false);
+                }
+            }
+            t = rb;
+        }
+        if (!tail && t == sh.A[j + 1] - 1 && t < t1) {  // the irregular attempt closing segment j
+            if (sh.seg_f[j] & 1) fn(t, sh.seg_q[j], true);
+            ++t;
+        }
+        ++j;
+    }
+}
+
+__global__ __launch_bounds__(kChainThreads) void ransac_chain_kernel(RansacState* __restrict__ st,
+                                                                     const ProbDev* __restrict__ probs,
+                                                                     int4* __restrict__ samples, int c1,
+                                                                     const uint8_t* __restrict__ flags, int wcap,
+                                                                     const int* __restrict__ irr,
+                                                                     const int* __restrict__ irr_cnt,
+                                                                     const uint32_t* __restrict__ pass_bits,
+                                                                     int irr_blocks) {
+    __shared__ ChainShared sh;
+    const int p = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
     RansacState S = st[p];
     if (!S.active || S.done || S.fail_iter != -1) return;
     const int target = min(c1, S.niters);
@@ -520,113 +716,374 @@ __global__ __launch_bounds__(64) void ransac_sample_kernel(RansacState* __restri
     const long long wbase = S.stream_pos;
     const int wlen = window_len(S, c1, wcap);
     const uint8_t* F = flags + (long long)p * wcap;
+    const uint32_t* PB = pass_bits + (long long)p * (wcap / 32);
+    const int nb = min((wlen + kIrrBlock - 1) / kIrrBlock, kIrrCap);  // boff has kIrrCap + 1 slots
+    // stage the irregular list: blocks up to the first overflowing one, at most kChainEntries entries
+    {
+        const int cnt = tid < nb ? irr_cnt[(long long)p * irr_blocks + tid] : 0;
+        const int bad = tid < nb && cnt < 0 ? tid : INT_MAX;
+        int total;
+        const int off = block_excl_sum(max(cnt, 0), sh.wred, total);
+        const int over = tid < nb && off + max(cnt, 0) > kChainEntries ? tid : INT_MAX;
+        const int cut = min(min(block_min(bad, sh.wred2), block_min(over, sh.wred)), nb);
+        if (tid <= nb) sh.boff[tid] = tid < nb ? off : 0;
+        __syncthreads();
+        if (tid == 0) {
+            sh.n_entries = cut > 0 ? sh.boff[cut - 1] + irr_cnt[(long long)p * irr_blocks + cut - 1] : 0;
+            sh.limit = min(wlen, cut * kIrrBlock);
+        }
+        __syncthreads();
+        for (int e = tid; e < sh.n_entries; e += kChainThreads) {
+            int lo = 0, hi = cut - 1;
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (sh.boff[mid] <= e) lo = mid; else hi = mid - 1;
+            }
+            const int q = irr[((long long)p * irr_blocks + lo) * kIrrCap + (e - sh.boff[lo])];
+            sh.q[e] = q;
+            sh.f[e] = F[q];
+        }
+        __syncthreads();
+    }
+    // walk the irregular attempts of the chain (one wave): segment j = the run s_j, s_j + 4, ...
+    // closed by the irregular attempt q_j; then an open tail run up to `limit`
+    if (tid < 64) {
+        int s = 0, nseg = 0, limit = sh.limit;
+        const int E = sh.n_entries;
+        bool stop = false;
+        for (int e0 = 0; e0 < E && !stop; e0 += 64) {
+            const int e = e0 + lane;
+            const int q = e < E ? sh.q[e] : INT_MAX;
+            const int f = e < E ? (int)sh.f[e] : 0;
+            for (;;) {
+                const unsigned long long m = __ballot(q >= s && q < limit && ((q - s) & 3) == 0);
+                if (!m) break;
+                const int k = __builtin_ctzll(m);
+                const int qq = uni(__shfl(q, k)), ff = uni(__shfl(f, k));
+                if (ff == kAttemptSerial || nseg == kChainSegs) {  // resolved by the walker
+                    limit = qq;
+                    stop = true;
+                    break;
+                }
+                if (lane == 0) {
+                    sh.seg_s[nseg] = s;
+                    sh.seg_q[nseg] = qq;
+                    sh.seg_f[nseg] = (uint8_t)ff;
+                }
+                ++nseg;
+                s = uni(qq + 4 + (ff >> 1));
+            }
+        }
+        if (lane == 0) {
+            sh.nseg = nseg;
+            sh.seg_s[nseg] = s;
+            sh.tail = s < limit ? (limit - s + 3) >> 2 : 0;
+            sh.s_end = s + 4 * sh.tail;
+        }
+    }
+    __syncthreads();
+    const int nseg = sh.nseg;
+    // attempt index of every segment start
+    {
+        int v[4], sum = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int j = 4 * tid + k;
+            v[k] = j < nseg ? ((sh.seg_q[j] - sh.seg_s[j]) >> 2) + 1 : (j == nseg ? sh.tail : 0);
+            sum += v[k];
+        }
+        int total;
+        int base = block_excl_sum(sum, sh.wred, total);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int j = 4 * tid + k;
+            if (j <= nseg + 1) sh.A[j] = base;
+            base += v[k];
+        }
+        __syncthreads();
+    }
+    const int T = sh.A[nseg + 1];  // attempts settled here
+    const int ch = (T + kChainThreads - 1) / kChainThreads;
+    const int t0 = min(T, tid * ch), t1 = min(T, t0 + ch);
+    int cnt = 0, first = -1, last = -1;
+    chain_visit(sh, PB, t0, t1, [&](int t, int, bool) {
+        if (first < 0) first = t;
+        last = t;
+        ++cnt;
+    });
+    // failure rule of getSubset: 10000 consecutive rejected attempts (runs here are < 10000 long,
+    // so a failure can only end a gap that starts at an earlier thread's last pass)
+    int total;
+    const int base = block_excl_sum(cnt, sh.wred, total);
+    const int v0 = -1 - S.fail_run;  // virtual pass before the chunk
+    int last_all;
+    const int prev = block_excl_max(cnt ? last : INT_MIN, v0, sh.wred2, last_all);
+    int ev = (cnt && first - prev - 1 >= 10000) ? prev + 10000 : kNoEvent;
+    if (tid == 0 && T - 1 - last_all >= 10000) ev = min(ev, last_all + 10000);
+    const int t_fail = block_min(ev, sh.wred);
+    const int need = target - S.produced;
+    if (tid == 0) sh.t_need = kNoEvent;
+    __syncthreads();
+    if (base < need && need <= base + cnt) {  // the attempt completing the chunk's last iteration
+        int k = need - base;
+        chain_visit(sh, PB, t0, t1, [&](int t, int pos, bool irr_att) {
+            if (--k == 0) {
+                sh.t_need = t;
+                sh.pos_need = pos;
+                sh.len_need = irr_att ? 4 + (F[pos] >> 1) : 4;
+            }
+        });
+    }
+    __syncthreads();
+    const int t_need = sh.t_need;
+    int keep;  // passes written (ranks [0, keep))
+    if (t_fail < t_need) {
+        int before = 0;
+        if (cnt && last < t_fail) before = cnt;
+        else if (cnt && first < t_fail)
+            chain_visit(sh, PB, t0, t1, [&](int t, int, bool) { before += t < t_fail; });
+        int tot_before;
+        block_excl_sum(before, sh.wred, tot_before);
+        keep = tot_before;
+    } else {
+        keep = t_need != kNoEvent ? need : total;
+    }
+    if (base < keep) {
+        int4* out = samples + probs[p].it_off + S.produced;
+        int r = base;
+        chain_visit(sh, PB, t0, t1, [&](int, int pos, bool irr_att) {
+            if (r < keep) out[r] = make_int4((int)(wbase + pos), irr_att ? -2 : -1, 0, 0);
+            ++r;
+        });
+    }
+    if (tid == 0) {
+        S.win_base = wbase;
+        S.win_len = wlen;
+        if (t_fail < t_need) {
+            S.produced += keep;
+            S.fail_iter = S.produced;  // getSubset returned false in this iteration
+            S.fail_run = 10000;
+        } else if (t_need != kNoEvent) {
+            S.produced = target;
+            S.stream_pos = wbase + sh.pos_need + sh.len_need;
+            S.fail_run = 0;
+        } else {
+            S.produced += total;
+            S.fail_run = total > 0 ? T - 1 - last_all : S.fail_run + T;
+            S.stream_pos = wbase + sh.s_end;
+        }
+        st[p] = S;
+    }
+    (void)lane;
+}
+
+// ------------------------------------------------------------------------------------------------
+// sample: walk the chain of getSubset attempts with the outcomes precomputed by
+// ransac_attempt_kernel; reproduces getSubset's redraw-on-repeat, the checkSubset rejections and
+// the 10000-attempt failure exactly (ptsetreg.cpp).
+//
+// The attempt flags stream through a 16 KiB LDS window.  A round reads 1 KiB of it (16 bytes per
+// lane: stream positions wb+16l .. wb+16l+15) and walks every attempt of the chain inside that
+// span: attempts start 4 draws apart (residue rho mod 4) until one redraws repeated indices, after
+// which the walk continues in the residue it lands on (a sub-round).  All bookkeeping is done on
+// ballot masks in scalar registers: attempt a = 4*lane + i of a sub-round is bit `lane` of mask i.
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void ransac_sample_kernel(RansacState* __restrict__ st,
+                                                           const ProbDev* __restrict__ probs,
+                                                           const float4* __restrict__ pts,
+                                                           const uint32_t* __restrict__ stream, long long slen,
+                                                           int4* __restrict__ samples, int c1,
+                                                           int* __restrict__ err, const uint8_t* __restrict__ flags,
+                                                           int wcap, int after_chain) {
+    __shared__ __attribute__((aligned(16))) uint8_t win[kFlagWin];
+    constexpr int BIG = 1 << 30;
+    const int p = blockIdx.x, lane = threadIdx.x;
+    RansacState S = st[p];
+    if (!S.active || S.done || S.fail_iter != -1) return;
+    const int target = min(c1, S.niters);
+    if (S.produced >= target) return;
+    // resume where ransac_chain_kernel stopped; flags[rel] is the attempt starting at wbase + rel
+    const long long wbase = after_chain ? S.win_base : S.stream_pos;
+    const int wlen = after_chain ? S.win_len : window_len(S, c1, wcap);
+    const uint8_t* F = flags + (long long)p * wcap;
     const unsigned N = (unsigned)S.n;
     const unsigned long long M = S.modM;
     const float4* P = pts + probs[p].good_off;
     int4* out = samples + probs[p].it_off;
-    long long pos = S.stream_pos;
+    long long rel = S.stream_pos - wbase;  // next attempt, relative to wbase
+    long long lb = -(1LL << 40);
     int produced = S.produced, fail_run = S.fail_run;
-    while (produced < target) {
-        int f[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const long long q = pos + 4LL * (4 * lane + i);
-            const long long rel = q - wbase;
-            f[i] = rel < wlen ? (int)F[rel] : attempt_flag(q, stream, slen, N, M, P);
-        }
-        // first attempt whose length is not 4 draws: later lanes' start positions are wrong
-        int lc = 4;
-#pragma unroll
-        for (int i = 3; i >= 0; --i) lc = (f[i] == kAttemptSerial || (f[i] >> 1) != 0) ? i : lc;
-        const unsigned long long cm = __ballot(lc < 4);
-        const int L = cm ? __ffsll((long long)cm) - 1 : 64;
-        const int afc = L < 64 ? 4 * L + __shfl(lc, L) : 256;
-        long long endfc = 0;
-        int fcpass = 0, fcres = 0;  // fcres: the attempt redrew repeated indices
-        int oob = 0;
-        if (afc < 256) {
-            const int ffc = __shfl(f[0], L);
-            int fsel = ffc;
-#pragma unroll
-            for (int i = 1; i < 4; ++i) {
-                const int fi = __shfl(f[i], L);
-                fsel = (afc - 4 * L) == i ? fi : fsel;
-            }
-            const long long qfc = pos + 4LL * afc;
-            if (fsel != kAttemptSerial) {
-                endfc = qfc + 4 + (fsel >> 1);
-                fcpass = fsel & 1;
-                fcres = 1;
-            } else {  // resolve here (stream end or a very long redraw run)
-                int idx[4] = {0, 0, 0, 0};
-                const int len = resolve_at(qfc, stream, slen, N, M, idx);
-                if (len == 0) {
-                    oob = 1;
+    bool stop_all = false;
+#ifdef MIM_SAMPLER_PROF
+    const unsigned long long t_start = wall_clock64();
+    int n_round = 0, n_sub = 0, n_fill = 0, n_unk = 0;
+    unsigned long long tp[6] = {0, 0, 0, 0, 0, 0}, tc = clock64();
+#define PROF_T(k) { const unsigned long long t_ = clock64(); tp[k] += t_ - tc; tc = t_; }
+    const int produced0 = produced;
+#define PROF_INC(x) ++x
+#else
+#define PROF_INC(x)
+#define PROF_T(k)
+#endif
+    while (!stop_all && produced < target) {
+        PROF_INC(n_round);
+        const long long wb = rel & ~15LL;
+        if (wb < lb || wb + 1024 > lb + kFlagWin) {  // refill the LDS window at wb
+            PROF_INC(n_fill);
+            lb = wb;
+            __syncthreads();
+#pragma unroll 4
+            for (int j = 0; j < kFlagWin / 1024; ++j) {
+                const long long r0 = lb + 16LL * (lane + 64 * j);
+                uint4 v;
+                if (r0 + 16 <= wlen) {
+                    v = *reinterpret_cast<const uint4*>(F + r0);
                 } else {
+                    uint32_t w4[4];
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        uint32_t w = 0;
+                        for (int b = 0; b < 4; ++b) {
+                            const long long r = r0 + 4 * k + b;
+                            w |= (uint32_t)(r < wlen ? F[r] : kFlagUnknown) << (8 * b);
+                        }
+                        w4[k] = w;
+                    }
+                    v = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+                }
+                *reinterpret_cast<uint4*>(win + 16 * (lane + 64 * j)) = v;
+            }
+            __syncthreads();
+        }
+        const uint4 w = *reinterpret_cast<const uint4*>(win + (wb - lb) + 16 * lane);
+        const uint32_t wd[4] = {w.x, w.y, w.z, w.w};
+        long long s = rel;  // chain position inside [wb, wb + 1024)
+        while (s < wb + 1024) {
+            PROF_INC(n_sub);
+            PROF_T(0);
+            const int rho = (int)(s - wb) & 3;
+            const int a0 = (int)(s - wb) >> 2;  // first attempt of this sub-round (a = 4 lane + i)
+            int f[4];
+            unsigned long long I[4], Pm[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int a = 4 * lane + i;
+                int fi = (int)((wd[i] >> (8 * rho)) & 0xFF);
+                if (a >= a0 && fi == kFlagUnknown) PROF_INC(n_unk);
+                if (a >= a0 && fi == kFlagUnknown)
+                    fi = attempt_flag(wbase + wb + 4LL * a + rho, stream, slen, N, M, P);
+                f[i] = fi;
+                const bool irr = fi == kAttemptSerial || (fi >> 1) != 0;
+                I[i] = __ballot(a >= a0 && irr);
+                Pm[i] = __ballot(a >= a0 && !irr && (fi & 1));
+            }
+            // first attempt whose length is not 4 draws (or must be resolved here)
+            PROF_T(1);
+            int afc = 256;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                if (I[i]) afc = min(afc, 4 * ctz64(I[i]) + i);
+            long long endfc = 0;  // chain position after the afc attempt
+            int fcpass = 0, fcres = 0;
+            if (afc < 256) {
+                const int fsel = uni(__shfl(f[afc & 3], afc >> 2));
+                const long long qfc = wb + 4LL * afc + rho;
+                if (fsel != kAttemptSerial) {
+                    endfc = qfc + 4 + (fsel >> 1);
+                    fcpass = fsel & 1;
+                    fcres = 1;
+                } else {  // resolve here (stream end or a very long redraw run)
+                    int idx[4] = {0, 0, 0, 0};
+                    const int len = resolve_at(wbase + qfc, stream, slen, N, M, idx);
+                    if (len == 0) {  // RNG stream exhausted: report, never guess
+                        if (lane == 0) atomicOr(err, 1);
+                        S.fail_iter = -2;
+                        stop_all = true;
+                        break;
+                    }
                     const float4 a = P[idx[0]], b = P[idx[1]], c = P[idx[2]], d = P[idx[3]];
                     const float s4[8] = {a.x, a.y, b.x, b.y, c.x, c.y, d.x, d.y};
                     const float t4[8] = {a.z, a.w, b.z, b.w, c.z, c.w, d.z, d.w};
-                    fcpass = check_subset(s4, t4) ? 1 : 0;
-                    fcres = len != 4;
-                    endfc = qfc + len;
+                    fcpass = uni(check_subset(s4, t4) ? 1 : 0);
+                    fcres = uni(len != 4);
+                    endfc = uni64(qfc + len);
                 }
-            }
-        }
-        if (oob) {  // RNG stream exhausted: report, never guess
-            if (lane == 0) atomicOr(err, 1);
-            S.fail_iter = -2;
-            break;
-        }
-        unsigned bits = 0;
+                // keep only passes before afc, then add afc itself
+                const int L = afc >> 2, e = afc & 3;
+                const unsigned long long below = L ? (~0ull >> (64 - L)) : 0ull;  // lanes < L
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int a = 4 * lane + i;
-            const bool ps = (a < afc && f[i] == 1) || (a == afc && fcpass);
-            bits |= ps ? (1u << i) : 0u;
-        }
-        const int nvalid = afc < 256 ? afc + 1 : 256;
-        const int c = __popc(bits);
-        const int E = wave_excl_prefix_sum(c);
-        const int tot = __shfl(E + c, 63);
-        const int a_p = wave_min(bits ? 4 * lane + __ffs(bits) - 1 : BIG);        // first pass
-        const int a_lp = wave_max(bits ? 4 * lane + 31 - __clz(bits) : -1);      // last pass
-        const int need = target - produced;
-        int at = BIG;
-        if (E < need && need <= E + c) {
-            int k = need - E;
+                for (int i = 0; i < 4; ++i) Pm[i] &= (i < e) ? (below | (1ull << L)) : below;
+                if (fcpass) Pm[e] |= 1ull << L;
+            }
+            PROF_T(2);
+            const int end = afc < 256 ? afc + 1 : 256;  // attempts a0 .. end-1 are walked
+            int tot = 0, a_p = BIG, a_lp = -1;
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                if ((bits >> i) & 1) {
-                    if (--k == 0 && at == BIG) at = 4 * lane + i;
+                tot += __popcll(Pm[i]);
+                if (Pm[i]) {
+                    a_p = min(a_p, 4 * ctz64(Pm[i]) + i);
+                    a_lp = max(a_lp, 4 * (63 - clz64(Pm[i])) + i);
                 }
             }
-        }
-        at = wave_min(at);
-        const int fails_before = a_p < BIG ? a_p : nvalid;
-        const int af = fail_run + fails_before >= 10000 ? 10000 - fail_run - 1 : BIG;  // 10000th failure
-        int stop = nvalid - 1, got = tot;
-        bool hit_t = false, hit_f = false;
-        if (at < BIG && at < af) { stop = at; hit_t = true; got = need; }
-        else if (af < BIG) { stop = af; hit_f = true; got = 0; }
+            unsigned bits = 0;
+            int E = 0;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int a = 4 * lane + i;
-            if (((bits >> i) & 1) && a <= stop) {
-                const int rank = E + __popc(bits & ((1u << i) - 1));
-                out[produced + rank] = make_int4((int)(pos + 4LL * a), (a == afc && fcres) ? -2 : -1, 0, 0);
+            for (int i = 0; i < 4; ++i) {
+                bits |= (unsigned)((Pm[i] >> lane) & 1ull) << i;
+                E += mbcnt64(Pm[i]);
             }
+            const int need = target - produced;
+            int at = BIG;  // attempt completing the chunk's last wanted iteration
+            if (tot >= need) {
+                const unsigned long long hm = __ballot(E < need && need <= E + __popc(bits));
+                const int Lh = ctz64(hm);
+                const unsigned hb = (unsigned)uni(__shfl((int)bits, Lh));
+                int k = need - uni(__shfl(E, Lh));
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    if (((hb >> i) & 1) && --k == 0) at = 4 * Lh + i;
+            }
+            PROF_T(3);
+            const int fails_before = (a_p < BIG ? a_p : end) - a0;
+            const int af = fail_run + fails_before >= 10000 ? a0 + (10000 - fail_run - 1) : BIG;  // 10000th failure
+            int stop = end - 1, got = tot;
+            bool hit_t = false, hit_f = false;
+            if (at < BIG && at < af) { stop = at; hit_t = true; got = need; }
+            else if (af < BIG) { stop = af; hit_f = true; got = 0; }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int a = 4 * lane + i;
+                if (((bits >> i) & 1) && a <= stop) {
+                    const int rank = E + __popc(bits & ((1u << i) - 1));
+                    out[produced + rank] = make_int4((int)(wbase + wb + 4LL * a + rho), (a == afc && fcres) ? -2 : -1, 0, 0);
+                }
+            }
+            PROF_T(4);
+            produced += got;
+            fail_run = hit_t ? 0 : (hit_f ? 10000 : (tot > 0 ? stop - a_lp : fail_run + (end - a0)));
+            s = uni64(stop == afc ? endfc : wb + 4LL * (stop + 1) + rho);
+            if (hit_f) {
+                S.fail_iter = produced;  // getSubset returned false in this iteration
+                stop_all = true;
+                break;
+            }
+            if (hit_t) { stop_all = true; break; }
         }
-        produced += got;
-        fail_run = hit_t ? 0 : (hit_f ? 10000 : (tot > 0 ? stop - a_lp : fail_run + nvalid));
-        pos = stop == afc ? endfc : pos + 4LL * (stop + 1);
-        if (hit_f) {
-            S.fail_iter = produced;  // getSubset returned false in this iteration
-            break;
-        }
-        if (hit_t) break;
+        rel = uni64(s);
     }
+#ifdef MIM_SAMPLER_PROF
+    if (lane == 0 && p < 3)
+        printf("[sampler] p=%d c1=%d produced %d->%d draws %lld rounds %d sub %d fills %d unknown %d wlen %d time %.1f us\n",
+               p, c1, produced0, produced, rel, n_round, n_sub, n_fill, n_unk, wlen,
+               (double)(wall_clock64() - t_start) / 100.0);
+    if (lane == 0 && p < 3)
+        printf("[sampler] p=%d cycles: outer %llu ballots %llu afc %llu count %llu store %llu\n", p, tp[0], tp[1], tp[2],
+               tp[3], tp[4]);
+#endif
+#undef PROF_INC
     if (lane == 0) {
-        S.stream_pos = pos;
+        S.stream_pos = wbase + rel;
         S.produced = produced;
         S.fail_run = fail_run;
         st[p] = S;
@@ -919,6 +1376,7 @@ __device__ __forceinline__ int wave_excl_prefix_max(int v) {
 // evaluated exactly by a GPU-wide grid (one lane each), then replayed in order per problem.
 constexpr int kCandWaves = 16;                 // exact-evaluation waves per problem and chunk
 constexpr int kCandCap = kCandWaves * 64;      // listed candidates per problem and chunk
+static_assert(kCandCap == kCandPerProblem, "candidate list layout shared with api.cpp");
 
 __global__ __launch_bounds__(64) void ransac_cand_kernel(RansacState* __restrict__ st,
                                                          const ProbDev* __restrict__ probs,
@@ -1637,19 +2095,31 @@ void ransac_enqueue(const RansacParams& prm, int n_probs, const ProbDev* probs, 
     ransac_init_kernel<<<(n_probs + 255) / 256, 256, 0, s>>>(b.state, n_good, n_probs, prm.max_iters, prm.min_good,
                                                              b.best_h);
     const int max_iters = prm.max_iters > 1 ? prm.max_iters : 1;
+    // MIM_SAMPLER_WALK=1: attempt-by-attempt walker only (reference mode for cross-checks)
+    const char* sw = getenv("MIM_SAMPLER_WALK");
+    const int use_chain = !(sw && sw[0] == '1');
     int c0 = 0, chunk = 4096;
     const float thr2 = (float)(prm.thresh * prm.thresh);
     while (c0 < max_iters) {
         const int c1 = (int)std::min<long long>((long long)c0 + chunk, max_iters);
         // attempt outcomes for a window of ~28 draws per wanted iteration (pass rate ~1/5), the walk
         // falls back to inline evaluation past the window
-        const int wcap = (int)std::min<long long>((long long)(c1 - c0) * 28 + 4096, b.flag_cap / std::max(n_probs, 1));
+        // (a multiple of 64: flags are read as 16-byte vectors, pass bits as 32-bit words)
+        const int wcap = (int)(std::min<long long>((long long)(c1 - c0) * 28 + 4096, b.flag_cap / std::max(n_probs, 1)) & ~63LL);
         const int bppw = (wcap + 255) / 256;
         ransac_attempt_kernel<<<n_probs * bppw, 256, 0, s>>>(b.state, probs, pts, b.stream, b.stream_len, b.flags, wcap,
                                                             bppw, c1);
         mark(mark_ctx, "attempt");
+        if (use_chain) {
+            const int bpp_irr = (wcap + kIrrBlock - 1) / kIrrBlock;
+            ransac_irr_kernel<<<n_probs * bpp_irr, 256, 0, s>>>(b.state, b.flags, wcap, bpp_irr, c1, b.irr,
+                                                               b.irr_cnt, b.pass_bits, b.irr_blocks);
+            ransac_chain_kernel<<<n_probs, kChainThreads, 0, s>>>(b.state, probs, b.samples, c1, b.flags, wcap, b.irr,
+                                                                  b.irr_cnt, b.pass_bits, b.irr_blocks);
+            mark(mark_ctx, "chain");
+        }
         ransac_sample_kernel<<<n_probs, 64, 0, s>>>(b.state, probs, pts, b.stream, b.stream_len, b.samples, c1, b.err,
-                                                    b.flags, wcap);
+                                                    b.flags, wcap, use_chain);
         mark(mark_ctx, "sample");
         const int bpp256 = (c1 - c0 + 255) / 256;
         if (exact_all) {  // reference mode: every hypothesis through runKernel + computeError

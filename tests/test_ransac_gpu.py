@@ -217,3 +217,78 @@ def test_mostly_degenerate_points(matcher, oracle):
         ok, Ho, mo = oracle.find_homography(src, dst, 5.0, iters, 0.995)
         assert (Hg is not None) == bool(ok)
         np.testing.assert_array_equal(mg, mo)
+
+
+@pytest.mark.parametrize("groups", ["2", "3"])
+def test_grouped_pipeline_identical(groups):
+    """Pipelined groups (problem ranges on their own streams) give the same records as one stream."""
+    import os
+    from computervision_objectdetection_featurematching_amd import Matcher, default_params
+    ds = make_dataset(2, 5, 1200, 2000, 400, inlier_frac=0.1, seed=4242)
+    outs = []
+    for g in ("1", groups):
+        os.environ["MIM_GROUPS"] = g
+        m = Matcher(0)
+        try:
+            q = [m.add_set(d, k) for d, k in zip(ds.model_desc, ds.model_kp)]
+            t = [m.add_set(d, k) for d, k in zip(ds.scene_desc, ds.scene_kp)]
+            res = m.match_batch([(q[a], t[b]) for a, b in ds.problems], default_params(max_iters=8000))
+            masks = [m.problem_detail(i, int(r["n_good"]))[2] for i, r in enumerate(res)]
+        finally:
+            m.close()
+            os.environ.pop("MIM_GROUPS", None)
+        outs.append((res, masks))
+    (r0, m0), (r1, m1) = outs
+    assert r0.tobytes() == r1.tobytes()
+    for a, b in zip(m0, m1):
+        np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.parametrize("n_off,iters", [(0, 2000), (3, 2000), (4, 20000)])
+def test_chain_sampler_rejection_runs(matcher, oracle, n_off, iters):
+    """n large enough for the chain sampler (few repeated-index redraws) with most subsets collinear:
+    runs of rejected attempts up to and past getSubset's 10000-attempt limit.  The refit of such a
+    degenerate inlier set is ill-conditioned, so the check is on the RANSAC trace, not on H."""
+    rng = np.random.default_rng(100 + n_off)
+    n = 300
+    src = np.c_[np.arange(n, dtype=np.float32) * 2, np.full(n, 100, np.float32)]
+    if n_off:
+        src[-n_off:] = rng.uniform(0, 400, size=(n_off, 2)).astype(np.float32)
+    dst = src * np.float32(1.1) + np.float32(3)
+    Hg, mg = matcher.find_homography(src, dst, 5.0, iters, 0.995)
+    rec = matcher.batch_results(1)[0]
+    r = oracle.ransac(src, dst, 5.0, 0.995, iters)
+    assert (Hg is not None) == bool(r["ok"])
+    np.testing.assert_array_equal(mg, r["mask"])
+    assert rec["iters"] == r["iters"], (rec["iters"], r["iters"])
+
+
+def test_chain_sampler_equals_walker():
+    """The chain sampler and the attempt-by-attempt walker (MIM_SAMPLER_WALK=1) give identical output."""
+    import os
+    from computervision_objectdetection_featurematching_amd import Matcher, default_params
+    ds = make_dataset(2, 3, 1500, 2500, 500, inlier_frac=0.08, seed=777)
+    sets = _adversarial_sets()
+    outs = []
+    for mode in ("0", "1"):
+        os.environ["MIM_SAMPLER_WALK"] = mode
+        m = Matcher(0)
+        try:
+            q = [m.add_set(d, k) for d, k in zip(ds.model_desc, ds.model_kp)]
+            t = [m.add_set(d, k) for d, k in zip(ds.scene_desc, ds.scene_kp)]
+            res = m.match_batch([(q[a], t[b]) for a, b in ds.problems], default_params(max_iters=30000))
+            masks = [m.problem_detail(i, int(r["n_good"]))[2] for i, r in enumerate(res)]
+            fh = []
+            for s_, d_ in sets:
+                fh.append(m.find_homography(s_, d_, 5.0, 20000) + (m.batch_results(1).tobytes(),))
+        finally:
+            m.close()
+            os.environ.pop("MIM_SAMPLER_WALK", None)
+        outs.append((res, masks, fh))
+    (r0, m0, f0), (r1, m1, f1) = outs
+    assert r0.tobytes() == r1.tobytes()
+    for a, b in zip(m0, m1):
+        np.testing.assert_array_equal(a, b)
+    for (ha, ma, ra), (hb, mb, rb) in zip(f0, f1):
+        np.testing.assert_array_equal(ma, mb)
+        assert ra == rb

@@ -1348,7 +1348,13 @@ __device__ int exact_count(const float4* __restrict__ P, int n, int4 s4, double*
     const float4 a = P[s4.x], b = P[s4.y], c = P[s4.z], d = P[s4.w];
     const float M[8] = {a.x, a.y, b.x, b.y, c.x, c.y, d.x, d.y};
     const float m[8] = {a.z, a.w, b.z, b.w, c.z, c.w, d.z, d.w};
+#ifdef MIM_REFINE_PROF
+    const unsigned long long e0 = clock64();
+#endif
     if (!run_kernel4<64>(M, m, D, H)) return -1;
+#ifdef MIM_REFINE_PROF
+    const unsigned long long e1 = clock64();
+#endif
     float Hf[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) Hf[i] = (float)H[i];
@@ -1357,6 +1363,9 @@ __device__ int exact_count(const float4* __restrict__ P, int n, int4 s4, double*
         const float4 q = P[i];
         cnt += reproj_err(Hf, q.x, q.y, q.z, q.w) <= thr2;
     }
+#ifdef MIM_REFINE_PROF
+    if (blockIdx.x < 3) printf("[exact] block %d lane %d: kernel4 %llu count %llu (n=%d)\n", blockIdx.x, (int)threadIdx.x, e1 - e0, clock64() - e1, n);
+#endif
     return cnt;
 }
 
@@ -1427,24 +1436,54 @@ __global__ __launch_bounds__(64) void ransac_exact_kernel(const RansacState* __r
     const RansacState S = st[p];
     if (!S.active || S.done) return;
     const int nc = min(ncand[p], kCandCap);
-    const int k = w * 64 + lane;
-    if (w * 64 >= nc) return;
-    if (k >= nc) return;
+    if (w * 64 >= nc) return;  // uniform over the wave
+    const bool valid = w * 64 + lane < nc;  // lanes past the list only join the counting
+    const int k = min(w * 64 + lane, nc - 1);
     const int t = cand[(long long)p * kCandCap + k];
     const long long o = (long long)p * kCandCap + k;
-    const int2 b = bounds[probs[p].it_off + t];
-    if (b.x == b.y) {  // lo == hi pins the exact count: no eigensolve needed
-        cex[o] = b.x;
-        cH[o * 9 + 8] = 0.0;  // H not computed (H22 of a computed model is never 0)
-        return;
+    const int2 bd = bounds[probs[p].it_off + t];
+    const bool tight = bd.x == bd.y;  // lo == hi pins the exact count: no eigensolve needed
+    double H[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    int ok = 0;
+    const float4* __restrict__ P = pts + probs[p].good_off;
+    if (valid && !tight) {
+        const int4 s4 = decode_sample(samples[probs[p].it_off + t], stream, (unsigned)S.n, S.modM);
+        const float4 a = P[s4.x], b = P[s4.y], c = P[s4.z], d = P[s4.w];
+        const float M[8] = {a.x, a.y, b.x, b.y, c.x, c.y, d.x, d.y};
+        const float m[8] = {a.z, a.w, b.z, b.w, c.z, c.w, d.z, d.w};
+        ok = run_kernel4<64>(M, m, sd + lane, H);
     }
-    double H[9];
-    const int ex = exact_count(pts + probs[p].good_off, S.n,
-                               decode_sample(samples[probs[p].it_off + t], stream, (unsigned)S.n, S.modM), sd + lane,
-                               thr2, H);
-    cex[o] = ex;
+    // findInliers of every solved candidate by the whole wave (computeError is per point: the count
+    // does not depend on the order)
+    float Hf[8];
 #pragma unroll
-    for (int i = 0; i < 9; ++i) cH[o * 9 + i] = H[i];
+    for (int i = 0; i < 8; ++i) Hf[i] = (float)H[i];
+    int ex = tight ? bd.x : -1;
+    unsigned long long todo = __ballot(ok != 0);
+    const int n = S.n;
+    while (todo) {
+        const int c = __builtin_ctzll(todo);
+        todo &= todo - 1;
+        float hc[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) hc[i] = __shfl(Hf[i], c);
+        int cnt = 0;
+        for (int i = lane; i < n; i += 64) {
+            const float4 q = P[i];
+            cnt += reproj_err(hc, q.x, q.y, q.z, q.w) <= thr2;
+        }
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) cnt += __shfl_xor(cnt, off);
+        if (lane == c) ex = cnt;
+    }
+    if (!valid) return;
+    cex[o] = ex;
+    if (tight) {
+        cH[o * 9 + 8] = 0.0;  // H not computed (H22 of a computed model is never 0)
+    } else {
+#pragma unroll
+        for (int i = 0; i < 9; ++i) cH[o * 9 + i] = H[i];
+    }
 }
 
 __global__ __launch_bounds__(64) void ransac_replay_kernel(RansacState* __restrict__ st,
@@ -1854,6 +1893,13 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                                                             int raw, const double* __restrict__ best_h, int exact_all) {
     __shared__ RefineShared sh;
     const int p = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+#ifdef MIM_REFINE_PROF
+    unsigned long long rt[8] = {0, 0, 0, 0, 0, 0, 0, 0}, rc = clock64();
+    int rp_recompute = 0, rp_chol_fail = 0;
+#define RPROF(k) { const unsigned long long t_ = clock64(); rt[k] += t_ - rc; rc = t_; }
+#else
+#define RPROF(k)
+#endif
     const RansacState S = st[p];
     const int ng = n_good_arr[p];
     const long long go = probs[p].good_off;
@@ -1891,6 +1937,9 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
             if (tid == 0 && !exact_all && best_h[(long long)p * 9 + 8] != 0.0) {
                 for (int i = 0; i < 9; ++i) sh.Hb[i] = best_h[(long long)p * 9 + i];  // from the exact pass
             } else if (tid == 0) {  // bestModel = runKernel(sample[best_iter]), bit-identical
+#ifdef MIM_REFINE_PROF
+                rp_recompute = 1;
+#endif
                 const int4 s4 = decode_sample(samples[probs[p].it_off + S.best_iter], stream, (unsigned)S.n, S.modM);
                 const float4 a = P[s4.x], b = P[s4.y], c = P[s4.z], d = P[s4.w];
                 const float M[8] = {a.x, a.y, b.x, b.y, c.x, c.y, d.x, d.y};
@@ -1898,6 +1947,7 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                 run_kernel4<1>(M, m, sh.J9, sh.Hb);
             }
             __syncthreads();
+            RPROF(0);
             float Hf[8];
             for (int i = 0; i < 8; ++i) Hf[i] = (float)sh.Hb[i];
             const float thr2 = (float)(prm.thresh * prm.thresh);
@@ -1926,6 +1976,7 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
             }
             if (tid == 0) sh.n_inl = base;
             __syncthreads();
+            RPROF(1);
             const int k = sh.n_inl;
             if (k > 0) {
                 // ---- refit: runKernel over all inliers (parallel sums; contract is |dH| <= 1e-4) ----
@@ -1962,6 +2013,7 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                             for (int kk = j; kk < 9; kk++, ++e) lt[e] += Lx[j] * Lx[kk] + Ly[j] * Ly[kk];
                     }
                     block_sum<45>(lt, sh.red);
+                    RPROF(2);
                     if (tid == 0) {
                         const double invHnorm[9] = {1. / smx, 0, cmx, 0, 1. / smy, cmy, 0, 0, 1};
                         const double Hnorm2[9] = {sMx, 0, -cMx * sMx, 0, sMy, -cMy * sMy, 0, 0, 1};
@@ -1974,6 +2026,7 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                 // ---- LMSolverImpl (levmarq.cpp) on H8 = H[0..7], maxIters 10, eps FLT_EPSILON ----
                 if (tid < 8) sh.x[tid] = sh.H[tid];
                 __syncthreads();
+                RPROF(3);
                 double x[8];
                 for (int i = 0; i < 8; ++i) x[i] = sh.x[i];
                 double A[64], v[8], Sv, rinf;
@@ -1990,7 +2043,12 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                         double Ap[64];
                         for (int i = 0; i < 64; ++i) Ap[i] = sh.A[i];
                         for (int i = 0; i < 8; ++i) Ap[9 * i] += sh.lambda * sh.D[i];
-                        if (!solve_chol8(Ap, sh.v, sh.d)) solve_eig8(Ap, sh.v, sh.d, sh.J9);
+                        if (!solve_chol8(Ap, sh.v, sh.d)) {
+#ifdef MIM_REFINE_PROF
+                            ++rp_chol_fail;
+#endif
+                            solve_eig8(Ap, sh.v, sh.d, sh.J9);
+                        }
                         double dinf = 0;
                         for (int i = 0; i < 8; ++i) {
                             sh.xd[i] = sh.x[i] - sh.d[i];
@@ -2054,6 +2112,12 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                 }
                 if (tid < 8) sh.H[tid] = sh.x[tid];
                 __syncthreads();
+                RPROF(4);
+#ifdef MIM_REFINE_PROF
+                if (tid == 0 && p < 4)
+                    printf("[refine] p=%d recompute %d: best %llu mask %llu sums %llu refitJacobi %llu LM %llu (iters %d chol_fail %d) k=%d\n",
+                           p, rp_recompute, rt[0], rt[1], rt[2], rt[3], rt[4], iter, rp_chol_fail, k);
+#endif
             } else if (tid == 0) {
                 for (int i = 0; i < 9; ++i) sh.H[i] = sh.Hb[i];
             }

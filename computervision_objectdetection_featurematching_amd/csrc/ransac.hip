@@ -433,11 +433,12 @@ __global__ void ransac_init_kernel(RansacState* __restrict__ st, const int* __re
 // below then only walks the chain of attempt start positions.  flag: 0 checkSubset fails,
 // 1 passes, 2 an index repeats (resolved serially by the walker), 3 beyond the RNG stream.
 // attempts precomputed ahead of the walker: the expected draws of the remaining iterations of the
-// chunk (draws per iteration measured so far, 28 before any) + 25 % + 4096, capped by the buffer
+// chunk (draws per iteration measured so far, 28 before any) + 6 % (25 % unmeasured) + 4096, capped by the buffer
 __device__ __forceinline__ int window_len(const RansacState& S, int c1, int wcap) {
     const int need = min(c1, S.niters) - S.produced;
     const double rate = S.produced > 0 ? (double)S.stream_pos / S.produced : 28.0;
-    const long long w = (long long)((double)need * rate * 1.25) + 4096;
+    // measured rate: the draws of ~46k iterations vary by < 0.5 % (1 sigma), 6 % + 4096 covers them
+    const long long w = (long long)((double)need * rate * (S.produced > 0 ? 1.06 : 1.25)) + 4096;
     return (int)min((long long)wcap, w) & ~63;  // whole 16-byte flag vectors and 32-bit pass words
 }
 

@@ -8,9 +8,10 @@
 // (v_mfma_f32_32x32x16_bf16, fp32 accumulate).  Every operand (0..255, -2q in -510..0) is exact in
 // bf16 and every partial sum is an integer of magnitude < 2^24, so D is exact in any order and
 // d = sqrtf(D + |q_j|^2) is bit-identical to OpenCV's sqrt(normL2Sqr_).
-// Top-2 selection keys on the float distance (ties -> lower train index), computed without a sqrt
-// per pair: a candidate beats the running 2nd best iff its integer d^2 is below the smallest
-// integer whose sqrtf equals the 2nd-best key.
+// Top-2 selection: OpenCV orders by the float distance sqrtf(d^2) (ties -> lower train index).  The
+// sweep keeps, branch-free, the two smallest (d^2, index) per query.  sqrtf is monotone and, below
+// 2^22, injective on integers, so that pair is OpenCV's top-2 whenever the 2nd d^2 < 4e6 (equal d^2
+// keep the lower index); other queries are rescanned exactly by knn2_rescan_kernel.
 //
 // Generic path (any other float rows): per-pair fp32 arithmetic in OpenCV's SSE normL2Sqr_ order
 // (4 accumulators x 4 lanes, no FMA), bit-identical to oracle/mim_oracle.c l2sqr_sse_order.
@@ -70,54 +71,49 @@ __global__ __launch_bounds__(256) void prep_set_kernel(const float* __restrict__
             const float* p = src + (size_t)row * kDim;
             for (int c = 0; c < kDim; ++c) s += p[c] * p[c];
         }
-        norm[row] = s;
+        norm[row] = row < n ? s : FLT_MAX;  // padded rows never win (copied as is by the DMA)
     }
     if (__any(bad) && (tid & 63) == 0) atomicOr(flags, 1);
 }
 
 // ------------------------------------------------------------------------------------------------
-// Running top-2 of one query inside one lane.  Candidates arrive in increasing train index, so an
-// equal key never displaces an earlier one (OpenCV's strict `d < dist[K-1]` / `dist[k] > d`).
+// Running top-2 of one query in the exact integer domain D = d^2 - |q|^2.  Candidates of one
+// selection arrive in increasing train index: strict `<` keeps the earlier of equal D.
 // ------------------------------------------------------------------------------------------------
-struct LaneTop2 {
-    float k1, k2;    // keys (distances), FLT_MAX = absent
-    int i1, i2;      // train indices, INT_MAX = absent
-    float d1, d2;    // exact squared distances of the two entries
-    float T;         // candidate test: D < T  <=>  sqrtf(D + qn) < k2
+struct LaneSel {
+    float m1, m2;  // two smallest D
+    int i1, i2;    // their train indices (INT_MAX = absent)
 };
 
-__device__ __forceinline__ void top2_init(LaneTop2& s) {
-    s.k1 = s.k2 = FLT_MAX;
+__device__ __forceinline__ void sel_init(LaneSel& s) {
+    s.m1 = s.m2 = FLT_MAX;
     s.i1 = s.i2 = INT_MAX;
-    s.d1 = s.d2 = 0.f;
-    s.T = FLT_MAX;
 }
 
-// smallest integer m with sqrtf(m) == key (key = sqrtf(d2), d2 an exact integer < 2^24)
-__device__ __forceinline__ float sqrt_class_floor(float d2, float key) {
-    float lo = d2;
-    while (lo >= 1.f && sqrtf(lo - 1.f) == key) lo -= 1.f;
-    return lo;
+// branch-free insertion of (v, idx): 7 VALU
+__device__ __forceinline__ void sel_push(LaneSel& s, float v, int idx) {
+    const bool c1 = v < s.m1, c2 = v < s.m2;
+    s.m2 = __builtin_amdgcn_fmed3f(s.m1, s.m2, v);
+    s.i2 = c2 ? (c1 ? s.i1 : idx) : s.i2;
+    s.m1 = fminf(s.m1, v);
+    s.i1 = c1 ? idx : s.i1;
 }
 
-// Candidate insertion inside one MFMA tile: d^2 = D + |q|^2 (exact), key = sqrtf(d^2).  Inside a
-// lane candidates come in increasing train index, so `key < k2` (strict) is OpenCV's rule; the
-// threshold T is refreshed once per tile (it only tightens, so the tile-start T is a valid filter).
-__device__ __forceinline__ void top2_insert_exact(LaneTop2& s, float D, float qn, int idx) {
-    const float d2 = D + qn;  // exact: integers < 2^24
-    const float key = sqrtf(d2);
-    if (key < s.k2) {
-        if (key < s.k1) {
-            s.k2 = s.k1; s.i2 = s.i1; s.d2 = s.d1;
-            s.k1 = key;  s.i1 = idx;  s.d1 = d2;
-        } else {
-            s.k2 = key; s.i2 = idx; s.d2 = d2;
-        }
+__device__ __forceinline__ bool dlt(float da, int ia, float db, int ib) { return da < db || (da == db && ia < ib); }
+
+// union of two selections over disjoint rows: two smallest (D, index)
+__device__ __forceinline__ LaneSel sel_merge(LaneSel a, const LaneSel& b) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const float w = k ? b.m2 : b.m1;
+        const int iw = k ? b.i2 : b.i1;
+        const bool l1 = dlt(w, iw, a.m1, a.i1), l2 = dlt(w, iw, a.m2, a.i2);
+        a.m2 = l1 ? a.m1 : (l2 ? w : a.m2);
+        a.i2 = l1 ? a.i1 : (l2 ? iw : a.i2);
+        a.m1 = l1 ? w : a.m1;
+        a.i1 = l1 ? iw : a.i1;
     }
-}
-
-__device__ __forceinline__ void top2_refresh(LaneTop2& s, float qn) {
-    s.T = (s.i2 == INT_MAX) ? FLT_MAX : sqrt_class_floor(s.d2, s.k2) - qn;
+    return a;
 }
 
 __device__ __forceinline__ bool key_less(float ka, int ia, float kb, int ib) {
@@ -139,19 +135,48 @@ __device__ __forceinline__ T2 top2_merge(T2 a, float k, int i) {
     return r;
 }
 
-// D values of one 32x32 MFMA tile for this lane's query: rows (g&3) + 8(g>>2) + 4h, g ascending.
-__device__ __forceinline__ void epilogue(const f32x16& acc, LaneTop2& s, float qn, int row0) {
-    float m = acc[0];
+constexpr int kRescan = -2;  // Top2::i2 marker: the split's top-2 needs the exact rescan
+
+// D value g of a 32x32 MFMA tile is train row (g&3) + 8(g>>2) + 4h of its 32-row block.  Indices
+// are stored without the lane's 4h (uniform, scalar) and corrected at the end.
+//   early tiles (the top-2 still changes often): every value is inserted branch-free into one of 2
+//     independent selections per query (partial k takes g & 1 == k: two shorter dependency chains);
+//   later tiles (the partials merged into one selection): 4 consecutive rows are tested at once
+//     against the 2nd best, the insertion runs only when some lane of the wave has a candidate.
+#ifndef MIM_KNN_EARLY
+#define MIM_KNN_EARLY 12
+#endif
+#ifndef MIM_KNN_GROUP
+#define MIM_KNN_GROUP 4
+#endif
+constexpr int kEarlyTiles = MIM_KNN_EARLY;
+constexpr int kGroup = MIM_KNN_GROUP;  // values tested together in the late tiles (4 or 8)
+
+// late tiles: the hit test of values g = kGroup*j .. kGroup*j + kGroup-1 (branch-free, scheduled
+// between the MFMAs); T = the lane's filter
+__device__ __forceinline__ bool sel_test(const f32x16& p, int j, float T) {
+    float m = fminf(fminf(p[kGroup * j], p[kGroup * j + 1]), p[kGroup * j + 2]);
 #pragma unroll
-    for (int g = 1; g < 16; ++g) m = fminf(m, acc[g]);
-    if (m < s.T) {
-        const float T = s.T;
+    for (int k = 3; k < kGroup; ++k) m = fminf(m, p[kGroup * j + k]);
+    return m < T;
+}
+
+// ... and the insertion of that group for the lanes that hit (rows in increasing order)
+__device__ __forceinline__ void sel_group(const f32x16& p, int j, LaneSel& s, int base) {
 #pragma unroll
-        for (int g = 0; g < 16; ++g) {
-            if (acc[g] < T) top2_insert_exact(s, acc[g], qn, row0 + (g & 3) + 8 * (g >> 2));
-        }
-        top2_refresh(s, qn);
+    for (int k = 0; k < kGroup; ++k) {
+        const int g = kGroup * j + k;
+        sel_push(s, p[g], base + (g & 3) + 8 * (g >> 2));
     }
+}
+
+// Filter of a lane in the late tiles: below its own 2nd best, and not above the other row half's
+// 2nd best (lanes l, l ^ 32 hold the same query; an equal D may still win on the lower index).
+__device__ __forceinline__ float sel_filter(const LaneSel& s) {
+    const int v = __float_as_int(s.m2);
+    const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    const float other = __int_as_float((threadIdx.x & 32) ? r[0] : r[1]);
+    return fminf(s.m2, other + 1.f);  // D are integers: other + 1 keeps D == other
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -162,7 +187,7 @@ __device__ __forceinline__ void epilogue(const f32x16& acc, LaneTop2& s, float q
 // ------------------------------------------------------------------------------------------------
 constexpr int kLdsTile = kTileBytes + 256;  // fragments + 64 norms
 
-__global__ __launch_bounds__(256, 2) void knn2_bf16_kernel(const ProbDev* __restrict__ probs,
+__global__ __launch_bounds__(256, 3) void knn2_bf16_kernel(const ProbDev* __restrict__ probs,
                                                           const KnnWork* __restrict__ works,
                                                           Top2* __restrict__ parts) {
     __shared__ __attribute__((aligned(16))) unsigned char smem[2 * kLdsTile];
@@ -170,7 +195,7 @@ __global__ __launch_bounds__(256, 2) void knn2_bf16_kernel(const ProbDev* __rest
     const ProbDev* P = probs + w.problem;
     if (*P->q.flags | *P->t.flags) return;  // not integer-valued: generic kernel handles it
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, h = lane >> 5, r = lane & 31;
-    const int nq = P->q.n, nt = P->t.n;
+    const int nq = P->q.n;
     const uint4* __restrict__ tsrc = reinterpret_cast<const uint4*>(P->t.frag);
     const float* __restrict__ tnorm = P->t.norm;
 
@@ -194,82 +219,176 @@ __global__ __launch_bounds__(256, 2) void knn2_bf16_kernel(const ProbDev* __rest
             qn[u] = qvalid ? P->q.norm[qtile * 64 + 32 * u + r] : 0.f;
         }
     }
-    LaneTop2 st[2];
-    top2_init(st[0]);
-    top2_init(st[1]);
-
-    // ---- train tile staging (HBM -> registers -> LDS, double buffered) ----
-    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-    typedef const __attribute__((address_space(1))) u32x4 gu4;
-    typedef const __attribute__((address_space(1))) float gf;
-    gu4* tg = (gu4*)tsrc;
-    gf* tng = (gf*)tnorm;
-    u32x4 s0, s1, s2, s3;
-    float sn = FLT_MAX;
-#define GLOAD(tile)                                                     \
-    do {                                                                \
-        const size_t b_ = (size_t)(tile) * 1024 + tid;                  \
-        s0 = tg[b_]; s1 = tg[b_ + 256]; s2 = tg[b_ + 512]; s3 = tg[b_ + 768]; \
-        if (tid < 64) {                                                 \
-            const int row_ = (tile) * 64 + tid;                         \
-            sn = row_ < nt ? tng[row_] : FLT_MAX; /* padded rows never win */ \
-        }                                                               \
-    } while (0)
-#define LSTORE(buf)                                                     \
-    do {                                                                \
-        u32x4* d_ = reinterpret_cast<u32x4*>(smem + (buf) * kLdsTile);  \
-        d_[tid] = s0; d_[tid + 256] = s1; d_[tid + 512] = s2; d_[tid + 768] = s3; \
-        if (tid < 64) reinterpret_cast<float*>(smem + (buf) * kLdsTile + kTileBytes)[tid] = sn; \
-    } while (0)
-
-    if (w.tile0 < w.tile1) {
-        GLOAD(w.tile0);
-        LSTORE(0);
+    LaneSel st[2][2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        sel_init(st[0][k]);
+        sel_init(st[1][k]);
     }
+
+    // ---- train tile staging: HBM -> LDS by DMA (global_load_lds, no VGPR staging), double
+    // buffered; the barrier ending an iteration retires the DMA of the next tile ----
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+#define GLDS(tile, buf)                                                                          \
+    do {                                                                                         \
+        const u32x4* g_ = reinterpret_cast<const u32x4*>(tsrc) + (size_t)(tile) * 1024 + tid;     \
+        u32x4* d_ = reinterpret_cast<u32x4*>(smem + (buf) * kLdsTile) + tid;                     \
+        __builtin_amdgcn_global_load_lds(g_, d_, 16, 0, 0);                                      \
+        __builtin_amdgcn_global_load_lds(g_ + 256, d_ + 256, 16, 0, 0);                          \
+        __builtin_amdgcn_global_load_lds(g_ + 512, d_ + 512, 16, 0, 0);                          \
+        __builtin_amdgcn_global_load_lds(g_ + 768, d_ + 768, 16, 0, 0);                          \
+        if (tid < 64)                                                                            \
+            __builtin_amdgcn_global_load_lds(tnorm + (size_t)(tile) * 64 + tid,                  \
+                                             reinterpret_cast<float*>(smem + (buf) * kLdsTile + kTileBytes) + tid, \
+                                             4, 0, 0);                                           \
+    } while (0)
+
+    if (w.tile0 < w.tile1) GLDS(w.tile0, 0);
     __syncthreads();
+    float T0 = FLT_MAX, T1 = FLT_MAX;  // late-tile filters
     for (int tile = w.tile0; tile < w.tile1; ++tile) {
         const int buf = (tile - w.tile0) & 1;
         const bool more = tile + 1 < w.tile1;
-        if (more) GLOAD(tile + 1);
+        if (more) GLDS(tile + 1, buf ^ 1);
         const bf16x8* A = reinterpret_cast<const bf16x8*>(smem + buf * kLdsTile);
         const float* tn = reinterpret_cast<const float*>(smem + buf * kLdsTile + kTileBytes);
+        const bool early = tile - w.tile0 < kEarlyTiles;
+        if (tile - w.tile0 == kEarlyTiles) {  // switch: fold the partials into selection 0
+            st[0][0] = sel_merge(st[0][0], st[0][1]);
+            st[1][0] = sel_merge(st[1][0], st[1][1]);
+            sel_init(st[0][1]);
+            sel_init(st[1][1]);
+            T0 = sel_filter(st[0][0]);
+            T1 = sel_filter(st[1][0]);
+        }
 #pragma unroll
         for (int u2 = 0; u2 < 2; ++u2) {
-            f32x16 c;
+            f32x16 acc0;
 #pragma unroll
             for (int gg = 0; gg < 4; ++gg) {
                 float4 v = *reinterpret_cast<const float4*>(tn + 32 * u2 + 8 * gg + 4 * h);
-                c[4 * gg + 0] = v.x; c[4 * gg + 1] = v.y; c[4 * gg + 2] = v.z; c[4 * gg + 3] = v.w;
+                acc0[4 * gg + 0] = v.x; acc0[4 * gg + 1] = v.y; acc0[4 * gg + 2] = v.z; acc0[4 * gg + 3] = v.w;
             }
-            f32x16 acc0 = c, acc1 = c;
+            f32x16 acc1 = acc0;
 #pragma unroll
             for (int s = 0; s < 8; ++s) {
                 const bf16x8 a = A[(u2 * 8 + s) * 64 + lane];
                 acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, B[0][s], acc0, 0, 0, 0);
                 acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, B[1][s], acc1, 0, 0, 0);
             }
-            const int row0 = tile * 64 + 32 * u2 + 4 * h;
-            epilogue(acc0, st[0], qn[0], row0);
-            epilogue(acc1, st[1], qn[1], row0);
+            const int row0 = tile * 64 + 32 * u2;
+#ifdef MIM_KNN_NOSEL  // timing probe only: MFMA loop without the selection (results invalid)
+            st[0][0].m1 = fminf(st[0][0].m1, fminf(acc0[0], acc0[15]));
+            st[1][0].m1 = fminf(st[1][0].m1, fminf(acc1[0], acc1[15]));
+            continue;
+#endif
+            if (early) {
+#pragma unroll
+                for (int g = 0; g < 16; ++g) {
+                    const int idx = row0 + (g & 3) + 8 * (g >> 2);
+                    sel_push(st[0][g & 1], acc0[g], idx);
+                    sel_push(st[1][g & 1], acc1[g], idx);
+                }
+            } else {
+                constexpr int NG = 16 / kGroup;
+                bool h0[NG], h1[NG];
+                bool any = false;
+#pragma unroll
+                for (int j = 0; j < NG; ++j) {
+                    h0[j] = sel_test(acc0, j, T0);
+                    h1[j] = sel_test(acc1, j, T1);
+                    any |= h0[j] | h1[j];
+                }
+                if (__builtin_expect(__any(any), 0)) {  // rare past the early tiles
+#pragma unroll
+                    for (int j = 0; j < NG; ++j) {
+                        if (__any(h0[j])) {
+                            if (h0[j]) sel_group(acc0, j, st[0][0], row0);
+                        }
+                        if (__any(h1[j])) {
+                            if (h1[j]) sel_group(acc1, j, st[1][0], row0);
+                        }
+                    }
+                    T0 = sel_filter(st[0][0]);
+                    T1 = sel_filter(st[1][0]);
+                }
+            }
         }
-        if (more) LSTORE(buf ^ 1);
         __syncthreads();
     }
-#undef GLOAD
-#undef LSTORE
+#undef GLDS
 
-    // ---- merge the two lane halves (h = 0/1 hold disjoint train rows of the same query) ----
+    // ---- merge partials and the two lane halves (disjoint train rows of the same query), keys ----
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-        T2 t{st[u].k1, st[u].i1, st[u].k2, st[u].i2};
-        const float ok1 = __shfl_xor(t.k1, 32), ok2 = __shfl_xor(t.k2, 32);
-        const int oi1 = __shfl_xor(t.i1, 32), oi2 = __shfl_xor(t.i2, 32);
-        t = top2_merge(t, ok1, oi1);
-        t = top2_merge(t, ok2, oi2);
+        LaneSel m = sel_merge(st[u][0], st[u][1]);
+        if (m.i1 != INT_MAX) m.i1 += 4 * h;
+        if (m.i2 != INT_MAX) m.i2 += 4 * h;
+        LaneSel o;
+        o.m1 = __shfl_xor(m.m1, 32); o.m2 = __shfl_xor(m.m2, 32);
+        o.i1 = __shfl_xor(m.i1, 32); o.i2 = __shfl_xor(m.i2, 32);
+        m = sel_merge(m, o);
         const int q = qtile * 64 + 32 * u + r;
         if (h == 0 && qvalid && q < nq) {
-            Top2 o{t.k1, t.i1, t.k2, t.i2};
-            parts[P->part_off + (long long)w.split * P->q_pad + q] = o;
+            const float qq = qn[u];
+            Top2 t;
+            t.k1 = m.i1 == INT_MAX ? FLT_MAX : sqrtf(m.m1 + qq);
+            t.k2 = m.i2 == INT_MAX ? FLT_MAX : sqrtf(m.m2 + qq);
+            t.i1 = m.i1;
+            t.i2 = m.i2;
+            // d^2 >= 4e6: distinct integers may share a key (sqrt class), where the lower index
+            // wins: rescan exactly.  Below, equal keys mean equal d^2, already in index order.
+            if (t.i2 != INT_MAX && m.m2 + qq >= 4.0e6f) t.i2 = kRescan;
+            parts[P->part_off + (long long)w.split * P->q_pad + q] = t;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Exact rescan of the queries the distance kernel marked (kRescan): one wave per query over the
+// work item's train rows, fp32 distances of integer rows (exact in any order), keys sqrtf(d^2),
+// (key, index) order.  Rare: the marked queries have a 3rd row in the 2nd key's sqrt class.
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void knn2_rescan_kernel(const ProbDev* __restrict__ probs,
+                                                          const KnnWork* __restrict__ works,
+                                                          Top2* __restrict__ parts) {
+    const KnnWork w = works[blockIdx.x];
+    const ProbDev* P = probs + w.problem;
+    if (*P->q.flags | *P->t.flags) return;  // generic kernel's parts are exact already
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int nq = P->q.n, nt = P->t.n;
+    Top2* out = parts + P->part_off + (long long)w.split * P->q_pad;
+    const int r0 = w.tile0 * 64, r1 = min(w.tile1 * 64, nt);
+    for (int k = 0; k < 256; k += 64) {
+        const int q = w.q0 + k + lane;
+        const bool marked = q < nq && out[q].i2 == kRescan;
+        unsigned long long m = __ballot(marked);
+        // waves take the marked queries round-robin
+        int pick = 0;
+        while (m) {
+            const int b = __builtin_ctzll(m);
+            m &= m - 1;
+            if ((pick++ & 3) != wave) continue;
+            const int qq = w.q0 + k + b;
+            const float* qv = P->q.f32 + (size_t)qq * kDim;
+            T2 t{FLT_MAX, INT_MAX, FLT_MAX, INT_MAX};
+            for (int row = r0 + lane; row < r1; row += 64) {
+                const float* tv = P->t.f32 + (size_t)row * kDim;
+                float d2 = 0.f;
+                for (int c = 0; c < kDim; ++c) {
+                    const float d = qv[c] - tv[c];
+                    d2 = fmaf(d, d, d2);  // integer terms, partial sums < 2^24: exact
+                }
+                t = top2_merge(t, sqrtf(d2), row);
+            }
+#pragma unroll
+            for (int off = 32; off >= 1; off >>= 1) {
+                const float ok1 = __shfl_xor(t.k1, off), ok2 = __shfl_xor(t.k2, off);
+                const int oi1 = __shfl_xor(t.i1, off), oi2 = __shfl_xor(t.i2, off);
+                t = top2_merge(t, ok1, oi1);
+                t = top2_merge(t, ok2, oi2);
+            }
+            if (lane == 0) out[qq] = Top2{t.k1, t.i1, t.k2, t.i2};
         }
     }
 }
@@ -422,6 +541,7 @@ void launch_prep_set(const float* src, int n, uint16_t* frag, float* norm, int* 
 void launch_knn(const ProbDev* probs, const KnnWork* works, int n_works, Top2* parts, hipStream_t st) {
     if (n_works <= 0) return;
     knn2_bf16_kernel<<<n_works, 256, 0, st>>>(probs, works, parts);
+    knn2_rescan_kernel<<<n_works, 256, 0, st>>>(probs, works, parts);
     knn2_f32_kernel<<<n_works, 256, 0, st>>>(probs, works, parts);
 }
 

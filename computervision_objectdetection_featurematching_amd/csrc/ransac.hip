@@ -1310,19 +1310,25 @@ __global__ __launch_bounds__(256) void ransac_bound_kernel(const RansacState* __
         }
         __syncthreads();
         if (count && !widen) {
+            // division-free test with sign-bit counting (v_cmp + v_addc cost ~2x a plain ALU op):
+            //   lo: e - tlo W^2 < 0,   not hi: thi W^2 - e < 0
+            int hineg = 0;
 #pragma unroll 4
             for (int i = 0; i < tpairs; ++i) {
                 const f4v a = tp[3 * i], m = tp[3 * i + 1], t = tp[3 * i + 2];
-                const f2v x = a.xy, y = a.zw;
-                const f2v W = pk_fma(h6, x, pk_fma(h7, y, f2v(1.f)));
-                const f2v ex = pk_fma(m.xy, W, pk_fma(h0, x, pk_fma(h1, y, h2)));
-                const f2v ey = pk_fma(m.zw, W, pk_fma(h3, x, pk_fma(h4, y, h5)));
-                const f2v e = pk_fma(ex, ex, ey * ey);
-                const f2v W2 = W * W;
-                const f2v L = t.xy * W2, U = t.zw * W2;
-                lo += (e.x < L.x) + (e.y < L.y);
-                hi += (e.x <= U.x) + (e.y <= U.y);
+#pragma unroll
+                for (int k = 0; k < 2; ++k) {
+                    const float x = a[k], y = a[2 + k];
+                    const float W = fmaf(Hf[6], x, fmaf(Hf[7], y, 1.f));
+                    const float ex = fmaf(m[k], W, fmaf(Hf[0], x, fmaf(Hf[1], y, Hf[2])));
+                    const float ey = fmaf(m[2 + k], W, fmaf(Hf[3], x, fmaf(Hf[4], y, Hf[5])));
+                    const float e = fmaf(ex, ex, ey * ey);
+                    const float W2 = W * W;
+                    lo += __float_as_uint(fmaf(-t[k], W2, e)) >> 31;
+                    hineg += __float_as_uint(fmaf(t[2 + k], W2, -e)) >> 31;
+                }
             }
+            hi += 2 * tpairs - hineg;
         } else if (count) {
             for (int i = 0; i < tpairs; ++i) {
                 const f4v a = tp[3 * i], m = tp[3 * i + 1], t = tp[3 * i + 2];

@@ -300,6 +300,284 @@ __device__ int run_kernel4(const float* M, const float* m, double* D, double* H)
 }
 
 // ------------------------------------------------------------------------------------------------
+// JacobiImpl_<double> for one 9x9 matrix on a group of 16 lanes (bit-identical to jacobi_fast).
+// One rotation touches 16 disjoint pairs — rows k, l of V (9 pairs) and the 7 (A(i,k), A(i,l)),
+// i != k, l — so slot j of the group rotates pair j.  The pivot search (OpenCV's first maximum over
+// the 16 cached row/column candidates) and the refresh of the caches of rows/columns k and l are
+// group reductions over DPP row permutations: no serial 16-step scans, no barriers.  State lives
+// in LDS (per group: A packed upper | W | V); lane j < 9 keeps indR[j], indC[j] in registers.
+// ------------------------------------------------------------------------------------------------
+constexpr int kJ9G = 36 + 9 + 81;  // doubles of LDS state per group
+
+__device__ __forceinline__ int dpp_row(int v, int ctrl) {
+    switch (ctrl) {  // constant after inlining
+        case 0: return __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false);   // quad_perm 1,0,3,2
+        case 1: return __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, false);   // quad_perm 2,3,0,1
+        case 2: return __builtin_amdgcn_update_dpp(0, v, 0x141, 0xF, 0xF, false);  // row_half_mirror
+        default: return __builtin_amdgcn_update_dpp(0, v, 0x140, 0xF, 0xF, false); // row_mirror
+    }
+}
+
+__device__ __forceinline__ double dpp_row_d(double v, int ctrl) {
+    const long long b = __double_as_longlong(v);
+    const int lo = dpp_row((int)(unsigned)b, ctrl), hi = dpp_row((int)(b >> 32), ctrl);
+    return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+
+// max over the 16 lanes of a DPP row (every lane receives it)
+__device__ __forceinline__ double row_max(double v) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) v = fmax(v, dpp_row_d(v, c));
+    return v;
+}
+
+// lanes of this lane's 16-lane group in a wave ballot, as bits 0..15
+__device__ __forceinline__ unsigned group_bits(unsigned long long m) {
+    return (unsigned)(m >> (threadIdx.x & 48)) & 0xFFFFu;
+}
+
+// First maximum of |A(idx, i)| over the slots' candidate indices (slots 9..15 carry the rotated
+// values, in increasing index order) plus, optionally, a zero entry at index `zi` (-1: none).
+__device__ __forceinline__ int refresh_argmax(double val, bool cand, int im, int zi) {
+    const double mx = row_max(cand ? val : -1.0);
+    const unsigned m = group_bits(__ballot(cand && val == mx));
+    const int first = m ? __shfl(im, (int)(threadIdx.x & 48) + __builtin_ctz(m), 64) : INT_MAX;
+    if (zi < 0) return first;
+    return mx > 0.0 ? first : min(first, zi);
+}
+
+// A/W/V: this group's LDS state (A packed strict upper, W diagonal) written by the caller.
+// Returns, in every slot, the row of V holding the eigenvector of the smallest eigenvalue after
+// OpenCV's descending selection sort.
+__device__ int jacobi9_group(double* __restrict__ A, double* __restrict__ W, double* __restrict__ V) {
+    constexpr int n = 9;
+    const int slot = threadIdx.x & 15;
+    const double eps = DBL_EPSILON;
+    for (int e = slot; e < n * n; e += 16) V[e] = (e % (n + 1) == 0) ? 1.0 : 0.0;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    int indR = 0, indC = 0;
+    if (slot < n - 1) {
+        int m = slot + 1;
+        double mv = fabs(A[pk<n>(slot, slot + 1)]);
+        for (int i = slot + 2; i < n; i++) {
+            const double val = fabs(A[pk<n>(slot, i)]);
+            if (mv < val) mv = val, m = i;
+        }
+        indR = m;
+    }
+    if (slot > 0 && slot < n) {
+        int m = 0;
+        double mv = fabs(A[pk<n>(0, slot)]);
+        for (int i = 1; i < slot; i++) {
+            const double val = fabs(A[pk<n>(i, slot)]);
+            if (mv < val) mv = val, m = i;
+        }
+        indC = m;
+    }
+    for (int iters = 0; iters < n * n * 30; iters++) {
+        // ---- pivot: OpenCV scans rows 0..7 (A(i, indR[i])) then columns 1..8 (A(indC[i], i)) and
+        // keeps the first strict maximum; slot i holds both of its candidates (row first) ----
+        double p = 0.0;
+        int pos = 99, kl = 0;
+        if (slot < n) {
+            const double vr = slot < n - 1 ? A[pk<n>(slot, indR)] : 0.0;
+            const double vc = slot > 0 ? A[pk<n>(indC, slot)] : 0.0;
+            const bool row = slot < n - 1 && (slot == 0 || fabs(vr) >= fabs(vc));
+            p = row ? vr : vc;
+            pos = row ? slot : slot + n - 2;
+            kl = row ? (slot | (indR << 8)) : (indC | (slot << 8));
+        }
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const double po = dpp_row_d(p, c);
+            const int poso = dpp_row(pos, c), klo = dpp_row(kl, c);
+            const bool take = fabs(po) > fabs(p) || (fabs(po) == fabs(p) && poso < pos);
+            p = take ? po : p;
+            pos = take ? poso : pos;
+            kl = take ? klo : kl;
+        }
+        if (fabs(p) <= eps) break;
+        const int k = kl & 255, l = kl >> 8;  // k < l
+        // ---- the pair of this slot ----
+        int im = slot - n;  // slots 9..15: the (slot-9)-th index outside {k, l}
+        if (im >= k) ++im;
+        if (im >= l) ++im;
+        const bool vslot = slot < n;
+        const int ia = vslot ? k * n + slot : pk_any<n>(im, k);
+        const int ib = vslot ? l * n + slot : pk_any<n>(im, l);
+        double* base = vslot ? V : A;
+        const double a0 = base[ia], b0 = base[ib];
+        const double wk = W[k], wl = W[l];
+        const double y = (wl - wk) * 0.5;
+        double t = fabs(y) + d_hypot(p, y);
+        double s = d_hypot(p, t);
+        const double c = t / s;
+        s = p / s;
+        t = (p / t) * p;
+        s = y < 0 ? -s : s;
+        t = y < 0 ? -t : t;
+        const double na = a0 * c - b0 * s;
+        const double nb = a0 * s + b0 * c;
+        base[ia] = na;
+        base[ib] = nb;
+        if (slot == 0) {
+            A[pk<n>(k, l)] = 0;
+            W[k] = wk - t;
+            W[l] = wl + t;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // ---- refresh the cached maxima of rows/columns k and l (row k: A(k,i) = na of the A
+        // slots, plus A(k,l) = 0; row l: nb, plus A(l,k) = 0) ----
+        const bool aslot = !vslot;
+        const double va = fabs(na), vb = fabs(nb);
+        const int rk = refresh_argmax(va, aslot && im > k, im, l);
+        const int ck = refresh_argmax(va, aslot && im < k, im, -1);
+        const int rl = refresh_argmax(vb, aslot && im > l, im, -1);
+        const int cl = refresh_argmax(vb, aslot && im < l, im, k);
+        if (slot == k) {
+            if (k < n - 1) indR = rk;
+            if (k > 0) indC = ck;
+        }
+        if (slot == l) {
+            if (l < n - 1) indR = rl;
+            if (l > 0) indC = cl;
+        }
+    }
+    // ---- OpenCV's selection sort (descending), tracked as a permutation ----
+    double Ws[n];
+    int perm[n];
+#pragma unroll
+    for (int i = 0; i < n; i++) {
+        Ws[i] = W[i];
+        perm[i] = i;
+    }
+#pragma unroll
+    for (int k = 0; k < n - 1; k++) {
+        int m = k;
+        double wm = Ws[k];
+#pragma unroll
+        for (int i = k + 1; i < n; i++)
+            if (wm < Ws[i]) wm = Ws[i], m = i;
+        const double wk = Ws[k];
+        const int pkk = perm[k];
+        int pm = perm[k];
+#pragma unroll
+        for (int i = k + 1; i < n; i++) pm = i == m ? perm[i] : pm;
+#pragma unroll
+        for (int i = k + 1; i < n; i++) {
+            if (i == m) {
+                Ws[i] = wk;
+                perm[i] = pkk;
+            }
+        }
+        Ws[k] = wm;
+        perm[k] = pm;
+    }
+    return perm[n - 1];
+}
+
+// normalized-DLT accumulation of runKernel for `count` points, entry e of LtL (upper incl. the
+// diagonal, row-major) computed by slot e % 16: every entry is the same sum in the same order as
+// run_kernel4 / the oracle (points in order, Lx then Ly).
+__device__ __forceinline__ void dlt_entries_group(const float* M, const float* m, int count, double cmx, double cmy,
+                                                  double cMx, double cMy, double smx, double smy, double sMx,
+                                                  double sMy, double* __restrict__ A, double* __restrict__ W) {
+    const int slot = threadIdx.x & 15;
+    for (int e = slot; e < 45; e += 16) {
+        int j = 0, r = e;
+        while (r >= 9 - j) { r -= 9 - j; ++j; }
+        const int kk = j + r;
+        double acc = 0;
+        for (int i = 0; i < count; i++) {
+            const double x = (m[2 * i] - cmx) * smx, y = (m[2 * i + 1] - cmy) * smy;
+            const double X = (M[2 * i] - cMx) * sMx, Y = (M[2 * i + 1] - cMy) * sMy;
+            const double Lx[9] = {X, Y, 1, 0, 0, 0, -x * X, -x * Y, -x};
+            const double Ly[9] = {0, 0, 0, X, Y, 1, -y * X, -y * Y, -y};
+            acc += Lx[j] * Lx[kk] + Ly[j] * Ly[kk];
+        }
+        if (kk == j) W[j] = acc;
+        else A[pk<9>(j, kk)] = acc;
+    }
+}
+
+// runKernel on the 4 points of a minimal sample, by a 16-lane group (bit-identical to run_kernel4).
+// D: the group's kJ9G doubles of LDS.  Every slot returns the result and H.
+__device__ int run_kernel4_group(const float* M, const float* m, double* D, double* H) {
+    const int count = 4;
+    double cMx = 0, cMy = 0, cmx = 0, cmy = 0, sMx = 0, sMy = 0, smx = 0, smy = 0;
+#pragma unroll
+    for (int i = 0; i < count; i++) {
+        cmx += m[2 * i]; cmy += m[2 * i + 1];
+        cMx += M[2 * i]; cMy += M[2 * i + 1];
+    }
+    cmx /= count; cmy /= count; cMx /= count; cMy /= count;
+#pragma unroll
+    for (int i = 0; i < count; i++) {
+        smx += fabs(m[2 * i] - cmx);
+        smy += fabs(m[2 * i + 1] - cmy);
+        sMx += fabs(M[2 * i] - cMx);
+        sMy += fabs(M[2 * i + 1] - cMy);
+    }
+    if (fabs(smx) < DBL_EPSILON || fabs(smy) < DBL_EPSILON || fabs(sMx) < DBL_EPSILON || fabs(sMy) < DBL_EPSILON)
+        return 0;
+    smx = count / smx; smy = count / smy; sMx = count / sMx; sMy = count / sMy;
+    double* A = D;
+    double* W = D + 36;
+    double* V = D + 45;
+    dlt_entries_group(M, m, count, cmx, cmy, cMx, cMy, smx, smy, sMx, sMy, A, W);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int r = jacobi9_group(A, W, V);
+    const double invHnorm[9] = {1. / smx, 0, cmx, 0, 1. / smy, cmy, 0, 0, 1};
+    const double Hnorm2[9] = {sMx, 0, -cMx * sMx, 0, sMy, -cMy * sMy, 0, 0, 1};
+    double H0[9], Ht[9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) H0[i] = V[r * 9 + i];
+    mat3_mul(invHnorm, H0, Ht);
+    mat3_mul(Ht, Hnorm2, H0);
+    const double sc = 1. / H0[8];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) H[i] = H0[i] * sc;
+    return 1;
+}
+
+// dlt_finish by a 16-lane group: lt (upper incl. diagonal, every slot holds it) -> H
+__device__ void dlt_finish_group(const double* lt, double* D, const double* invHnorm, const double* Hnorm2,
+                                 double* H) {
+    const int slot = threadIdx.x & 15;
+    double* A = D;
+    double* W = D + 36;
+    double* V = D + 45;
+    for (int e = slot; e < 45; e += 16) {
+        int j = 0, r = e;
+        while (r >= 9 - j) { r -= 9 - j; ++j; }
+        const int kk = j + r;
+        double v = 0;
+#pragma unroll
+        for (int q = 0; q < 45; ++q) v = q == e ? lt[q] : v;
+        if (kk == j) W[j] = v;
+        else A[pk<9>(j, kk)] = v;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int r = jacobi9_group(A, W, V);
+    double H0[9], Ht[9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) H0[i] = V[r * 9 + i];
+    mat3_mul(invHnorm, H0, Ht);
+    mat3_mul(Ht, Hnorm2, H0);
+    const double sc = 1. / H0[8];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) H[i] = H0[i] * sc;
+}
+
+// ------------------------------------------------------------------------------------------------
 // checkSubset (fundam.cpp haveCollinearPoints + the Marquez-Neila orientation test), fp64
 // ------------------------------------------------------------------------------------------------
 __device__ __forceinline__ bool collinear4(const float* xy) {
@@ -1427,6 +1705,11 @@ __global__ __launch_bounds__(64) void ransac_cand_kernel(RansacState* __restrict
     }
 }
 
+// Exact evaluation of the listed candidates: 4 per wave, each solved by a 16-lane group
+// (cooperative Jacobi), then counted by the whole wave.
+constexpr int kExactGroups = 4;
+constexpr int kExactWaves = kCandCap / kExactGroups;
+
 __global__ __launch_bounds__(64) void ransac_exact_kernel(const RansacState* __restrict__ st,
                                                           const ProbDev* __restrict__ probs,
                                                           const float4* __restrict__ pts,
@@ -1435,17 +1718,17 @@ __global__ __launch_bounds__(64) void ransac_exact_kernel(const RansacState* __r
                                                           const int* __restrict__ cand, const int* __restrict__ ncand,
                                                           const int2* __restrict__ bounds,
                                                           int* __restrict__ cex, double* __restrict__ cH, float thr2) {
-    __shared__ double sd[kJ9D * 64];
+    __shared__ double sd[kExactGroups * kJ9G];
     // problem-minor block order: the first (and usually only) busy wave of every problem comes
     // first and lands on all 8 XCDs (blocks b and b+8 share an XCD under round-robin dispatch)
-    const int np = gridDim.x / kCandWaves;
-    const int p = blockIdx.x % np, w = blockIdx.x / np, lane = threadIdx.x;
+    const int np = gridDim.x / kExactWaves;
+    const int p = blockIdx.x % np, w = blockIdx.x / np, lane = threadIdx.x, grp = lane >> 4, slot = lane & 15;
     const RansacState S = st[p];
     if (!S.active || S.done) return;
     const int nc = min(ncand[p], kCandCap);
-    if (w * 64 >= nc) return;  // uniform over the wave
-    const bool valid = w * 64 + lane < nc;  // lanes past the list only join the counting
-    const int k = min(w * 64 + lane, nc - 1);
+    if (w * kExactGroups >= nc) return;  // uniform over the wave
+    const bool valid = w * kExactGroups + grp < nc;  // groups past the list only join the counting
+    const int k = min(w * kExactGroups + grp, nc - 1);
     const int t = cand[(long long)p * kCandCap + k];
     const long long o = (long long)p * kCandCap + k;
     const int2 bd = bounds[probs[p].it_off + t];
@@ -1453,12 +1736,12 @@ __global__ __launch_bounds__(64) void ransac_exact_kernel(const RansacState* __r
     double H[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
     int ok = 0;
     const float4* __restrict__ P = pts + probs[p].good_off;
-    if (valid && !tight) {
+    if (valid && !tight) {  // uniform over the group
         const int4 s4 = decode_sample(samples[probs[p].it_off + t], stream, (unsigned)S.n, S.modM);
         const float4 a = P[s4.x], b = P[s4.y], c = P[s4.z], d = P[s4.w];
         const float M[8] = {a.x, a.y, b.x, b.y, c.x, c.y, d.x, d.y};
         const float m[8] = {a.z, a.w, b.z, b.w, c.z, c.w, d.z, d.w};
-        ok = run_kernel4<64>(M, m, sd + lane, H);
+        ok = run_kernel4_group(M, m, sd + grp * kJ9G, H);
     }
     // findInliers of every solved candidate by the whole wave (computeError is per point: the count
     // does not depend on the order)
@@ -1466,7 +1749,7 @@ __global__ __launch_bounds__(64) void ransac_exact_kernel(const RansacState* __r
 #pragma unroll
     for (int i = 0; i < 8; ++i) Hf[i] = (float)H[i];
     int ex = tight ? bd.x : -1;
-    unsigned long long todo = __ballot(ok != 0);
+    unsigned long long todo = __ballot(ok != 0 && slot == 0);
     const int n = S.n;
     while (todo) {
         const int c = __builtin_ctzll(todo);
@@ -1483,7 +1766,7 @@ __global__ __launch_bounds__(64) void ransac_exact_kernel(const RansacState* __r
         for (int off = 32; off >= 1; off >>= 1) cnt += __shfl_xor(cnt, off);
         if (lane == c) ex = cnt;
     }
-    if (!valid) return;
+    if (!valid || slot != 0) return;
     cex[o] = ex;
     if (tight) {
         cH[o * 9 + 8] = 0.0;  // H not computed (H22 of a computed model is never 0)
@@ -1923,13 +2206,18 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
     }
     int ok = 0;
     if (!S.active) {  // n == 4: findHomography calls runKernel directly, mask = ones, no refine
-        if (tid == 0) {
+        if (tid < 16) {  // one 16-lane group
             float M[8], m[8];
             for (int i = 0; i < 4; ++i) {
                 const float4 q = P[i];
                 M[2 * i] = q.x; M[2 * i + 1] = q.y; m[2 * i] = q.z; m[2 * i + 1] = q.w;
             }
-            sh.flag = run_kernel4<1>(M, m, sh.J9, sh.H);
+            double Hl[9];
+            const int f = run_kernel4_group(M, m, sh.J9, Hl);
+            if (tid == 0) {
+                sh.flag = f;
+                for (int i = 0; i < 9; ++i) sh.H[i] = Hl[i];
+            }
         }
         __syncthreads();
         ok = sh.flag;
@@ -1943,7 +2231,8 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
             // bestModel = runKernel(sample[best_iter]) (bit-identical to the hypo kernel's)
             if (tid == 0 && !exact_all && best_h[(long long)p * 9 + 8] != 0.0) {
                 for (int i = 0; i < 9; ++i) sh.Hb[i] = best_h[(long long)p * 9 + i];  // from the exact pass
-            } else if (tid == 0) {  // bestModel = runKernel(sample[best_iter]), bit-identical
+            } else if (tid < 16 && (exact_all || best_h[(long long)p * 9 + 8] == 0.0)) {
+                // bestModel = runKernel(sample[best_iter]), bit-identical, by one 16-lane group
 #ifdef MIM_REFINE_PROF
                 rp_recompute = 1;
 #endif
@@ -1951,7 +2240,10 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                 const float4 a = P[s4.x], b = P[s4.y], c = P[s4.z], d = P[s4.w];
                 const float M[8] = {a.x, a.y, b.x, b.y, c.x, c.y, d.x, d.y};
                 const float m[8] = {a.z, a.w, b.z, b.w, c.z, c.w, d.z, d.w};
-                run_kernel4<1>(M, m, sh.J9, sh.Hb);
+                double Hl[9];
+                run_kernel4_group(M, m, sh.J9, Hl);
+                if (tid == 0)
+                    for (int i = 0; i < 9; ++i) sh.Hb[i] = Hl[i];
             }
             __syncthreads();
             RPROF(0);
@@ -2021,10 +2313,13 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                     }
                     block_sum<45>(lt, sh.red);
                     RPROF(2);
-                    if (tid == 0) {
+                    if (tid < 16) {  // one 16-lane group
                         const double invHnorm[9] = {1. / smx, 0, cmx, 0, 1. / smy, cmy, 0, 0, 1};
                         const double Hnorm2[9] = {sMx, 0, -cMx * sMx, 0, sMy, -cMy * sMy, 0, 0, 1};
-                        dlt_finish<1>(lt, sh.J9, invHnorm, Hnorm2, sh.H);
+                        double Hl[9];
+                        dlt_finish_group(lt, sh.J9, invHnorm, Hnorm2, Hl);
+                        if (tid == 0)
+                            for (int i = 0; i < 9; ++i) sh.H[i] = Hl[i];
                     }
                 } else if (tid == 0) {
                     for (int i = 0; i < 9; ++i) sh.H[i] = sh.Hb[i];  // runKernel returned 0: H kept
@@ -2217,7 +2512,7 @@ void ransac_enqueue(const RansacParams& prm, int n_probs, const ProbDev* probs, 
                 for (int v : h) { sum += v; mx = std::max(mx, v); }
                 fprintf(stderr, "[mim] chunk [%d,%d): candidates mean %.1f max %d\n", c0, c1, (double)sum / n_probs, mx);
             }
-            ransac_exact_kernel<<<n_probs * kCandWaves, 64, 0, s>>>(b.state, probs, pts, b.samples, b.stream, b.cand,
+            ransac_exact_kernel<<<n_probs * kExactWaves, 64, 0, s>>>(b.state, probs, pts, b.samples, b.stream, b.cand,
                                                                    b.ncand, b.bounds, b.cex, b.cH, thr2);
             mark(mark_ctx, "exact");
             ransac_replay_kernel<<<n_probs, 64, 0, s>>>(b.state, probs, pts, b.samples, b.stream, b.bounds, b.cand,

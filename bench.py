@@ -28,7 +28,19 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, no sparsity)
+PEAK_F32_VALU_TFLOPS = 157.3  # MI355X fp32 vector (VALU) peak
 PEAK_HBM_GBS = 8000.0
+FLOP_PER_POINT_EVAL = 17      # one fp32 reprojection test of a hypothesis on a point
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
+
+
+def pmc_traffic(kernel):
+    """HBM bytes per step of `kernel` from the committed rocprofv3 PMC passes (or None)."""
+    try:
+        with open(TRAFFIC_FILE) as f:
+            return json.load(f)["kernels"][kernel]["hbm_bytes_per_step"]
+    except (OSError, KeyError, ValueError):
+        return None
 
 
 def parse():
@@ -120,7 +132,8 @@ def main():
         step()
         if not args.no_timing:
             m.batch_results(n_probs)  # collects this step's HIP events (sync)
-            for k in ("knn", "ratio", "attempt", "chain", "sample", "hypo", "score", "cand", "exact", "select", "refine"):
+            for k in ("knn", "ratio", "attempt", "chain", "sample", "hypo", "score", "cand", "exact", "select",
+                      "refine"):
                 kern[k] = kern.get(k, 0.0) + max(m.kernel_ms(k), 0.0)
     torch.cuda.synchronize()
     if world > 1:
@@ -136,18 +149,35 @@ def main():
     if rank == 0:
         knn_flops = 2.0 * cfg["nq"] * cfg["nt"] * 128 * n_probs
         knn_bytes = (4 * 128 * (cfg["nq"] + cfg["nt"]) + 16 * cfg["nq"]) * n_probs
+        # bound kernel: every produced iteration's hypothesis is tested on every good match
+        point_evals = float(np.sum(res["iters"].astype(np.float64) * res["n_good"]))
         steps = max(args.steps, 1)
         kavg = {k: v / steps for k, v in kern.items()}
         dom = max(kavg, key=kavg.get) if kavg else None
-        roof = None
+        rooflines = {}
         if kavg.get("knn", 0) > 0:
             ach = knn_flops / (kavg["knn"] * 1e-3) / 1e12
-            roof = {"kernel": "knn2_bf16 (distance + top-2)", "bound": "mfma", "achieved": round(ach, 2),
-                    "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s", "frac": round(ach / PEAK_BF16_TFLOPS, 4),
-                    "traffic": None, "algorithmic_bytes": knn_bytes,
-                    "achieved_hbm_GBs": round(knn_bytes / (kavg["knn"] * 1e-3) / 1e9, 1),
-                    "dominant_kernel_by_time": dom,
-                    "kernel_ms_per_step": {k: round(v, 3) for k, v in kavg.items()}}
+            t = pmc_traffic("knn2_bf16_kernel")
+            rooflines["knn"] = {"kernel": "knn2_bf16 (distance GEMM + top-2 selection), 1 launch/step", "bound": "mfma",
+                                "achieved": round(ach, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                                "frac": round(ach / PEAK_BF16_TFLOPS, 4), "traffic": t,
+                                "algorithmic_bytes": knn_bytes,
+                                "achieved_hbm_GBs": round(knn_bytes / (kavg["knn"] * 1e-3) / 1e9, 1)}
+        if kavg.get("score", 0) > 0:
+            ach = FLOP_PER_POINT_EVAL * point_evals / (kavg["score"] * 1e-3) / 1e12
+            t = pmc_traffic("ransac_bound_kernel")
+            rooflines["score"] = {"kernel": "ransac_bound (closed-form hypotheses, bounded inlier counts), 2 launches/step",
+                                  "bound": "valu", "achieved": round(ach, 2), "peak": PEAK_F32_VALU_TFLOPS,
+                                  "unit": "TFLOP/s", "frac": round(ach / PEAK_F32_VALU_TFLOPS, 4), "traffic": t,
+                                  "point_evals_per_step": point_evals,
+                                  "hypothesis_point_evals_per_s": round(point_evals / (kavg["score"] * 1e-3), 1)}
+        roof = None
+        if rooflines:
+            key = max(rooflines, key=lambda k: kavg.get(k, 0))  # the dominant of the two hot kernels
+            roof = dict(rooflines[key])
+            roof["dominant_kernel_by_time"] = dom
+            roof["kernel_ms_per_step"] = {k: round(v, 3) for k, v in kavg.items()}
+            roof["others"] = {k: v for k, v in rooflines.items() if k != key}
         accepted = int((res["status"] == 0).sum())
         out = {
             "metric": "matches+homographies/sec (10k x 10k SIFT, 50k RANSAC iters)" if args.config == "c3"

@@ -5,19 +5,19 @@
 // calib3d/src/ptsetreg.cpp (RANSACPointSetRegistrator::run/getSubset/findInliers,
 // RANSACUpdateNumIters), calib3d/src/levmarq.cpp (LMSolverImpl), core/src/lapack.cpp (Jacobi).
 //
-// The sequential RANSAC loop is re-cut into data-parallel stages with identical results:
-//   sample  one wave per problem replays cv::RNG((uint64)-1) + getSubset + checkSubset with 64
-//           speculative subset attempts per round (attempt j assumed to start 4j draws ahead; the
-//           first attempt with a repeated index is resolved serially and later lanes re-issued);
-//   hypo    one lane per iteration: normalized DLT + OpenCV's Jacobi eigensolver in fp64, bit-exact
-//           (matrix state lives in LDS, [element][lane] interleaved: conflict-free dynamic indexing);
-//   score   one lane per iteration, points streamed through scalar loads: fp32 computeError,
-//           no FMA contraction, IEEE division — the reference's float arithmetic bit for bit;
-//   select  one wave per problem replays "goodCount > max(best,3)" + RANSACUpdateNumIters in
-//           iteration order (ballot over 64 iterations at a time);
-//   refine  one block per problem: best mask, inlier compaction, refit DLT and 10-iteration
+// The sequential RANSAC loop is re-cut into data-parallel stages with identical results
+// (DESIGN.md section 4):
+//   attempt  every getSubset attempt outcome of a window of stream positions, GPU-wide;
+//   irr/chain  the chain of attempt start positions walked over its repeated-index redraws only,
+//           passing attempts ranked and written in parallel (sample: exact attempt-by-attempt walker
+//           for whatever the chain kernel leaves);
+//   bound    closed-form homography per iteration + lower/upper bounds of its inlier count;
+//   cand/exact/replay  only iterations that can be a new best are solved with OpenCV's exact
+//           arithmetic (normalized DLT + JacobiImpl_ on a 16-lane group, bit-identical), counted,
+//           and replayed in iteration order with RANSACUpdateNumIters;
+//   refine   one block per problem: best mask, inlier compaction, refit DLT and 10-iteration
 //           Levenberg-Marquardt in fp64 (block reductions), determinant and gates.
-// Chunks of iterations grow geometrically so adaptive termination (niters) stops the work early.
+// Reference mode (MIM_RANSAC_EXACT=1): hypo/score/select evaluate every iteration exactly.
 #include <float.h>
 
 #include <algorithm>

@@ -1672,36 +1672,51 @@ constexpr int kCandWaves = 16;                 // exact-evaluation waves per pro
 constexpr int kCandCap = kCandWaves * 64;      // listed candidates per problem and chunk
 static_assert(kCandCap == kCandPerProblem, "candidate list layout shared with api.cpp");
 
-__global__ __launch_bounds__(64) void ransac_cand_kernel(RansacState* __restrict__ st,
-                                                         const ProbDev* __restrict__ probs,
-                                                         const int2* __restrict__ bounds, int c1,
-                                                         int* __restrict__ cand, int* __restrict__ ncand) {
-    const int p = blockIdx.x, lane = threadIdx.x;
-    RansacState S = st[p];
-    int nc_total = 0;
-    if (S.active && !S.done) {
-        const int2* Bd = bounds + probs[p].it_off;
-        const int end = min(c1, S.produced);
+// Candidates of one chunk: iteration t is listed iff hi_t > max(3, maxGoodCount, earlier lower
+// bounds) — a prefix maximum over the chunk, computed by a 1024-thread block (contiguous ranges
+// per thread, block max-scan, ordered compaction).
+constexpr int kCandThreads = 1024;
+
+__global__ __launch_bounds__(kCandThreads) void ransac_cand_kernel(RansacState* __restrict__ st,
+                                                                   const ProbDev* __restrict__ probs,
+                                                                   const int2* __restrict__ bounds, int c1,
+                                                                   int* __restrict__ cand, int* __restrict__ ncand) {
+    __shared__ int wred[kCandThreads / 64], wred2[kCandThreads / 64];
+    const int p = blockIdx.x, tid = threadIdx.x;
+    const RansacState S = st[p];
+    if (!S.active || S.done) {
+        if (tid == 0) ncand[p] = 0;
+        return;
+    }
+    const int2* Bd = bounds + probs[p].it_off;
+    const int t0 = S.next_iter, t1 = max(t0, min(min(c1, S.produced), S.niters));
+    const int ch = (t1 - t0 + kCandThreads - 1) / kCandThreads;
+    const int a = min(t1, t0 + tid * ch), e = min(t1, a + ch);
+    int lmax = INT_MIN;
+    for (int t = a; t < e; ++t) lmax = max(lmax, Bd[t].x);
+    const int init = max(3, max(S.max_good, S.lo_max));
+    int all;
+    const int run0 = block_excl_max(lmax, init, wred, all);  // bound before this thread's first iteration
+    int cnt = 0, run = run0;
+    for (int t = a; t < e; ++t) {
+        const int2 b = Bd[t];
+        cnt += b.y > run;
+        run = max(run, b.x);
+    }
+    int total;
+    int o = block_excl_sum(cnt, wred2, total);
+    if (cnt && o < kCandCap) {  // ordered list (beyond the capacity the replay kernel rescans)
         int* C = cand + (long long)p * kCandCap;
-        for (int base = S.next_iter; base < end && base < S.niters; base += 64) {
-            const int t = base + lane;
-            const bool valid = t < end;
-            const int2 b = valid ? Bd[t] : make_int2(-1, -1);
-            const int lb = max(max(3, max(S.max_good, S.lo_max)), wave_excl_prefix_max(b.x));
-            const bool c = valid && t < S.niters && b.y > lb;
-            S.lo_max = max(S.lo_max, wave_max(b.x));
-            const unsigned long long cm = __ballot(c);
-            const int pos = __builtin_amdgcn_mbcnt_hi((uint32_t)(cm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)cm, 0));
-            if (c) {
-                // beyond the list capacity the replay kernel evaluates inline (marked by -t-1)
-                if (nc_total + pos < kCandCap) C[nc_total + pos] = t;
-            }
-            nc_total += __popcll(cm);
+        run = run0;
+        for (int t = a; t < e && o < kCandCap; ++t) {
+            const int2 b = Bd[t];
+            if (b.y > run) C[o++] = t;
+            run = max(run, b.x);
         }
     }
-    if (lane == 0) {
-        ncand[p] = nc_total;
-        st[p].lo_max = S.lo_max;
+    if (tid == 0) {
+        ncand[p] = total;
+        st[p].lo_max = max(S.lo_max, all);
     }
 }
 
@@ -2502,7 +2517,7 @@ void ransac_enqueue(const RansacParams& prm, int n_probs, const ProbDev* probs, 
             ransac_bound_kernel<<<n_probs * bpp256, 256, 0, s>>>(b.state, probs, pts, b.samples, b.stream, b.bounds, c0, c1,
                                                                 bpp256, thr2);
             mark(mark_ctx, "score");
-            ransac_cand_kernel<<<n_probs, 64, 0, s>>>(b.state, probs, b.bounds, c1, b.cand, b.ncand);
+            ransac_cand_kernel<<<n_probs, kCandThreads, 0, s>>>(b.state, probs, b.bounds, c1, b.cand, b.ncand);
             mark(mark_ctx, "cand");
             if (getenv("MIM_DEBUG_NCAND")) {
                 std::vector<int> h(n_probs);

@@ -132,7 +132,7 @@ def main():
         step()
         if not args.no_timing:
             m.batch_results(n_probs)  # collects this step's HIP events (sync)
-            for k in ("knn", "ratio", "attempt", "chain", "sample", "hypo", "score", "cand", "exact", "select",
+            for k in ("knn", "ratio", "attempt", "chain", "check", "sample", "hypo", "score", "cand", "exact", "select",
                       "refine"):
                 kern[k] = kern.get(k, 0.0) + max(m.kernel_ms(k), 0.0)
     torch.cuda.synchronize()

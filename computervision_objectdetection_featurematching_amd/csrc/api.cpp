@@ -27,6 +27,7 @@ void launch_knn(const ProbDev* probs, const KnnWork* works, int n_works, Top2* p
 void launch_ratio(const ProbDev* probs, int n_probs, const Top2* parts, float ratio, int32_t* good_q,
                   int32_t* good_t, float4* pts, int* n_good, int32_t* knn_idx, float* knn_dist,
                   hipStream_t st);
+size_t ransac_chain_bytes();
 void ransac_enqueue(const RansacParams& prm, int n_probs, const ProbDev* probs, const float4* pts,
                     const int* n_good, const RansacBufs& b, uint8_t* masks, mim_result* results, int raw,
                     hipStream_t s, void (*mark)(void*, const char*), void* mark_ctx, int exact_all);
@@ -96,7 +97,7 @@ struct SetRec {
 namespace mim {
 // RANSAC workspace (definition shared with ransac.hip through this layout)
 struct RansacWs {
-    DevBuf state, samples, hyp, counts, bounds, flags, irr, irr_cnt, pass_bits, best_h, cand, ncand, cex, cH, stream,
+    DevBuf state, samples, hyp, counts, bounds, flags, irr, irr_cnt, pass_bits, chains, best_h, cand, ncand, cex, cH, stream,
         scratch, inl, err;
     long long stream_len = 0;
 };
@@ -210,7 +211,7 @@ void mim_ctx_destroy(mim_ctx* c) {
     c->arena.release();
     for (DevBuf* b : {&c->probs, &c->works, &c->parts, &c->good_q, &c->good_t, &c->pts, &c->n_good,
                       &c->results, &c->masks, &c->knn_idx, &c->knn_dist, &c->rws.state, &c->rws.samples,
-                      &c->rws.hyp, &c->rws.counts, &c->rws.bounds, &c->rws.flags, &c->rws.irr, &c->rws.irr_cnt, &c->rws.pass_bits, &c->rws.best_h, &c->rws.cand, &c->rws.ncand, &c->rws.cex, &c->rws.cH, &c->rws.stream, &c->rws.scratch, &c->rws.inl, &c->rws.err})
+                      &c->rws.hyp, &c->rws.counts, &c->rws.bounds, &c->rws.flags, &c->rws.irr, &c->rws.irr_cnt, &c->rws.pass_bits, &c->rws.chains, &c->rws.best_h, &c->rws.cand, &c->rws.ncand, &c->rws.cex, &c->rws.cH, &c->rws.stream, &c->rws.scratch, &c->rws.inl, &c->rws.err})
         b->release();
     if (c->own) (void)hipStreamDestroy(c->own);
     delete c;
@@ -597,6 +598,7 @@ static mim_status ransac_prepare(mim_ctx* c, int n, const mim_params* prm, Ransa
     HIPCHK(c, c->rws.irr.ensure(sizeof(int) * (size_t)std::max(n, 1) * irr_blocks * kIrrCap));
     HIPCHK(c, c->rws.irr_cnt.ensure(sizeof(int) * (size_t)std::max(n, 1) * irr_blocks));
     HIPCHK(c, c->rws.pass_bits.ensure((size_t)flag_cap / 8));
+    HIPCHK(c, c->rws.chains.ensure(ransac_chain_bytes() * (size_t)std::max(n, 1)));
     HIPCHK(c, c->rws.best_h.ensure(sizeof(double) * 9 * std::max(n, 1)));
     const size_t cap = (size_t)std::max(n, 1) * kCandPerProblem;
     HIPCHK(c, c->rws.cand.ensure(sizeof(int) * cap));
@@ -625,6 +627,7 @@ static mim_status ransac_prepare(mim_ctx* c, int n, const mim_params* prm, Ransa
     b.irr_cnt = c->rws.irr_cnt.as<int>();
     b.pass_bits = c->rws.pass_bits.as<uint32_t>();
     b.irr_blocks = irr_blocks;
+    b.chains = c->rws.chains.p;
     b.stream = c->rws.stream.as<uint32_t>();
     b.stream_len = c->rws.stream_len;
     b.inl = c->rws.inl.as<float4>();
@@ -652,6 +655,7 @@ static mim_status ransac_enqueue_range(mim_ctx* c, int p0, int np, const RansacB
     g.irr += (long long)p0 * b.irr_blocks * kIrrCap;
     g.irr_cnt += (long long)p0 * b.irr_blocks;
     g.pass_bits += (long long)p0 * flag_per / 32;
+    g.chains = static_cast<char*>(b.chains) + (size_t)p0 * ransac_chain_bytes();
     g.best_h += 9LL * p0;
     g.cand += (long long)p0 * kCandPerProblem;
     g.ncand += p0;

@@ -90,12 +90,16 @@ __device__ __forceinline__ void sel_init(LaneSel& s) {
     s.i1 = s.i2 = INT_MAX;
 }
 
+// min without IEEE-mode operand canonicalisation (fminf emits v_max x,x per operand): D values are
+// finite integers or FLT_MAX, never NaN, and >= -FLT_MAX
+__device__ __forceinline__ float dmin(float a, float b) { return __builtin_amdgcn_fmed3f(a, b, -FLT_MAX); }
+
 // branch-free insertion of (v, idx): 7 VALU
 __device__ __forceinline__ void sel_push(LaneSel& s, float v, int idx) {
     const bool c1 = v < s.m1, c2 = v < s.m2;
     s.m2 = __builtin_amdgcn_fmed3f(s.m1, s.m2, v);
     s.i2 = c2 ? (c1 ? s.i1 : idx) : s.i2;
-    s.m1 = fminf(s.m1, v);
+    s.m1 = dmin(s.m1, v);
     s.i1 = c1 ? idx : s.i1;
 }
 
@@ -139,8 +143,9 @@ constexpr int kRescan = -2;  // Top2::i2 marker: the split's top-2 needs the exa
 
 // D value g of a 32x32 MFMA tile is train row (g&3) + 8(g>>2) + 4h of its 32-row block.  Indices
 // are stored without the lane's 4h (uniform, scalar) and corrected at the end.
-//   early tiles (the top-2 still changes often): every value is inserted branch-free into one of 2
-//     independent selections per query (partial k takes g & 1 == k: two shorter dependency chains);
+//   early tiles (the top-2 still changes often): every value is inserted branch-free (kPartials
+//     independent selections per query: 1 measured best, it keeps the kernel at 128 VGPRs = 4
+//     waves/SIMD);
 //   later tiles (the partials merged into one selection): 4 consecutive rows are tested at once
 //     against the 2nd best, the insertion runs only when some lane of the wave has a candidate.
 #ifndef MIM_KNN_EARLY
@@ -149,15 +154,22 @@ constexpr int kRescan = -2;  // Top2::i2 marker: the split's top-2 needs the exa
 #ifndef MIM_KNN_GROUP
 #define MIM_KNN_GROUP 4
 #endif
+#ifndef MIM_KNN_PREFETCH
+#define MIM_KNN_PREFETCH 0
+#endif
+#ifndef MIM_KNN_PARTIALS
+#define MIM_KNN_PARTIALS 1
+#endif
+constexpr int kPartials = MIM_KNN_PARTIALS;  // independent early-tile selections per query (1 or 2)
 constexpr int kEarlyTiles = MIM_KNN_EARLY;
 constexpr int kGroup = MIM_KNN_GROUP;  // values tested together in the late tiles (4 or 8)
 
 // late tiles: the hit test of values g = kGroup*j .. kGroup*j + kGroup-1 (branch-free, scheduled
 // between the MFMAs); T = the lane's filter
 __device__ __forceinline__ bool sel_test(const f32x16& p, int j, float T) {
-    float m = fminf(fminf(p[kGroup * j], p[kGroup * j + 1]), p[kGroup * j + 2]);
+    float m = dmin(dmin(p[kGroup * j], p[kGroup * j + 1]), dmin(p[kGroup * j + 2], p[kGroup * j + 3]));
 #pragma unroll
-    for (int k = 3; k < kGroup; ++k) m = fminf(m, p[kGroup * j + k]);
+    for (int k = 4; k < kGroup; k += 2) m = dmin(m, dmin(p[kGroup * j + k], p[kGroup * j + k + 1]));
     return m < T;
 }
 
@@ -176,7 +188,7 @@ __device__ __forceinline__ float sel_filter(const LaneSel& s) {
     const int v = __float_as_int(s.m2);
     const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
     const float other = __int_as_float((threadIdx.x & 32) ? r[0] : r[1]);
-    return fminf(s.m2, other + 1.f);  // D are integers: other + 1 keeps D == other
+    return dmin(s.m2, other + 1.f);  // D are integers: other + 1 keeps D == other
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -187,7 +199,10 @@ __device__ __forceinline__ float sel_filter(const LaneSel& s) {
 // ------------------------------------------------------------------------------------------------
 constexpr int kLdsTile = kTileBytes + 256;  // fragments + 64 norms
 
-__global__ __launch_bounds__(256, 3) void knn2_bf16_kernel(const ProbDev* __restrict__ probs,
+#ifndef MIM_KNN_OCC
+#define MIM_KNN_OCC 4
+#endif
+__global__ __launch_bounds__(256, MIM_KNN_OCC) void knn2_bf16_kernel(const ProbDev* __restrict__ probs,
                                                           const KnnWork* __restrict__ works,
                                                           Top2* __restrict__ parts) {
     __shared__ __attribute__((aligned(16))) unsigned char smem[2 * kLdsTile];
@@ -270,12 +285,23 @@ __global__ __launch_bounds__(256, 3) void knn2_bf16_kernel(const ProbDev* __rest
                 acc0[4 * gg + 0] = v.x; acc0[4 * gg + 1] = v.y; acc0[4 * gg + 2] = v.z; acc0[4 * gg + 3] = v.w;
             }
             f32x16 acc1 = acc0;
+#if MIM_KNN_PREFETCH
+            bf16x8 af[8];  // all 8 A fragments of the half-tile issued before the first MFMA
+#pragma unroll
+            for (int s = 0; s < 8; ++s) af[s] = A[(u2 * 8 + s) * 64 + lane];
+#pragma unroll
+            for (int s = 0; s < 8; ++s) {
+                acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[s], B[0][s], acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[s], B[1][s], acc1, 0, 0, 0);
+            }
+#else
 #pragma unroll
             for (int s = 0; s < 8; ++s) {
                 const bf16x8 a = A[(u2 * 8 + s) * 64 + lane];
                 acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, B[0][s], acc0, 0, 0, 0);
                 acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, B[1][s], acc1, 0, 0, 0);
             }
+#endif
             const int row0 = tile * 64 + 32 * u2;
 #ifdef MIM_KNN_NOSEL  // timing probe only: MFMA loop without the selection (results invalid)
             st[0][0].m1 = fminf(st[0][0].m1, fminf(acc0[0], acc0[15]));
@@ -286,8 +312,8 @@ __global__ __launch_bounds__(256, 3) void knn2_bf16_kernel(const ProbDev* __rest
 #pragma unroll
                 for (int g = 0; g < 16; ++g) {
                     const int idx = row0 + (g & 3) + 8 * (g >> 2);
-                    sel_push(st[0][g & 1], acc0[g], idx);
-                    sel_push(st[1][g & 1], acc1[g], idx);
+                    sel_push(st[0][g % kPartials], acc0[g], idx);
+                    sel_push(st[1][g % kPartials], acc1[g], idx);
                 }
             } else {
                 constexpr int NG = 16 / kGroup;

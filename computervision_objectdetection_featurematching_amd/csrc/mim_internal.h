@@ -97,7 +97,8 @@ struct RansacBufs {
     long long flag_cap;       // bytes of `flags`
     int* irr;                 // [problem][block][kIrrCap] positions of irregular attempts (chain sampler)
     int* irr_cnt;             // [problem][block] their count (-1: more than kIrrCap)
-    uint32_t* pass_bits;      // [problem][window / 32] bit per position: a regular attempt that passes
+    uint32_t* pass_bits;      // [problem][window / 32] bit per chain attempt: checkSubset passes
+    void* chains;             // [problem] ChainSegs (ransac.hip): the walked chain of the chunk
     int irr_blocks;           // list blocks per problem
     const uint32_t* stream;   // raw cv::RNG((uint64)-1).next() stream shared by every problem
     long long stream_len;

@@ -741,9 +741,27 @@ __device__ __forceinline__ int attempt_flag(long long q, const uint32_t* __restr
     return ((len - 4) << 1) | (check_subset(s4, t4) ? 1 : 0);
 }
 
+// The chain only visits ~1/4 of the window's positions (attempts start 4 draws apart), so the
+// attempt kernel records the draws an attempt would consume (its repeated-index redraws) for every
+// position, and checkSubset runs later for the chain's attempts only (ransac_check_kernel).
+// kPassUnknown marks such a flag: bits 1..6 valid, bit 0 not evaluated.
+constexpr int kPassUnknown = 0x80;
+
+__device__ __forceinline__ int attempt_len_flag(long long q, const uint32_t* __restrict__ stream, long long slen,
+                                                unsigned N, unsigned long long M) {
+    if (q + 4 > slen) return kAttemptSerial;
+    int idx[4] = {(int)fastmod(stream[q], M, N), (int)fastmod(stream[q + 1], M, N),
+                  (int)fastmod(stream[q + 2], M, N), (int)fastmod(stream[q + 3], M, N)};
+    int len = 4;
+    if (idx[1] == idx[0] || idx[2] == idx[0] || idx[2] == idx[1] || idx[3] == idx[0] || idx[3] == idx[1] ||
+        idx[3] == idx[2]) {
+        len = resolve_at(q, stream, slen, N, M, idx);
+        if (len == 0 || len > 67) return kAttemptSerial;
+    }
+    return ((len - 4) << 1) | kPassUnknown;
+}
+
 __global__ __launch_bounds__(256) void ransac_attempt_kernel(const RansacState* __restrict__ st,
-                                                             const ProbDev* __restrict__ probs,
-                                                             const float4* __restrict__ pts,
                                                              const uint32_t* __restrict__ stream, long long slen,
                                                              uint8_t* __restrict__ flags, int wcap, int bpp, int c1) {
     const int p = blockIdx.x / bpp;
@@ -751,8 +769,7 @@ __global__ __launch_bounds__(256) void ransac_attempt_kernel(const RansacState* 
     const RansacState S = st[p];
     if (!S.active || S.done || S.fail_iter != -1 || S.produced >= min(c1, S.niters)) return;
     if (off >= window_len(S, c1, wcap)) return;
-    flags[(long long)p * wcap + off] =
-        (uint8_t)attempt_flag(S.stream_pos + off, stream, slen, (unsigned)S.n, S.modM, pts + probs[p].good_off);
+    flags[(long long)p * wcap + off] = (uint8_t)attempt_len_flag(S.stream_pos + off, stream, slen, (unsigned)S.n, S.modM);
 }
 
 __device__ __forceinline__ int wave_excl_prefix_sum(int v) {
@@ -806,7 +823,7 @@ __device__ __forceinline__ int mbcnt64(unsigned long long m) {
 __global__ __launch_bounds__(256) void ransac_irr_kernel(const RansacState* __restrict__ st,
                                                          const uint8_t* __restrict__ flags, int wcap, int bpp,
                                                          int c1, int* __restrict__ irr, int* __restrict__ irr_cnt,
-                                                         uint32_t* __restrict__ pass_bits, int irr_blocks) {
+                                                         int irr_blocks) {
     __shared__ int wsum[4];
     const int p = blockIdx.x / bpp, b = blockIdx.x % bpp, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const RansacState S = st[p];
@@ -823,23 +840,16 @@ __global__ __launch_bounds__(256) void ransac_irr_kernel(const RansacState* __re
         if (r0 + 16 * k + 16 <= wlen) v = *reinterpret_cast<const uint4*>(F + r0 + 16 * k);
         wd[4 * k] = v.x; wd[4 * k + 1] = v.y; wd[4 * k + 2] = v.z; wd[4 * k + 3] = v.w;
     }
-    // positions past wlen (a partial last vector) read as 0 = regular, failing: the chain kernel never
-    // walks past wlen
-    uint64_t irrm = 0, pass = 0;
+    // irregular: a repeated-index redraw (len > 4) or resolved by the walker (0xFF); positions past
+    // wlen (a partial last vector) read as regular: the chain kernels never walk past wlen
+    uint64_t irrm = 0;
 #pragma unroll
     for (int k = 0; k < 16; ++k)
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            const uint32_t f = (wd[k] >> (8 * j)) & 0xFF;
-            const int bit = 4 * k + j;
-            irrm |= (uint64_t)(f >= 2) << bit;
-            pass |= (uint64_t)(f == 1) << bit;
+            const uint32_t f = (wd[k] >> (8 * j)) & 0x7F;
+            irrm |= (uint64_t)(f >= 2) << (4 * k + j);
         }
-    if (r0 < wlen) {
-        uint32_t* PB = pass_bits + (long long)p * (wcap / 32) + r0 / 32;
-        PB[0] = (uint32_t)pass;
-        PB[1] = (uint32_t)(pass >> 32);
-    }
     const int c = __popcll(irrm);
     int incl = c;
 #pragma unroll
@@ -867,22 +877,31 @@ __global__ __launch_bounds__(256) void ransac_irr_kernel(const RansacState* __re
 }
 
 constexpr int kChainThreads = 1024;
-constexpr int kChainEntries = 8192;  // irregular attempts staged in LDS
-constexpr int kChainSegs = 4 * kChainThreads - 2;  // runs (segments) walked per chunk
+constexpr int kChainEntries = 8192;                 // irregular attempts staged in LDS
+constexpr int kChainSegs = 4 * kChainThreads - 2;   // runs (segments) walked per chunk
 constexpr int kNoEvent = INT_MAX;
 
-struct ChainShared {
-    int q[kChainEntries];
-    uint8_t f[kChainEntries];
+// The walked chain of one problem and chunk (global, between the walk, check and count kernels).
+// Segment j: the regular attempts seg_s[j], seg_s[j] + 4, ... closed by the irregular attempt
+// seg_q[j]; segment nseg is the open tail run from seg_s[nseg] (tail attempts).  A[j] = chain index
+// of the segment's first attempt, A[nseg + 1] = T attempts in all.
+struct ChainSegs {
+    int nseg, tail, s_end, T;
+    long long wbase;
+    int wlen, pad;
+    int A[kChainSegs + 2];
     int seg_s[kChainSegs + 1];
     int seg_q[kChainSegs];
     uint8_t seg_f[kChainSegs];
-    int A[kChainSegs + 2];      // first attempt index of each segment (+ tail, + end)
-    int boff[kIrrCap + 1];      // list block -> first entry (exclusive scan of the counts)
+};
+
+struct ChainWalkShared {
+    int q[kChainEntries];
+    uint8_t f[kChainEntries];
+    int boff[kIrrCap + 1];
     int wred[kChainThreads / 64];
     int wred2[kChainThreads / 64];
-    int n_entries, limit, nseg, s_end, tail;
-    int t_need, pos_need, len_need;
+    int n_entries, limit, nseg, tail;
 };
 
 __device__ __forceinline__ int block_excl_sum(int v, int* wred, int& total) {
@@ -938,66 +957,24 @@ __device__ __forceinline__ int block_min(int v, int* wred) {
     return r;
 }
 
-// Visit the passing attempts with chain index in [t0, t1), in order: fn(t, rel_pos, irregular).
-template <class Fn>
-__device__ __forceinline__ void chain_visit(const ChainShared& sh, const uint32_t* __restrict__ PB, int t0, int t1,
-                                            Fn&& fn) {
-    if (t0 >= t1) return;
-    int lo = 0, hi = sh.nseg;  // segment j (tail = nseg) with A[j] <= t0 < A[j+1]
-    while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (sh.A[mid] <= t0) lo = mid; else hi = mid - 1;
-    }
-    int j = lo, t = t0;
-    while (t < t1) {
-        const bool tail = j == sh.nseg;
-        const int Aj = sh.A[j], sj = sh.seg_s[j];
-        const int reg_end = tail ? sh.A[j + 1] : sh.A[j + 1] - 1;  // attempts before the irregular one
-        const int rb = min(t1, reg_end);
-        if (t < rb) {
-            const int P0 = sj + 4 * (t - Aj), P1 = sj + 4 * (rb - Aj);
-            const uint32_t res = 0x11111111u << (sj & 3);
-            for (int w = P0 >> 5; w <= (P1 - 1) >> 5; ++w) {
-                const int lo_b = max(P0 - 32 * w, 0), hi_b = min(P1 - 32 * w, 32);
-                const uint32_t rm = (hi_b == 32 ? 0xFFFFFFFFu : ((1u << hi_b) - 1)) & ~((1u << lo_b) - 1);
-                uint32_t bits = PB[w] & res & rm;
-                while (bits) {
-                    const int bit = __builtin_ctz(bits);
-                    bits &= bits - 1;
-                    const int pos = 32 * w + bit;
-                    fn(Aj + ((pos - sj) >> 2), pos, false);
-                }
-            }
-            t = rb;
-        }
-        if (!tail && t == sh.A[j + 1] - 1 && t < t1) {  // the irregular attempt closing segment j
-            if (sh.seg_f[j] & 1) fn(t, sh.seg_q[j], true);
-            ++t;
-        }
-        ++j;
-    }
-}
-
-__global__ __launch_bounds__(kChainThreads) void ransac_chain_kernel(RansacState* __restrict__ st,
-                                                                     const ProbDev* __restrict__ probs,
-                                                                     int4* __restrict__ samples, int c1,
-                                                                     const uint8_t* __restrict__ flags, int wcap,
-                                                                     const int* __restrict__ irr,
-                                                                     const int* __restrict__ irr_cnt,
-                                                                     const uint32_t* __restrict__ pass_bits,
-                                                                     int irr_blocks) {
-    __shared__ ChainShared sh;
+// ---- walk: stage the irregular list in LDS, follow the chain over it (one wave) ----
+__global__ __launch_bounds__(kChainThreads) void ransac_walk_kernel(const RansacState* __restrict__ st,
+                                                                    const uint8_t* __restrict__ flags, int wcap,
+                                                                    int c1, const int* __restrict__ irr,
+                                                                    const int* __restrict__ irr_cnt, int irr_blocks,
+                                                                    ChainSegs* __restrict__ chains) {
+    __shared__ ChainWalkShared sh;
     const int p = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
-    RansacState S = st[p];
-    if (!S.active || S.done || S.fail_iter != -1) return;
-    const int target = min(c1, S.niters);
-    if (S.produced >= target) return;
-    const long long wbase = S.stream_pos;
+    const RansacState S = st[p];
+    ChainSegs* G = chains + p;
+    if (!S.active || S.done || S.fail_iter != -1 || S.produced >= min(c1, S.niters)) {
+        if (tid == 0) G->T = -1;  // nothing to do this chunk
+        return;
+    }
     const int wlen = window_len(S, c1, wcap);
     const uint8_t* F = flags + (long long)p * wcap;
-    const uint32_t* PB = pass_bits + (long long)p * (wcap / 32);
     const int nb = min((wlen + kIrrBlock - 1) / kIrrBlock, kIrrCap);  // boff has kIrrCap + 1 slots
-    // stage the irregular list: blocks up to the first overflowing one, at most kChainEntries entries
+    // blocks up to the first overflowing one, at most kChainEntries entries
     {
         const int cnt = tid < nb ? irr_cnt[(long long)p * irr_blocks + tid] : 0;
         const int bad = tid < nb && cnt < 0 ? tid : INT_MAX;
@@ -1024,8 +1001,6 @@ __global__ __launch_bounds__(kChainThreads) void ransac_chain_kernel(RansacState
         }
         __syncthreads();
     }
-    // walk the irregular attempts of the chain (one wave): segment j = the run s_j, s_j + 4, ...
-    // closed by the irregular attempt q_j; then an open tail run up to `limit`
     if (tid < 64) {
         int s = 0, nseg = 0, limit = sh.limit;
         const int E = sh.n_entries;
@@ -1045,52 +1020,159 @@ __global__ __launch_bounds__(kChainThreads) void ransac_chain_kernel(RansacState
                     break;
                 }
                 if (lane == 0) {
-                    sh.seg_s[nseg] = s;
-                    sh.seg_q[nseg] = qq;
-                    sh.seg_f[nseg] = (uint8_t)ff;
+                    G->seg_s[nseg] = s;
+                    G->seg_q[nseg] = qq;
+                    G->seg_f[nseg] = (uint8_t)ff;
                 }
                 ++nseg;
-                s = uni(qq + 4 + (ff >> 1));
+                s = uni(qq + 4 + ((ff & 0x7F) >> 1));
             }
         }
         if (lane == 0) {
+            const int tail = s < limit ? (limit - s + 3) >> 2 : 0;
+            G->seg_s[nseg] = s;
             sh.nseg = nseg;
-            sh.seg_s[nseg] = s;
-            sh.tail = s < limit ? (limit - s + 3) >> 2 : 0;
-            sh.s_end = s + 4 * sh.tail;
+            sh.tail = tail;
+            G->nseg = nseg;
+            G->tail = tail;
+            G->s_end = s + 4 * tail;
+            G->wbase = S.stream_pos;
+            G->wlen = wlen;
         }
     }
     __syncthreads();
     const int nseg = sh.nseg;
-    // attempt index of every segment start
-    {
-        int v[4], sum = 0;
+    // chain index of every segment start
+    int v[4], sum = 0;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int j = 4 * tid + k;
-            v[k] = j < nseg ? ((sh.seg_q[j] - sh.seg_s[j]) >> 2) + 1 : (j == nseg ? sh.tail : 0);
-            sum += v[k];
-        }
-        int total;
-        int base = block_excl_sum(sum, sh.wred, total);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int j = 4 * tid + k;
-            if (j <= nseg + 1) sh.A[j] = base;
-            base += v[k];
-        }
-        __syncthreads();
+    for (int k = 0; k < 4; ++k) {
+        const int j = 4 * tid + k;
+        v[k] = j < nseg ? ((G->seg_q[j] - G->seg_s[j]) >> 2) + 1 : (j == nseg ? sh.tail : 0);
+        sum += v[k];
     }
-    const int T = sh.A[nseg + 1];  // attempts settled here
-    const int ch = (T + kChainThreads - 1) / kChainThreads;
-    const int t0 = min(T, tid * ch), t1 = min(T, t0 + ch);
+    int total;
+    int base = block_excl_sum(sum, sh.wred, total);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int j = 4 * tid + k;
+        if (j <= nseg + 1) G->A[j] = base;
+        base += v[k];
+    }
+    if (tid == 0) G->T = total;
+}
+
+// position of chain attempt t in segment j (A[j] <= t < A[j+1]); irregular: the closing attempt
+__device__ __forceinline__ int chain_pos(const ChainSegs* G, int j, int t, bool& irregular) {
+    irregular = j < G->nseg && t == G->A[j + 1] - 1;
+    return irregular ? G->seg_q[j] : G->seg_s[j] + 4 * (t - G->A[j]);
+}
+
+__device__ __forceinline__ int chain_seg(const ChainSegs* G, int t) {
+    int lo = 0, hi = G->nseg;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (G->A[mid] <= t) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+}
+
+// ---- check: checkSubset of every attempt on the walked chain (one thread per attempt) ----
+constexpr int kCheckBlock = 256;
+
+__global__ __launch_bounds__(kCheckBlock) void ransac_check_kernel(const ChainSegs* __restrict__ chains,
+                                                                   const ProbDev* __restrict__ probs,
+                                                                   const float4* __restrict__ pts,
+                                                                   const RansacState* __restrict__ st,
+                                                                   const uint32_t* __restrict__ stream, long long slen,
+                                                                   uint32_t* __restrict__ pass_bits, int wcap, int bpp) {
+    const int p = blockIdx.x / bpp, lane = threadIdx.x & 63;
+    const ChainSegs* G = chains + p;
+    const int T = G->T;
+    const int t = (blockIdx.x % bpp) * kCheckBlock + threadIdx.x;
+    if ((blockIdx.x % bpp) * kCheckBlock >= T) return;  // T < 0: nothing this chunk
+    const RansacState S = st[p];
+    __shared__ int j0;
+    if (threadIdx.x == 0) j0 = chain_seg(G, min(t, T - 1));  // the block's first attempt
+    __syncthreads();
+    bool pass = false;
+    if (t < T) {
+        int j = j0;
+        while (j < G->nseg && t >= G->A[j + 1]) ++j;  // a block spans a few segments at most
+        bool irregular;
+        const long long q = G->wbase + chain_pos(G, j, t, irregular);
+        const unsigned N = (unsigned)S.n;
+        int idx[4];
+        if (!irregular) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) idx[k] = (int)fastmod(stream[q + k], S.modM, N);
+        } else {
+            resolve_at(q, stream, slen, N, S.modM, idx);  // the walk only listed resolvable ones
+        }
+        const float4* P = pts + probs[p].good_off;
+        const float4 a = P[idx[0]], b = P[idx[1]], c = P[idx[2]], d = P[idx[3]];
+        const float s4[8] = {a.x, a.y, b.x, b.y, c.x, c.y, d.x, d.y};
+        const float t4[8] = {a.z, a.w, b.z, b.w, c.z, c.w, d.z, d.w};
+        pass = check_subset(s4, t4);
+    }
+    const unsigned long long m = __ballot(pass);
+    uint32_t* PB = pass_bits + (long long)p * (wcap / 32);
+    const int w0 = ((blockIdx.x % bpp) * kCheckBlock + (threadIdx.x & ~63)) >> 5;  // 2 words per wave
+    if (lane == 0 && w0 * 32 < T) PB[w0] = (uint32_t)m;
+    if (lane == 32 && (w0 + 1) * 32 < T) PB[w0 + 1] = (uint32_t)(m >> 32);
+}
+
+// ---- count: ranks of the passing attempts, getSubset's failure rule, samples, state ----
+// Visit the passing attempts with chain index in [t0, t1), in order: fn(t).
+template <class Fn>
+__device__ __forceinline__ void pass_visit(const uint32_t* __restrict__ PB, int t0, int t1, Fn&& fn) {
+    for (int w = t0 >> 5; w <= (t1 - 1) >> 5 && t0 < t1; ++w) {
+        const int lo_b = max(t0 - 32 * w, 0), hi_b = min(t1 - 32 * w, 32);
+        const uint32_t rm = (hi_b == 32 ? 0xFFFFFFFFu : ((1u << hi_b) - 1)) & ~((1u << lo_b) - 1);
+        uint32_t bits = PB[w] & rm;
+        while (bits) {
+            const int bit = __builtin_ctz(bits);
+            bits &= bits - 1;
+            fn(32 * w + bit);
+        }
+    }
+}
+
+struct ChainCountShared {
+    int wred[kChainThreads / 64];
+    int wred2[kChainThreads / 64];
+    int t_need;
+};
+
+__global__ __launch_bounds__(kChainThreads) void ransac_count_kernel(RansacState* __restrict__ st,
+                                                                     const ProbDev* __restrict__ probs,
+                                                                     const ChainSegs* __restrict__ chains,
+                                                                     const uint32_t* __restrict__ pass_bits,
+                                                                     const uint8_t* __restrict__ flags, int wcap,
+                                                                     int4* __restrict__ samples, int c1) {
+    __shared__ ChainCountShared sh;
+    const int p = blockIdx.x, tid = threadIdx.x;
+    const ChainSegs* G = chains + p;
+    const int T = G->T;
+    if (T < 0) return;
+    RansacState S = st[p];
+    const int target = min(c1, S.niters);
+    const long long wbase = G->wbase;
+    const uint32_t* PB = pass_bits + (long long)p * (wcap / 32);
+    // contiguous ranges of attempts, whole 32-bit words per thread
+    const int words = (T + 31) >> 5;
+    const int wpt = (words + kChainThreads - 1) / kChainThreads;
+    const int t0 = min(T, tid * wpt * 32), t1 = min(T, t0 + wpt * 32);
     int cnt = 0, first = -1, last = -1;
-    chain_visit(sh, PB, t0, t1, [&](int t, int, bool) {
-        if (first < 0) first = t;
-        last = t;
-        ++cnt;
-    });
-    // failure rule of getSubset: 10000 consecutive rejected attempts (runs here are < 10000 long,
+    for (int w = t0 >> 5; 32 * w < t1; ++w) {
+        const int hi_b = min(t1 - 32 * w, 32);
+        const uint32_t bits = PB[w] & (hi_b == 32 ? 0xFFFFFFFFu : ((1u << hi_b) - 1));
+        if (bits) {
+            if (first < 0) first = 32 * w + __builtin_ctz(bits);
+            last = 32 * w + 31 - __builtin_clz(bits);
+            cnt += __popc(bits);
+        }
+    }
+    // failure rule of getSubset: 10000 consecutive rejected attempts (ranges here are < 10000 long,
     // so a failure can only end a gap that starts at an earlier thread's last pass)
     int total;
     const int base = block_excl_sum(cnt, sh.wred, total);
@@ -1105,12 +1187,8 @@ __global__ __launch_bounds__(kChainThreads) void ransac_chain_kernel(RansacState
     __syncthreads();
     if (base < need && need <= base + cnt) {  // the attempt completing the chunk's last iteration
         int k = need - base;
-        chain_visit(sh, PB, t0, t1, [&](int t, int pos, bool irr_att) {
-            if (--k == 0) {
-                sh.t_need = t;
-                sh.pos_need = pos;
-                sh.len_need = irr_att ? 4 + (F[pos] >> 1) : 4;
-            }
+        pass_visit(PB, t0, t1, [&](int t) {
+            if (--k == 0) sh.t_need = t;
         });
     }
     __syncthreads();
@@ -1119,8 +1197,7 @@ __global__ __launch_bounds__(kChainThreads) void ransac_chain_kernel(RansacState
     if (t_fail < t_need) {
         int before = 0;
         if (cnt && last < t_fail) before = cnt;
-        else if (cnt && first < t_fail)
-            chain_visit(sh, PB, t0, t1, [&](int t, int, bool) { before += t < t_fail; });
+        else if (cnt && first < t_fail) pass_visit(PB, t0, t1, [&](int t) { before += t < t_fail; });
         int tot_before;
         block_excl_sum(before, sh.wred, tot_before);
         keep = tot_before;
@@ -1129,32 +1206,48 @@ __global__ __launch_bounds__(kChainThreads) void ransac_chain_kernel(RansacState
     }
     if (base < keep) {
         int4* out = samples + probs[p].it_off + S.produced;
-        int r = base;
-        chain_visit(sh, PB, t0, t1, [&](int, int pos, bool irr_att) {
-            if (r < keep) out[r] = make_int4((int)(wbase + pos), irr_att ? -2 : -1, 0, 0);
+        int r = base, j = -1, a_next = 0, a_j = 0, s_j = 0, q_j = 0;
+        pass_visit(PB, t0, t1, [&](int t) {
+            if (r < keep) {
+                if (j < 0 || t >= a_next) {  // passes come in increasing t: segment data cached
+                    j = j < 0 ? chain_seg(G, t) : j + 1;
+                    while (j < G->nseg && t >= G->A[j + 1]) ++j;
+                    a_j = G->A[j];
+                    a_next = G->A[j + 1];
+                    s_j = G->seg_s[j];
+                    q_j = j < G->nseg ? G->seg_q[j] : 0;
+                }
+                const bool irregular = j < G->nseg && t == a_next - 1;
+                const int pos = irregular ? q_j : s_j + 4 * (t - a_j);
+                out[r] = make_int4((int)(wbase + pos), irregular ? -2 : -1, 0, 0);
+            }
             ++r;
         });
     }
     if (tid == 0) {
         S.win_base = wbase;
-        S.win_len = wlen;
+        S.win_len = G->wlen;
         if (t_fail < t_need) {
             S.produced += keep;
             S.fail_iter = S.produced;  // getSubset returned false in this iteration
             S.fail_run = 10000;
         } else if (t_need != kNoEvent) {
+            const int j = chain_seg(G, t_need);
+            bool irregular;
+            const int pos = chain_pos(G, j, t_need, irregular);
+            const int len = irregular ? 4 + ((flags[(long long)p * wcap + pos] & 0x7F) >> 1) : 4;
             S.produced = target;
-            S.stream_pos = wbase + sh.pos_need + sh.len_need;
+            S.stream_pos = wbase + pos + len;
             S.fail_run = 0;
         } else {
             S.produced += total;
             S.fail_run = total > 0 ? T - 1 - last_all : S.fail_run + T;
-            S.stream_pos = wbase + sh.s_end;
+            S.stream_pos = wbase + G->s_end;
         }
         st[p] = S;
     }
-    (void)lane;
 }
+
 
 // ------------------------------------------------------------------------------------------------
 // sample: walk the chain of getSubset attempts with the outcomes precomputed by
@@ -1249,7 +1342,8 @@ __global__ __launch_bounds__(64) void ransac_sample_kernel(RansacState* __restri
                 const int a = 4 * lane + i;
                 int fi = (int)((wd[i] >> (8 * rho)) & 0xFF);
                 if (a >= a0 && fi == kFlagUnknown) PROF_INC(n_unk);
-                if (a >= a0 && fi == kFlagUnknown)
+                // outside the window, or checkSubset not evaluated yet (kPassUnknown): evaluate here
+                if (a >= a0 && (fi == kFlagUnknown || (fi != kAttemptSerial && (fi & kPassUnknown))))
                     fi = attempt_flag(wbase + wb + 4LL * a + rho, stream, slen, N, M, P);
                 f[i] = fi;
                 const bool irr = fi == kAttemptSerial || (fi >> 1) != 0;
@@ -2469,6 +2563,8 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
 // ------------------------------------------------------------------------------------------------
 // host orchestration (called by api.cpp with the ctx mutex held)
 // ------------------------------------------------------------------------------------------------
+size_t ransac_chain_bytes() { return sizeof(ChainSegs); }
+
 void ransac_enqueue(const RansacParams& prm, int n_probs, const ProbDev* probs, const float4* pts,
                     const int* n_good, const RansacBufs& b, uint8_t* masks, mim_result* results, int raw,
                     hipStream_t s, void (*mark)(void*, const char*), void* mark_ctx, int exact_all) {
@@ -2488,15 +2584,22 @@ void ransac_enqueue(const RansacParams& prm, int n_probs, const ProbDev* probs, 
         // (a multiple of 64: flags are read as 16-byte vectors, pass bits as 32-bit words)
         const int wcap = (int)(std::min<long long>((long long)(c1 - c0) * 28 + 4096, b.flag_cap / std::max(n_probs, 1)) & ~63LL);
         const int bppw = (wcap + 255) / 256;
-        ransac_attempt_kernel<<<n_probs * bppw, 256, 0, s>>>(b.state, probs, pts, b.stream, b.stream_len, b.flags, wcap,
-                                                            bppw, c1);
+        ransac_attempt_kernel<<<n_probs * bppw, 256, 0, s>>>(b.state, b.stream, b.stream_len, b.flags, wcap, bppw, c1);
         mark(mark_ctx, "attempt");
         if (use_chain) {
+            ChainSegs* chains = reinterpret_cast<ChainSegs*>(b.chains);
             const int bpp_irr = (wcap + kIrrBlock - 1) / kIrrBlock;
             ransac_irr_kernel<<<n_probs * bpp_irr, 256, 0, s>>>(b.state, b.flags, wcap, bpp_irr, c1, b.irr,
-                                                               b.irr_cnt, b.pass_bits, b.irr_blocks);
-            ransac_chain_kernel<<<n_probs, kChainThreads, 0, s>>>(b.state, probs, b.samples, c1, b.flags, wcap, b.irr,
-                                                                  b.irr_cnt, b.pass_bits, b.irr_blocks);
+                                                               b.irr_cnt, b.irr_blocks);
+            ransac_walk_kernel<<<n_probs, kChainThreads, 0, s>>>(b.state, b.flags, wcap, c1, b.irr, b.irr_cnt,
+                                                                 b.irr_blocks, chains);
+            mark(mark_ctx, "chain");
+            const int bpp_chk = (wcap / 4 + kCheckBlock) / kCheckBlock;  // T <= wlen / 4 + 1
+            ransac_check_kernel<<<n_probs * bpp_chk, kCheckBlock, 0, s>>>(chains, probs, pts, b.state, b.stream,
+                                                                          b.stream_len, b.pass_bits, wcap, bpp_chk);
+            mark(mark_ctx, "check");
+            ransac_count_kernel<<<n_probs, kChainThreads, 0, s>>>(b.state, probs, chains, b.pass_bits, b.flags, wcap,
+                                                                  b.samples, c1);
             mark(mark_ctx, "chain");
         }
         ransac_sample_kernel<<<n_probs, 64, 0, s>>>(b.state, probs, pts, b.stream, b.stream_len, b.samples, c1, b.err,

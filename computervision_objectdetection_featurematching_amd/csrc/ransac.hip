@@ -885,10 +885,14 @@ constexpr int kNoEvent = INT_MAX;
 // Segment j: the regular attempts seg_s[j], seg_s[j] + 4, ... closed by the irregular attempt
 // seg_q[j]; segment nseg is the open tail run from seg_s[nseg] (tail attempts).  A[j] = chain index
 // of the segment's first attempt, A[nseg + 1] = T attempts in all.
+constexpr int kCheckBlock = 256;
+constexpr int kChainBlk = 8192;  // check blocks per chunk: >= max window / 4 / kCheckBlock
+
 struct ChainSegs {
     int nseg, tail, s_end, T;
     long long wbase;
     int wlen, pad;
+    int blk_seg[kChainBlk];  // segment holding attempt b * kCheckBlock
     int A[kChainSegs + 2];
     int seg_s[kChainSegs + 1];
     int seg_q[kChainSegs];
@@ -1056,6 +1060,9 @@ __global__ __launch_bounds__(kChainThreads) void ransac_walk_kernel(const Ransac
     for (int k = 0; k < 4; ++k) {
         const int j = 4 * tid + k;
         if (j <= nseg + 1) G->A[j] = base;
+        if (j <= nseg)  // the check blocks whose first attempt falls in segment j
+            for (int b = (base + kCheckBlock - 1) / kCheckBlock; b * kCheckBlock < base + v[k] && b < kChainBlk; ++b)
+                G->blk_seg[b] = j;
         base += v[k];
     }
     if (tid == 0) G->T = total;
@@ -1077,7 +1084,6 @@ __device__ __forceinline__ int chain_seg(const ChainSegs* G, int t) {
 }
 
 // ---- check: checkSubset of every attempt on the walked chain (one thread per attempt) ----
-constexpr int kCheckBlock = 256;
 
 __global__ __launch_bounds__(kCheckBlock) void ransac_check_kernel(const ChainSegs* __restrict__ chains,
                                                                    const ProbDev* __restrict__ probs,
@@ -1091,12 +1097,10 @@ __global__ __launch_bounds__(kCheckBlock) void ransac_check_kernel(const ChainSe
     const int t = (blockIdx.x % bpp) * kCheckBlock + threadIdx.x;
     if ((blockIdx.x % bpp) * kCheckBlock >= T) return;  // T < 0: nothing this chunk
     const RansacState S = st[p];
-    __shared__ int j0;
-    if (threadIdx.x == 0) j0 = chain_seg(G, min(t, T - 1));  // the block's first attempt
-    __syncthreads();
+    const int b = blockIdx.x % bpp;
     bool pass = false;
     if (t < T) {
-        int j = j0;
+        int j = b < kChainBlk ? G->blk_seg[b] : chain_seg(G, t);  // segment of the block's first attempt
         while (j < G->nseg && t >= G->A[j + 1]) ++j;  // a block spans a few segments at most
         bool irregular;
         const long long q = G->wbase + chain_pos(G, j, t, irregular);
@@ -1593,6 +1597,9 @@ typedef float f2v __attribute__((ext_vector_type(2)));
 typedef float f4v __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ f2v pk_fma(f2v a, f2v b, f2v c) { return __builtin_elementwise_fma(a, b, c); }
 
+// kLo = false (chunks after the first, once maxGoodCount is known): only the upper bound is
+// counted, lo = 0 — the candidate rule then rests on maxGoodCount and the earlier chunks' bounds.
+template <bool kLo>
 __global__ __launch_bounds__(256) void ransac_bound_kernel(const RansacState* __restrict__ st,
                                                            const ProbDev* __restrict__ probs,
                                                            const float4* __restrict__ pts,
@@ -1696,7 +1703,7 @@ __global__ __launch_bounds__(256) void ransac_bound_kernel(const RansacState* __
                     const float ey = fmaf(m[2 + k], W, fmaf(Hf[3], x, fmaf(Hf[4], y, Hf[5])));
                     const float e = fmaf(ex, ex, ey * ey);
                     const float W2 = W * W;
-                    lo += __float_as_uint(fmaf(-t[k], W2, e)) >> 31;
+                    if (kLo) lo += __float_as_uint(fmaf(-t[k], W2, e)) >> 31;
                     hineg += __float_as_uint(fmaf(t[2 + k], W2, -e)) >> 31;
                 }
             }
@@ -1714,7 +1721,7 @@ __global__ __launch_bounds__(256) void ransac_bound_kernel(const RansacState* __
                                 fabsf(a.y) + fabsf(a.w) + fabsf(m.y) + fabsf(m.w)};
                 const f2v wid = sc * pk_fma(f2v(k2), sc, f2v(k1));
                 const f2v L = (t.xy - wid) * W2, U = (t.zw + wid) * W2;
-                lo += (e.x < L.x) + (e.y < L.y);
+                if (kLo) lo += (e.x < L.x) + (e.y < L.y);
                 hi += (e.x <= U.x) + (e.y <= U.y);
             }
         }
@@ -2617,8 +2624,12 @@ void ransac_enqueue(const RansacParams& prm, int n_probs, const ProbDev* probs, 
             ransac_select_kernel<<<n_probs, 64, 0, s>>>(b.state, probs, b.counts, c1, prm.conf);
             mark(mark_ctx, "select");
         } else {
-            ransac_bound_kernel<<<n_probs * bpp256, 256, 0, s>>>(b.state, probs, pts, b.samples, b.stream, b.bounds, c0, c1,
-                                                                bpp256, thr2);
+            if (c0 == 0)
+                ransac_bound_kernel<true><<<n_probs * bpp256, 256, 0, s>>>(b.state, probs, pts, b.samples, b.stream,
+                                                                          b.bounds, c0, c1, bpp256, thr2);
+            else
+                ransac_bound_kernel<false><<<n_probs * bpp256, 256, 0, s>>>(b.state, probs, pts, b.samples, b.stream,
+                                                                           b.bounds, c0, c1, bpp256, thr2);
             mark(mark_ctx, "score");
             ransac_cand_kernel<<<n_probs, kCandThreads, 0, s>>>(b.state, probs, b.bounds, c1, b.cand, b.ncand);
             mark(mark_ctx, "cand");

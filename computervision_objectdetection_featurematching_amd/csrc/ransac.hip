@@ -2258,7 +2258,60 @@ __device__ bool solve_chol8(const double* A, const double* b, double* x) {
     return true;
 }
 
+// max |diag(A^-1)| through the scaled Cholesky factor (A = S^-1 L L^T S^-1, S = diag(A)^-1/2):
+// diag(A^-1)_i = S_i^2 * sum_k (L^-1)_{k,i}^2.  For the positive-definite LM normal matrices this is
+// the pseudo-inverse of cv::invert(DECOMP_EIG) to rounding (contract |dH| <= 1e-4); returns false
+// when the factorisation is not safe, and the caller falls back to the eigen path.
+__device__ bool inv_diag_max_chol8(const double* A, double& maxval) {
+    double sc[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        if (!(A[9 * i] > 0)) return false;
+        sc[i] = 1.0 / sqrt(A[9 * i]);
+    }
+    double L[8][8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        double sjj = 1.0;
+#pragma unroll
+        for (int k = 0; k < j; ++k) sjj -= L[j][k] * L[j][k];
+        if (!(sjj > 1e-10)) return false;
+        const double ljj = sqrt(sjj);
+        L[j][j] = ljj;
+#pragma unroll
+        for (int i = j + 1; i < 8; ++i) {
+            double sij = A[8 * i + j] * sc[i] * sc[j];
+#pragma unroll
+            for (int k = 0; k < j; ++k) sij -= L[i][k] * L[j][k];
+            L[i][j] = sij / ljj;
+        }
+    }
+    double Li[8][8];  // L^-1 (lower)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        Li[j][j] = 1.0 / L[j][j];
+#pragma unroll
+        for (int i = j + 1; i < 8; ++i) {
+            double s = 0;
+#pragma unroll
+            for (int k = j; k < i; ++k) s += L[i][k] * Li[k][j];
+            Li[i][j] = -s / L[i][i];
+        }
+    }
+    maxval = DBL_EPSILON;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        double d = 0;
+#pragma unroll
+        for (int k = i; k < 8; ++k) d += Li[k][i] * Li[k][i];
+        maxval = fmax(maxval, fabs(d * sc[i] * sc[i]));
+    }
+    return true;
+}
+
 __device__ double inv_diag_max8(const double* A, double* J) {
+    double mv;
+    if (inv_diag_max_chol8(A, mv)) return mv;
     double w[8], V[64];
     eig8(A, J, w, V);
     double threshold = 0;

@@ -92,6 +92,51 @@ struct SetRec {
     SetDev d;
 };
 
+// Pinned staging for the per-batch tables, two generations: a batch's host->device table copies
+// are stream-ordered, so the host never waits for the previous batch; a generation is rewritten
+// only after the event of its last copy (two batches back) has completed.
+struct PinnedStage {
+    char* p[2] = {nullptr, nullptr};
+    size_t cap[2] = {0, 0};
+    hipEvent_t ev[2] = {nullptr, nullptr};
+    bool used[2] = {false, false};
+    int par = 0;
+    hipError_t acquire(size_t bytes, char** out) {
+        par ^= 1;
+        if (used[par]) {
+            hipError_t e = hipEventSynchronize(ev[par]);
+            if (e != hipSuccess) return e;
+        }
+        if (!ev[par]) {
+            hipError_t e = hipEventCreateWithFlags(&ev[par], hipEventDisableTiming);
+            if (e != hipSuccess) return e;
+        }
+        if (bytes > cap[par]) {
+            if (p[par]) (void)hipHostFree(p[par]);
+            p[par] = nullptr;
+            cap[par] = 0;
+            hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&p[par]), std::max(bytes, (size_t)1 << 16));
+            if (e != hipSuccess) return e;
+            cap[par] = std::max(bytes, (size_t)1 << 16);
+        }
+        *out = p[par];
+        return hipSuccess;
+    }
+    hipError_t release_after(hipStream_t s) {  // the copies from the current generation are enqueued
+        used[par] = true;
+        return hipEventRecord(ev[par], s);
+    }
+    void destroy() {
+        for (int i = 0; i < 2; ++i) {
+            if (ev[i]) (void)hipEventSynchronize(ev[i]);
+            if (p[i]) (void)hipHostFree(p[i]);
+            if (ev[i]) (void)hipEventDestroy(ev[i]);
+            p[i] = nullptr;
+            ev[i] = nullptr;
+        }
+    }
+};
+
 }  // namespace
 
 namespace mim {
@@ -117,6 +162,7 @@ struct mim_ctx {
     std::vector<KnnWork> h_works;
     int n_works = 0;
     std::vector<long long> h_good_off;
+    PinnedStage stage;
     int last_n = 0;
     // MIM_RANSAC_EXACT=1: evaluate every hypothesis exactly (reference mode for cross-checks)
     int exact_all = 0;
@@ -138,7 +184,9 @@ struct mim_ctx {
         std::string name;
         hipStream_t s;
         hipEvent_t e;
+        int seq;  // batch the event belongs to: spans are taken within one batch only
     };
+    int ev_seq = 0;
     std::vector<Ev> evs;
     std::map<std::string, double> last_ms;
 };
@@ -208,6 +256,7 @@ void mim_ctx_destroy(mim_ctx* c) {
         if (c->ev_join[g]) (void)hipEventDestroy(c->ev_join[g]);
     }
     if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+    c->stage.destroy();
     c->arena.release();
     for (DevBuf* b : {&c->probs, &c->works, &c->parts, &c->good_q, &c->good_t, &c->pts, &c->n_good,
                       &c->results, &c->masks, &c->knn_idx, &c->knn_dist, &c->rws.state, &c->rws.samples,
@@ -296,7 +345,8 @@ mim_status mim_sets_clear(mim_ctx* c) {
     if (!c) return MIM_EINVAL;
     std::lock_guard<std::mutex> lk(c->mu);
     HIPCHK(c, hipSetDevice(c->device));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    // no host wait: every write into the arena (prep kernels, copies of host rows) is ordered on the
+    // ctx stream after the previous batch, whose groups join back into that stream
     c->sets.clear();
     c->arena.rewind();
     return MIM_OK;
@@ -316,7 +366,6 @@ static int pick_groups(int n) {
 }
 
 static mim_status build_tables(mim_ctx* c, const mim_problem* problems, int n, int max_iters, int groups = 1) {
-    HIPCHK(c, hipStreamSynchronize(c->stream));  // previous batch done with the tables
     c->h_probs.assign(n, ProbDev{});
     long long part = 0, good = 0, it = 0;
     int total_qblocks = 0;
@@ -378,10 +427,15 @@ static mim_status build_tables(mim_ctx* c, const mim_problem* problems, int n, i
     HIPCHK(c, c->pts.ensure(sizeof(float4) * good));
     HIPCHK(c, c->n_good.ensure(sizeof(int) * std::max(n, 1)));
     HIPCHK(c, c->masks.ensure(good));
-    HIPCHK(c, hipMemcpyAsync(c->probs.p, c->h_probs.data(), sizeof(ProbDev) * n, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(c, hipMemcpyAsync(c->works.p, works.data(), sizeof(KnnWork) * works.size(), hipMemcpyHostToDevice,
-                             c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));  // pageable sources: copy complete before reuse
+    // the device tables are rewritten in stream order (after the previous batch's kernels)
+    const size_t pb = sizeof(ProbDev) * n, wb = sizeof(KnnWork) * works.size();
+    char* st = nullptr;
+    HIPCHK(c, c->stage.acquire(pb + wb, &st));
+    memcpy(st, c->h_probs.data(), pb);
+    memcpy(st + pb, works.data(), wb);
+    HIPCHK(c, hipMemcpyAsync(c->probs.p, st, pb, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->works.p, st + pb, wb, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, c->stage.release_after(c->stream));
     c->h_good_off.resize(n);
     for (int i = 0; i < n; ++i) c->h_good_off[i] = c->h_probs[i].good_off;
     c->last_n = n;
@@ -398,22 +452,24 @@ static void ev_mark(mim_ctx* c, const char* name) {
     hipEvent_t e;
     if (hipEventCreate(&e) != hipSuccess) return;
     (void)hipEventRecord(e, c->cur);
-    c->evs.push_back({name, c->cur, e});
+    if (!strcmp(name, "begin")) ++c->ev_seq;
+    c->evs.push_back({name, c->cur, e, c->ev_seq});
 }
 
 static void ev_collect(mim_ctx* c) {
     if (c->evs.empty()) return;
     for (auto& e : c->evs) (void)hipEventSynchronize(e.e);
     c->last_ms.clear();
-    std::map<hipStream_t, hipEvent_t> prev;
+    // kernel time summed over every batch since the last collection
+    std::map<hipStream_t, const mim_ctx::Ev*> prev;
     for (auto& e : c->evs) {
         auto it = prev.find(e.s);
-        if (it != prev.end()) {
+        if (it != prev.end() && it->second->seq == e.seq) {
             float ms = 0;
-            (void)hipEventElapsedTime(&ms, it->second, e.e);
+            (void)hipEventElapsedTime(&ms, it->second->e, e.e);
             c->last_ms[e.name] += ms;
         }
-        prev[e.s] = e.e;
+        prev[e.s] = &e;
     }
     for (auto& e : c->evs) (void)hipEventDestroy(e.e);
     c->evs.clear();

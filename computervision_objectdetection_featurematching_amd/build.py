@@ -17,6 +17,9 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=o
          "-Wno-unused-result", "-Wno-unused-function"]
 # extra defines for diagnostic builds (e.g. MIM_EXTRA_FLAGS=-DMIM_SAMPLER_PROF)
 FLAGS += os.environ.get("MIM_EXTRA_FLAGS", "").split()
+# per-source flags: the RANSAC kernels are scalar fp32/fp64 code; v2f32 packing (v_pk_fma_f32 issues
+# at half rate on gfx950 and needs SGPR-pair shuffles for uniform operands) only costs there
+SRC_FLAGS = {"ransac.hip": ["-fno-slp-vectorize"]}
 
 
 def sources():
@@ -39,7 +42,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
     objs = []
     for src in sources():
         obj = os.path.join(LIBDIR, os.path.basename(src) + ".o")
-        cmd = [HIPCC, *FLAGS, "-c", src, "-o", obj]
+        cmd = [HIPCC, *FLAGS, *SRC_FLAGS.get(os.path.basename(src), []), "-c", src, "-o", obj]
         if verbose:
             print(" ".join(cmd))
         subprocess.check_call(cmd)

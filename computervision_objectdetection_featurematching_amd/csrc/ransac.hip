@@ -1597,8 +1597,10 @@ typedef float f2v __attribute__((ext_vector_type(2)));
 typedef float f4v __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ f2v pk_fma(f2v a, f2v b, f2v c) { return __builtin_elementwise_fma(a, b, c); }
 
-// kLo = false (chunks after the first, once maxGoodCount is known): only the upper bound is
+// kLo = false (chunks after the first, once maxGoodCount is known): only an upper bound is
 // counted, lo = 0 — the candidate rule then rests on maxGoodCount and the earlier chunks' bounds.
+// That upper bound uses the box max(|ex|, |ey|) <= sqrt(t_hi) |W|, implied by the disc
+// ex^2 + ey^2 <= t_hi W^2: hi_box >= hi, at 11.5 instead of 13.5 VALU operations per point.
 template <bool kLo>
 __global__ __launch_bounds__(256) void ransac_bound_kernel(const RansacState* __restrict__ st,
                                                            const ProbDev* __restrict__ probs,
@@ -1684,11 +1686,31 @@ __global__ __launch_bounds__(256) void ransac_bound_kernel(const RansacState* __
             const float d0 = fmaf(1e-7f * s0, s0, 0.5f), d1 = fmaf(1e-7f * s1, s1, 0.5f);
             tp[3 * i] = f4v{q0.x, q1.x, q0.y, q1.y};
             tp[3 * i + 1] = f4v{-q0.z, -q1.z, -q0.w, -q1.w};
-            tp[3 * i + 2] = has1 ? f4v{thr2 - d0, thr2 - d1, thr2 + d0, thr2 + d1}
-                                 : f4v{thr2 - d0, -1.f, thr2 + d0, -1.f};
+            // kLo: {t_lo0, t_lo1, t_hi0, t_hi1}; otherwise {sqrt(t_hi0), sqrt(t_hi1), t_hi0, t_hi1}
+            // (square roots rounded up by 1e-6 relative, far above the fp32 sqrt error)
+            const float a0 = kLo ? thr2 - d0 : sqrtf(thr2 + d0) * (1.f + 1e-6f);
+            const float a1 = kLo ? thr2 - d1 : sqrtf(thr2 + d1) * (1.f + 1e-6f);
+            tp[3 * i + 2] = has1 ? f4v{a0, a1, thr2 + d0, thr2 + d1} : f4v{a0, -1.f, thr2 + d0, -1.f};
         }
         __syncthreads();
-        if (count && !widen) {
+        if (count && !widen && !kLo) {
+            // box test max(|ex|, |ey|) <= sqrt(t_hi) |W|, counted by sign bit (overflow: inf -> out,
+            // inf - inf = +NaN -> in)
+            int bneg = 0;
+#pragma unroll 4
+            for (int i = 0; i < tpairs; ++i) {
+                const f4v a = tp[3 * i], m = tp[3 * i + 1], t = tp[3 * i + 2];
+#pragma unroll
+                for (int k = 0; k < 2; ++k) {
+                    const float x = a[k], y = a[2 + k];
+                    const float W = fmaf(Hf[6], x, fmaf(Hf[7], y, 1.f));
+                    const float ex = fmaf(m[k], W, fmaf(Hf[0], x, fmaf(Hf[1], y, Hf[2])));
+                    const float ey = fmaf(m[2 + k], W, fmaf(Hf[3], x, fmaf(Hf[4], y, Hf[5])));
+                    bneg += __float_as_uint(fmaf(t[k], fabsf(W), -fmaxf(fabsf(ex), fabsf(ey)))) >> 31;
+                }
+            }
+            hi += 2 * tpairs - bneg;
+        } else if (count && !widen) {
             // division-free test with sign-bit counting (v_cmp + v_addc cost ~2x a plain ALU op):
             //   lo: e - tlo W^2 < 0,   not hi: thi W^2 - e < 0
             int hineg = 0;

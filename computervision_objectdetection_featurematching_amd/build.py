@@ -18,8 +18,9 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=o
 # extra defines for diagnostic builds (e.g. MIM_EXTRA_FLAGS=-DMIM_SAMPLER_PROF)
 FLAGS += os.environ.get("MIM_EXTRA_FLAGS", "").split()
 # per-source flags: the RANSAC kernels are scalar fp32/fp64 code; v2f32 packing (v_pk_fma_f32 issues
-# at half rate on gfx950 and needs SGPR-pair shuffles for uniform operands) only costs there
-SRC_FLAGS = {"ransac.hip": ["-fno-slp-vectorize"]}
+# at half rate on gfx950 and needs SGPR-pair shuffles for uniform operands) only costs there; MFMA
+# results in VGPRs (the bound kernel reads every accumulator with VALU ops, AGPRs would need a copy)
+SRC_FLAGS = {"ransac.hip": ["-fno-slp-vectorize", "-mllvm", "-amdgpu-mfma-vgpr-form"]}
 
 
 def sources():

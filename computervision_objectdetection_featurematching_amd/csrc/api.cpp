@@ -143,7 +143,7 @@ namespace mim {
 // RANSAC workspace (definition shared with ransac.hip through this layout)
 struct RansacWs {
     DevBuf state, samples, hyp, counts, bounds, flags, irr, irr_cnt, pass_bits, chains, best_h, cand, ncand, cex, cH, stream,
-        scratch, inl, err;
+        scratch, inl, tiles, err;
     long long stream_len = 0;
 };
 }  // namespace mim
@@ -260,7 +260,7 @@ void mim_ctx_destroy(mim_ctx* c) {
     c->arena.release();
     for (DevBuf* b : {&c->probs, &c->works, &c->parts, &c->good_q, &c->good_t, &c->pts, &c->n_good,
                       &c->results, &c->masks, &c->knn_idx, &c->knn_dist, &c->rws.state, &c->rws.samples,
-                      &c->rws.hyp, &c->rws.counts, &c->rws.bounds, &c->rws.flags, &c->rws.irr, &c->rws.irr_cnt, &c->rws.pass_bits, &c->rws.chains, &c->rws.best_h, &c->rws.cand, &c->rws.ncand, &c->rws.cex, &c->rws.cH, &c->rws.stream, &c->rws.scratch, &c->rws.inl, &c->rws.err})
+                      &c->rws.hyp, &c->rws.counts, &c->rws.bounds, &c->rws.flags, &c->rws.irr, &c->rws.irr_cnt, &c->rws.pass_bits, &c->rws.chains, &c->rws.best_h, &c->rws.cand, &c->rws.ncand, &c->rws.cex, &c->rws.cH, &c->rws.stream, &c->rws.scratch, &c->rws.inl, &c->rws.tiles, &c->rws.err})
         b->release();
     if (c->own) (void)hipStreamDestroy(c->own);
     delete c;
@@ -390,7 +390,7 @@ static mim_status build_tables(mim_ctx* c, const mim_problem* problems, int n, i
         P.part_off = part;
         part += (long long)nsplit * P.q_pad;
         P.good_off = good;
-        good += std::max(P.q.n, 1);
+        good += (std::max(P.q.n, 1) + 31) & ~31;  // 32-aligned: the MFMA bound's point tiles
         P.it_off = it;
         it += std::max(max_iters, 1);
         for (int qb_i = 0; qb_i < qb; ++qb_i)
@@ -662,6 +662,7 @@ static mim_status ransac_prepare(mim_ctx* c, int n, const mim_params* prm, Ransa
     HIPCHK(c, c->rws.cex.ensure(sizeof(int) * cap));
     HIPCHK(c, c->rws.cH.ensure(sizeof(double) * 9 * cap));
     HIPCHK(c, c->rws.inl.ensure(sizeof(float4) * good_total));
+    HIPCHK(c, c->rws.tiles.ensure(sizeof(uint4) * 128 * ((good_total + 31) / 32)));
     HIPCHK(c, c->rws.err.ensure(sizeof(int) * 4));
     HIPCHK(c, c->results.ensure(sizeof(mim_result) * std::max(n, 1)));
     HIPCHK(c, c->masks.ensure(good_total));
@@ -687,6 +688,7 @@ static mim_status ransac_prepare(mim_ctx* c, int n, const mim_params* prm, Ransa
     b.stream = c->rws.stream.as<uint32_t>();
     b.stream_len = c->rws.stream_len;
     b.inl = c->rws.inl.as<float4>();
+    b.tiles = c->rws.tiles.as<uint4>();
     b.err = c->rws.err.as<int>();
     rp = RansacParams{};
     rp.thresh = prm->ransac_thresh > 0 ? prm->ransac_thresh : 3.0;  // findHomography: thresh <= 0 -> 3

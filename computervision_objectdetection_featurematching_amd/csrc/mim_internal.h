@@ -63,6 +63,8 @@ struct RansacState {
     unsigned long long modM;  // Lemire fast-modulo constant for % n (RNG::uniform(0, n))
     long long win_base;    // stream position of flags[0] of the current chunk's attempt window
     int win_len;           // attempts precomputed in that window
+    float sa, sb;          // power-of-two scales of the source / destination coordinates (MFMA bound)
+    float smax;            // max over points of |x|+|y|+|u|+|v| (MFMA bound margin)
 };
 
 struct RansacParams {
@@ -103,6 +105,7 @@ struct RansacBufs {
     const uint32_t* stream;   // raw cv::RNG((uint64)-1).next() stream shared by every problem
     long long stream_len;
     float4* inl;              // [good_off + k] compressed inliers for the refit (scratch)
+    uint4* tiles;             // [good_off / 32 + tile][2][64] f16 MFMA operand tiles of the points
     int* err;                 // device error word (bit0: RNG stream exhausted)
 };
 }  // namespace mim

@@ -1597,6 +1597,53 @@ typedef float f2v __attribute__((ext_vector_type(2)));
 typedef float f4v __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ f2v pk_fma(f2v a, f2v b, f2v c) { return __builtin_elementwise_fma(a, b, c); }
 
+// Closed-form hypothesis of the bound kernels for the sample s4: Hd = H / H[8] (fp64); invalid =
+// runKernel's degeneracy test; uncertain = no usable bound (conditioning screen, H[8] ~ 0, non-finite);
+// eta > 0 widens the margin (poorly conditioned samples).
+__device__ __forceinline__ void bound_hypothesis(const float4* __restrict__ P, int4 s4, double (&Hd)[8],
+                                                 bool& invalid, bool& uncertain, float& eta) {
+    const float4 q0 = P[s4.x], q1 = P[s4.y], q2 = P[s4.z], q3 = P[s4.w];
+    // runKernel's own degeneracy test (exact, cheap): spread < DBL_EPSILON -> no model
+    const float M[8] = {q0.x, q0.y, q1.x, q1.y, q2.x, q2.y, q3.x, q3.y};
+    const float m[8] = {q0.z, q0.w, q1.z, q1.w, q2.z, q2.w, q3.z, q3.w};
+    double cMx = 0, cMy = 0, cmx = 0, cmy = 0, sMx = 0, sMy = 0, smx = 0, smy = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        cmx += m[2 * i]; cmy += m[2 * i + 1];
+        cMx += M[2 * i]; cMy += M[2 * i + 1];
+    }
+    cmx /= 4; cmy /= 4; cMx /= 4; cMy /= 4;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        smx += fabs(m[2 * i] - cmx); smy += fabs(m[2 * i + 1] - cmy);
+        sMx += fabs(M[2 * i] - cMx); sMy += fabs(M[2 * i + 1] - cMy);
+    }
+    invalid = fabs(smx) < DBL_EPSILON || fabs(smy) < DBL_EPSILON || fabs(sMx) < DBL_EPSILON ||
+              fabs(sMy) < DBL_EPSILON;
+    const double sx[4] = {q0.x, q1.x, q2.x, q3.x}, sy[4] = {q0.y, q1.y, q2.y, q3.y};
+    const double dx[4] = {q0.z, q1.z, q2.z, q3.z}, dy[4] = {q0.w, q1.w, q2.w, q3.w};
+    const double rho = fmin(min_rel_area(sx, sy), min_rel_area(dx, dy));
+    uncertain = !(rho >= kScreenArea);
+    if (rho < kScreenTight) eta = (float)(1e-14 / (rho * rho));
+    double Qs[9], Qd[9], Ai[9], H[9];
+    square_to_quad(sx, sy, Qs);
+    square_to_quad(dx, dy, Qd);
+    // adjugate of Qs (inverse up to scale)
+    Ai[0] = Qs[4] * Qs[8] - Qs[5] * Qs[7]; Ai[1] = Qs[2] * Qs[7] - Qs[1] * Qs[8]; Ai[2] = Qs[1] * Qs[5] - Qs[2] * Qs[4];
+    Ai[3] = Qs[5] * Qs[6] - Qs[3] * Qs[8]; Ai[4] = Qs[0] * Qs[8] - Qs[2] * Qs[6]; Ai[5] = Qs[2] * Qs[3] - Qs[0] * Qs[5];
+    Ai[6] = Qs[3] * Qs[7] - Qs[4] * Qs[6]; Ai[7] = Qs[1] * Qs[6] - Qs[0] * Qs[7]; Ai[8] = Qs[0] * Qs[4] - Qs[1] * Qs[3];
+    mat3_mul(Qd, Ai, H);
+    double hmax = 0;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) hmax = fmax(hmax, fabs(H[i]));
+    uncertain |= !(fabs(H[8]) > 1e-9 * hmax);  // also catches NaN
+    const double inv = 1.0 / H[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) Hd[i] = H[i] * inv;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) uncertain |= !isfinite((float)Hd[i]);
+}
+
 // kLo = false (chunks after the first, once maxGoodCount is known): only an upper bound is
 // counted, lo = 0 — the candidate rule then rests on maxGoodCount and the earlier chunks' bounds.
 // That upper bound uses the box max(|ex|, |ey|) <= sqrt(t_hi) |W|, implied by the disc
@@ -1624,46 +1671,10 @@ __global__ __launch_bounds__(256) void ransac_bound_kernel(const RansacState* __
     float Hf[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (act) {
         const int4 s4 = decode_sample(samples[o], stream, (unsigned)n, S.modM);
-        const float4 q0 = P[s4.x], q1 = P[s4.y], q2 = P[s4.z], q3 = P[s4.w];
-        // runKernel's own degeneracy test (exact, cheap): spread < DBL_EPSILON -> no model
-        const float M[8] = {q0.x, q0.y, q1.x, q1.y, q2.x, q2.y, q3.x, q3.y};
-        const float m[8] = {q0.z, q0.w, q1.z, q1.w, q2.z, q2.w, q3.z, q3.w};
-        double cMx = 0, cMy = 0, cmx = 0, cmy = 0, sMx = 0, sMy = 0, smx = 0, smy = 0;
+        double Hd[8];
+        bound_hypothesis(P, s4, Hd, invalid, uncertain, eta);
 #pragma unroll
-        for (int i = 0; i < 4; i++) {
-            cmx += m[2 * i]; cmy += m[2 * i + 1];
-            cMx += M[2 * i]; cMy += M[2 * i + 1];
-        }
-        cmx /= 4; cmy /= 4; cMx /= 4; cMy /= 4;
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-            smx += fabs(m[2 * i] - cmx); smy += fabs(m[2 * i + 1] - cmy);
-            sMx += fabs(M[2 * i] - cMx); sMy += fabs(M[2 * i + 1] - cMy);
-        }
-        invalid = fabs(smx) < DBL_EPSILON || fabs(smy) < DBL_EPSILON || fabs(sMx) < DBL_EPSILON ||
-                  fabs(sMy) < DBL_EPSILON;
-        const double sx[4] = {q0.x, q1.x, q2.x, q3.x}, sy[4] = {q0.y, q1.y, q2.y, q3.y};
-        const double dx[4] = {q0.z, q1.z, q2.z, q3.z}, dy[4] = {q0.w, q1.w, q2.w, q3.w};
-        const double rho = fmin(min_rel_area(sx, sy), min_rel_area(dx, dy));
-        uncertain = !(rho >= kScreenArea);
-        if (rho < kScreenTight) eta = (float)(1e-14 / (rho * rho));
-        double Qs[9], Qd[9], Ai[9], H[9];
-        square_to_quad(sx, sy, Qs);
-        square_to_quad(dx, dy, Qd);
-        // adjugate of Qs (inverse up to scale)
-        Ai[0] = Qs[4] * Qs[8] - Qs[5] * Qs[7]; Ai[1] = Qs[2] * Qs[7] - Qs[1] * Qs[8]; Ai[2] = Qs[1] * Qs[5] - Qs[2] * Qs[4];
-        Ai[3] = Qs[5] * Qs[6] - Qs[3] * Qs[8]; Ai[4] = Qs[0] * Qs[8] - Qs[2] * Qs[6]; Ai[5] = Qs[2] * Qs[3] - Qs[0] * Qs[5];
-        Ai[6] = Qs[3] * Qs[7] - Qs[4] * Qs[6]; Ai[7] = Qs[1] * Qs[6] - Qs[0] * Qs[7]; Ai[8] = Qs[0] * Qs[4] - Qs[1] * Qs[3];
-        mat3_mul(Qd, Ai, H);
-        double hmax = 0;
-#pragma unroll
-        for (int i = 0; i < 9; ++i) hmax = fmax(hmax, fabs(H[i]));
-        uncertain |= !(fabs(H[8]) > 1e-9 * hmax);  // also catches NaN
-        const double inv = 1.0 / H[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) Hf[i] = (float)(H[i] * inv);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) uncertain |= !isfinite(Hf[i]);
+        for (int i = 0; i < 8; ++i) Hf[i] = (float)Hd[i];
     }
     const bool count = act && !invalid && !uncertain;
     // per-point margins computed at staging: err bound 0.5 px^2 + 1e-7 (|x|+|y|+|u|+|v|)^2 around the
@@ -1749,6 +1760,237 @@ __global__ __launch_bounds__(256) void ransac_bound_kernel(const RansacState* __
         }
     }
     if (act) bounds[o] = invalid ? make_int2(-1, -1) : (uncertain ? make_int2(0, n) : make_int2(lo, hi));
+}
+
+// ------------------------------------------------------------------------------------------------
+// Upper bounds on the matrix cores (chunks after the first).  Per (hypothesis, point) the box test
+// needs ex = X - uW, ey = Y - vW and W: three dot products of length 6 between the hypothesis and
+// the point, i.e. three small GEMMs [points x 16] x [16 x hypotheses] on v_mfma_f32_32x32x16_f16.
+// Coordinates are scaled by powers of two into [-1, 1] (x' = sa x, u' = sb u, exact), the
+// hypothesis H' = diag(sb, sb, 1) H diag(1/sa, 1/sa, 1) by a power of two into [-1, 1] (h8 = 2^-e
+// exact in f16 for e <= 24), and every factor is split into f16 hi + lo: a*b ~ ah*bh + ah*bl +
+// al*bh, so each of the six products takes 3 K-slots (2 for the factors that are exact: 1 and h8):
+//   point   ax = [xh xl xh  yh yl yh  1 1 | uxh uxl uxh  uyh uyl uyh  uh ul]
+//   hyp     bx = [h0h h0h h0l  h1h h1h h1l  h2h h2l | -h6h -h6h -h6l  -h7h -h7h -h7l  -h8 -h8]
+//   (ay, by: v and h3 h4 h5; W = ax . [h6h h6h h6l h7h h7h h7l h8 0 | 0 ...]).
+// Error of each computed quantity (|factors| <= 1, f16 split 2^-22 per factor and 2^-22 per dropped
+// al*bl, fp32 products u'x' 2^-24, fp32 accumulation of <= 16 terms of total magnitude <= 6):
+// < 1e-5 in these units; kMfmaErr = 2^-15 = 3.05e-5.  A point is out of the box only if
+//   max(|ex|, |ey|) > C |W| + (1 + C) kMfmaErr,  C = sb sqrt(thr2 + d_max (+ widening)) (1 + 1e-6)
+// with d_max the largest per-point margin of the problem, so the count of the rest bounds the
+// exact inlier count from above exactly as the fp32 box test does ("Bounds").
+// MI355X MFMA keeps f16 subnormal operands (tools/probe/f16_probe.hip).
+// ------------------------------------------------------------------------------------------------
+typedef _Float16 h8v __attribute__((ext_vector_type(8)));
+typedef float f16acc __attribute__((ext_vector_type(16)));
+constexpr float kMfmaErr = 0x1p-15f;
+constexpr int kTileChunk = 16;  // 32-point tiles per LDS stage of the MFMA bound kernel (32 KiB)
+
+__device__ __forceinline__ void split_f16(float a, _Float16& hi, _Float16& lo) {
+    hi = (_Float16)a;
+    lo = (_Float16)(a - (float)hi);  // a - hi is exact in fp32
+}
+__device__ __forceinline__ void split_f16(double a, _Float16& hi, _Float16& lo) {
+    hi = (_Float16)(float)a;
+    lo = (_Float16)(float)(a - (double)(float)hi);
+}
+
+// Point tiles of every active problem, once per batch: scales, then per 32-point tile the A-operand
+// fragments of lane l (row l & 31, k = 8 (l >> 5) .. + 7) for ax and ay.  Rows past n are zero.
+__global__ __launch_bounds__(256) void ransac_tiles_kernel(RansacState* __restrict__ st,
+                                                           const ProbDev* __restrict__ probs,
+                                                           const float4* __restrict__ pts,
+                                                           uint4* __restrict__ tiles) {
+    __shared__ float red[3][4];
+    const int p = blockIdx.x, tid = threadIdx.x;
+    RansacState* Sp = st + p;
+    if (!Sp->active || Sp->done) return;
+    const int n = Sp->n;
+    const long long go = probs[p].good_off;  // multiple of 32 (build_tables)
+    const float4* __restrict__ P = pts + go;
+    float mxy = 0.f, muv = 0.f, ms = 0.f;
+    for (int i = tid; i < n; i += 256) {
+        const float4 q = P[i];
+        mxy = fmaxf(mxy, fmaxf(fabsf(q.x), fabsf(q.y)));
+        muv = fmaxf(muv, fmaxf(fabsf(q.z), fabsf(q.w)));
+        ms = fmaxf(ms, fabsf(q.x) + fabsf(q.y) + fabsf(q.z) + fabsf(q.w));
+    }
+    for (int off = 32; off >= 1; off >>= 1) {
+        mxy = fmaxf(mxy, __shfl_xor(mxy, off));
+        muv = fmaxf(muv, __shfl_xor(muv, off));
+        ms = fmaxf(ms, __shfl_xor(ms, off));
+    }
+    if ((tid & 63) == 0) {
+        red[0][tid >> 6] = mxy;
+        red[1][tid >> 6] = muv;
+        red[2][tid >> 6] = ms;
+    }
+    __syncthreads();
+    mxy = fmaxf(fmaxf(red[0][0], red[0][1]), fmaxf(red[0][2], red[0][3]));
+    muv = fmaxf(fmaxf(red[1][0], red[1][1]), fmaxf(red[1][2], red[1][3]));
+    ms = fmaxf(fmaxf(red[2][0], red[2][1]), fmaxf(red[2][2], red[2][3]));
+    int ea = 0, eb = 0;
+    (void)frexpf(mxy, &ea);  // mxy < 2^ea
+    (void)frexpf(muv, &eb);
+    const float sa = ldexpf(1.f, -ea), sb = ldexpf(1.f, -eb);
+    if (tid == 0) {
+        Sp->sa = sa;
+        Sp->sb = sb;
+        Sp->smax = ms;
+    }
+    uint4* __restrict__ T = tiles + (go >> 5) * 128;
+    const int nt = (n + 31) >> 5;
+    const _Float16 one = (_Float16)1.f;
+    for (int i = tid; i < nt * 32; i += 256) {
+        h8v lo = {}, axh = {}, ayh = {};
+        if (i < n) {
+            const float4 q = P[i];
+            const float x = q.x * sa, y = q.y * sa, u = q.z * sb, v = q.w * sb;
+            _Float16 a, b;
+            split_f16(x, a, b); lo[0] = a; lo[1] = b; lo[2] = a;
+            split_f16(y, a, b); lo[3] = a; lo[4] = b; lo[5] = a;
+            lo[6] = one; lo[7] = one;
+            split_f16(u * x, a, b); axh[0] = a; axh[1] = b; axh[2] = a;
+            split_f16(u * y, a, b); axh[3] = a; axh[4] = b; axh[5] = a;
+            split_f16(u, a, b); axh[6] = a; axh[7] = b;
+            split_f16(v * x, a, b); ayh[0] = a; ayh[1] = b; ayh[2] = a;
+            split_f16(v * y, a, b); ayh[3] = a; ayh[4] = b; ayh[5] = a;
+            split_f16(v, a, b); ayh[6] = a; ayh[7] = b;
+        }
+        uint4* t = T + (i >> 5) * 128;
+        const int r = i & 31;
+        t[r] = __builtin_bit_cast(uint4, lo);        // ax, lanes 0-31
+        t[32 + r] = __builtin_bit_cast(uint4, axh);  // ax, lanes 32-63
+        t[64 + r] = __builtin_bit_cast(uint4, lo);   // ay, lanes 0-31
+        t[96 + r] = __builtin_bit_cast(uint4, ayh);  // ay, lanes 32-63
+    }
+}
+
+// Upper bounds of the inlier counts of 256 consecutive iterations per block (64 per wave: two
+// column blocks of 32 hypotheses), the point tiles staged through LDS and shared by the 4 waves.
+__global__ __launch_bounds__(256) void ransac_bound_mfma_kernel(const RansacState* __restrict__ st,
+                                                                const ProbDev* __restrict__ probs,
+                                                                const float4* __restrict__ pts,
+                                                                const int4* __restrict__ samples,
+                                                                const uint32_t* __restrict__ stream,
+                                                                const uint4* __restrict__ tiles,
+                                                                int2* __restrict__ bounds, int c0, int c1, int bpp,
+                                                                float thr2) {
+    __shared__ uint4 lt[kTileChunk * 128];
+    const int p = blockIdx.x / bpp;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int it = c0 + (blockIdx.x % bpp) * 256 + tid;
+    const RansacState S = st[p];
+    if (!S.active || S.done) return;  // uniform over the block
+    if (c0 + (blockIdx.x % bpp) * 256 >= min(c1, S.produced)) return;  // whole block idle
+    const bool act = it < c1 && it < S.produced;
+    const long long o = probs[p].it_off + it;
+    const long long go = probs[p].good_off;
+    const float4* __restrict__ P = pts + go;
+    const int n = S.n;
+    bool uncertain = false, invalid = false;
+    float eta = 0.f;
+    double Hd[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (act) {
+        const int4 s4 = decode_sample(samples[o], stream, (unsigned)n, S.modM);
+        bound_hypothesis(P, s4, Hd, invalid, uncertain, eta);
+    }
+    // H' in scaled coordinates, then scaled by 2^-e into [-1, 1]
+    const double rs = (double)S.sb / (double)S.sa;
+    double h[9] = {Hd[0] * rs, Hd[1] * rs, Hd[2] * S.sb, Hd[3] * rs, Hd[4] * rs, Hd[5] * S.sb,
+                   Hd[6] / S.sa, Hd[7] / S.sa, 1.0};
+    double hm = 0;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) hm = fmax(hm, fabs(h[i]));
+    int e = 0;
+    (void)frexp(hm, &e);  // hm < 2^e, e >= 1 (h8 = 1)
+    uncertain |= e > 24;  // h8 = 2^-e would not be an f16
+    const bool count = act && !invalid && !uncertain;
+    const double sc = ldexp(1.0, -e);
+#pragma unroll
+    for (int i = 0; i < 9; ++i) h[i] *= sc;
+    // per-hypothesis box constants (d_max and, for poorly conditioned samples, the widening at smax)
+    float tt = thr2 + fmaf(1e-7f * S.smax, S.smax, 0.5f);
+    if (eta > 0.f) tt += S.smax * fmaf(eta * eta, S.smax, 10.2f * eta);
+    const float C = S.sb * sqrtf(tt) * (1.f + 1e-6f);
+    const float E = (1.f + C) * kMfmaErr * (1.f + 1e-6f);
+    // B-operand fragments of the own hypothesis: k 0-7 (bx, by, bw) and k 8-15 (shared by bx, by)
+    h8v fx = {}, fy = {}, fw = {}, fn = {};
+    if (count) {
+        _Float16 a, b;
+        split_f16(h[0], a, b); fx[0] = a; fx[1] = a; fx[2] = b;
+        split_f16(h[1], a, b); fx[3] = a; fx[4] = a; fx[5] = b;
+        split_f16(h[2], a, b); fx[6] = a; fx[7] = b;
+        split_f16(h[3], a, b); fy[0] = a; fy[1] = a; fy[2] = b;
+        split_f16(h[4], a, b); fy[3] = a; fy[4] = a; fy[5] = b;
+        split_f16(h[5], a, b); fy[6] = a; fy[7] = b;
+        split_f16(h[6], a, b); fw[0] = a; fw[1] = a; fw[2] = b;
+        split_f16(h[7], a, b); fw[3] = a; fw[4] = a; fw[5] = b;
+        fw[6] = (_Float16)(float)h[8];  // 2^-e: exact
+        fn = -fw;
+        fn[7] = fn[6];
+    }
+    // column block 0 = hypotheses (lanes) 0-31, block 1 = 32-63; lane l holds column l & 31 at
+    // k = 8 (l >> 5) .. + 7, so half the fragments come from the partner lane l ^ 32:
+    // low lanes need the partner's fx, fy, fw (block 1), high lanes the partner's fn (block 0)
+    const bool lowh = lane < 32;
+    const uint4 ux = __builtin_bit_cast(uint4, fx), uy = __builtin_bit_cast(uint4, fy);
+    const uint4 uw = __builtin_bit_cast(uint4, fw), un = __builtin_bit_cast(uint4, fn);
+    const uint4 s1 = lowh ? un : ux;
+    uint4 r1, r2, r3;
+    r1.x = __shfl_xor(s1.x, 32); r1.y = __shfl_xor(s1.y, 32); r1.z = __shfl_xor(s1.z, 32); r1.w = __shfl_xor(s1.w, 32);
+    r2.x = __shfl_xor(uy.x, 32); r2.y = __shfl_xor(uy.y, 32); r2.z = __shfl_xor(uy.z, 32); r2.w = __shfl_xor(uy.w, 32);
+    r3.x = __shfl_xor(uw.x, 32); r3.y = __shfl_xor(uw.y, 32); r3.z = __shfl_xor(uw.z, 32); r3.w = __shfl_xor(uw.w, 32);
+    const uint4 zero4 = make_uint4(0, 0, 0, 0);
+    const h8v b0x = __builtin_bit_cast(h8v, lowh ? ux : r1);
+    const h8v b0y = __builtin_bit_cast(h8v, lowh ? uy : r1);
+    const h8v b0w = __builtin_bit_cast(h8v, lowh ? uw : zero4);
+    const h8v b1x = __builtin_bit_cast(h8v, lowh ? r1 : un);
+    const h8v b1y = __builtin_bit_cast(h8v, lowh ? r2 : un);
+    const h8v b1w = __builtin_bit_cast(h8v, lowh ? r3 : zero4);
+    const float Cp = __shfl_xor(C, 32), Ep = __shfl_xor(E, 32);
+    const float C0 = lowh ? C : Cp, E0 = lowh ? E : Ep, C1 = lowh ? Cp : C, E1 = lowh ? Ep : E;
+    const bool wave_counts = __any(count);
+    float big = INFINITY;
+    asm volatile("" : "+v"(big));
+    const uint4* __restrict__ T = tiles + (go >> 5) * 128;
+    const int nt = (n + 31) >> 5;
+    unsigned out0 = 0, out1 = 0;
+    for (int t0 = 0; t0 < nt; t0 += kTileChunk) {
+        const int tc = min(kTileChunk, nt - t0);
+        __syncthreads();
+        for (int i = tid; i < tc * 128; i += 256) lt[i] = T[(long long)t0 * 128 + i];
+        __syncthreads();
+        if (!wave_counts) continue;
+        for (int t = 0; t < tc; ++t) {
+            const h8v ax = __builtin_bit_cast(h8v, lt[t * 128 + lane]);
+            const h8v ay = __builtin_bit_cast(h8v, lt[t * 128 + 64 + lane]);
+            const f16acc zc = {};
+            const f16acc ex0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ax, b0x, zc, 0, 0, 0);
+            const f16acc ey0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ay, b0y, zc, 0, 0, 0);
+            const f16acc w0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ax, b0w, zc, 0, 0, 0);
+            const f16acc ex1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ax, b1x, zc, 0, 0, 0);
+            const f16acc ey1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ay, b1y, zc, 0, 0, 0);
+            const f16acc w1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ax, b1w, zc, 0, 0, 0);
+            unsigned bits0 = 0, bits1 = 0;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                // sign bit of R - max(|ex|, |ey|), R = C |W| + E: set when the point is out of the box
+                // (med3(a, b, big) = max(a, b) without the NaN canonicalisation of fmaxf; big is
+                // opaque so the compiler cannot turn the med3 back into a max)
+                const float d0 = fmaf(C0, fabsf(w0[r]), E0) - __builtin_amdgcn_fmed3f(fabsf(ex0[r]), fabsf(ey0[r]), big);
+                const float d1 = fmaf(C1, fabsf(w1[r]), E1) - __builtin_amdgcn_fmed3f(fabsf(ex1[r]), fabsf(ey1[r]), big);
+                bits0 = __builtin_amdgcn_alignbit(bits0, __float_as_uint(d0), 31);
+                bits1 = __builtin_amdgcn_alignbit(bits1, __float_as_uint(d1), 31);
+            }
+            out0 += __popc(bits0);
+            out1 += __popc(bits1);
+        }
+    }
+    // rows (points) of a column are split over lanes l and l ^ 32
+    const unsigned o0 = out0 + __shfl_xor(out0, 32), o1 = out1 + __shfl_xor(out1, 32);
+    const int outs = (int)(lowh ? o0 : o1);
+    if (act) bounds[o] = invalid ? make_int2(-1, -1) : (uncertain ? make_int2(0, n) : make_int2(0, n - outs));
 }
 
 // exact count of one hypothesis (runKernel + computeError + findInliers, bit-exact)
@@ -2659,6 +2901,10 @@ void ransac_enqueue(const RansacParams& prm, int n_probs, const ProbDev* probs, 
     const int use_chain = !(sw && sw[0] == '1');
     int c0 = 0, chunk = 4096;
     const float thr2 = (float)(prm.thresh * prm.thresh);
+    // MIM_BOUND_VALU=1: later chunks on the fp32 VALU bound kernel (cross-check mode)
+    const char* bv = getenv("MIM_BOUND_VALU");
+    const bool bound_mfma = !(bv && bv[0] == '1');
+    if (!exact_all && bound_mfma) ransac_tiles_kernel<<<n_probs, 256, 0, s>>>(b.state, probs, pts, b.tiles);
     while (c0 < max_iters) {
         const int c1 = (int)std::min<long long>((long long)c0 + chunk, max_iters);
         // attempt outcomes for a window of ~28 draws per wanted iteration (pass rate ~1/5), the walk
@@ -2702,6 +2948,9 @@ void ransac_enqueue(const RansacParams& prm, int n_probs, const ProbDev* probs, 
             if (c0 == 0)
                 ransac_bound_kernel<true><<<n_probs * bpp256, 256, 0, s>>>(b.state, probs, pts, b.samples, b.stream,
                                                                           b.bounds, c0, c1, bpp256, thr2);
+            else if (bound_mfma)
+                ransac_bound_mfma_kernel<<<n_probs * bpp256, 256, 0, s>>>(b.state, probs, pts, b.samples, b.stream,
+                                                                          b.tiles, b.bounds, c0, c1, bpp256, thr2);
             else
                 ransac_bound_kernel<false><<<n_probs * bpp256, 256, 0, s>>>(b.state, probs, pts, b.samples, b.stream,
                                                                            b.bounds, c0, c1, bpp256, thr2);

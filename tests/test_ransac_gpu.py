@@ -206,6 +206,40 @@ def test_filtered_equals_exact_all(oracle):
         assert (ha is None) == (hb is None) and (ha is None or np.array_equal(ha, hb))
 
 
+def test_bound_mfma_equals_valu():
+    """Later RANSAC chunks bound the inlier counts on the matrix cores (f16 hi/lo split GEMMs) by
+    default; the fp32 VALU bound kernel (MIM_BOUND_VALU=1) must lead to the identical output, and so
+    must the all-exact reference mode (both bounds are only filters)."""
+    import os
+    from computervision_objectdetection_featurematching_amd import Matcher, default_params
+    ds = make_dataset(2, 3, 1500, 2500, 500, inlier_frac=0.08, seed=2718)
+    sets = _adversarial_sets()
+    outs = []
+    for key, mode in (("MIM_BOUND_VALU", "0"), ("MIM_BOUND_VALU", "1"), ("MIM_RANSAC_EXACT", "1")):
+        os.environ[key] = mode
+        m = Matcher(0)
+        try:
+            q = [m.add_set(d, k) for d, k in zip(ds.model_desc, ds.model_kp)]
+            t = [m.add_set(d, k) for d, k in zip(ds.scene_desc, ds.scene_kp)]
+            res = m.match_batch([(q[a], t[b]) for a, b in ds.problems], default_params(max_iters=12000))
+            masks = [m.problem_detail(i, int(r["n_good"]))[2] for i, r in enumerate(res)]
+            fh = []
+            for s_, d_ in sets:
+                fh.append(m.find_homography(s_, d_, 5.0, 12000) + (m.batch_results(1).tobytes(),))
+        finally:
+            m.close()
+            os.environ.pop(key, None)
+        outs.append((res, masks, fh))
+    r0, m0, f0 = outs[0]
+    for r1, m1, f1 in outs[1:]:
+        assert r0.tobytes() == r1.tobytes()
+        for a, b in zip(m0, m1):
+            np.testing.assert_array_equal(a, b)
+        for (ha, ma, ra), (hb, mb, rb) in zip(f0, f1):
+            np.testing.assert_array_equal(ma, mb)
+            assert ra == rb
+
+
 def test_mostly_degenerate_points(matcher, oracle):
     """Most 4-subsets collinear: long runs of rejected getSubset attempts, many redraws."""
     rng = np.random.default_rng(17)

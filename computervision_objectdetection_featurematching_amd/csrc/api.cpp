@@ -22,7 +22,7 @@
 #include "mim_internal.h"
 
 namespace mim {
-void launch_prep_set(const float* src, int n, uint16_t* frag, float* norm, int* flags, hipStream_t st);
+void launch_prep_batch(const PrepJob* jobs, int njobs, int total_tiles, hipStream_t st);
 void launch_knn(const ProbDev* probs, const KnnWork* works, int n_works, Top2* parts, hipStream_t st);
 void launch_ratio(const ProbDev* probs, int n_probs, const Top2* parts, float ratio, int32_t* good_q,
                   int32_t* good_t, float4* pts, int* n_good, int32_t* knn_idx, float* knn_dist,
@@ -163,6 +163,11 @@ struct mim_ctx {
     int n_works = 0;
     std::vector<long long> h_good_off;
     PinnedStage stage;
+    // sets created since the last batch: their prep runs as one launch at the next build_tables
+    std::vector<PrepJob> pend;
+    std::vector<int> pend_set;
+    PinnedStage prep_stage;
+    DevBuf prep_jobs;
     int last_n = 0;
     // MIM_RANSAC_EXACT=1: evaluate every hypothesis exactly (reference mode for cross-checks)
     int exact_all = 0;
@@ -257,10 +262,11 @@ void mim_ctx_destroy(mim_ctx* c) {
     }
     if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
     c->stage.destroy();
+    c->prep_stage.destroy();
     c->arena.release();
     for (DevBuf* b : {&c->probs, &c->works, &c->parts, &c->good_q, &c->good_t, &c->pts, &c->n_good,
                       &c->results, &c->masks, &c->knn_idx, &c->knn_dist, &c->rws.state, &c->rws.samples,
-                      &c->rws.hyp, &c->rws.counts, &c->rws.bounds, &c->rws.flags, &c->rws.irr, &c->rws.irr_cnt, &c->rws.pass_bits, &c->rws.chains, &c->rws.best_h, &c->rws.cand, &c->rws.ncand, &c->rws.cex, &c->rws.cH, &c->rws.stream, &c->rws.scratch, &c->rws.inl, &c->rws.tiles, &c->rws.err})
+                      &c->rws.hyp, &c->rws.counts, &c->rws.bounds, &c->rws.flags, &c->rws.irr, &c->rws.irr_cnt, &c->rws.pass_bits, &c->rws.chains, &c->rws.best_h, &c->rws.cand, &c->rws.ncand, &c->rws.cex, &c->rws.cH, &c->rws.stream, &c->rws.scratch, &c->rws.inl, &c->rws.tiles, &c->rws.err, &c->prep_jobs})
         b->release();
     if (c->own) (void)hipStreamDestroy(c->own);
     delete c;
@@ -305,11 +311,9 @@ static mim_status set_create_locked(mim_ctx* c, const float* desc, const float* 
     r.d.n = n;
     r.d.n_tiles = (n + 63) / 64;
     const size_t tiles = (size_t)std::max(r.d.n_tiles, 1);
-    void *frag, *norm, *flags;
+    void *frag, *norm;
     HIPCHK(c, c->arena.alloc(tiles * kTileBytes, &frag));
     HIPCHK(c, c->arena.alloc(tiles * 64 * sizeof(float), &norm));
-    HIPCHK(c, c->arena.alloc(sizeof(int) * 4, &flags));
-    HIPCHK(c, hipMemsetAsync(flags, 0, sizeof(int) * 4, c->stream));
     const float* f32 = desc;
     const float* kpd = kp;
     if (!on_device && n > 0) {
@@ -325,12 +329,41 @@ static mim_status set_create_locked(mim_ctx* c, const float* desc, const float* 
     r.d.norm = (const float*)norm;
     r.d.f32 = f32;
     r.d.kp = (const float2*)kpd;
-    r.d.flags = (int*)flags;
-    launch_prep_set(f32, n, (uint16_t*)frag, (float*)norm, (int*)flags, c->stream);
-    HIPCHK(c, hipGetLastError());
+    r.d.flags = nullptr;  // assigned when the prep is flushed
     if (!on_device) HIPCHK(c, hipStreamSynchronize(c->stream));  // host buffers may go away
     *set_id = (int32_t)c->sets.size();
+    c->pend.push_back(PrepJob{f32, (uint16_t*)frag, (float*)norm, nullptr, n, 0});
+    c->pend_set.push_back(*set_id);
     c->sets.push_back(r);
+    return MIM_OK;
+}
+
+// Preps of the sets created since the last flush: one flags block, one memset, one launch.
+static mim_status flush_preps(mim_ctx* c) {
+    const int nj = (int)c->pend.size();
+    if (nj == 0) return MIM_OK;
+    void* flags;
+    HIPCHK(c, c->arena.alloc(sizeof(int) * 4 * (size_t)nj, &flags));
+    HIPCHK(c, hipMemsetAsync(flags, 0, sizeof(int) * 4 * (size_t)nj, c->stream));
+    int tiles = 0;
+    for (int j = 0; j < nj; ++j) {
+        PrepJob& J = c->pend[j];
+        J.flags = static_cast<int*>(flags) + 4 * j;
+        J.tile0 = tiles;
+        tiles += (J.n + 63) / 64;
+        c->sets[c->pend_set[j]].d.flags = J.flags;
+    }
+    const size_t bytes = sizeof(PrepJob) * nj;
+    HIPCHK(c, c->prep_jobs.ensure(bytes));
+    char* st = nullptr;
+    HIPCHK(c, c->prep_stage.acquire(bytes, &st));
+    memcpy(st, c->pend.data(), bytes);
+    HIPCHK(c, hipMemcpyAsync(c->prep_jobs.p, st, bytes, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, c->prep_stage.release_after(c->stream));
+    launch_prep_batch(c->prep_jobs.as<PrepJob>(), nj, tiles, c->stream);
+    HIPCHK(c, hipGetLastError());
+    c->pend.clear();
+    c->pend_set.clear();
     return MIM_OK;
 }
 
@@ -348,6 +381,8 @@ mim_status mim_sets_clear(mim_ctx* c) {
     // no host wait: every write into the arena (prep kernels, copies of host rows) is ordered on the
     // ctx stream after the previous batch, whose groups join back into that stream
     c->sets.clear();
+    c->pend.clear();
+    c->pend_set.clear();
     c->arena.rewind();
     return MIM_OK;
 }
@@ -366,6 +401,8 @@ static int pick_groups(int n) {
 }
 
 static mim_status build_tables(mim_ctx* c, const mim_problem* problems, int n, int max_iters, int groups = 1) {
+    mim_status fs = flush_preps(c);  // the sets' device tiles and flags, before ProbDev copies them
+    if (fs != MIM_OK) return fs;
     c->h_probs.assign(n, ProbDev{});
     long long part = 0, good = 0, it = 0;
     int total_qblocks = 0;

@@ -30,11 +30,9 @@ typedef __attribute__((ext_vector_type(16))) float f32x16;
 // row = 32u + (lane & 31), col = 16s + 8(lane >> 5) + j — exactly the per-lane operand of
 // v_mfma_f32_32x32x16_bf16, so one 1 KiB wave load = one fragment, fully coalesced.
 // ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void prep_set_kernel(const float* __restrict__ src, int n,
-                                                       uint16_t* __restrict__ frag,
-                                                       float* __restrict__ norm,
-                                                       int* __restrict__ flags) {
-    const int tile = blockIdx.x, tid = threadIdx.x;
+__device__ __forceinline__ void prep_tile(const float* __restrict__ src, int n, uint16_t* __restrict__ frag,
+                                          float* __restrict__ norm, int* __restrict__ flags, int tile) {
+    const int tid = threadIdx.x;
     int bad = 0;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -74,6 +72,19 @@ __global__ __launch_bounds__(256) void prep_set_kernel(const float* __restrict__
         norm[row] = row < n ? s : FLT_MAX;  // padded rows never win (copied as is by the DMA)
     }
     if (__any(bad) && (tid & 63) == 0) atomicOr(flags, 1);
+}
+
+// Every set created since the last batch in one launch: block b preps tile b - tile0 of the last
+// job with tile0 <= b (jobs ascending in tile0; sets without rows own no tile).
+__global__ __launch_bounds__(256) void prep_batch_kernel(const PrepJob* __restrict__ jobs, int njobs) {
+    int lo = 0, hi = njobs - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (jobs[mid].tile0 <= (int)blockIdx.x) lo = mid;
+        else hi = mid - 1;
+    }
+    const PrepJob J = jobs[lo];
+    prep_tile(J.src, J.n, J.frag, J.norm, J.flags, (int)blockIdx.x - J.tile0);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -557,9 +568,8 @@ __global__ __launch_bounds__(1024) void ratio_compact_kernel(const ProbDev* __re
 // ------------------------------------------------------------------------------------------------
 // host-side launchers (called from api.cpp)
 // ------------------------------------------------------------------------------------------------
-void launch_prep_set(const float* src, int n, uint16_t* frag, float* norm, int* flags, hipStream_t st) {
-    const int tiles = (n + 63) / 64;
-    if (tiles > 0) prep_set_kernel<<<tiles, 256, 0, st>>>(src, n, frag, norm, flags);
+void launch_prep_batch(const PrepJob* jobs, int njobs, int total_tiles, hipStream_t st) {
+    if (njobs > 0 && total_tiles > 0) prep_batch_kernel<<<total_tiles, 256, 0, st>>>(jobs, njobs);
 }
 
 // Both kernels are enqueued; each block reads its problem's integrality flags (set by prep on the

@@ -23,6 +23,16 @@ struct SetDev {
     int* flags;            // bit0: a value is not an integer in [0,255]
 };
 
+// Deferred prep of one set (bf16 fragments, norms, integrality flag), batched per match call.
+struct PrepJob {
+    const float* src;
+    uint16_t* frag;
+    float* norm;
+    int* flags;
+    int n;
+    int tile0;  // first block of this set in the batched launch
+};
+
 struct Top2 {  // partial top-2 of one query over one train split; key = distance (float)
     float k1; int i1; float k2; int i2;
 };

@@ -7,7 +7,7 @@ gates, /root/reference/src/TestsDetector.cpp:58-95) over one batch of problems:
   10,000 x 10,000 128-D SIFT-like descriptors per problem, RANSAC maxIters 50,000, conf 0.995,
   8 % geometric inliers among 2,000 planted matches (no early termination: SURVEY.md App. B).
 Inputs (descriptors + keypoints) are resident in HBM before the timed region; each step registers
-the 32 scene sets (bf16 fragment layout prep is inside the step) and runs the batch.  Multi-GPU:
+the 32 scene sets (i8 fragment layout prep is inside the step) and runs the batch.  Multi-GPU:
 one process per GPU, each rank owns its own 32 scenes (weak scaling, no data-path collective); the
 per-problem result records are all-gathered over RCCL at the end of every step.
 
@@ -27,7 +27,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, no sparsity)
+PEAK_I8_TOPS = 5000.0       # MI355X dense i8 MFMA = 2x dense bf16 2.5 PF (MI355X_MICROARCH.md, no sparsity)
 PEAK_F32_VALU_TFLOPS = 157.3  # MI355X fp32 vector (VALU) peak
 PEAK_HBM_GBS = 8000.0
 FLOP_PER_POINT_EVAL = 17      # one fp32 reprojection test of a hypothesis on a point
@@ -157,10 +157,12 @@ def main():
         rooflines = {}
         if kavg.get("knn", 0) > 0:
             ach = knn_flops / (kavg["knn"] * 1e-3) / 1e12
-            t = pmc_traffic("knn2_bf16_kernel")
-            rooflines["knn"] = {"kernel": "knn2_bf16 (distance GEMM + top-2 selection), 1 launch/step", "bound": "mfma",
-                                "achieved": round(ach, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                                "frac": round(ach / PEAK_BF16_TFLOPS, 4), "traffic": t,
+            t = pmc_traffic("knn2_i8_kernel")
+            rooflines["knn"] = {"kernel": "knn2_i8 (distance GEMM on i8 MFMA, exact integer, + top-2 selection), "
+                                          "1 launch/step; flops = 2*Nq*Nt*128 integer ops, peak = dense i8",
+                                "bound": "mfma",
+                                "achieved": round(ach, 2), "peak": PEAK_I8_TOPS, "unit": "TFLOP/s",
+                                "frac": round(ach / PEAK_I8_TOPS, 4), "traffic": t,
                                 "algorithmic_bytes": knn_bytes,
                                 "achieved_hbm_GBs": round(knn_bytes / (kavg["knn"] * 1e-3) / 1e9, 1)}
         if kavg.get("score", 0) > 0:
@@ -185,7 +187,7 @@ def main():
             "value": round(value, 3), "unit": "problems/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(1e3 * el / args.steps, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None,
-            "dtype": "bf16-MFMA exact-int distances (fp32 acc), fp64 DLT/Jacobi, fp32 reprojection",
+            "dtype": "i8-MFMA exact-int distances (i32 acc), fp64 DLT/Jacobi, fp32 reprojection",
             "data": "synthetic SIFT-like integer descriptors (seeded), planted 8% geometric inliers",
             "config": {"workload": f"{args.config}: {cfg['n_models']} models x {cfg['n_scenes']} scenes per GPU, "
                                    f"{cfg['nq']}x{cfg['nt']} descriptors, maxIters {cfg['max_iters']}",

@@ -313,7 +313,7 @@ static mim_status set_create_locked(mim_ctx* c, const float* desc, const float* 
     const size_t tiles = (size_t)std::max(r.d.n_tiles, 1);
     void *frag, *norm;
     HIPCHK(c, c->arena.alloc(tiles * kTileBytes, &frag));
-    HIPCHK(c, c->arena.alloc(tiles * 64 * sizeof(float), &norm));
+    HIPCHK(c, c->arena.alloc(tiles * 128 * sizeof(int), &norm));
     const float* f32 = desc;
     const float* kpd = kp;
     if (!on_device && n > 0) {
@@ -325,14 +325,14 @@ static mim_status set_create_locked(mim_ctx* c, const float* desc, const float* 
         f32 = (const float*)df;
         kpd = (const float*)dk;
     }
-    r.d.frag = (const uint16_t*)frag;
-    r.d.norm = (const float*)norm;
+    r.d.frag = (const int8_t*)frag;
+    r.d.norm = (const int*)norm;
     r.d.f32 = f32;
     r.d.kp = (const float2*)kpd;
     r.d.flags = nullptr;  // assigned when the prep is flushed
     if (!on_device) HIPCHK(c, hipStreamSynchronize(c->stream));  // host buffers may go away
     *set_id = (int32_t)c->sets.size();
-    c->pend.push_back(PrepJob{f32, (uint16_t*)frag, (float*)norm, nullptr, n, 0});
+    c->pend.push_back(PrepJob{f32, (int8_t*)frag, (int*)norm, nullptr, n, 0});
     c->pend_set.push_back(*set_id);
     c->sets.push_back(r);
     return MIM_OK;

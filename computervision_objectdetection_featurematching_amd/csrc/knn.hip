@@ -4,14 +4,15 @@
 // /root/reference/src/TestsDetector.cpp:36,60,66-72 (OpenCV: matchers.cpp knnMatchImpl ->
 // batch_distance.cpp batchDistance(K=2) -> normL2Sqr_).
 //
-// Exact path (SIFT rows: integers in [0,255]): D[i][j] = |t_i|^2 - 2 q_j.t_i on the bf16 MFMA
-// (v_mfma_f32_32x32x16_bf16, fp32 accumulate).  Every operand (0..255, -2q in -510..0) is exact in
-// bf16 and every partial sum is an integer of magnitude < 2^24, so D is exact in any order and
-// d = sqrtf(D + |q_j|^2) is bit-identical to OpenCV's sqrt(normL2Sqr_).
+// Exact path (SIFT rows: integers in [0,255]): rows are shifted to d' = d - 128 in [-128,127], exact
+// in i8, and |q - t|^2 = |q'|^2 + |t'|^2 - 2 q'.t'.  q'.t' runs on the i8 MFMA
+// (v_mfma_i32_32x32x32_i8, i32 accumulate: 2x the bf16 rate), so every distance is an exact integer
+// and d = sqrtf(d^2) is bit-identical to OpenCV's sqrt(normL2Sqr_).
 // Top-2 selection: OpenCV orders by the float distance sqrtf(d^2) (ties -> lower train index).  The
-// sweep keeps, branch-free, the two smallest (d^2, index) per query.  sqrtf is monotone and, below
-// 2^22, injective on integers, so that pair is OpenCV's top-2 whenever the 2nd d^2 < 4e6 (equal d^2
-// keep the lower index); other queries are rescanned exactly by knn2_rescan_kernel.
+// sweep keeps, branch-free, the two smallest (D = d^2 - |q'|^2, index) per query.  sqrtf is
+// monotone and, below 2^22, injective on integers, so that pair is OpenCV's top-2 whenever the 2nd
+// d^2 < 4e6 (equal d^2 keep the lower index); other queries are rescanned exactly by
+// knn2_rescan_kernel.
 //
 // Generic path (any other float rows): per-pair fp32 arithmetic in OpenCV's SSE normL2Sqr_ order
 // (4 accumulators x 4 lanes, no FMA), bit-identical to oracle/mim_oracle.c l2sqr_sse_order.
@@ -21,55 +22,56 @@
 
 namespace mim {
 
-typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
-typedef __attribute__((ext_vector_type(16))) float f32x16;
+typedef __attribute__((ext_vector_type(4))) int i32x4;
+typedef __attribute__((ext_vector_type(16))) int i32x16;
 
 // ------------------------------------------------------------------------------------------------
-// prep: fp32 rows -> bf16 fragment-major tiles + squared norms + integrality flag.
-// Fragment-major: a tile of 64 rows is [u 0..1][kstep s 0..7][lane 0..63][j 0..7] with
-// row = 32u + (lane & 31), col = 16s + 8(lane >> 5) + j — exactly the per-lane operand of
-// v_mfma_f32_32x32x16_bf16, so one 1 KiB wave load = one fragment, fully coalesced.
+// prep: fp32 rows -> i8 fragment-major tiles of d - 128 + squared norms + integrality flag.
+// Fragment-major: a tile of 64 rows is [u 0..1][kstep s 0..3][lane 0..63][j 0..15] with
+// row = 32u + (lane & 31), col = 32s + 16(lane >> 5) + j — the per-lane operand of
+// v_mfma_i32_32x32x32_i8 (query and train use the same k order, so the product is k-order free);
+// one 1 KiB wave load = one fragment, fully coalesced.
+// Norms per tile: [64] n2 = |d - 128|^2 (exact integer), [64] -floor(n2 / 2); padded rows INT_MAX.
 // ------------------------------------------------------------------------------------------------
-__device__ __forceinline__ void prep_tile(const float* __restrict__ src, int n, uint16_t* __restrict__ frag,
-                                          float* __restrict__ norm, int* __restrict__ flags, int tile) {
+__device__ __forceinline__ void prep_tile(const float* __restrict__ src, int n, int8_t* __restrict__ frag,
+                                          int* __restrict__ norm, int* __restrict__ flags, int tile) {
     const int tid = threadIdx.x;
     int bad = 0;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < 2; ++k) {
         const int ci = k * 256 + tid;  // output chunk (16 B) within the tile
-        const int u = ci >> 9, s = (ci >> 6) & 7, lane = ci & 63;
+        const int u = ci >> 8, s = (ci >> 6) & 3, lane = ci & 63;
         const int row = tile * 64 + 32 * u + (lane & 31);
-        const int col = 16 * s + 8 * (lane >> 5);
-        uint16_t o[8];
+        const int col = 32 * s + 16 * (lane >> 5);
+        uint32_t o[4] = {0, 0, 0, 0};
         if (row < n) {
             const float4* p = reinterpret_cast<const float4*>(src + (size_t)row * kDim + col);
-            float4 a = p[0], b = p[1];
-            float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                bad |= !(v[j] >= 0.f && v[j] <= 255.f && v[j] == rintf(v[j]));
-                __bf16 hb = (__bf16)v[j];
-                o[j] = __builtin_bit_cast(uint16_t, hb);
+            for (int c = 0; c < 4; ++c) {
+                const float4 a = p[c];
+                const float v[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    bad |= !(v[j] >= 0.f && v[j] <= 255.f && v[j] == rintf(v[j]));
+                    o[c] |= (uint32_t)(((int)v[j] - 128) & 0xff) << (8 * j);
+                }
             }
-        } else {
-#pragma unroll
-            for (int j = 0; j < 8; ++j) o[j] = 0;
         }
-        uint4 w;
-        w.x = o[0] | (uint32_t(o[1]) << 16);
-        w.y = o[2] | (uint32_t(o[3]) << 16);
-        w.z = o[4] | (uint32_t(o[5]) << 16);
-        w.w = o[6] | (uint32_t(o[7]) << 16);
-        reinterpret_cast<uint4*>(frag)[(size_t)tile * 1024 + ci] = w;
+        reinterpret_cast<uint4*>(frag)[(size_t)tile * 512 + ci] = make_uint4(o[0], o[1], o[2], o[3]);
     }
     if (tid < 64) {
         const int row = tile * 64 + tid;
         float s = 0.f;
         if (row < n) {
             const float* p = src + (size_t)row * kDim;
-            for (int c = 0; c < kDim; ++c) s += p[c] * p[c];
+            for (int c = 0; c < kDim; ++c) {
+                const float d = p[c] - 128.f;
+                s += d * d;  // exact for integer rows (< 2^22)
+            }
         }
-        norm[row] = row < n ? s : FLT_MAX;  // padded rows never win (copied as is by the DMA)
+        const int n2 = row < n ? (int)s : INT_MAX;  // padded rows never win (copied as is by the DMA)
+        norm[(size_t)tile * 128 + tid] = n2;
+        norm[(size_t)tile * 128 + 64 + tid] = -(n2 >> 1);
     }
     if (__any(bad) && (tid & 63) == 0) atomicOr(flags, 1);
 }
@@ -88,39 +90,35 @@ __global__ __launch_bounds__(256) void prep_batch_kernel(const PrepJob* __restri
 }
 
 // ------------------------------------------------------------------------------------------------
-// Running top-2 of one query in the exact integer domain D = d^2 - |q|^2.  Candidates of one
+// Running top-2 of one query in the exact integer domain D = d^2 - |q'|^2.  Candidates of one
 // selection arrive in increasing train index: strict `<` keeps the earlier of equal D.
 // ------------------------------------------------------------------------------------------------
 struct LaneSel {
-    float m1, m2;  // two smallest D
-    int i1, i2;    // their train indices (INT_MAX = absent)
+    int m1, m2;  // two smallest D (INT_MAX = absent)
+    int i1, i2;  // their train indices (INT_MAX = absent)
 };
 
 __device__ __forceinline__ void sel_init(LaneSel& s) {
-    s.m1 = s.m2 = FLT_MAX;
+    s.m1 = s.m2 = INT_MAX;
     s.i1 = s.i2 = INT_MAX;
 }
 
-// min without IEEE-mode operand canonicalisation (fminf emits v_max x,x per operand): D values are
-// finite integers or FLT_MAX, never NaN, and >= -FLT_MAX
-__device__ __forceinline__ float dmin(float a, float b) { return __builtin_amdgcn_fmed3f(a, b, -FLT_MAX); }
-
 // branch-free insertion of (v, idx): 7 VALU
-__device__ __forceinline__ void sel_push(LaneSel& s, float v, int idx) {
+__device__ __forceinline__ void sel_push(LaneSel& s, int v, int idx) {
     const bool c1 = v < s.m1, c2 = v < s.m2;
-    s.m2 = __builtin_amdgcn_fmed3f(s.m1, s.m2, v);
+    s.m2 = max(s.m1, min(s.m2, v));  // med3(m1, m2, v) with m1 <= m2
     s.i2 = c2 ? (c1 ? s.i1 : idx) : s.i2;
-    s.m1 = dmin(s.m1, v);
+    s.m1 = min(s.m1, v);
     s.i1 = c1 ? idx : s.i1;
 }
 
-__device__ __forceinline__ bool dlt(float da, int ia, float db, int ib) { return da < db || (da == db && ia < ib); }
+__device__ __forceinline__ bool dlt(int da, int ia, int db, int ib) { return da < db || (da == db && ia < ib); }
 
 // union of two selections over disjoint rows: two smallest (D, index)
 __device__ __forceinline__ LaneSel sel_merge(LaneSel a, const LaneSel& b) {
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
-        const float w = k ? b.m2 : b.m1;
+        const int w = k ? b.m2 : b.m1;
         const int iw = k ? b.i2 : b.i1;
         const bool l1 = dlt(w, iw, a.m1, a.i1), l2 = dlt(w, iw, a.m2, a.i2);
         a.m2 = l1 ? a.m1 : (l2 ? w : a.m2);
@@ -152,70 +150,67 @@ __device__ __forceinline__ T2 top2_merge(T2 a, float k, int i) {
 
 constexpr int kRescan = -2;  // Top2::i2 marker: the split's top-2 needs the exact rescan
 
-// D value g of a 32x32 MFMA tile is train row (g&3) + 8(g>>2) + 4h of its 32-row block.  Indices
-// are stored without the lane's 4h (uniform, scalar) and corrected at the end.
-//   early tiles (the top-2 still changes often): every value is inserted branch-free (kPartials
-//     independent selections per query: 1 measured best, it keeps the kernel at 128 VGPRs = 4
-//     waves/SIMD);
-//   later tiles (the partials merged into one selection): 4 consecutive rows are tested at once
-//     against the 2nd best, the insertion runs only when some lane of the wave has a candidate.
+// Accumulator value g of a 32x32 MFMA tile is train row (g&3) + 8(g>>2) + 4h of its 32-row block.
+// Indices are stored without the lane's 4h (uniform, scalar) and corrected at the end.
+//   early tiles (the top-2 still changes often): C = 0, D = n2 - 2 q'.t' inserted branch-free;
+//   later tiles: C = -floor(n2/2), so the MFMA yields R = q'.t' - floor(n2/2) and
+//     D = (n2 & 1) - 2R.  kGroup consecutive rows are tested at once against the lane's threshold
+//     on R (a superset of the rows that can enter the top-2); the exact insertion runs only when
+//     some lane of the wave has a candidate.
 #ifndef MIM_KNN_EARLY
 #define MIM_KNN_EARLY 12
 #endif
 #ifndef MIM_KNN_GROUP
 #define MIM_KNN_GROUP 4
 #endif
-#ifndef MIM_KNN_PREFETCH
-#define MIM_KNN_PREFETCH 0
-#endif
-#ifndef MIM_KNN_PARTIALS
-#define MIM_KNN_PARTIALS 1
-#endif
-constexpr int kPartials = MIM_KNN_PARTIALS;  // independent early-tile selections per query (1 or 2)
 constexpr int kEarlyTiles = MIM_KNN_EARLY;
 constexpr int kGroup = MIM_KNN_GROUP;  // values tested together in the late tiles (4 or 8)
 
 // late tiles: the hit test of values g = kGroup*j .. kGroup*j + kGroup-1 (branch-free, scheduled
-// between the MFMAs); T = the lane's filter
-__device__ __forceinline__ bool sel_test(const f32x16& p, int j, float T) {
-    float m = dmin(dmin(p[kGroup * j], p[kGroup * j + 1]), dmin(p[kGroup * j + 2], p[kGroup * j + 3]));
+// between the MFMAs); T = the lane's threshold on R
+__device__ __forceinline__ bool sel_test(const i32x16& p, int j, int T) {
+    int m = max(max(p[kGroup * j], p[kGroup * j + 1]), max(p[kGroup * j + 2], p[kGroup * j + 3]));
 #pragma unroll
-    for (int k = 4; k < kGroup; k += 2) m = dmin(m, dmin(p[kGroup * j + k], p[kGroup * j + k + 1]));
-    return m < T;
+    for (int k = 4; k < kGroup; k += 2) m = max(m, max(p[kGroup * j + k], p[kGroup * j + k + 1]));
+    return m >= T;
 }
 
-// ... and the insertion of that group for the lanes that hit (rows in increasing order)
-__device__ __forceinline__ void sel_group(const f32x16& p, int j, LaneSel& s, int base) {
+// ... and the exact insertion of that group for the lanes that hit (rows in increasing order);
+// tn = the LDS norms of the half tile's 32 rows
+__device__ __forceinline__ void sel_group(const i32x16& p, int j, LaneSel& s, int base, const int* tn) {
 #pragma unroll
     for (int k = 0; k < kGroup; ++k) {
         const int g = kGroup * j + k;
-        sel_push(s, p[g], base + (g & 3) + 8 * (g >> 2));
+        const int row = (g & 3) + 8 * (g >> 2);
+        sel_push(s, (tn[row] & 1) - 2 * p[g], base + row);
     }
 }
 
-// Filter of a lane in the late tiles: below its own 2nd best, and not above the other row half's
-// 2nd best (lanes l, l ^ 32 hold the same query; an equal D may still win on the lower index).
-__device__ __forceinline__ float sel_filter(const LaneSel& s) {
-    const int v = __float_as_int(s.m2);
+// Threshold on R of a lane in the late tiles.  A row matters iff D < own 2nd best and D <= the
+// other row half's 2nd best (lanes l, l ^ 32 hold the same query; an equal D may still win on the
+// lower index): D <= Dt = min(m2 - 1, other).  D = p - 2R with p in {0,1} gives R >= -floor(Dt/2).
+__device__ __forceinline__ int sel_filter(const LaneSel& s) {
+    const int v = s.m2;
     const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
-    const float other = __int_as_float((threadIdx.x & 32) ? r[0] : r[1]);
-    return dmin(s.m2, other + 1.f);  // D are integers: other + 1 keeps D == other
+    const int other = (threadIdx.x & 32) ? (int)r[0] : (int)r[1];
+    const int dt = min(s.m2 - 1, other);
+    return -(dt >> 1);
 }
 
 // ------------------------------------------------------------------------------------------------
 // Exact distance kernel.  Block = 4 waves = 256 queries (each wave: two 32-query MFMA column
-// tiles, their -2q fragments held in VGPRs for the whole sweep).  Train tiles of 64 rows stream
-// HBM -> registers -> LDS (double buffer, one barrier per tile); each wave reads the 16 KiB tile
-// as 16 conflict-free ds_read_b128 and issues 32 MFMAs per tile.
+// tiles, their q' fragments held in VGPRs for the whole sweep).  Train tiles of 64 rows stream
+// HBM -> LDS by DMA (double buffer, one barrier per tile); each wave reads the 8 KiB tile as 8
+// conflict-free ds_read_b128 and issues 16 i8 MFMAs per tile.
 // ------------------------------------------------------------------------------------------------
-constexpr int kLdsTile = kTileBytes + 256;  // fragments + 64 norms
+constexpr int kLdsTile = kTileBytes + 512;  // fragments + 2 x 64 norms
 
 #ifndef MIM_KNN_OCC
 #define MIM_KNN_OCC 4
 #endif
-__global__ __launch_bounds__(256, MIM_KNN_OCC) void knn2_bf16_kernel(const ProbDev* __restrict__ probs,
-                                                          const KnnWork* __restrict__ works,
-                                                          Top2* __restrict__ parts) {
+__global__ __launch_bounds__(256, MIM_KNN_OCC) void knn2_i8_kernel(const ProbDev* __restrict__ probs,
+                                                                 const KnnWork* __restrict__ works,
+                                                                 Top2* __restrict__ parts) {
     __shared__ __attribute__((aligned(16))) unsigned char smem[2 * kLdsTile];
     const KnnWork w = works[blockIdx.x];
     const ProbDev* P = probs + w.problem;
@@ -223,110 +218,96 @@ __global__ __launch_bounds__(256, MIM_KNN_OCC) void knn2_bf16_kernel(const ProbD
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, h = lane >> 5, r = lane & 31;
     const int nq = P->q.n;
     const uint4* __restrict__ tsrc = reinterpret_cast<const uint4*>(P->t.frag);
-    const float* __restrict__ tnorm = P->t.norm;
+    const int* __restrict__ tnorm = P->t.norm;
 
-    // ---- query fragments: B[k][j] = -2 q_j[k] (exact in bf16) ----
+    // ---- query fragments q' ----
     const int qtile = (w.q0 >> 6) + wave;
     const bool qvalid = qtile < P->q.n_tiles;
-    bf16x8 B[2][8];
-    float qn[2] = {0.f, 0.f};
+    i32x4 B[2][4];
+    int qn[2] = {0, 0};
     {
-        const uint4* qsrc = reinterpret_cast<const uint4*>(P->q.frag) + (size_t)(qvalid ? qtile : 0) * 1024;
+        const uint4* qsrc = reinterpret_cast<const uint4*>(P->q.frag) + (size_t)(qvalid ? qtile : 0) * 512;
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
 #pragma unroll
-            for (int s = 0; s < 8; ++s) {
-                uint4 v = qvalid ? qsrc[(u * 8 + s) * 64 + lane] : make_uint4(0, 0, 0, 0);
-                bf16x8 b = __builtin_bit_cast(bf16x8, v);
-#pragma unroll
-                for (int j = 0; j < 8; ++j) b[j] = (__bf16)(-2.f * (float)b[j]);
-                B[u][s] = b;
+            for (int s = 0; s < 4; ++s) {
+                const uint4 v = qvalid ? qsrc[(u * 4 + s) * 64 + lane] : make_uint4(0, 0, 0, 0);
+                B[u][s] = __builtin_bit_cast(i32x4, v);
             }
-            qn[u] = qvalid ? P->q.norm[qtile * 64 + 32 * u + r] : 0.f;
+            qn[u] = qvalid ? P->q.norm[(size_t)qtile * 128 + 32 * u + r] : 0;
         }
     }
-    LaneSel st[2][2];
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-        sel_init(st[0][k]);
-        sel_init(st[1][k]);
-    }
+    LaneSel st[2];
+    sel_init(st[0]);
+    sel_init(st[1]);
 
     // ---- train tile staging: HBM -> LDS by DMA (global_load_lds, no VGPR staging), double
     // buffered; the barrier ending an iteration retires the DMA of the next tile ----
     typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 #define GLDS(tile, buf)                                                                          \
     do {                                                                                         \
-        const u32x4* g_ = reinterpret_cast<const u32x4*>(tsrc) + (size_t)(tile) * 1024 + tid;     \
+        const u32x4* g_ = reinterpret_cast<const u32x4*>(tsrc) + (size_t)(tile) * 512 + tid;      \
         u32x4* d_ = reinterpret_cast<u32x4*>(smem + (buf) * kLdsTile) + tid;                     \
         __builtin_amdgcn_global_load_lds(g_, d_, 16, 0, 0);                                      \
         __builtin_amdgcn_global_load_lds(g_ + 256, d_ + 256, 16, 0, 0);                          \
-        __builtin_amdgcn_global_load_lds(g_ + 512, d_ + 512, 16, 0, 0);                          \
-        __builtin_amdgcn_global_load_lds(g_ + 768, d_ + 768, 16, 0, 0);                          \
-        if (tid < 64)                                                                            \
-            __builtin_amdgcn_global_load_lds(tnorm + (size_t)(tile) * 64 + tid,                  \
-                                             reinterpret_cast<float*>(smem + (buf) * kLdsTile + kTileBytes) + tid, \
+        if (tid < 128)                                                                           \
+            __builtin_amdgcn_global_load_lds(tnorm + (size_t)(tile) * 128 + tid,                 \
+                                             reinterpret_cast<int*>(smem + (buf) * kLdsTile + kTileBytes) + tid, \
                                              4, 0, 0);                                           \
     } while (0)
 
     if (w.tile0 < w.tile1) GLDS(w.tile0, 0);
     __syncthreads();
-    float T0 = FLT_MAX, T1 = FLT_MAX;  // late-tile filters
+    int T0 = INT_MIN, T1 = INT_MIN;  // late-tile thresholds on R
     for (int tile = w.tile0; tile < w.tile1; ++tile) {
         const int buf = (tile - w.tile0) & 1;
         const bool more = tile + 1 < w.tile1;
         if (more) GLDS(tile + 1, buf ^ 1);
-        const bf16x8* A = reinterpret_cast<const bf16x8*>(smem + buf * kLdsTile);
-        const float* tn = reinterpret_cast<const float*>(smem + buf * kLdsTile + kTileBytes);
+        const i32x4* A = reinterpret_cast<const i32x4*>(smem + buf * kLdsTile);
+        const int* tn = reinterpret_cast<const int*>(smem + buf * kLdsTile + kTileBytes);
         const bool early = tile - w.tile0 < kEarlyTiles;
-        if (tile - w.tile0 == kEarlyTiles) {  // switch: fold the partials into selection 0
-            st[0][0] = sel_merge(st[0][0], st[0][1]);
-            st[1][0] = sel_merge(st[1][0], st[1][1]);
-            sel_init(st[0][1]);
-            sel_init(st[1][1]);
-            T0 = sel_filter(st[0][0]);
-            T1 = sel_filter(st[1][0]);
+        if (tile - w.tile0 == kEarlyTiles) {
+            T0 = sel_filter(st[0]);
+            T1 = sel_filter(st[1]);
         }
 #pragma unroll
         for (int u2 = 0; u2 < 2; ++u2) {
-            f32x16 acc0;
-#pragma unroll
-            for (int gg = 0; gg < 4; ++gg) {
-                float4 v = *reinterpret_cast<const float4*>(tn + 32 * u2 + 8 * gg + 4 * h);
-                acc0[4 * gg + 0] = v.x; acc0[4 * gg + 1] = v.y; acc0[4 * gg + 2] = v.z; acc0[4 * gg + 3] = v.w;
-            }
-            f32x16 acc1 = acc0;
-#if MIM_KNN_PREFETCH
-            bf16x8 af[8];  // all 8 A fragments of the half-tile issued before the first MFMA
-#pragma unroll
-            for (int s = 0; s < 8; ++s) af[s] = A[(u2 * 8 + s) * 64 + lane];
-#pragma unroll
-            for (int s = 0; s < 8; ++s) {
-                acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[s], B[0][s], acc0, 0, 0, 0);
-                acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[s], B[1][s], acc1, 0, 0, 0);
-            }
-#else
-#pragma unroll
-            for (int s = 0; s < 8; ++s) {
-                const bf16x8 a = A[(u2 * 8 + s) * 64 + lane];
-                acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, B[0][s], acc0, 0, 0, 0);
-                acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, B[1][s], acc1, 0, 0, 0);
-            }
-#endif
             const int row0 = tile * 64 + 32 * u2;
-#ifdef MIM_KNN_NOSEL  // timing probe only: MFMA loop without the selection (results invalid)
-            st[0][0].m1 = fminf(st[0][0].m1, fminf(acc0[0], acc0[15]));
-            st[1][0].m1 = fminf(st[1][0].m1, fminf(acc1[0], acc1[15]));
-            continue;
-#endif
+            const int* tnu = tn + 32 * u2 + 4 * h;
             if (early) {
+                i32x16 acc0 = {}, acc1 = {};
 #pragma unroll
-                for (int g = 0; g < 16; ++g) {
-                    const int idx = row0 + (g & 3) + 8 * (g >> 2);
-                    sel_push(st[0][g % kPartials], acc0[g], idx);
-                    sel_push(st[1][g % kPartials], acc1[g], idx);
+                for (int s = 0; s < 4; ++s) {
+                    const i32x4 a = A[(u2 * 4 + s) * 64 + lane];
+                    acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, B[0][s], acc0, 0, 0, 0);
+                    acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, B[1][s], acc1, 0, 0, 0);
+                }
+#pragma unroll
+                for (int gg = 0; gg < 4; ++gg) {
+                    const int4 n = *reinterpret_cast<const int4*>(tnu + 8 * gg);
+                    const int nv[4] = {n.x, n.y, n.z, n.w};
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const int g = 4 * gg + k;
+                        const int idx = row0 + k + 8 * gg;
+                        sel_push(st[0], nv[k] - 2 * acc0[g], idx);
+                        sel_push(st[1], nv[k] - 2 * acc1[g], idx);
+                    }
                 }
             } else {
+                i32x16 acc0;
+#pragma unroll
+                for (int gg = 0; gg < 4; ++gg) {
+                    const int4 n = *reinterpret_cast<const int4*>(tnu + 64 + 8 * gg);
+                    acc0[4 * gg + 0] = n.x; acc0[4 * gg + 1] = n.y; acc0[4 * gg + 2] = n.z; acc0[4 * gg + 3] = n.w;
+                }
+                i32x16 acc1 = acc0;
+#pragma unroll
+                for (int s = 0; s < 4; ++s) {
+                    const i32x4 a = A[(u2 * 4 + s) * 64 + lane];
+                    acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, B[0][s], acc0, 0, 0, 0);
+                    acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, B[1][s], acc1, 0, 0, 0);
+                }
                 constexpr int NG = 16 / kGroup;
                 bool h0[NG], h1[NG];
                 bool any = false;
@@ -340,14 +321,14 @@ __global__ __launch_bounds__(256, MIM_KNN_OCC) void knn2_bf16_kernel(const ProbD
 #pragma unroll
                     for (int j = 0; j < NG; ++j) {
                         if (__any(h0[j])) {
-                            if (h0[j]) sel_group(acc0, j, st[0][0], row0);
+                            if (h0[j]) sel_group(acc0, j, st[0], row0, tnu);
                         }
                         if (__any(h1[j])) {
-                            if (h1[j]) sel_group(acc1, j, st[1][0], row0);
+                            if (h1[j]) sel_group(acc1, j, st[1], row0, tnu);
                         }
                     }
-                    T0 = sel_filter(st[0][0]);
-                    T1 = sel_filter(st[1][0]);
+                    T0 = sel_filter(st[0]);
+                    T1 = sel_filter(st[1]);
                 }
             }
         }
@@ -355,10 +336,10 @@ __global__ __launch_bounds__(256, MIM_KNN_OCC) void knn2_bf16_kernel(const ProbD
     }
 #undef GLDS
 
-    // ---- merge partials and the two lane halves (disjoint train rows of the same query), keys ----
+    // ---- merge the two lane halves (disjoint train rows of the same query), keys ----
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-        LaneSel m = sel_merge(st[u][0], st[u][1]);
+        LaneSel m = st[u];
         if (m.i1 != INT_MAX) m.i1 += 4 * h;
         if (m.i2 != INT_MAX) m.i2 += 4 * h;
         LaneSel o;
@@ -367,15 +348,16 @@ __global__ __launch_bounds__(256, MIM_KNN_OCC) void knn2_bf16_kernel(const ProbD
         m = sel_merge(m, o);
         const int q = qtile * 64 + 32 * u + r;
         if (h == 0 && qvalid && q < nq) {
-            const float qq = qn[u];
+            const int qq = qn[u];
             Top2 t;
-            t.k1 = m.i1 == INT_MAX ? FLT_MAX : sqrtf(m.m1 + qq);
-            t.k2 = m.i2 == INT_MAX ? FLT_MAX : sqrtf(m.m2 + qq);
+            const int d1 = m.m1 + qq, d2 = m.m2 + qq;  // exact d^2 (< 2^23)
+            t.k1 = m.i1 == INT_MAX ? FLT_MAX : sqrtf((float)d1);
+            t.k2 = m.i2 == INT_MAX ? FLT_MAX : sqrtf((float)d2);
             t.i1 = m.i1;
             t.i2 = m.i2;
             // d^2 >= 4e6: distinct integers may share a key (sqrt class), where the lower index
             // wins: rescan exactly.  Below, equal keys mean equal d^2, already in index order.
-            if (t.i2 != INT_MAX && m.m2 + qq >= 4.0e6f) t.i2 = kRescan;
+            if (t.i2 != INT_MAX && d2 >= 4000000) t.i2 = kRescan;
             parts[P->part_off + (long long)w.split * P->q_pad + q] = t;
         }
     }
@@ -576,7 +558,7 @@ void launch_prep_batch(const PrepJob* jobs, int njobs, int total_tiles, hipStrea
 // device) and only the matching kernel does the work, so no host round trip is needed.
 void launch_knn(const ProbDev* probs, const KnnWork* works, int n_works, Top2* parts, hipStream_t st) {
     if (n_works <= 0) return;
-    knn2_bf16_kernel<<<n_works, 256, 0, st>>>(probs, works, parts);
+    knn2_i8_kernel<<<n_works, 256, 0, st>>>(probs, works, parts);
     knn2_rescan_kernel<<<n_works, 256, 0, st>>>(probs, works, parts);
     knn2_f32_kernel<<<n_works, 256, 0, st>>>(probs, works, parts);
 }

@@ -1,5 +1,5 @@
 // mim_internal.h — device-side data layout shared by the HIP kernels and the host launcher.
-// See DESIGN.md "Data layout in HBM".  gfx950 only (wave64, bf16 MFMA 32x32x16).
+// See DESIGN.md "Data layout in HBM".  gfx950 only (wave64, i8 MFMA 32x32x32, f16/fp64 RANSAC).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -8,14 +8,14 @@ namespace mim {
 
 constexpr int kDim = 128;          // SIFT descriptor length (TestsDetector.cpp:60 operands)
 constexpr int kTileRows = 64;      // descriptor rows per staged tile
-constexpr int kTileBytes = kTileRows * kDim * 2;  // 16 KiB of bf16 per tile
+constexpr int kTileBytes = kTileRows * kDim;  // 8 KiB of i8 per tile
 constexpr int kWave = 64;
 
 // One descriptor set = one ObjectModel view (objectModel.hpp:11-16) or one scaled scene
 // (TestsDetector.cpp:104-106), resident in HBM.
 struct SetDev {
-    const uint16_t* frag;  // bf16 bits, "fragment-major" tiles: [tile][u 0..1][kstep 0..7][lane 0..63][8]
-    const float* norm;     // |d|^2 per row (exact integer for integer rows), n_pad entries
+    const int8_t* frag;    // d - 128 as i8, "fragment-major" tiles: [tile][u 0..1][kstep 0..3][lane 0..63][16]
+    const int* norm;       // per tile: [64] |d - 128|^2, then [64] -floor(|d - 128|^2 / 2) (padding: INT_MAX)
     const float* f32;      // row-major n x 128 fp32 (the caller's CV_32F rows)
     const float2* kp;      // KeyPoint::pt per row
     int n;
@@ -23,11 +23,11 @@ struct SetDev {
     int* flags;            // bit0: a value is not an integer in [0,255]
 };
 
-// Deferred prep of one set (bf16 fragments, norms, integrality flag), batched per match call.
+// Deferred prep of one set (i8 fragments, norms, integrality flag), batched per match call.
 struct PrepJob {
     const float* src;
-    uint16_t* frag;
-    float* norm;
+    int8_t* frag;
+    int* norm;
     int* flags;
     int n;
     int tile0;  // first block of this set in the batched launch

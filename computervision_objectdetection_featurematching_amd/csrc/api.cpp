@@ -313,7 +313,7 @@ static mim_status set_create_locked(mim_ctx* c, const float* desc, const float* 
     const size_t tiles = (size_t)std::max(r.d.n_tiles, 1);
     void *frag, *norm;
     HIPCHK(c, c->arena.alloc(tiles * kTileBytes, &frag));
-    HIPCHK(c, c->arena.alloc(tiles * 128 * sizeof(int), &norm));
+    HIPCHK(c, c->arena.alloc(tiles * kNormWords * sizeof(int), &norm));
     const float* f32 = desc;
     const float* kpd = kp;
     if (!on_device && n > 0) {
@@ -410,7 +410,7 @@ static mim_status build_tables(mim_ctx* c, const mim_problem* problems, int n, i
         const int qs = problems[i].query_set, ts = problems[i].train_set;
         if (qs < 0 || qs >= (int)c->sets.size() || ts < 0 || ts >= (int)c->sets.size())
             return fail(c, MIM_EINVAL, "problem %d: bad set id (%d, %d)", i, qs, ts);
-        total_qblocks += (c->sets[qs].d.n + 255) / 256;
+        total_qblocks += (c->sets[qs].d.n + kKnnBlockQ - 1) / kKnnBlockQ;
     }
     // split the train side until the grid has ~2 blocks per CU
     const int target = 512;
@@ -419,11 +419,11 @@ static mim_status build_tables(mim_ctx* c, const mim_problem* problems, int n, i
         ProbDev& P = c->h_probs[i];
         P.q = c->sets[problems[i].query_set].d;
         P.t = c->sets[problems[i].train_set].d;
-        const int qb = (P.q.n + 255) / 256;
+        const int qb = (P.q.n + kKnnBlockQ - 1) / kKnnBlockQ;
         int nsplit = total_qblocks > 0 ? (target + total_qblocks - 1) / total_qblocks : 1;
         nsplit = std::max(1, std::min(nsplit, std::max(P.t.n_tiles, 1)));
         P.nsplit = nsplit;
-        P.q_pad = qb * 256;
+        P.q_pad = qb * kKnnBlockQ;
         P.part_off = part;
         part += (long long)nsplit * P.q_pad;
         P.good_off = good;
@@ -434,7 +434,7 @@ static mim_status build_tables(mim_ctx* c, const mim_problem* problems, int n, i
             for (int s = 0; s < nsplit; ++s) {
                 const int t0 = (int)((long long)P.t.n_tiles * s / nsplit);
                 const int t1 = (int)((long long)P.t.n_tiles * (s + 1) / nsplit);
-                per_prob[i].push_back(KnnWork{i, qb_i * 256, t0, t1, s});
+                per_prob[i].push_back(KnnWork{i, qb_i * kKnnBlockQ, t0, t1, s});
             }
     }
     // problem groups (contiguous ranges), each with its own contiguous slice of the work list;
@@ -586,7 +586,7 @@ mim_status mim_ratio_filter(mim_ctx* c, const int32_t* idx, const float* dist, i
                         b < 0 ? INT_MAX : b};
         max_t = std::max(max_t, std::max(a, b));
     }
-    const int q_pad = (nq + 255) / 256 * 256;
+    const int q_pad = (nq + kKnnBlockQ - 1) / kKnnBlockQ * kKnnBlockQ;
     const size_t nkp = (size_t)std::max(nq, max_t + 1);
     HIPCHK(c, c->parts.ensure(sizeof(Top2) * q_pad));
     HIPCHK(c, c->rws.scratch.ensure(sizeof(float2) * nkp));

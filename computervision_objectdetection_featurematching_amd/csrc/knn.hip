@@ -4,15 +4,17 @@
 // /root/reference/src/TestsDetector.cpp:36,60,66-72 (OpenCV: matchers.cpp knnMatchImpl ->
 // batch_distance.cpp batchDistance(K=2) -> normL2Sqr_).
 //
-// Exact path (SIFT rows: integers in [0,255]): rows are shifted to d' = d - 128 in [-128,127], exact
-// in i8, and |q - t|^2 = |q'|^2 + |t'|^2 - 2 q'.t'.  q'.t' runs on the i8 MFMA
-// (v_mfma_i32_32x32x32_i8, i32 accumulate: 2x the bf16 rate), so every distance is an exact integer
-// and d = sqrtf(d^2) is bit-identical to OpenCV's sqrt(normL2Sqr_).
+// Exact path (SIFT rows: integers in [0,255]): a set is stored once as t'' = 127 - t in [-128,127]
+// (exact in i8); as a query the same bytes give q' = q - 128 = ~t''.  Then q - t = q' + t'' + 1 and
+//   |q - t|^2 = n2(t) + 2 q'.t'' + c(q),   n2(t) = |t - 128|^2,  c(q) = |q - 128|^2 + 2 sum(q - 128),
+// with q'.t'' on the i8 MFMA (v_mfma_i32_32x32x32_i8, i32 accumulate: 2x the bf16 rate).  Every
+// distance is an exact integer, so d = sqrtf(d^2) is bit-identical to OpenCV's sqrt(normL2Sqr_)
+// (SURVEY.md Appendix B).  The accumulator starts at floor(n2/2), so the MFMA yields
+// R = q'.t'' + floor(n2/2) and D = d^2 - c(q) = 2R + (n2 & 1) (one v_lshl_add_u32).
 // Top-2 selection: OpenCV orders by the float distance sqrtf(d^2) (ties -> lower train index).  The
-// sweep keeps, branch-free, the two smallest (D = d^2 - |q'|^2, index) per query.  sqrtf is
-// monotone and, below 2^22, injective on integers, so that pair is OpenCV's top-2 whenever the 2nd
-// d^2 < 4e6 (equal d^2 keep the lower index); other queries are rescanned exactly by
-// knn2_rescan_kernel.
+// sweep keeps, branch-free, the two smallest (D, index) per query.  sqrtf is monotone and, below
+// 2^22, injective on integers, so that pair is OpenCV's top-2 whenever the 2nd d^2 < 4e6 (equal d^2
+// keep the lower index); other queries are rescanned exactly by knn2_rescan_kernel.
 //
 // Generic path (any other float rows): per-pair fp32 arithmetic in OpenCV's SSE normL2Sqr_ order
 // (4 accumulators x 4 lanes, no FMA), bit-identical to oracle/mim_oracle.c l2sqr_sse_order.
@@ -24,14 +26,17 @@ namespace mim {
 
 typedef __attribute__((ext_vector_type(4))) int i32x4;
 typedef __attribute__((ext_vector_type(16))) int i32x16;
+typedef const __attribute__((address_space(1))) i32x4 gi32x4;  // global (not flat) loads
+typedef const __attribute__((address_space(1))) int gint;
 
 // ------------------------------------------------------------------------------------------------
-// prep: fp32 rows -> i8 fragment-major tiles of d - 128 + squared norms + integrality flag.
+// prep: fp32 rows -> i8 fragment-major tiles of 127 - d + norms + integrality flag.
 // Fragment-major: a tile of 64 rows is [u 0..1][kstep s 0..3][lane 0..63][j 0..15] with
 // row = 32u + (lane & 31), col = 32s + 16(lane >> 5) + j — the per-lane operand of
 // v_mfma_i32_32x32x32_i8 (query and train use the same k order, so the product is k-order free);
 // one 1 KiB wave load = one fragment, fully coalesced.
-// Norms per tile: [64] n2 = |d - 128|^2 (exact integer), [64] -floor(n2 / 2); padded rows INT_MAX.
+// Norm block per tile (kNormWords): [64] floor(n2/2), [64] n2 & 1 (the train side, staged to LDS),
+// [64] c (the query side); padded rows floor(n2/2) = 2^30 - 1, n2 & 1 = 1, so D = INT_MAX.
 // ------------------------------------------------------------------------------------------------
 __device__ __forceinline__ void prep_tile(const float* __restrict__ src, int n, int8_t* __restrict__ frag,
                                           int* __restrict__ norm, int* __restrict__ flags, int tile) {
@@ -53,7 +58,7 @@ __device__ __forceinline__ void prep_tile(const float* __restrict__ src, int n, 
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     bad |= !(v[j] >= 0.f && v[j] <= 255.f && v[j] == rintf(v[j]));
-                    o[c] |= (uint32_t)(((int)v[j] - 128) & 0xff) << (8 * j);
+                    o[c] |= (uint32_t)((127 - (int)v[j]) & 0xff) << (8 * j);
                 }
             }
         }
@@ -61,17 +66,19 @@ __device__ __forceinline__ void prep_tile(const float* __restrict__ src, int n, 
     }
     if (tid < 64) {
         const int row = tile * 64 + tid;
-        float s = 0.f;
+        int n2 = 0, sum = 0;
         if (row < n) {
             const float* p = src + (size_t)row * kDim;
             for (int c = 0; c < kDim; ++c) {
-                const float d = p[c] - 128.f;
-                s += d * d;  // exact for integer rows (< 2^22)
+                const int d = (int)p[c] - 128;  // garbage for non-integer rows (flagged, unused)
+                n2 += d * d;
+                sum += d;
             }
         }
-        const int n2 = row < n ? (int)s : INT_MAX;  // padded rows never win (copied as is by the DMA)
-        norm[(size_t)tile * 128 + tid] = n2;
-        norm[(size_t)tile * 128 + 64 + tid] = -(n2 >> 1);
+        int* nb = norm + (size_t)tile * kNormWords;
+        nb[tid] = row < n ? n2 >> 1 : (1 << 30) - 1;
+        nb[64 + tid] = row < n ? n2 & 1 : 1;
+        nb[128 + tid] = n2 + 2 * sum;
     }
     if (__any(bad) && (tid & 63) == 0) atomicOr(flags, 1);
 }
@@ -90,7 +97,7 @@ __global__ __launch_bounds__(256) void prep_batch_kernel(const PrepJob* __restri
 }
 
 // ------------------------------------------------------------------------------------------------
-// Running top-2 of one query in the exact integer domain D = d^2 - |q'|^2.  Candidates of one
+// Running top-2 of one query in the exact integer domain D = d^2 - c(q).  Candidates of one
 // selection arrive in increasing train index: strict `<` keeps the earlier of equal D.
 // ------------------------------------------------------------------------------------------------
 struct LaneSel {
@@ -106,7 +113,7 @@ __device__ __forceinline__ void sel_init(LaneSel& s) {
 // branch-free insertion of (v, idx): 7 VALU
 __device__ __forceinline__ void sel_push(LaneSel& s, int v, int idx) {
     const bool c1 = v < s.m1, c2 = v < s.m2;
-    s.m2 = max(s.m1, min(s.m2, v));  // med3(m1, m2, v) with m1 <= m2
+    s.m2 = max(min(s.m1, s.m2), min(max(s.m1, s.m2), v));  // med3 (one v_med3_i32)
     s.i2 = c2 ? (c1 ? s.i1 : idx) : s.i2;
     s.m1 = min(s.m1, v);
     s.i1 = c1 ? idx : s.i1;
@@ -152,66 +159,50 @@ constexpr int kRescan = -2;  // Top2::i2 marker: the split's top-2 needs the exa
 
 // Accumulator value g of a 32x32 MFMA tile is train row (g&3) + 8(g>>2) + 4h of its 32-row block.
 // Indices are stored without the lane's 4h (uniform, scalar) and corrected at the end.
-//   early tiles (the top-2 still changes often): C = 0, D = n2 - 2 q'.t' inserted branch-free;
-//   later tiles: C = -floor(n2/2), so the MFMA yields R = q'.t' - floor(n2/2) and
-//     D = (n2 & 1) - 2R.  kGroup consecutive rows are tested at once against the lane's threshold
-//     on R (a superset of the rows that can enter the top-2); the exact insertion runs only when
-//     some lane of the wave has a candidate.
+//   early tiles (the top-2 still changes often): every D = 2R + p inserted branch-free;
+//   later tiles: the min of a lane's 16 R is tested against the lane's threshold on R (a superset of
+//     the rows that can enter the top-2); the exact insertion runs only for the 4-row groups in
+//     which some lane of the wave has a candidate.
 #ifndef MIM_KNN_EARLY
-#define MIM_KNN_EARLY 12
-#endif
-#ifndef MIM_KNN_GROUP
-#define MIM_KNN_GROUP 4
+#define MIM_KNN_EARLY 4
 #endif
 constexpr int kEarlyTiles = MIM_KNN_EARLY;
-constexpr int kGroup = MIM_KNN_GROUP;  // values tested together in the late tiles (4 or 8)
-
-// late tiles: the hit test of values g = kGroup*j .. kGroup*j + kGroup-1 (branch-free, scheduled
-// between the MFMAs); T = the lane's threshold on R
-__device__ __forceinline__ bool sel_test(const i32x16& p, int j, int T) {
-    int m = max(max(p[kGroup * j], p[kGroup * j + 1]), max(p[kGroup * j + 2], p[kGroup * j + 3]));
-#pragma unroll
-    for (int k = 4; k < kGroup; k += 2) m = max(m, max(p[kGroup * j + k], p[kGroup * j + k + 1]));
-    return m >= T;
-}
-
-// ... and the exact insertion of that group for the lanes that hit (rows in increasing order);
-// tn = the LDS norms of the half tile's 32 rows
-__device__ __forceinline__ void sel_group(const i32x16& p, int j, LaneSel& s, int base, const int* tn) {
-#pragma unroll
-    for (int k = 0; k < kGroup; ++k) {
-        const int g = kGroup * j + k;
-        const int row = (g & 3) + 8 * (g >> 2);
-        sel_push(s, (tn[row] & 1) - 2 * p[g], base + row);
-    }
-}
 
 // Threshold on R of a lane in the late tiles.  A row matters iff D < own 2nd best and D <= the
 // other row half's 2nd best (lanes l, l ^ 32 hold the same query; an equal D may still win on the
-// lower index): D <= Dt = min(m2 - 1, other).  D = p - 2R with p in {0,1} gives R >= -floor(Dt/2).
+// lower index): D <= Dt = min(m2 - 1, other).  D = 2R + p with p in {0,1} gives R <= floor(Dt/2).
 __device__ __forceinline__ int sel_filter(const LaneSel& s) {
     const int v = s.m2;
     const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
     const int other = (threadIdx.x & 32) ? (int)r[0] : (int)r[1];
     const int dt = min(s.m2 - 1, other);
-    return -(dt >> 1);
+    return dt >> 1;
 }
 
+__device__ __forceinline__ int dval(int R, int p) { return (R << 1) + p; }  // v_lshl_add_u32
+
 // ------------------------------------------------------------------------------------------------
-// Exact distance kernel.  Block = 4 waves = 256 queries (each wave: two 32-query MFMA column
-// tiles, their q' fragments held in VGPRs for the whole sweep).  Train tiles of 64 rows stream
-// HBM -> LDS by DMA (double buffer, one barrier per tile); each wave reads the 8 KiB tile as 8
-// conflict-free ds_read_b128 and issues 16 i8 MFMAs per tile.
+// Exact distance kernel.  Block = kKnnWaves waves = kKnnBlockQ queries (each wave: kKnnQT 32-query
+// MFMA column tiles, their q' fragments held in VGPRs for the whole sweep).  Train rows stream
+// HBM -> registers -> LDS in stages of kKnnStage 64-row tiles (double buffer, one barrier per
+// stage); per tile a wave reads the 8 KiB of fragments as 8 conflict-free ds_read_b128 and issues
+// 8 kKnnQT i8 MFMAs.
 // ------------------------------------------------------------------------------------------------
-constexpr int kLdsTile = kTileBytes + 512;  // fragments + 2 x 64 norms
+constexpr int kLdsTile = kTileBytes + 512;  // fragments + the train half of the norm block
+constexpr int kStage = kKnnStage;
+constexpr int kThreads = 64 * kKnnWaves;
+constexpr int kStageChunks = kStage * kTileBytes / 16 / kThreads;  // 16-B fragment chunks per thread
+constexpr int kStageNorms = kStage * 128;                           // norm words per stage
+static_assert(kStageChunks * 16 * kThreads == kStage * kTileBytes, "stage split");
+static_assert(kStageNorms <= kThreads, "one norm word per thread");
 
 #ifndef MIM_KNN_OCC
 #define MIM_KNN_OCC 4
 #endif
-__global__ __launch_bounds__(256, MIM_KNN_OCC) void knn2_i8_kernel(const ProbDev* __restrict__ probs,
-                                                                 const KnnWork* __restrict__ works,
-                                                                 Top2* __restrict__ parts) {
-    __shared__ __attribute__((aligned(16))) unsigned char smem[2 * kLdsTile];
+__global__ __launch_bounds__(kThreads, MIM_KNN_OCC) void knn2_i8_kernel(  // OCC = waves per SIMD
+    const ProbDev* __restrict__ probs, const KnnWork* __restrict__ works, Top2* __restrict__ parts) {
+    constexpr int QT = kKnnQT;
+    __shared__ __attribute__((aligned(16))) unsigned char smem[2 * kStage * kLdsTile];
     const KnnWork w = works[blockIdx.x];
     const ProbDev* P = probs + w.problem;
     if (*P->q.flags | *P->t.flags) return;  // not integer-valued: generic kernel handles it
@@ -220,125 +211,188 @@ __global__ __launch_bounds__(256, MIM_KNN_OCC) void knn2_i8_kernel(const ProbDev
     const uint4* __restrict__ tsrc = reinterpret_cast<const uint4*>(P->t.frag);
     const int* __restrict__ tnorm = P->t.norm;
 
-    // ---- query fragments q' ----
-    const int qtile = (w.q0 >> 6) + wave;
-    const bool qvalid = qtile < P->q.n_tiles;
-    i32x4 B[2][4];
-    int qn[2] = {0, 0};
-    {
-        const uint4* qsrc = reinterpret_cast<const uint4*>(P->q.frag) + (size_t)(qvalid ? qtile : 0) * 512;
+    // ---- query fragments q': column tile u = query rows qbase + 32u .. + 31 ----
+    const int qbase = w.q0 + wave * 32 * QT;
+    i32x4 B[QT][4];
+    int qn[QT];
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < QT; ++u) {
+        const int qr = qbase + 32 * u, qt = qr >> 6, qh = (qr >> 5) & 1;
+        const bool ok = qt < P->q.n_tiles;
+        const int qtc = ok ? qt : 0;  // rows past the set: loaded from tile 0, never written out
+        const gi32x4* qsrc = (const gi32x4*)(P->q.frag) + (size_t)qtc * 512;
 #pragma unroll
-            for (int s = 0; s < 4; ++s) {
-                const uint4 v = qvalid ? qsrc[(u * 4 + s) * 64 + lane] : make_uint4(0, 0, 0, 0);
-                B[u][s] = __builtin_bit_cast(i32x4, v);
-            }
-            qn[u] = qvalid ? P->q.norm[(size_t)qtile * 128 + 32 * u + r] : 0;
-        }
+        for (int s = 0; s < 4; ++s) B[u][s] = ~qsrc[(qh * 4 + s) * 64 + lane];  // q' = ~t''
+        qn[u] = ((const gint*)P->q.norm)[(size_t)qtc * kNormWords + 128 + 32 * qh + r];
     }
-    LaneSel st[2];
-    sel_init(st[0]);
-    sel_init(st[1]);
+    LaneSel st[QT];
+    int T[QT];  // late-tile thresholds on R
+#pragma unroll
+    for (int u = 0; u < QT; ++u) {
+        sel_init(st[u]);
+        T[u] = INT_MAX;
+    }
 
-    // ---- train tile staging: HBM -> LDS by DMA (global_load_lds, no VGPR staging), double
-    // buffered; the barrier ending an iteration retires the DMA of the next tile ----
-    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-#define GLDS(tile, buf)                                                                          \
-    do {                                                                                         \
-        const u32x4* g_ = reinterpret_cast<const u32x4*>(tsrc) + (size_t)(tile) * 512 + tid;      \
-        u32x4* d_ = reinterpret_cast<u32x4*>(smem + (buf) * kLdsTile) + tid;                     \
-        __builtin_amdgcn_global_load_lds(g_, d_, 16, 0, 0);                                      \
-        __builtin_amdgcn_global_load_lds(g_ + 256, d_ + 256, 16, 0, 0);                          \
-        if (tid < 128)                                                                           \
-            __builtin_amdgcn_global_load_lds(tnorm + (size_t)(tile) * 128 + tid,                 \
-                                             reinterpret_cast<int*>(smem + (buf) * kLdsTile + kTileBytes) + tid, \
-                                             4, 0, 0);                                           \
-    } while (0)
-
-    if (w.tile0 < w.tile1) GLDS(w.tile0, 0);
-    __syncthreads();
-    int T0 = INT_MIN, T1 = INT_MIN;  // late-tile thresholds on R
-    for (int tile = w.tile0; tile < w.tile1; ++tile) {
-        const int buf = (tile - w.tile0) & 1;
-        const bool more = tile + 1 < w.tile1;
-        if (more) GLDS(tile + 1, buf ^ 1);
-        const i32x4* A = reinterpret_cast<const i32x4*>(smem + buf * kLdsTile);
-        const int* tn = reinterpret_cast<const int*>(smem + buf * kLdsTile + kTileBytes);
-        const bool early = tile - w.tile0 < kEarlyTiles;
-        if (tile - w.tile0 == kEarlyTiles) {
-            T0 = sel_filter(st[0]);
-            T1 = sel_filter(st[1]);
+    // ---- staging: HBM -> registers (issued before the stage's compute) -> LDS (after it), double
+    // buffered.  (LDS DMA would make the compiler wait for the next stage's DMA before every LDS
+    // read of the current one: it cannot tell the buffers apart.)  LDS stage layout: kStage x
+    // [8 KiB fragments | 512 B norms]; tiles past the work item's range are not loaded.
+    i32x4 stg[kStageChunks];
+    int stgn = 0;
+    auto stage_load = [&](int t0) {
+#pragma unroll
+        for (int c = 0; c < kStageChunks; ++c) {
+            const int ci = c * kThreads + tid, tt = ci >> 9;
+            if (kStage == 1 || t0 + tt < w.tile1) stg[c] = ((const gi32x4*)tsrc)[(size_t)t0 * 512 + ci];
         }
+        if (tid < kStageNorms && (kStage == 1 || t0 + (tid >> 7) < w.tile1))
+            stgn = ((const gint*)tnorm)[(size_t)t0 * kNormWords + (tid >> 7) * kNormWords + (tid & 127)];
+    };
+    auto stage_store = [&](int buf) {
+        unsigned char* base = smem + buf * kStage * kLdsTile;
+#pragma unroll
+        for (int c = 0; c < kStageChunks; ++c) {
+            const int ci = c * kThreads + tid, tt = ci >> 9;
+            reinterpret_cast<i32x4*>(base + tt * kLdsTile)[ci & 511] = stg[c];
+        }
+        if (tid < kStageNorms) reinterpret_cast<int*>(base + (tid >> 7) * kLdsTile + kTileBytes)[tid & 127] = stgn;
+    };
+
+    if (w.tile0 < w.tile1) {
+        stage_load(w.tile0);
+        stage_store(0);
+    }
+    __syncthreads();
+    // retire every prologue load (q' fragments included) here: with one still pending at the loop
+    // entry the waitcnt pass keeps a vmcnt(0) in the loop, i.e. waits for the next stage's loads
+    __builtin_amdgcn_s_waitcnt(0);
+
+    // the 32x32 block u2 of a tile: accumulators start at floor(n2/2) (LDS), R = q'.t'' + floor(n2/2)
+    auto block_mfma = [&](const unsigned char* tb, int u2, i32x16 (&acc)[QT]) {
+        const i32x4* A = reinterpret_cast<const i32x4*>(tb);
+        const int* tnu = reinterpret_cast<const int*>(tb + kTileBytes) + 32 * u2 + 4 * h;
+#pragma unroll
+        for (int gg = 0; gg < 4; ++gg) {
+            const int4 n = *reinterpret_cast<const int4*>(tnu + 8 * gg);
+            acc[0][4 * gg + 0] = n.x; acc[0][4 * gg + 1] = n.y; acc[0][4 * gg + 2] = n.z; acc[0][4 * gg + 3] = n.w;
+        }
+#pragma unroll
+        for (int u = 1; u < QT; ++u) acc[u] = acc[0];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            const i32x4 a = A[(u2 * 4 + s) * 64 + lane];
+#pragma unroll
+            for (int u = 0; u < QT; ++u) acc[u] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, B[u][s], acc[u], 0, 0, 0);
+        }
+    };
+    // early tiles: every value inserted branch-free
+    auto tile_early = [&](const unsigned char* tb, int tile) {
+        const int* tn = reinterpret_cast<const int*>(tb + kTileBytes);
 #pragma unroll
         for (int u2 = 0; u2 < 2; ++u2) {
             const int row0 = tile * 64 + 32 * u2;
-            const int* tnu = tn + 32 * u2 + 4 * h;
-            if (early) {
-                i32x16 acc0 = {}, acc1 = {};
+            const int* tpu = tn + 64 + 32 * u2 + 4 * h;  // n2 & 1
+            i32x16 acc[QT];
+            block_mfma(tb, u2, acc);
 #pragma unroll
-                for (int s = 0; s < 4; ++s) {
-                    const i32x4 a = A[(u2 * 4 + s) * 64 + lane];
-                    acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, B[0][s], acc0, 0, 0, 0);
-                    acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, B[1][s], acc1, 0, 0, 0);
-                }
+            for (int gg = 0; gg < 4; ++gg) {
+                const int4 n = *reinterpret_cast<const int4*>(tpu + 8 * gg);
+                const int pv[4] = {n.x, n.y, n.z, n.w};
 #pragma unroll
-                for (int gg = 0; gg < 4; ++gg) {
-                    const int4 n = *reinterpret_cast<const int4*>(tnu + 8 * gg);
-                    const int nv[4] = {n.x, n.y, n.z, n.w};
+                for (int k = 0; k < 4; ++k) {
 #pragma unroll
-                    for (int k = 0; k < 4; ++k) {
-                        const int g = 4 * gg + k;
-                        const int idx = row0 + k + 8 * gg;
-                        sel_push(st[0], nv[k] - 2 * acc0[g], idx);
-                        sel_push(st[1], nv[k] - 2 * acc1[g], idx);
-                    }
-                }
-            } else {
-                i32x16 acc0;
-#pragma unroll
-                for (int gg = 0; gg < 4; ++gg) {
-                    const int4 n = *reinterpret_cast<const int4*>(tnu + 64 + 8 * gg);
-                    acc0[4 * gg + 0] = n.x; acc0[4 * gg + 1] = n.y; acc0[4 * gg + 2] = n.z; acc0[4 * gg + 3] = n.w;
-                }
-                i32x16 acc1 = acc0;
-#pragma unroll
-                for (int s = 0; s < 4; ++s) {
-                    const i32x4 a = A[(u2 * 4 + s) * 64 + lane];
-                    acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, B[0][s], acc0, 0, 0, 0);
-                    acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, B[1][s], acc1, 0, 0, 0);
-                }
-                constexpr int NG = 16 / kGroup;
-                bool h0[NG], h1[NG];
-                bool any = false;
-#pragma unroll
-                for (int j = 0; j < NG; ++j) {
-                    h0[j] = sel_test(acc0, j, T0);
-                    h1[j] = sel_test(acc1, j, T1);
-                    any |= h0[j] | h1[j];
-                }
-                if (__builtin_expect(__any(any), 0)) {  // rare past the early tiles
-#pragma unroll
-                    for (int j = 0; j < NG; ++j) {
-                        if (__any(h0[j])) {
-                            if (h0[j]) sel_group(acc0, j, st[0], row0, tnu);
-                        }
-                        if (__any(h1[j])) {
-                            if (h1[j]) sel_group(acc1, j, st[1], row0, tnu);
-                        }
-                    }
-                    T0 = sel_filter(st[0]);
-                    T1 = sel_filter(st[1]);
+                    for (int u = 0; u < QT; ++u) sel_push(st[u], dval(acc[u][4 * gg + k], pv[k]), row0 + k + 8 * gg);
                 }
             }
         }
+    };
+    // late tiles: one min over a lane's 16 R per column tile against its threshold, the exact
+    // insertion only in groups some lane hits
+    auto tile_late = [&](const unsigned char* tb, int tile) {
+        const int* tn = reinterpret_cast<const int*>(tb + kTileBytes);
+#pragma unroll
+        for (int u2 = 0; u2 < 2; ++u2) {
+            const int row0 = tile * 64 + 32 * u2;
+            const int* tpu = tn + 64 + 32 * u2 + 4 * h;  // n2 & 1
+            i32x16 acc[QT];
+            block_mfma(tb, u2, acc);
+#ifdef MIM_KNN_NOSEL  // timing probe only: MFMA loop without the selection (results invalid)
+#pragma unroll
+            for (int u = 0; u < QT; ++u) {
+                int x = acc[u][0];
+#pragma unroll
+                for (int g = 1; g < 16; ++g) x ^= acc[u][g];
+                st[u].m1 = min(st[u].m1, x);
+                st[u].i1 = min(st[u].i1, x);
+            }
+            continue;
+#endif
+            int mn[QT];
+            bool hit = false;
+#pragma unroll
+            for (int u = 0; u < QT; ++u) {
+                const i32x16& p = acc[u];
+                int m = min(min(p[0], p[1]), p[2]);
+#pragma unroll
+                for (int g = 3; g < 15; g += 2) m = min(min(m, p[g]), p[g + 1]);
+                mn[u] = min(m, p[15]);
+                hit |= mn[u] <= T[u];
+            }
+            if (__builtin_expect(__ballot(hit) != 0, 0)) {  // ~1 insertion per wave and half tile
+#pragma unroll
+                for (int u = 0; u < QT; ++u) {
+                    if (__ballot(mn[u] <= T[u])) {
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) {
+                            const i32x16& p = acc[u];
+                            const int gm = min(min(p[4 * j], p[4 * j + 1]), min(p[4 * j + 2], p[4 * j + 3]));
+                            if (__ballot(gm <= T[u])) {
+                                const int4 n = *reinterpret_cast<const int4*>(tpu + 8 * j);
+                                const int pv[4] = {n.x, n.y, n.z, n.w};
+                                if (gm <= T[u]) {
+#pragma unroll
+                                    for (int k = 0; k < 4; ++k)
+                                        sel_push(st[u], dval(p[4 * j + k], pv[k]), row0 + 8 * j + k);
+                                }
+                            }
+                        }
+                        T[u] = sel_filter(st[u]);
+                    }
+                }
+            }
+        }
+    };
+
+    const int tile_e = min(w.tile1, w.tile0 + (kEarlyTiles + kStage - 1) / kStage * kStage);
+    int stage = w.tile0;
+    for (; stage < tile_e; stage += kStage) {
+        const int buf = ((stage - w.tile0) / kStage) & 1;
+        const bool more = stage + kStage < w.tile1;
+        if (more) stage_load(stage + kStage);
+        const unsigned char* sb = smem + buf * kStage * kLdsTile;
+#pragma unroll
+        for (int ts = 0; ts < kStage; ++ts)
+            if (kStage == 1 || stage + ts < w.tile1) tile_early(sb + ts * kLdsTile, stage + ts);
+        if (more) stage_store(buf ^ 1);
         __syncthreads();
     }
-#undef GLDS
+#pragma unroll
+    for (int u = 0; u < QT; ++u) T[u] = sel_filter(st[u]);
+    for (; stage < w.tile1; stage += kStage) {
+        const int buf = ((stage - w.tile0) / kStage) & 1;
+        const bool more = stage + kStage < w.tile1;
+        if (more) stage_load(stage + kStage);
+        const unsigned char* sb = smem + buf * kStage * kLdsTile;
+#pragma unroll
+        for (int ts = 0; ts < kStage; ++ts)
+            if (kStage == 1 || stage + ts < w.tile1) tile_late(sb + ts * kLdsTile, stage + ts);
+        if (more) stage_store(buf ^ 1);
+        __syncthreads();
+    }
 
     // ---- merge the two lane halves (disjoint train rows of the same query), keys ----
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < QT; ++u) {
         LaneSel m = st[u];
         if (m.i1 != INT_MAX) m.i1 += 4 * h;
         if (m.i2 != INT_MAX) m.i2 += 4 * h;
@@ -346,11 +400,11 @@ __global__ __launch_bounds__(256, MIM_KNN_OCC) void knn2_i8_kernel(const ProbDev
         o.m1 = __shfl_xor(m.m1, 32); o.m2 = __shfl_xor(m.m2, 32);
         o.i1 = __shfl_xor(m.i1, 32); o.i2 = __shfl_xor(m.i2, 32);
         m = sel_merge(m, o);
-        const int q = qtile * 64 + 32 * u + r;
-        if (h == 0 && qvalid && q < nq) {
+        const int q = qbase + 32 * u + r;
+        if (h == 0 && q < nq) {
             const int qq = qn[u];
             Top2 t;
-            const int d1 = m.m1 + qq, d2 = m.m2 + qq;  // exact d^2 (< 2^23)
+            const int d1 = m.m1 + qq, d2 = m.m2 + qq;  // exact d^2 = D + c(q) (< 2^23)
             t.k1 = m.i1 == INT_MAX ? FLT_MAX : sqrtf((float)d1);
             t.k2 = m.i2 == INT_MAX ? FLT_MAX : sqrtf((float)d2);
             t.i1 = m.i1;
@@ -378,7 +432,7 @@ __global__ __launch_bounds__(256) void knn2_rescan_kernel(const ProbDev* __restr
     const int nq = P->q.n, nt = P->t.n;
     Top2* out = parts + P->part_off + (long long)w.split * P->q_pad;
     const int r0 = w.tile0 * 64, r1 = min(w.tile1 * 64, nt);
-    for (int k = 0; k < 256; k += 64) {
+    for (int k = 0; k < kKnnBlockQ; k += 64) {
         const int q = w.q0 + k + lane;
         const bool marked = q < nq && out[q].i2 == kRescan;
         unsigned long long m = __ballot(marked);
@@ -447,7 +501,8 @@ __global__ __launch_bounds__(256) void knn2_f32_kernel(const ProbDev* __restrict
     if (!(*P->q.flags | *P->t.flags)) return;  // integer-valued: exact MFMA kernel handles it
     const int tid = threadIdx.x;
     const int nq = P->q.n, nt = P->t.n;
-    const int q = w.q0 + tid;
+  for (int qo = 0; qo < kKnnBlockQ; qo += 256) {  // the work item's queries, 256 per pass
+    const int q = w.q0 + qo + tid;
     float qv[kDim];
     const bool qvalid = q < nq;
 #pragma unroll
@@ -480,6 +535,7 @@ __global__ __launch_bounds__(256) void knn2_f32_kernel(const ProbDev* __restrict
         }
     }
     if (qvalid) parts[P->part_off + (long long)w.split * P->q_pad + q] = Top2{k1, i1, k2, i2};
+  }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -558,7 +614,7 @@ void launch_prep_batch(const PrepJob* jobs, int njobs, int total_tiles, hipStrea
 // device) and only the matching kernel does the work, so no host round trip is needed.
 void launch_knn(const ProbDev* probs, const KnnWork* works, int n_works, Top2* parts, hipStream_t st) {
     if (n_works <= 0) return;
-    knn2_i8_kernel<<<n_works, 256, 0, st>>>(probs, works, parts);
+    knn2_i8_kernel<<<n_works, kThreads, 0, st>>>(probs, works, parts);
     knn2_rescan_kernel<<<n_works, 256, 0, st>>>(probs, works, parts);
     knn2_f32_kernel<<<n_works, 256, 0, st>>>(probs, works, parts);
 }

@@ -9,13 +9,27 @@ namespace mim {
 constexpr int kDim = 128;          // SIFT descriptor length (TestsDetector.cpp:60 operands)
 constexpr int kTileRows = 64;      // descriptor rows per staged tile
 constexpr int kTileBytes = kTileRows * kDim;  // 8 KiB of i8 per tile
+constexpr int kNormWords = 3 * kTileRows;      // norm block per tile (knn.hip prep_tile)
 constexpr int kWave = 64;
+#ifndef MIM_KNN_QT
+#define MIM_KNN_QT 2
+#endif
+#ifndef MIM_KNN_WAVES
+#define MIM_KNN_WAVES 8
+#endif
+#ifndef MIM_KNN_STAGE
+#define MIM_KNN_STAGE 4
+#endif
+constexpr int kKnnQT = MIM_KNN_QT;             // 32-query MFMA column tiles per wave (distance kernel)
+constexpr int kKnnWaves = MIM_KNN_WAVES;       // waves per distance-kernel block
+constexpr int kKnnStage = MIM_KNN_STAGE;       // 64-row train tiles per LDS stage (per barrier)
+constexpr int kKnnBlockQ = kKnnWaves * 32 * kKnnQT;  // queries per distance-kernel work item
 
 // One descriptor set = one ObjectModel view (objectModel.hpp:11-16) or one scaled scene
 // (TestsDetector.cpp:104-106), resident in HBM.
 struct SetDev {
-    const int8_t* frag;    // d - 128 as i8, "fragment-major" tiles: [tile][u 0..1][kstep 0..3][lane 0..63][16]
-    const int* norm;       // per tile: [64] |d - 128|^2, then [64] -floor(|d - 128|^2 / 2) (padding: INT_MAX)
+    const int8_t* frag;    // 127 - d as i8, "fragment-major" tiles: [tile][u 0..1][kstep 0..3][lane 0..63][16]
+    const int* norm;       // per tile kNormWords: floor(n2/2), n2 & 1, c (knn.hip prep_tile)
     const float* f32;      // row-major n x 128 fp32 (the caller's CV_32F rows)
     const float2* kp;      // KeyPoint::pt per row
     int n;
@@ -41,16 +55,16 @@ struct Top2 {  // partial top-2 of one query over one train split; key = distanc
 struct ProbDev {
     SetDev q, t;
     int nsplit;          // train splits for the distance kernel
-    int q_pad;           // nq rounded up to 256
+    int q_pad;           // nq rounded up to kKnnBlockQ
     long long part_off;  // into Top2 partials: [split][q_pad]
     long long good_off;  // into good arrays (capacity nq)
     long long it_off;    // into per-iteration arrays (capacity max_iters)
 };
 
-// Work item of the distance kernel: 256 queries x a train tile range of one problem.
+// Work item of the distance kernel: kKnnBlockQ queries x a train tile range of one problem.
 struct KnnWork {
     int problem;
-    int q0;        // first query row (multiple of 256)
+    int q0;        // first query row (multiple of kKnnBlockQ)
     int tile0;     // train tiles [tile0, tile1)
     int tile1;
     int split;

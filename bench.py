@@ -167,7 +167,7 @@ def main():
                                 "achieved_hbm_GBs": round(knn_bytes / (kavg["knn"] * 1e-3) / 1e9, 1)}
         if kavg.get("score", 0) > 0:
             ach = FLOP_PER_POINT_EVAL * point_evals / (kavg["score"] * 1e-3) / 1e12
-            t = pmc_traffic("ransac_bound_kernel")
+            t = pmc_traffic("ransac_bound")
             rooflines["score"] = {"kernel": "ransac_bound (closed-form hypotheses, bounded inlier counts), 2 launches/step",
                                   "bound": "valu", "achieved": round(ach, 2), "peak": PEAK_F32_VALU_TFLOPS,
                                   "unit": "TFLOP/s", "frac": round(ach / PEAK_F32_VALU_TFLOPS, 4), "traffic": t,

@@ -15,7 +15,7 @@ STATUS_NAMES = {0: "accepted", 1: "few_good", 2: "empty_H", 3: "few_inliers", 4:
 # every symbol include/mim.h declares (checked by tests/test_abi.py)
 EXPORTS = [
     "mim_version", "mim_default_params", "mim_ctx_create", "mim_ctx_destroy", "mim_last_error",
-    "mim_ctx_set_stream", "mim_synchronize", "mim_set_create", "mim_sets_clear", "mim_knn2_l2",
+    "mim_ctx_set_stream", "mim_ctx_get_stream", "mim_synchronize", "mim_set_create", "mim_sets_clear", "mim_knn2_l2",
     "mim_ratio_filter", "mim_find_homography", "mim_batch_run", "mim_batch_results",
     "mim_batch_results_dev", "mim_batch_results_copy", "mim_batch_problem_detail", "mim_knn2_sets_dev", "mim_last_kernel_ms",
     "mim_set_timing",
@@ -90,6 +90,8 @@ def load():
     L.mim_last_error.argtypes = [vp]
     L.mim_last_error.restype = C.c_char_p
     L.mim_ctx_set_stream.argtypes = [vp, vp]
+    L.mim_ctx_get_stream.argtypes = [vp]
+    L.mim_ctx_get_stream.restype = vp
     L.mim_synchronize.argtypes = [vp]
     L.mim_set_create.argtypes = [vp, f32p, f32p, i32, i32, i32, C.POINTER(C.c_int32)]
     L.mim_sets_clear.argtypes = [vp]

@@ -281,6 +281,8 @@ mim_status mim_ctx_set_stream(mim_ctx* c, void* stream) {
     return MIM_OK;
 }
 
+void* mim_ctx_get_stream(const mim_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
 mim_status mim_synchronize(mim_ctx* c) {
     if (!c) return MIM_EINVAL;
     HIPCHK(c, hipSetDevice(c->device));
@@ -659,8 +661,10 @@ static mim_status ensure_stream(mim_ctx* c, long long need) {
         h[(size_t)i] = (uint32_t)st;
     }
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    HIPCHK(c, c->rws.stream.ensure(sizeof(uint32_t) * len));
+    // 64 zero draws of padding: the draw prefetches of resolve_at may read up to 7 past the end
+    HIPCHK(c, c->rws.stream.ensure(sizeof(uint32_t) * (len + 64)));
     HIPCHK(c, hipMemcpy(c->rws.stream.p, h.data(), sizeof(uint32_t) * len, hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemset((uint32_t*)c->rws.stream.p + len, 0, sizeof(uint32_t) * 64));
     c->rws.stream_len = len;
     return MIM_OK;
 }

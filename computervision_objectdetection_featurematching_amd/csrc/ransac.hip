@@ -349,7 +349,7 @@ __device__ __forceinline__ int refresh_argmax(double val, bool cand, int im, int
 // A/W/V: this group's LDS state (A packed strict upper, W diagonal) written by the caller.
 // Returns, in every slot, the row of V holding the eigenvector of the smallest eigenvalue after
 // OpenCV's descending selection sort.
-__device__ int jacobi9_group(double* __restrict__ A, double* __restrict__ W, double* __restrict__ V) {
+__device__ __forceinline__ int jacobi9_group(double* __restrict__ A, double* __restrict__ W, double* __restrict__ V) {
     constexpr int n = 9;
     const int slot = threadIdx.x & 15;
     const double eps = DBL_EPSILON;
@@ -648,13 +648,13 @@ __device__ __forceinline__ int resolve_at(long long q, const uint32_t* __restric
     unsigned buf[8];
     long long bq = q, r = q;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) buf[k] = q + k < slen ? stream[q + k] : 0u;
+    for (int k = 0; k < 8; ++k) buf[k] = stream[min(q + k, slen - 1)];  // unconditional: one latency
     for (int i = 0; i < 4; ++i) {
         for (;;) {
             if (r >= slen) return 0;
             if (r >= bq + 8) {
 #pragma unroll
-                for (int k = 0; k < 8; ++k) buf[k] = r + k < slen ? stream[r + k] : 0u;
+                for (int k = 0; k < 8; ++k) buf[k] = stream[min(r + k, slen - 1)];
                 bq = r;
             }
             unsigned raw = buf[0];
@@ -747,29 +747,56 @@ __device__ __forceinline__ int attempt_flag(long long q, const uint32_t* __restr
 // kPassUnknown marks such a flag: bits 1..6 valid, bit 0 not evaluated.
 constexpr int kPassUnknown = 0x80;
 
-__device__ __forceinline__ int attempt_len_flag(long long q, const uint32_t* __restrict__ stream, long long slen,
-                                                unsigned N, unsigned long long M) {
-    if (q + 4 > slen) return kAttemptSerial;
-    int idx[4] = {(int)fastmod(stream[q], M, N), (int)fastmod(stream[q + 1], M, N),
-                  (int)fastmod(stream[q + 2], M, N), (int)fastmod(stream[q + 3], M, N)};
-    int len = 4;
-    if (idx[1] == idx[0] || idx[2] == idx[0] || idx[2] == idx[1] || idx[3] == idx[0] || idx[3] == idx[1] ||
-        idx[3] == idx[2]) {
-        len = resolve_at(q, stream, slen, N, M, idx);
-        if (len == 0 || len > 67) return kAttemptSerial;
-    }
-    return ((len - 4) << 1) | kPassUnknown;
+// RNG::uniform(0, n) for n < 2^31 on the fp64 pipe (full rate on gfx950; the 64-bit Lemire product
+// is six quarter-rate integer multiplies): x = a * fl(1/n) is within 2^-20 of a/n, so floor(x) is
+// the quotient or off by one, and the exact fp64 remainder a - q*n (all terms < 2^33) is corrected
+// into [0, n) by one add or subtract.
+__device__ __forceinline__ unsigned mod_f64(unsigned a, double inv_n, double n) {
+    const double x = (double)a;
+    double r = fma(-floor(x * inv_n), n, x);
+    r = r < 0 ? r + n : r;
+    r = r >= n ? r - n : r;
+    return (unsigned)r;
 }
+
+constexpr int kAttemptPerThread = 8;  // window positions per thread (11 draws reduced for 8 attempts)
 
 __global__ __launch_bounds__(256) void ransac_attempt_kernel(const RansacState* __restrict__ st,
                                                              const uint32_t* __restrict__ stream, long long slen,
                                                              uint8_t* __restrict__ flags, int wcap, int bpp, int c1) {
     const int p = blockIdx.x / bpp;
-    const int off = (blockIdx.x % bpp) * 256 + threadIdx.x;
+    const int off = ((blockIdx.x % bpp) * 256 + threadIdx.x) * kAttemptPerThread;
     const RansacState S = st[p];
     if (!S.active || S.done || S.fail_iter != -1 || S.produced >= min(c1, S.niters)) return;
-    if (off >= window_len(S, c1, wcap)) return;
-    flags[(long long)p * wcap + off] = (uint8_t)attempt_len_flag(S.stream_pos + off, stream, slen, (unsigned)S.n, S.modM);
+    if (off >= window_len(S, c1, wcap)) return;  // the window length is a multiple of 64
+    const long long q0 = S.stream_pos + off;
+    const unsigned N = (unsigned)S.n;
+    const double n = (double)N, inv_n = 1.0 / n;
+    constexpr int D = kAttemptPerThread + 3;
+    // unconditional (clamped) loads: all D in flight at once, positions past the stream masked after
+    uint32_t raw[D];
+#pragma unroll
+    for (int k = 0; k < D; ++k) raw[k] = stream[min(q0 + k, slen - 1)];
+    int u[D];
+#pragma unroll
+    for (int k = 0; k < D; ++k) u[k] = q0 + k < slen ? (int)mod_f64(raw[k], inv_n, n) : -1 - k;
+    uint32_t w[2] = {0, 0};
+#pragma unroll
+    for (int j = 0; j < kAttemptPerThread; ++j) {
+        int f;
+        if (q0 + j + 4 > slen) {
+            f = kAttemptSerial;
+        } else if (u[j + 1] == u[j] || u[j + 2] == u[j] || u[j + 2] == u[j + 1] || u[j + 3] == u[j] ||
+                   u[j + 3] == u[j + 1] || u[j + 3] == u[j + 2]) {
+            int idx[4];
+            const int len = resolve_at(q0 + j, stream, slen, N, S.modM, idx);
+            f = (len == 0 || len > 67) ? kAttemptSerial : (((len - 4) << 1) | kPassUnknown);
+        } else {
+            f = kPassUnknown;
+        }
+        w[j >> 2] |= (uint32_t)f << (8 * (j & 3));
+    }
+    *reinterpret_cast<uint2*>(flags + (long long)p * wcap + off) = make_uint2(w[0], w[1]);
 }
 
 __device__ __forceinline__ int wave_excl_prefix_sum(int v) {
@@ -1098,12 +1125,33 @@ __global__ __launch_bounds__(kCheckBlock) void ransac_check_kernel(const ChainSe
     if ((blockIdx.x % bpp) * kCheckBlock >= T) return;  // T < 0: nothing this chunk
     const RansacState S = st[p];
     const int b = blockIdx.x % bpp;
+    // segment data of the block's first 4 segments in one round of (uniform, scalar) loads
+    const int nseg = G->nseg;
+    const int j0 = b < kChainBlk ? G->blk_seg[b] : chain_seg(G, b * kCheckBlock);
+    int segA[5], segS[4], segQ[4];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) segA[k] = G->A[min(j0 + k, nseg + 1)];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        segS[k] = G->seg_s[min(j0 + k, nseg)];
+        segQ[k] = G->seg_q[min(j0 + k, max(nseg - 1, 0))];
+    }
     bool pass = false;
     if (t < T) {
-        int j = b < kChainBlk ? G->blk_seg[b] : chain_seg(G, t);  // segment of the block's first attempt
-        while (j < G->nseg && t >= G->A[j + 1]) ++j;  // a block spans a few segments at most
+        int k = 0;
+#pragma unroll
+        for (int i = 1; i < 4; ++i) k += (j0 + i <= nseg) && t >= segA[i];
+        int j = j0 + k;
         bool irregular;
-        const long long q = G->wbase + chain_pos(G, j, t, irregular);
+        int pos;
+        if (j < nseg && t >= segA[k + 1]) {  // a block spanning more than 4 segments (rare)
+            while (j < nseg && t >= G->A[j + 1]) ++j;
+            pos = chain_pos(G, j, t, irregular);
+        } else {
+            irregular = j < nseg && t == segA[k + 1] - 1;
+            pos = irregular ? segQ[k] : segS[k] + 4 * (t - segA[k]);
+        }
+        const long long q = G->wbase + pos;
         const unsigned N = (unsigned)S.n;
         int idx[4];
         if (!irregular) {
@@ -1127,16 +1175,27 @@ __global__ __launch_bounds__(kCheckBlock) void ransac_check_kernel(const ChainSe
 
 // ---- count: ranks of the passing attempts, getSubset's failure rule, samples, state ----
 // Visit the passing attempts with chain index in [t0, t1), in order: fn(t).
+// (words fetched 8 at a time with unconditional loads: one memory latency per 8 words)
 template <class Fn>
 __device__ __forceinline__ void pass_visit(const uint32_t* __restrict__ PB, int t0, int t1, Fn&& fn) {
-    for (int w = t0 >> 5; w <= (t1 - 1) >> 5 && t0 < t1; ++w) {
-        const int lo_b = max(t0 - 32 * w, 0), hi_b = min(t1 - 32 * w, 32);
-        const uint32_t rm = (hi_b == 32 ? 0xFFFFFFFFu : ((1u << hi_b) - 1)) & ~((1u << lo_b) - 1);
-        uint32_t bits = PB[w] & rm;
-        while (bits) {
-            const int bit = __builtin_ctz(bits);
-            bits &= bits - 1;
-            fn(32 * w + bit);
+    if (t0 >= t1) return;
+    const int wl = (t1 - 1) >> 5;
+    for (int w0 = t0 >> 5; w0 <= wl; w0 += 8) {
+        uint32_t wd[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) wd[k] = PB[min(w0 + k, wl)];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int w = w0 + k;
+            if (w > wl) break;
+            const int lo_b = max(t0 - 32 * w, 0), hi_b = min(t1 - 32 * w, 32);
+            const uint32_t rm = (hi_b == 32 ? 0xFFFFFFFFu : ((1u << hi_b) - 1)) & ~((1u << lo_b) - 1);
+            uint32_t bits = wd[k] & rm;
+            while (bits) {
+                const int bit = __builtin_ctz(bits);
+                bits &= bits - 1;
+                fn(32 * w + bit);
+            }
         }
     }
 }
@@ -1167,15 +1226,11 @@ __global__ __launch_bounds__(kChainThreads) void ransac_count_kernel(RansacState
     const int wpt = (words + kChainThreads - 1) / kChainThreads;
     const int t0 = min(T, tid * wpt * 32), t1 = min(T, t0 + wpt * 32);
     int cnt = 0, first = -1, last = -1;
-    for (int w = t0 >> 5; 32 * w < t1; ++w) {
-        const int hi_b = min(t1 - 32 * w, 32);
-        const uint32_t bits = PB[w] & (hi_b == 32 ? 0xFFFFFFFFu : ((1u << hi_b) - 1));
-        if (bits) {
-            if (first < 0) first = 32 * w + __builtin_ctz(bits);
-            last = 32 * w + 31 - __builtin_clz(bits);
-            cnt += __popc(bits);
-        }
-    }
+    pass_visit(PB, t0, t1, [&](int t) {
+        if (first < 0) first = t;
+        last = t;
+        ++cnt;
+    });
     // failure rule of getSubset: 10000 consecutive rejected attempts (ranges here are < 10000 long,
     // so a failure can only end a gap that starts at an earlier thread's last pass)
     int total;
@@ -2057,16 +2112,31 @@ __global__ __launch_bounds__(kCandThreads) void ransac_cand_kernel(RansacState* 
     const int t0 = S.next_iter, t1 = max(t0, min(min(c1, S.produced), S.niters));
     const int ch = (t1 - t0 + kCandThreads - 1) / kCandThreads;
     const int a = min(t1, t0 + tid * ch), e = min(t1, a + ch);
+    // batches of 16 unconditional (clamped) loads: one memory latency per batch, not per iteration
+    constexpr int kB = 16;
     int lmax = INT_MIN;
-    for (int t = a; t < e; ++t) lmax = max(lmax, Bd[t].x);
+    for (int t = a; t < e; t += kB) {
+        int2 v[kB];
+#pragma unroll
+        for (int k = 0; k < kB; ++k) v[k] = Bd[min(t + k, e - 1)];
+#pragma unroll
+        for (int k = 0; k < kB; ++k) lmax = t + k < e ? max(lmax, v[k].x) : lmax;
+    }
     const int init = max(3, max(S.max_good, S.lo_max));
     int all;
     const int run0 = block_excl_max(lmax, init, wred, all);  // bound before this thread's first iteration
     int cnt = 0, run = run0;
-    for (int t = a; t < e; ++t) {
-        const int2 b = Bd[t];
-        cnt += b.y > run;
-        run = max(run, b.x);
+    for (int t = a; t < e; t += kB) {
+        int2 v[kB];
+#pragma unroll
+        for (int k = 0; k < kB; ++k) v[k] = Bd[min(t + k, e - 1)];
+#pragma unroll
+        for (int k = 0; k < kB; ++k) {
+            if (t + k < e) {
+                cnt += v[k].y > run;
+                run = max(run, v[k].x);
+            }
+        }
     }
     int total;
     int o = block_excl_sum(cnt, wred2, total);
@@ -2116,6 +2186,9 @@ __global__ __launch_bounds__(64) void ransac_exact_kernel(const RansacState* __r
     double H[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
     int ok = 0;
     const float4* __restrict__ P = pts + probs[p].good_off;
+#ifdef MIM_REFINE_PROF
+    const unsigned long long x0 = clock64();
+#endif
     if (valid && !tight) {  // uniform over the group
         const int4 s4 = decode_sample(samples[probs[p].it_off + t], stream, (unsigned)S.n, S.modM);
         const float4 a = P[s4.x], b = P[s4.y], c = P[s4.z], d = P[s4.w];
@@ -2123,6 +2196,10 @@ __global__ __launch_bounds__(64) void ransac_exact_kernel(const RansacState* __r
         const float m[8] = {a.z, a.w, b.z, b.w, c.z, c.w, d.z, d.w};
         ok = run_kernel4_group(M, m, sd + grp * kJ9G, H);
     }
+#ifdef MIM_REFINE_PROF
+    const unsigned long long x1 = clock64();
+    if (p < 3 && lane == 0) printf("[exact] p=%d w=%d nc=%d tight=%d solve %llu\n", p, w, ncand[p], (int)tight, x1 - x0);
+#endif
     // findInliers of every solved candidate by the whole wave (computeError is per point: the count
     // does not depend on the order)
     float Hf[8];
@@ -2911,7 +2988,7 @@ void ransac_enqueue(const RansacParams& prm, int n_probs, const ProbDev* probs, 
         // falls back to inline evaluation past the window
         // (a multiple of 64: flags are read as 16-byte vectors, pass bits as 32-bit words)
         const int wcap = (int)(std::min<long long>((long long)(c1 - c0) * 28 + 4096, b.flag_cap / std::max(n_probs, 1)) & ~63LL);
-        const int bppw = (wcap + 255) / 256;
+        const int bppw = (wcap + 256 * kAttemptPerThread - 1) / (256 * kAttemptPerThread);
         ransac_attempt_kernel<<<n_probs * bppw, 256, 0, s>>>(b.state, b.stream, b.stream_len, b.flags, wcap, bppw, c1);
         mark(mark_ctx, "attempt");
         if (use_chain) {

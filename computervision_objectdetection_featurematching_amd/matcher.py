@@ -70,6 +70,10 @@ class Matcher:
     def set_stream(self, stream_handle: int | None):
         self._check(self.L.mim_ctx_set_stream(self._ctx, C.c_void_p(stream_handle or 0)))
 
+    def stream_handle(self) -> int:
+        """The HIP stream this matcher enqueues on (wrap with torch.cuda.ExternalStream)."""
+        return int(self.L.mim_ctx_get_stream(self._ctx) or 0)
+
     def synchronize(self):
         self._check(self.L.mim_synchronize(self._ctx))
 

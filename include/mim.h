@@ -79,6 +79,8 @@ void mim_ctx_destroy(struct mim_ctx* ctx);
 const char* mim_last_error(const struct mim_ctx* ctx);
 /* Use an external HIP stream (hipStream_t cast to void*); NULL restores the ctx's own stream. */
 mim_status mim_ctx_set_stream(struct mim_ctx* ctx, void* stream);
+/* The HIP stream the ctx currently enqueues on (its own non-blocking stream unless set above). */
+void* mim_ctx_get_stream(const struct mim_ctx* ctx);
 mim_status mim_synchronize(struct mim_ctx* ctx);
 
 /* ---- descriptor sets: ObjectModel views and scene scales -------------------------------------

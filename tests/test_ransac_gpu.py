@@ -326,3 +326,35 @@ def test_chain_sampler_equals_walker():
     for (ha, ma, ra), (hb, mb, rb) in zip(f0, f1):
         np.testing.assert_array_equal(ma, mb)
         assert ra == rb
+
+
+def test_concurrent_contexts_identical():
+    """Two contexts with batches in flight at once on their own streams (bench.py --inflight 2) give
+    the records and masks of one context run alone: contexts share no device state."""
+    from computervision_objectdetection_featurematching_amd import Matcher, default_params
+    ds = make_dataset(2, 4, 1200, 2000, 400, inlier_frac=0.1, seed=777)
+    prm = default_params(max_iters=8000)
+    pairs = ds.problems
+
+    def run(ms):
+        for m in ms:  # enqueue every context's batch before collecting any
+            q = [m.add_set(d, k) for d, k in zip(ds.model_desc, ds.model_kp)]
+            t = [m.add_set(d, k) for d, k in zip(ds.scene_desc, ds.scene_kp)]
+            m.match_batch_async([(q[a], t[b]) for a, b in pairs], prm)
+        out = []
+        for m in ms:
+            res = m.batch_results(len(pairs))
+            out.append((res, [m.problem_detail(i, int(r["n_good"]))[2] for i, r in enumerate(res)]))
+        return out
+
+    solo = Matcher(0)
+    duo = [Matcher(0), Matcher(0)]
+    try:
+        (r0, m0), = run([solo])
+        for r1, m1 in run(duo):
+            assert r0.tobytes() == r1.tobytes()
+            for a, b in zip(m0, m1):
+                np.testing.assert_array_equal(a, b)
+    finally:
+        for m in [solo] + duo:
+            m.close()

@@ -747,56 +747,99 @@ __device__ __forceinline__ int attempt_flag(long long q, const uint32_t* __restr
 // kPassUnknown marks such a flag: bits 1..6 valid, bit 0 not evaluated.
 constexpr int kPassUnknown = 0x80;
 
-// RNG::uniform(0, n) for n < 2^31 on the fp64 pipe (full rate on gfx950; the 64-bit Lemire product
-// is six quarter-rate integer multiplies): x = a * fl(1/n) is within 2^-20 of a/n, so floor(x) is
-// the quotient or off by one, and the exact fp64 remainder a - q*n (all terms < 2^33) is corrected
-// into [0, n) by one add or subtract.
-__device__ __forceinline__ unsigned mod_f64(unsigned a, double inv_n, double n) {
-    const double x = (double)a;
-    double r = fma(-floor(x * inv_n), n, x);
-    r = r < 0 ? r + n : r;
-    r = r >= n ? r - n : r;
-    return (unsigned)r;
+// RNG::uniform(0, n) = next() % n by Barrett reduction: m = floor((2^32 - 1) / n) >= 2^32/n - 1, so
+// q = mulhi(a, m) is the quotient or one less and a - q*n lies in [0, 2n); one unsigned min folds it
+// into [0, n).  For n > 256 the quotient fits 24 bits and q*n is the full-rate v_mul_u32_u24 (the
+// 64-bit Lemire product of fastmod is six quarter-rate multiplies).
+template <bool kNgt256>
+__device__ __forceinline__ unsigned mod_barrett(unsigned a, unsigned m, unsigned n) {
+    const unsigned q = __umulhi(a, m);
+    const unsigned r = a - (kNgt256 ? __umul24(q, n) : q * n);
+    return min(r, r - n);
 }
 
 constexpr int kAttemptPerThread = 8;  // window positions per thread (11 draws reduced for 8 attempts)
+
+constexpr int kAttemptRounds = 1;     // 2048-position rounds per block
+constexpr int kAttemptExtra = 4;      // redraws resolved from registers (more: resolve_at)
+
+// getSubset's draw loop for the attempt whose first draw is u[j] (ptsetreg.cpp: redraw while the
+// index repeats an earlier one of the sample), over the reduced draws held in registers.  Returns
+// the draws consumed, or 0 if more than the D - j registers would be needed.
+template <int D>
+__device__ __forceinline__ int redraw_len(const unsigned (&u)[D], int j) {
+    unsigned a0 = u[j], a1 = 0, a2 = 0;
+    int c = 1, len = 0;
+#pragma unroll
+    for (int k = 1; k < D; ++k) {
+        if (k <= j) continue;
+        const unsigned v = u[k];
+        const bool dup = v == a0 || (c > 1 && v == a1) || (c > 2 && v == a2);
+        const bool take = len == 0 && !dup;
+        a1 = take && c == 1 ? v : a1;
+        a2 = take && c == 2 ? v : a2;
+        len = take && c == 3 ? k - j + 1 : len;
+        c += take ? 1 : 0;
+    }
+    return len;
+}
 
 __global__ __launch_bounds__(256) void ransac_attempt_kernel(const RansacState* __restrict__ st,
                                                              const uint32_t* __restrict__ stream, long long slen,
                                                              uint8_t* __restrict__ flags, int wcap, int bpp, int c1) {
     const int p = blockIdx.x / bpp;
-    const int off = ((blockIdx.x % bpp) * 256 + threadIdx.x) * kAttemptPerThread;
     const RansacState S = st[p];
     if (!S.active || S.done || S.fail_iter != -1 || S.produced >= min(c1, S.niters)) return;
-    if (off >= window_len(S, c1, wcap)) return;  // the window length is a multiple of 64
-    const long long q0 = S.stream_pos + off;
-    const unsigned N = (unsigned)S.n;
-    const double n = (double)N, inv_n = 1.0 / n;
-    constexpr int D = kAttemptPerThread + 3;
-    // unconditional (clamped) loads: all D in flight at once, positions past the stream masked after
-    uint32_t raw[D];
+    const int wlen = window_len(S, c1, wcap);  // a multiple of 64
+    // stream positions fit 32 bits (the stream is capped at 2^28 draws)
+    const int last = (int)slen - 1;
+    const unsigned N = (unsigned)S.n, mB = 0xFFFFFFFFu / N;
+    const bool big = N > 256 && N < (1u << 24);  // q and n both fit 24 bits
+    constexpr int D = kAttemptPerThread + 3 + kAttemptExtra;
+    for (int r = 0; r < kAttemptRounds; ++r) {
+        const int off = (((blockIdx.x % bpp) * kAttemptRounds + r) * 256 + threadIdx.x) * kAttemptPerThread;
+        if (off >= wlen) break;
+        const int q0 = (int)S.stream_pos + off;
+        // unconditional (clamped) loads, all in flight at once; positions whose 4 draws pass the
+        // stream end are flagged for the walker below, so the clamped values are never used
+        unsigned u[D];
 #pragma unroll
-    for (int k = 0; k < D; ++k) raw[k] = stream[min(q0 + k, slen - 1)];
-    int u[D];
+        for (int k = 0; k < D; ++k) u[k] = stream[min(q0 + k, last)];
+        if (big) {
 #pragma unroll
-    for (int k = 0; k < D; ++k) u[k] = q0 + k < slen ? (int)mod_f64(raw[k], inv_n, n) : -1 - k;
-    uint32_t w[2] = {0, 0};
-#pragma unroll
-    for (int j = 0; j < kAttemptPerThread; ++j) {
-        int f;
-        if (q0 + j + 4 > slen) {
-            f = kAttemptSerial;
-        } else if (u[j + 1] == u[j] || u[j + 2] == u[j] || u[j + 2] == u[j + 1] || u[j + 3] == u[j] ||
-                   u[j + 3] == u[j + 1] || u[j + 3] == u[j + 2]) {
-            int idx[4];
-            const int len = resolve_at(q0 + j, stream, slen, N, S.modM, idx);
-            f = (len == 0 || len > 67) ? kAttemptSerial : (((len - 4) << 1) | kPassUnknown);
+            for (int k = 0; k < D; ++k) u[k] = mod_barrett<true>(u[k], mB, N);
         } else {
-            f = kPassUnknown;
+#pragma unroll
+            for (int k = 0; k < D; ++k) u[k] = mod_barrett<false>(u[k], mB, N);
         }
-        w[j >> 2] |= (uint32_t)f << (8 * (j & 3));
+        // repeated index among the 4 draws of position j: pairs at distance 1, 2, 3, each tested once
+        constexpr int D0 = kAttemptPerThread + 3;
+        bool d1[D0 - 1], d2[D0 - 2], d3[D0 - 3];
+#pragma unroll
+        for (int k = 0; k < D0 - 1; ++k) d1[k] = u[k] == u[k + 1];
+#pragma unroll
+        for (int k = 0; k < D0 - 2; ++k) d2[k] = u[k] == u[k + 2];
+#pragma unroll
+        for (int k = 0; k < D0 - 3; ++k) d3[k] = u[k] == u[k + 3];
+        uint32_t w[2] = {0, 0};
+#pragma unroll
+        for (int j = 0; j < kAttemptPerThread; ++j) {
+            const bool rep = d1[j] | d1[j + 1] | d1[j + 2] | d2[j] | d2[j + 1] | d3[j];
+            int f = kPassUnknown;
+            if (q0 + j + 4 > (int)slen) {
+                f = kAttemptSerial;
+            } else if (rep) {
+                int len = redraw_len(u, j);
+                if (len == 0 || q0 + j + len > (int)slen) {  // long redraw run or near the stream end
+                    int idx[4];
+                    len = resolve_at(q0 + j, stream, slen, N, S.modM, idx);
+                }
+                f = (len == 0 || len > 67) ? kAttemptSerial : (((len - 4) << 1) | kPassUnknown);
+            }
+            w[j >> 2] |= (uint32_t)f << (8 * (j & 3));
+        }
+        *reinterpret_cast<uint2*>(flags + (long long)p * wcap + off) = make_uint2(w[0], w[1]);
     }
-    *reinterpret_cast<uint2*>(flags + (long long)p * wcap + off) = make_uint2(w[0], w[1]);
 }
 
 __device__ __forceinline__ int wave_excl_prefix_sum(int v) {
@@ -2988,7 +3031,7 @@ void ransac_enqueue(const RansacParams& prm, int n_probs, const ProbDev* probs, 
         // falls back to inline evaluation past the window
         // (a multiple of 64: flags are read as 16-byte vectors, pass bits as 32-bit words)
         const int wcap = (int)(std::min<long long>((long long)(c1 - c0) * 28 + 4096, b.flag_cap / std::max(n_probs, 1)) & ~63LL);
-        const int bppw = (wcap + 256 * kAttemptPerThread - 1) / (256 * kAttemptPerThread);
+        const int bppw = (wcap + 256 * kAttemptPerThread * kAttemptRounds - 1) / (256 * kAttemptPerThread * kAttemptRounds);
         ransac_attempt_kernel<<<n_probs * bppw, 256, 0, s>>>(b.state, b.stream, b.stream_len, b.flags, wcap, bppw, c1);
         mark(mark_ctx, "attempt");
         if (use_chain) {

@@ -1686,20 +1686,11 @@ __device__ __forceinline__ double min_rel_area(const double* x, const double* y)
 constexpr double kScreenArea = 1e-7;
 constexpr double kScreenTight = 2e-5;
 
-constexpr int kBoundTile = 1024;  // points per LDS tile of the bound kernel (24 KiB: 6 blocks per CU)
-
-// The bound kernel evaluates two points per lane and instruction with packed fp32 (v_pk_fma_f32,
-// v_pk_mul_f32): points are staged in LDS as pairs {x0,x1,y0,y1} {-u0,-u1,-v0,-v1} {lo0,lo1,hi0,hi1}.
-// The reprojection test runs division-free: |(X,Y) - W (u,v)|^2 against thr * W^2.
-typedef float f2v __attribute__((ext_vector_type(2)));
-typedef float f4v __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ f2v pk_fma(f2v a, f2v b, f2v c) { return __builtin_elementwise_fma(a, b, c); }
-
 // Closed-form hypothesis of the bound kernels for the sample s4: Hd = H / H[8] (fp64); invalid =
 // runKernel's degeneracy test; uncertain = no usable bound (conditioning screen, H[8] ~ 0, non-finite);
 // eta > 0 widens the margin (poorly conditioned samples).
 __device__ __forceinline__ void bound_hypothesis(const float4* __restrict__ P, int4 s4, double (&Hd)[8],
-                                                 bool& invalid, bool& uncertain, float& eta) {
+                                                 bool& invalid, bool& uncertain, float& eta, double& eta_model) {
     const float4 q0 = P[s4.x], q1 = P[s4.y], q2 = P[s4.z], q3 = P[s4.w];
     // runKernel's own degeneracy test (exact, cheap): spread < DBL_EPSILON -> no model
     const float M[8] = {q0.x, q0.y, q1.x, q1.y, q2.x, q2.y, q3.x, q3.y};
@@ -1722,7 +1713,8 @@ __device__ __forceinline__ void bound_hypothesis(const float4* __restrict__ P, i
     const double dx[4] = {q0.z, q1.z, q2.z, q3.z}, dy[4] = {q0.w, q1.w, q2.w, q3.w};
     const double rho = fmin(min_rel_area(sx, sy), min_rel_area(dx, dy));
     uncertain = !(rho >= kScreenArea);
-    if (rho < kScreenTight) eta = (float)(1e-14 / (rho * rho));
+    eta_model = 1e-14 / (rho * rho);  // the disagreement model at this sample's conditioning
+    if (rho < kScreenTight) eta = (float)eta_model;
     double Qs[9], Qd[9], Ai[9], H[9];
     square_to_quad(sx, sy, Qs);
     square_to_quad(dx, dy, Qd);
@@ -1740,124 +1732,6 @@ __device__ __forceinline__ void bound_hypothesis(const float4* __restrict__ P, i
     for (int i = 0; i < 8; ++i) Hd[i] = H[i] * inv;
 #pragma unroll
     for (int i = 0; i < 8; ++i) uncertain |= !isfinite((float)Hd[i]);
-}
-
-// kLo = false (chunks after the first, once maxGoodCount is known): only an upper bound is
-// counted, lo = 0 — the candidate rule then rests on maxGoodCount and the earlier chunks' bounds.
-// That upper bound uses the box max(|ex|, |ey|) <= sqrt(t_hi) |W|, implied by the disc
-// ex^2 + ey^2 <= t_hi W^2: hi_box >= hi, at 11.5 instead of 13.5 VALU operations per point.
-template <bool kLo>
-__global__ __launch_bounds__(256) void ransac_bound_kernel(const RansacState* __restrict__ st,
-                                                           const ProbDev* __restrict__ probs,
-                                                           const float4* __restrict__ pts,
-                                                           const int4* __restrict__ samples,
-                                                           const uint32_t* __restrict__ stream,
-                                                           int2* __restrict__ bounds, int c0, int c1, int bpp,
-                                                           float thr2) {
-    __shared__ f4v tp[3 * (kBoundTile / 2)];
-    const int p = blockIdx.x / bpp;
-    const int it = c0 + (blockIdx.x % bpp) * 256 + threadIdx.x;
-    const RansacState S = st[p];
-    if (!S.active || S.done) return;  // uniform over the block
-    if (c0 + (blockIdx.x % bpp) * 256 >= min(c1, S.produced)) return;  // whole block idle
-    const bool act = it < c1 && it < S.produced;
-    const long long o = probs[p].it_off + it;
-    const float4* __restrict__ P = pts + probs[p].good_off;
-    const int n = S.n;
-    bool uncertain = false, invalid = false;
-    float eta = 0.f;  // widened-margin coefficient for poorly conditioned samples
-    float Hf[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (act) {
-        const int4 s4 = decode_sample(samples[o], stream, (unsigned)n, S.modM);
-        double Hd[8];
-        bound_hypothesis(P, s4, Hd, invalid, uncertain, eta);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) Hf[i] = (float)Hd[i];
-    }
-    const bool count = act && !invalid && !uncertain;
-    // per-point margins computed at staging: err bound 0.5 px^2 + 1e-7 (|x|+|y|+|u|+|v|)^2 around the
-    // squared threshold (+ the widening for poorly conditioned samples)
-    const float k1 = 10.2f * eta, k2 = eta * eta;
-    const bool widen = __any(eta > 0.f);  // rare (~4e-2 of waves): the wave takes the widened loop
-    const f2v h0 = Hf[0], h1 = Hf[1], h2 = Hf[2], h3 = Hf[3], h4 = Hf[4], h5 = Hf[5], h6 = Hf[6], h7 = Hf[7];
-    int lo = 0, hi = 0;
-    for (int b0 = 0; b0 < n; b0 += kBoundTile) {
-        const int tn = min(kBoundTile, n - b0);
-        const int tpairs = (tn + 1) >> 1;
-        __syncthreads();
-        for (int i = threadIdx.x; i < tpairs; i += 256) {
-            const float4 q0 = P[b0 + 2 * i];
-            // odd tail: a point at the origin with negative thresholds never counts
-            const bool has1 = 2 * i + 1 < tn;
-            const float4 q1 = has1 ? P[b0 + 2 * i + 1] : make_float4(0.f, 0.f, 0.f, 0.f);
-            const float s0 = fabsf(q0.x) + fabsf(q0.y) + fabsf(q0.z) + fabsf(q0.w);
-            const float s1 = fabsf(q1.x) + fabsf(q1.y) + fabsf(q1.z) + fabsf(q1.w);
-            const float d0 = fmaf(1e-7f * s0, s0, 0.5f), d1 = fmaf(1e-7f * s1, s1, 0.5f);
-            tp[3 * i] = f4v{q0.x, q1.x, q0.y, q1.y};
-            tp[3 * i + 1] = f4v{-q0.z, -q1.z, -q0.w, -q1.w};
-            // kLo: {t_lo0, t_lo1, t_hi0, t_hi1}; otherwise {sqrt(t_hi0), sqrt(t_hi1), t_hi0, t_hi1}
-            // (square roots rounded up by 1e-6 relative, far above the fp32 sqrt error)
-            const float a0 = kLo ? thr2 - d0 : sqrtf(thr2 + d0) * (1.f + 1e-6f);
-            const float a1 = kLo ? thr2 - d1 : sqrtf(thr2 + d1) * (1.f + 1e-6f);
-            tp[3 * i + 2] = has1 ? f4v{a0, a1, thr2 + d0, thr2 + d1} : f4v{a0, -1.f, thr2 + d0, -1.f};
-        }
-        __syncthreads();
-        if (count && !widen && !kLo) {
-            // box test max(|ex|, |ey|) <= sqrt(t_hi) |W|, counted by sign bit (overflow: inf -> out,
-            // inf - inf = +NaN -> in)
-            int bneg = 0;
-#pragma unroll 4
-            for (int i = 0; i < tpairs; ++i) {
-                const f4v a = tp[3 * i], m = tp[3 * i + 1], t = tp[3 * i + 2];
-#pragma unroll
-                for (int k = 0; k < 2; ++k) {
-                    const float x = a[k], y = a[2 + k];
-                    const float W = fmaf(Hf[6], x, fmaf(Hf[7], y, 1.f));
-                    const float ex = fmaf(m[k], W, fmaf(Hf[0], x, fmaf(Hf[1], y, Hf[2])));
-                    const float ey = fmaf(m[2 + k], W, fmaf(Hf[3], x, fmaf(Hf[4], y, Hf[5])));
-                    bneg += __float_as_uint(fmaf(t[k], fabsf(W), -fmaxf(fabsf(ex), fabsf(ey)))) >> 31;
-                }
-            }
-            hi += 2 * tpairs - bneg;
-        } else if (count && !widen) {
-            // division-free test with sign-bit counting (v_cmp + v_addc cost ~2x a plain ALU op):
-            //   lo: e - tlo W^2 < 0,   not hi: thi W^2 - e < 0
-            int hineg = 0;
-#pragma unroll 4
-            for (int i = 0; i < tpairs; ++i) {
-                const f4v a = tp[3 * i], m = tp[3 * i + 1], t = tp[3 * i + 2];
-#pragma unroll
-                for (int k = 0; k < 2; ++k) {
-                    const float x = a[k], y = a[2 + k];
-                    const float W = fmaf(Hf[6], x, fmaf(Hf[7], y, 1.f));
-                    const float ex = fmaf(m[k], W, fmaf(Hf[0], x, fmaf(Hf[1], y, Hf[2])));
-                    const float ey = fmaf(m[2 + k], W, fmaf(Hf[3], x, fmaf(Hf[4], y, Hf[5])));
-                    const float e = fmaf(ex, ex, ey * ey);
-                    const float W2 = W * W;
-                    if (kLo) lo += __float_as_uint(fmaf(-t[k], W2, e)) >> 31;
-                    hineg += __float_as_uint(fmaf(t[2 + k], W2, -e)) >> 31;
-                }
-            }
-            hi += 2 * tpairs - hineg;
-        } else if (count) {
-            for (int i = 0; i < tpairs; ++i) {
-                const f4v a = tp[3 * i], m = tp[3 * i + 1], t = tp[3 * i + 2];
-                const f2v x = a.xy, y = a.zw;
-                const f2v W = pk_fma(h6, x, pk_fma(h7, y, f2v(1.f)));
-                const f2v ex = pk_fma(m.xy, W, pk_fma(h0, x, pk_fma(h1, y, h2)));
-                const f2v ey = pk_fma(m.zw, W, pk_fma(h3, x, pk_fma(h4, y, h5)));
-                const f2v e = pk_fma(ex, ex, ey * ey);
-                const f2v W2 = W * W;
-                const f2v sc = {fabsf(a.x) + fabsf(a.z) + fabsf(m.x) + fabsf(m.z),
-                                fabsf(a.y) + fabsf(a.w) + fabsf(m.y) + fabsf(m.w)};
-                const f2v wid = sc * pk_fma(f2v(k2), sc, f2v(k1));
-                const f2v L = (t.xy - wid) * W2, U = (t.zw + wid) * W2;
-                if (kLo) lo += (e.x < L.x) + (e.y < L.y);
-                hi += (e.x <= U.x) + (e.y <= U.y);
-            }
-        }
-    }
-    if (act) bounds[o] = invalid ? make_int2(-1, -1) : (uncertain ? make_int2(0, n) : make_int2(lo, hi));
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1966,6 +1840,16 @@ __global__ __launch_bounds__(256) void ransac_tiles_kernel(RansacState* __restri
 
 // Upper bounds of the inlier counts of 256 consecutive iterations per block (64 per wave: two
 // column blocks of 32 hypotheses), the point tiles staged through LDS and shared by the 4 waves.
+// kLo (first chunk): also a lower bound from the octagon inscribed in the inner disc,
+//   max(|ex|, |ey|, (|ex| + |ey|)/sqrt 2) < C_lo |W| - (C_lo + sqrt 2) kMfmaErr - sqrt 2 A,
+//   C_lo = sb sqrt(thr2 - d_max (- widening)) cos(pi/8),
+// which implies ex^2 + ey^2 < (thr2 - d) W^2 for every point's margin d <= d_max.
+// A (both bounds): absolute slack on |X - uW|, |Y - vW| for OpenCV's own fp32 evaluation of
+// computeError and the closed-form/eigenvector disagreement, which the relative margin d cannot
+// cover near the hypothesis' horizon (|W| -> 0): X and W each carry an absolute error of
+// gamma * (sum of |terms|), gamma = 4 ulp(1/2) (float cast of H, product, two sums) + eta, so
+// |X_c/W_c - u| moves by <= (err_X + (|u| + 6) err_W) / |W|, i.e. |ex| by <= A.
+template <bool kLo>
 __global__ __launch_bounds__(256) void ransac_bound_mfma_kernel(const RansacState* __restrict__ st,
                                                                 const ProbDev* __restrict__ probs,
                                                                 const float4* __restrict__ pts,
@@ -1989,9 +1873,10 @@ __global__ __launch_bounds__(256) void ransac_bound_mfma_kernel(const RansacStat
     bool uncertain = false, invalid = false;
     float eta = 0.f;
     double Hd[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    double eta_model = 0;
     if (act) {
         const int4 s4 = decode_sample(samples[o], stream, (unsigned)n, S.modM);
-        bound_hypothesis(P, s4, Hd, invalid, uncertain, eta);
+        bound_hypothesis(P, s4, Hd, invalid, uncertain, eta, eta_model);
     }
     // H' in scaled coordinates, then scaled by 2^-e into [-1, 1]
     const double rs = (double)S.sb / (double)S.sa;
@@ -2011,7 +1896,24 @@ __global__ __launch_bounds__(256) void ransac_bound_mfma_kernel(const RansacStat
     float tt = thr2 + fmaf(1e-7f * S.smax, S.smax, 0.5f);
     if (eta > 0.f) tt += S.smax * fmaf(eta * eta, S.smax, 10.2f * eta);
     const float C = S.sb * sqrtf(tt) * (1.f + 1e-6f);
-    const float E = (1.f + C) * kMfmaErr * (1.f + 1e-6f);
+    // near-horizon slack A (pixel units, |x|, |y| < 1/sa and |u|, |v| < 1/sb), in the scaled units of
+    // the MFMA outputs, with the sample's modelled closed-form/eigenvector disagreement eta_model
+    const double mx = 1.0 / S.sa, mu = 1.0 / S.sb;
+    const double gam = 4.0 * 0x1p-24 + fmin(eta_model, 1.0);
+    const double ax = fmax((fabs(Hd[0]) + fabs(Hd[1])) * mx + fabs(Hd[2]), (fabs(Hd[3]) + fabs(Hd[4])) * mx + fabs(Hd[5]));
+    const double aw = (fabs(Hd[6]) + fabs(Hd[7])) * mx + 1.0;
+    const float A = (float)(gam * (ax + (mu + 6.0) * aw) * S.sb * sc * (1.0 + 1e-6));
+    const float E = (1.f + C) * kMfmaErr * (1.f + 1e-6f) + A;
+    float CL = 0.f, EL = 0.f;
+    if (kLo) {
+        float tl = thr2 - fmaf(1e-7f * S.smax, S.smax, 0.5f);
+        if (eta > 0.f) tl -= S.smax * fmaf(eta * eta, S.smax, 10.2f * eta);
+        // octagon inscribed in the disc of radius sqrt(tl): apothem h = sqrt(tl) cos(pi/8),
+        // max(|ex|, |ey|) <= h |W| and (|ex| + |ey|) / sqrt(2) <= h |W|; the sum carries twice the
+        // error of one coordinate, hence sqrt(2) (kMfmaErr + A) beside h kMfmaErr from |W|
+        CL = S.sb * sqrtf(fmaxf(tl, 0.f)) * 0.92387953f * (1.f - 1e-6f);
+        EL = ((CL + 1.41421357f) * kMfmaErr + 1.41421357f * A) * (1.f + 1e-6f);
+    }
     // B-operand fragments of the own hypothesis: k 0-7 (bx, by, bw) and k 8-15 (shared by bx, by)
     h8v fx = {}, fy = {}, fw = {}, fn = {};
     if (count) {
@@ -2048,12 +1950,17 @@ __global__ __launch_bounds__(256) void ransac_bound_mfma_kernel(const RansacStat
     const h8v b1w = __builtin_bit_cast(h8v, lowh ? r3 : zero4);
     const float Cp = __shfl_xor(C, 32), Ep = __shfl_xor(E, 32);
     const float C0 = lowh ? C : Cp, E0 = lowh ? E : Ep, C1 = lowh ? Cp : C, E1 = lowh ? Ep : E;
+    float CL0 = 0.f, EL0 = 0.f, CL1 = 0.f, EL1 = 0.f;
+    if (kLo) {
+        const float CLp = __shfl_xor(CL, 32), ELp = __shfl_xor(EL, 32);
+        CL0 = lowh ? CL : CLp; EL0 = lowh ? EL : ELp; CL1 = lowh ? CLp : CL; EL1 = lowh ? ELp : EL;
+    }
     const bool wave_counts = __any(count);
     float big = INFINITY;
     asm volatile("" : "+v"(big));
     const uint4* __restrict__ T = tiles + (go >> 5) * 128;
     const int nt = (n + 31) >> 5;
-    unsigned out0 = 0, out1 = 0;
+    unsigned out0 = 0, out1 = 0, in0 = 0, in1 = 0;
     for (int t0 = 0; t0 < nt; t0 += kTileChunk) {
         const int tc = min(kTileChunk, nt - t0);
         __syncthreads();
@@ -2070,25 +1977,44 @@ __global__ __launch_bounds__(256) void ransac_bound_mfma_kernel(const RansacStat
             const f16acc ex1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ax, b1x, zc, 0, 0, 0);
             const f16acc ey1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ay, b1y, zc, 0, 0, 0);
             const f16acc w1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ax, b1w, zc, 0, 0, 0);
-            unsigned bits0 = 0, bits1 = 0;
+            unsigned bits0 = 0, bits1 = 0, lb0 = 0, lb1 = 0;
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 // sign bit of R - max(|ex|, |ey|), R = C |W| + E: set when the point is out of the box
                 // (med3(a, b, big) = max(a, b) without the NaN canonicalisation of fmaxf; big is
                 // opaque so the compiler cannot turn the med3 back into a max)
-                const float d0 = fmaf(C0, fabsf(w0[r]), E0) - __builtin_amdgcn_fmed3f(fabsf(ex0[r]), fabsf(ey0[r]), big);
-                const float d1 = fmaf(C1, fabsf(w1[r]), E1) - __builtin_amdgcn_fmed3f(fabsf(ex1[r]), fabsf(ey1[r]), big);
+                const float m0 = __builtin_amdgcn_fmed3f(fabsf(ex0[r]), fabsf(ey0[r]), big);
+                const float m1 = __builtin_amdgcn_fmed3f(fabsf(ex1[r]), fabsf(ey1[r]), big);
+                const float d0 = fmaf(C0, fabsf(w0[r]), E0) - m0;
+                const float d1 = fmaf(C1, fabsf(w1[r]), E1) - m1;
                 bits0 = __builtin_amdgcn_alignbit(bits0, __float_as_uint(d0), 31);
                 bits1 = __builtin_amdgcn_alignbit(bits1, __float_as_uint(d1), 31);
+                if (kLo) {  // sign bit of max(|ex|, |ey|, (|ex| + |ey|) / sqrt 2) - R_lo: set when surely in
+                    const float o0 = __builtin_amdgcn_fmed3f(m0, (fabsf(ex0[r]) + fabsf(ey0[r])) * 0.70710677f, big);
+                    const float o1 = __builtin_amdgcn_fmed3f(m1, (fabsf(ex1[r]) + fabsf(ey1[r])) * 0.70710677f, big);
+                    const float l0 = o0 - fmaf(CL0, fabsf(w0[r]), -EL0);
+                    const float l1 = o1 - fmaf(CL1, fabsf(w1[r]), -EL1);
+                    lb0 = __builtin_amdgcn_alignbit(lb0, __float_as_uint(l0), 31);
+                    lb1 = __builtin_amdgcn_alignbit(lb1, __float_as_uint(l1), 31);
+                }
             }
             out0 += __popc(bits0);
             out1 += __popc(bits1);
+            if (kLo) {
+                in0 += __popc(lb0);
+                in1 += __popc(lb1);
+            }
         }
     }
     // rows (points) of a column are split over lanes l and l ^ 32
     const unsigned o0 = out0 + __shfl_xor(out0, 32), o1 = out1 + __shfl_xor(out1, 32);
     const int outs = (int)(lowh ? o0 : o1);
-    if (act) bounds[o] = invalid ? make_int2(-1, -1) : (uncertain ? make_int2(0, n) : make_int2(0, n - outs));
+    int lo = 0;
+    if (kLo) {
+        const unsigned i0 = in0 + __shfl_xor(in0, 32), i1 = in1 + __shfl_xor(in1, 32);
+        lo = (int)(lowh ? i0 : i1);  // zero-padded rows (ex = ey = W = 0) give m - R_lo = E_lo > 0: never "in"
+    }
+    if (act) bounds[o] = invalid ? make_int2(-1, -1) : (uncertain ? make_int2(0, n) : make_int2(lo, n - outs));
 }
 
 // exact count of one hypothesis (runKernel + computeError + findInliers, bit-exact)
@@ -2115,6 +2041,64 @@ __device__ int exact_count(const float4* __restrict__ P, int n, int4 s4, double*
     if (blockIdx.x < 3) printf("[exact] block %d lane %d: kernel4 %llu count %llu (n=%d)\n", blockIdx.x, (int)threadIdx.x, e1 - e0, clock64() - e1, n);
 #endif
     return cnt;
+}
+
+// Debug check of the bound kernels (MIM_CHECK_BOUNDS=1): the exact count of every iteration of
+// the chunk (runKernel + computeError, bit-exact, one lane each) against its [lo, hi] bracket.
+// stats: [0] iterations checked, [1] lo > exact, [2] hi < exact, [3] validity disagreements,
+// [4] sum of hi - lo, [5] iterations with lo == hi.
+__global__ __launch_bounds__(64) void ransac_bound_check_kernel(const RansacState* __restrict__ st,
+                                                                const ProbDev* __restrict__ probs,
+                                                                const float4* __restrict__ pts,
+                                                                const int4* __restrict__ samples,
+                                                                const uint32_t* __restrict__ stream,
+                                                                const int2* __restrict__ bounds, int c0, int c1,
+                                                                int bpp, float thr2, unsigned long long* stats) {
+    __shared__ double sd[kJ9D * 64];
+    const int p = blockIdx.x / bpp, lane = threadIdx.x;
+    const int it = c0 + (blockIdx.x % bpp) * 64 + lane;
+    const RansacState S = st[p];
+    if (!S.active || S.done) return;
+    if (!(it < c1 && it < S.produced)) return;
+    const long long o = probs[p].it_off + it;
+    double H[9];
+    const int ex = exact_count(pts + probs[p].good_off, S.n, decode_sample(samples[o], stream, (unsigned)S.n, S.modM),
+                               sd + lane, thr2, H);
+    const int2 b = bounds[o];
+    atomicAdd(stats + 0, 1ull);
+    if ((b.x == -1) != (ex == -1)) atomicAdd(stats + 3, 1ull);
+    if (ex >= 0 && b.x >= 0) {
+        if (b.x > ex) atomicAdd(stats + 1, 1ull);
+        if (b.y < ex) atomicAdd(stats + 2, 1ull);
+        if (b.x > ex || b.y < ex) {  // details of a violation (debug path only)
+            double Hd[8];
+            bool inv = false, unc = false;
+            float eta = 0.f;
+            double eta_m = 0;
+            bound_hypothesis(pts + probs[p].good_off, decode_sample(samples[o], stream, (unsigned)S.n, S.modM), Hd,
+                             inv, unc, eta, eta_m);
+            double dmax = 0;
+            for (int i = 0; i < 8; ++i) dmax = fmax(dmax, fabs(Hd[i] - H[i]) / (fabs(H[i]) + 1e-12));
+            printf("[mim] bound violation p=%d it=%d exact=%d lo=%d hi=%d eta=%g uncertain=%d max_rel_dH=%g\n", p, it,
+                   ex, b.x, b.y, (double)eta, (int)unc, dmax);
+            float Hf[8], Hb[8];
+            for (int i = 0; i < 8; ++i) { Hf[i] = (float)H[i]; Hb[i] = (float)Hd[i]; }
+            const float4* P = pts + probs[p].good_off;
+            for (int i = 0; i < S.n; ++i) {
+                const float4 q = P[i];
+                const float err = reproj_err(Hf, q.x, q.y, q.z, q.w);
+                const float W = fmaf(Hb[6], q.x, fmaf(Hb[7], q.y, 1.f));
+                const float exx = fmaf(-q.z, W, fmaf(Hb[0], q.x, fmaf(Hb[1], q.y, Hb[2])));
+                const float eyy = fmaf(-q.w, W, fmaf(Hb[3], q.x, fmaf(Hb[4], q.y, Hb[5])));
+                const float eb = fmaf(exx, exx, eyy * eyy) / (W * W);
+                if ((err <= thr2) != (eb <= thr2) || fabsf(err - eb) > 0.1f)
+                    printf("[mim]   pt %d (%g %g -> %g %g) exact err %.6g bound-form err %.6g W %g\n", i, q.x, q.y, q.z, q.w,
+                           (double)err, (double)eb, (double)W);
+            }
+        }
+        atomicAdd(stats + 4, (unsigned long long)(b.y - b.x));
+        if (b.x == b.y) atomicAdd(stats + 5, 1ull);
+    }
 }
 
 __device__ __forceinline__ int wave_excl_prefix_max(int v) {
@@ -3021,10 +3005,7 @@ void ransac_enqueue(const RansacParams& prm, int n_probs, const ProbDev* probs, 
     const int use_chain = !(sw && sw[0] == '1');
     int c0 = 0, chunk = 4096;
     const float thr2 = (float)(prm.thresh * prm.thresh);
-    // MIM_BOUND_VALU=1: later chunks on the fp32 VALU bound kernel (cross-check mode)
-    const char* bv = getenv("MIM_BOUND_VALU");
-    const bool bound_mfma = !(bv && bv[0] == '1');
-    if (!exact_all && bound_mfma) ransac_tiles_kernel<<<n_probs, 256, 0, s>>>(b.state, probs, pts, b.tiles);
+    if (!exact_all) ransac_tiles_kernel<<<n_probs, 256, 0, s>>>(b.state, probs, pts, b.tiles);
     while (c0 < max_iters) {
         const int c1 = (int)std::min<long long>((long long)c0 + chunk, max_iters);
         // attempt outcomes for a window of ~28 draws per wanted iteration (pass rate ~1/5), the walk
@@ -3066,15 +3047,27 @@ void ransac_enqueue(const RansacParams& prm, int n_probs, const ProbDev* probs, 
             mark(mark_ctx, "select");
         } else {
             if (c0 == 0)
-                ransac_bound_kernel<true><<<n_probs * bpp256, 256, 0, s>>>(b.state, probs, pts, b.samples, b.stream,
-                                                                          b.bounds, c0, c1, bpp256, thr2);
-            else if (bound_mfma)
-                ransac_bound_mfma_kernel<<<n_probs * bpp256, 256, 0, s>>>(b.state, probs, pts, b.samples, b.stream,
-                                                                          b.tiles, b.bounds, c0, c1, bpp256, thr2);
+                ransac_bound_mfma_kernel<true><<<n_probs * bpp256, 256, 0, s>>>(b.state, probs, pts, b.samples, b.stream,
+                                                                                b.tiles, b.bounds, c0, c1, bpp256, thr2);
             else
-                ransac_bound_kernel<false><<<n_probs * bpp256, 256, 0, s>>>(b.state, probs, pts, b.samples, b.stream,
-                                                                           b.bounds, c0, c1, bpp256, thr2);
+                ransac_bound_mfma_kernel<false><<<n_probs * bpp256, 256, 0, s>>>(b.state, probs, pts, b.samples, b.stream,
+                                                                                 b.tiles, b.bounds, c0, c1, bpp256, thr2);
             mark(mark_ctx, "score");
+            if (getenv("MIM_CHECK_BOUNDS")) {  // debug: every bracket against the exact count
+                unsigned long long* dst = nullptr;
+                unsigned long long h[6] = {0, 0, 0, 0, 0, 0};
+                if (hipMalloc(&dst, sizeof h) == hipSuccess) {
+                    (void)hipMemsetAsync(dst, 0, sizeof h, s);
+                    const int bpp64 = (c1 - c0 + 63) / 64;
+                    ransac_bound_check_kernel<<<n_probs * bpp64, 64, 0, s>>>(b.state, probs, pts, b.samples, b.stream,
+                                                                             b.bounds, c0, c1, bpp64, thr2, dst);
+                    (void)hipMemcpyAsync(h, dst, sizeof h, hipMemcpyDeviceToHost, s);
+                    (void)hipStreamSynchronize(s);
+                    (void)hipFree(dst);
+                }
+                fprintf(stderr, "[mim] bound check chunk [%d,%d): checked %llu lo_viol %llu hi_viol %llu valid_mismatch %llu "
+                        "mean_width %.2f tight %llu\n", c0, c1, h[0], h[1], h[2], h[3], h[0] ? (double)h[4] / h[0] : 0.0, h[5]);
+            }
             ransac_cand_kernel<<<n_probs, kCandThreads, 0, s>>>(b.state, probs, b.bounds, c1, b.cand, b.ncand);
             mark(mark_ctx, "cand");
             if (getenv("MIM_DEBUG_NCAND")) {

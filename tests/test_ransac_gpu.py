@@ -206,16 +206,16 @@ def test_filtered_equals_exact_all(oracle):
         assert (ha is None) == (hb is None) and (ha is None or np.array_equal(ha, hb))
 
 
-def test_bound_mfma_equals_valu():
-    """Later RANSAC chunks bound the inlier counts on the matrix cores (f16 hi/lo split GEMMs) by
-    default; the fp32 VALU bound kernel (MIM_BOUND_VALU=1) must lead to the identical output, and so
-    must the all-exact reference mode (both bounds are only filters)."""
+def test_bound_mfma_equals_exact_all():
+    """RANSAC bounds the inlier counts on the matrix cores (f16 hi/lo split GEMMs) and evaluates only
+    the candidates exactly; the all-exact reference mode (MIM_RANSAC_EXACT=1: runKernel + computeError
+    for every iteration) must give the identical output (the bounds are only filters)."""
     import os
     from computervision_objectdetection_featurematching_amd import Matcher, default_params
     ds = make_dataset(2, 3, 1500, 2500, 500, inlier_frac=0.08, seed=2718)
     sets = _adversarial_sets()
     outs = []
-    for key, mode in (("MIM_BOUND_VALU", "0"), ("MIM_BOUND_VALU", "1"), ("MIM_RANSAC_EXACT", "1")):
+    for key, mode in (("MIM_RANSAC_EXACT", "0"), ("MIM_RANSAC_EXACT", "1")):
         os.environ[key] = mode
         m = Matcher(0)
         try:
@@ -358,3 +358,31 @@ def test_concurrent_contexts_identical():
     finally:
         for m in [solo] + duo:
             m.close()
+
+
+def test_bound_brackets_exact_counts(capfd):
+    """MIM_CHECK_BOUNDS=1: every iteration's [lo, hi] from the MFMA bound kernel brackets its exact
+    OpenCV inlier count (runKernel + computeError, bit-exact), in chunk 1 (lo and hi) and later chunks,
+    on the synthetic workload and on the adversarial sets (near-collinear clusters put points close to
+    the horizon of many hypotheses, where OpenCV's own fp32 evaluation is far from the true error)."""
+    import os
+    import re
+    from computervision_objectdetection_featurematching_amd import Matcher, default_params
+    ds = make_dataset(2, 2, 1200, 2000, 400, inlier_frac=0.1, seed=99)
+    os.environ["MIM_CHECK_BOUNDS"] = "1"
+    m = Matcher(0)
+    try:
+        q = [m.add_set(d, k) for d, k in zip(ds.model_desc, ds.model_kp)]
+        t = [m.add_set(d, k) for d, k in zip(ds.scene_desc, ds.scene_kp)]
+        m.match_batch([(q[a], t[b]) for a, b in ds.problems], default_params(max_iters=6000))
+        for s_, d_ in _adversarial_sets():
+            m.find_homography(s_, d_, 5.0, 6000)
+    finally:
+        m.close()
+        os.environ.pop("MIM_CHECK_BOUNDS", None)
+    cap = capfd.readouterr()
+    err = cap.err
+    lines = re.findall(r"checked (\d+) lo_viol (\d+) hi_viol (\d+) valid_mismatch (\d+)", err)
+    assert lines and sum(int(c) for c, *_ in lines) > 10000
+    for c, lo_v, hi_v, vm in lines:
+        assert (lo_v, hi_v, vm) == ("0", "0", "0"), err + cap.out

@@ -577,6 +577,102 @@ __device__ void dlt_finish_group(const double* lt, double* D, const double* invH
     for (int i = 0; i < 9; ++i) H[i] = H0[i] * sc;
 }
 
+// Refit eigenvector by inverse iteration (one lane).  The refit's runKernel over all inliers needs
+// H only to the findHomography contract (LM refines it next; the RANSAC mask is already final), so
+// instead of the ~140-rotation Jacobi, the eigenvector of the smallest eigenvalue of LtL comes from
+// inverse iteration on the Cholesky factor of LtL + delta I (delta = 1e-10 trace: same eigenvectors,
+// positive definite), started from the RANSAC best model in the refit's normalized coordinates.
+// Returns false (caller falls back to the Jacobi) when the factorisation fails, the iteration does not
+// settle within 8 steps, or the Rayleigh residual |A x - (x'Ax) x| exceeds 1e-9 trace.
+__device__ bool refit_inverse_iteration(const double* lt, const double* x0, double* x) {
+    double a[9][9], L[9][9];
+    {
+        int e = 0;
+#pragma unroll
+        for (int j = 0; j < 9; ++j)
+#pragma unroll
+            for (int k = j; k < 9; ++k, ++e) a[j][k] = a[k][j] = lt[e];
+    }
+    double tr = 0;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) tr += a[i][i];
+    if (!(tr > 0) || !isfinite(tr)) return false;
+    const double delta = 1e-10 * tr;
+#pragma unroll
+    for (int j = 0; j < 9; ++j) {
+        double s = a[j][j] + delta;
+#pragma unroll
+        for (int k = 0; k < j; ++k) s -= L[j][k] * L[j][k];
+        if (!(s > 0.5 * delta)) return false;
+        const double d = sqrt(s), id = 1.0 / d;
+        L[j][j] = d;
+#pragma unroll
+        for (int i = j + 1; i < 9; ++i) {
+            double t = a[i][j];
+#pragma unroll
+            for (int k = 0; k < j; ++k) t -= L[i][k] * L[j][k];
+            L[i][j] = t * id;
+        }
+    }
+    double v[9], nrm = 0;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) nrm += x0[i] * x0[i];
+    if (!(nrm > 0) || !isfinite(nrm)) return false;
+    nrm = 1.0 / sqrt(nrm);
+#pragma unroll
+    for (int i = 0; i < 9; ++i) v[i] = x0[i] * nrm;
+    bool settled = false;
+    for (int it = 0; it < 8 && !settled; ++it) {
+        double y[9], z[9];
+#pragma unroll
+        for (int i = 0; i < 9; ++i) {
+            double t = v[i];
+#pragma unroll
+            for (int k = 0; k < i; ++k) t -= L[i][k] * y[k];
+            y[i] = t / L[i][i];
+        }
+#pragma unroll
+        for (int i = 8; i >= 0; --i) {
+            double t = y[i];
+#pragma unroll
+            for (int k = i + 1; k < 9; ++k) t -= L[k][i] * z[k];
+            z[i] = t / L[i][i];
+        }
+        double zn = 0, dot = 0;
+#pragma unroll
+        for (int i = 0; i < 9; ++i) {
+            zn += z[i] * z[i];
+            dot += z[i] * v[i];
+        }
+        if (!(zn > 0) || !isfinite(zn)) return false;
+        zn = (dot < 0 ? -1.0 : 1.0) / sqrt(zn);
+        double dmax = 0;
+#pragma unroll
+        for (int i = 0; i < 9; ++i) {
+            const double w = z[i] * zn;
+            dmax = fmax(dmax, fabs(w - v[i]));
+            v[i] = w;
+        }
+        settled = it >= 1 && dmax < 1e-15;
+    }
+    double Av[9], rq = 0;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+        double t = 0;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) t += a[i][k] * v[k];
+        Av[i] = t;
+        rq += v[i] * t;
+    }
+    double res = 0;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) res = fmax(res, fabs(Av[i] - rq * v[i]));
+    if (!(res <= 1e-9 * tr)) return false;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) x[i] = v[i];
+    return true;
+}
+
 // ------------------------------------------------------------------------------------------------
 // checkSubset (fundam.cpp haveCollinearPoints + the Marquez-Neila orientation test), fp64
 // ------------------------------------------------------------------------------------------------
@@ -2850,9 +2946,27 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                     }
                     block_sum<45>(lt, sh.red);
                     RPROF(2);
-                    if (tid < 16) {  // one 16-lane group
-                        const double invHnorm[9] = {1. / smx, 0, cmx, 0, 1. / smy, cmy, 0, 0, 1};
-                        const double Hnorm2[9] = {sMx, 0, -cMx * sMx, 0, sMy, -cMy * sMy, 0, 0, 1};
+                    const double invHnorm[9] = {1. / smx, 0, cmx, 0, 1. / smy, cmy, 0, 0, 1};
+                    const double Hnorm2[9] = {sMx, 0, -cMx * sMx, 0, sMy, -cMy * sMy, 0, 0, 1};
+                    if (tid == 0) {
+                        // start: bestModel in the normalized coordinates of the refit,
+                        // H0 = Hnorm_dst Hb Hnorm2^-1 (runKernel maps H = invHnorm H0 Hnorm2)
+                        const double Nd[9] = {smx, 0, -cmx * smx, 0, smy, -cmy * smy, 0, 0, 1};
+                        const double N2i[9] = {1. / sMx, 0, cMx, 0, 1. / sMy, cMy, 0, 0, 1};
+                        double T1[9], H0[9], ev[9];
+                        mat3_mul(Nd, sh.Hb, T1);
+                        mat3_mul(T1, N2i, H0);
+                        sh.flag = refit_inverse_iteration(lt, H0, ev) ? 1 : 0;
+                        if (sh.flag) {
+                            double Ht[9], Hn[9];
+                            mat3_mul(invHnorm, ev, Ht);
+                            mat3_mul(Ht, Hnorm2, Hn);
+                            const double sc = 1. / Hn[8];
+                            for (int i = 0; i < 9; ++i) sh.H[i] = Hn[i] * sc;
+                        }
+                    }
+                    __syncthreads();
+                    if (!sh.flag && tid < 16) {  // fallback: the Jacobi of runKernel, one 16-lane group
                         double Hl[9];
                         dlt_finish_group(lt, sh.J9, invHnorm, Hnorm2, Hl);
                         if (tid == 0)
@@ -2953,9 +3067,9 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                 __syncthreads();
                 RPROF(4);
 #ifdef MIM_REFINE_PROF
-                if (tid == 0 && p < 4)
-                    printf("[refine] p=%d recompute %d: best %llu mask %llu sums %llu refitJacobi %llu LM %llu (iters %d chol_fail %d) k=%d\n",
-                           p, rp_recompute, rt[0], rt[1], rt[2], rt[3], rt[4], iter, rp_chol_fail, k);
+                if (tid == 0)
+                    printf("[refine] p=%d recompute %d: best %llu mask %llu sums %llu refit %llu LM %llu (iters %d chol_fail %d) k=%d invit %d\n",
+                           p, rp_recompute, rt[0], rt[1], rt[2], rt[3], rt[4], iter, rp_chol_fail, k, sh.flag);
 #endif
             } else if (tid == 0) {
                 for (int i = 0; i < 9; ++i) sh.H[i] = sh.Hb[i];

@@ -338,10 +338,18 @@ __device__ __forceinline__ unsigned group_bits(unsigned long long m) {
 
 // First maximum of |A(idx, i)| over the slots' candidate indices (slots 9..15 carry the rotated
 // values, in increasing index order) plus, optionally, a zero entry at index `zi` (-1: none).
-__device__ __forceinline__ int refresh_argmax(double val, bool cand, int im, int zi) {
+// The index of the first maximal slot j is recomputed from j (the (j-9)-th index outside {k, l})
+// instead of being fetched from that lane: no LDS round trip.
+__device__ __forceinline__ int refresh_argmax(double val, bool cand, int k, int l, int zi) {
     const double mx = row_max(cand ? val : -1.0);
-    const unsigned m = group_bits(__ballot(cand && val == mx));
-    const int first = m ? __shfl(im, (int)(threadIdx.x & 48) + __builtin_ctz(m), 64) : INT_MAX;
+    const unsigned m = group_bits(__ballot(cand & (val == mx)));
+    int first = INT_MAX;
+    if (m) {
+        int im = __builtin_ctz(m) - 9;
+        im += im >= k;
+        im += im >= l;
+        first = im;
+    }
     if (zi < 0) return first;
     return mx > 0.0 ? first : min(first, zi);
 }
@@ -393,7 +401,8 @@ __device__ __forceinline__ int jacobi9_group(double* __restrict__ A, double* __r
         for (int c = 0; c < 4; ++c) {
             const double po = dpp_row_d(p, c);
             const int poso = dpp_row(pos, c), klo = dpp_row(kl, c);
-            const bool take = fabs(po) > fabs(p) || (fabs(po) == fabs(p) && poso < pos);
+            // bitwise: no short-circuit branches
+            const bool take = (fabs(po) > fabs(p)) | ((fabs(po) == fabs(p)) & (poso < pos));
             p = take ? po : p;
             pos = take ? poso : pos;
             kl = take ? klo : kl;
@@ -434,10 +443,10 @@ __device__ __forceinline__ int jacobi9_group(double* __restrict__ A, double* __r
         // slots, plus A(k,l) = 0; row l: nb, plus A(l,k) = 0) ----
         const bool aslot = !vslot;
         const double va = fabs(na), vb = fabs(nb);
-        const int rk = refresh_argmax(va, aslot && im > k, im, l);
-        const int ck = refresh_argmax(va, aslot && im < k, im, -1);
-        const int rl = refresh_argmax(vb, aslot && im > l, im, -1);
-        const int cl = refresh_argmax(vb, aslot && im < l, im, k);
+        const int rk = refresh_argmax(va, aslot & (im > k), k, l, l);
+        const int ck = refresh_argmax(va, aslot & (im < k), k, l, -1);
+        const int rl = refresh_argmax(vb, aslot & (im > l), k, l, -1);
+        const int cl = refresh_argmax(vb, aslot & (im < l), k, l, k);
         if (slot == k) {
             if (k < n - 1) indR = rk;
             if (k > 0) indC = ck;
@@ -731,10 +740,15 @@ __device__ int update_num_iters(double p, double ep, int model_points, int max_i
 }
 
 // ------------------------------------------------------------------------------------------------
-// RNG::uniform(0, n) = next() % n via Lemire's exact fast modulo (M = 2^64 / n + 1)
+// RNG::uniform(0, n) = next() % n by Barrett reduction with m = M >> 32 = floor(2^32 / n), where
+// M = floor((2^64 - 1) / n) + 1 is the per-problem constant (RansacState::modM), 2 <= n < 2^32:
+// m <= 2^32/n and m >= 2^32/n - 1, so q = mulhi(a, m) is the quotient or one less and a - q n lies
+// in [0, 2n); one unsigned min folds it (two quarter-rate multiplies instead of Lemire's six).
 // ------------------------------------------------------------------------------------------------
 __device__ __forceinline__ unsigned fastmod(unsigned a, unsigned long long M, unsigned d) {
-    return (unsigned)__umul64hi(M * (unsigned long long)a, (unsigned long long)d);
+    const unsigned q = __umulhi(a, (unsigned)(M >> 32));
+    const unsigned r = a - q * d;
+    return min(r, r - d);
 }
 
 // getSubset's draw loop for one attempt starting at stream position q: redraw while an index

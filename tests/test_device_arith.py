@@ -43,3 +43,22 @@ def test_q_times_n_fits_24_bits_above_256():
     # the device uses v_mul_u32_u24 for q*n when n > 256: q < 2^24 and n < 2^24 there
     for n in [257, 2000, 65535, (1 << 24) - 1]:
         assert ((2**32 - 1) // n) < (1 << 24)
+
+
+def fastmod_from_M(a, n):
+    """csrc/ransac.hip fastmod: Barrett with m = M >> 32, M = floor((2^64-1)/n) + 1 (RansacState::modM)."""
+    a = a.astype(np.uint64)
+    M = ((2**64 - 1) // n + 1) % 2**64
+    m = np.uint64(M >> 32)
+    q = (a * m) >> np.uint64(32)
+    r = (a - q * np.uint64(n)) & np.uint64(0xFFFFFFFF)
+    r2 = (r - np.uint64(n)) & np.uint64(0xFFFFFFFF)
+    return np.minimum(r, r2)
+
+
+def test_fastmod_from_lemire_constant():
+    rng = np.random.default_rng(11)
+    for n in [2, 3, 4, 5, 1024, 1999, 2000, 4096, 65536, 65537, 999983, (1 << 31) - 1, 1 << 31, (1 << 32) - 1]:
+        a = np.concatenate([rng.integers(0, 1 << 32, size=200_000, dtype=np.uint64),
+                            np.array([0, 1, n - 1, n, n + 1, (1 << 32) - 1], dtype=np.uint64) % np.uint64(1 << 32)])
+        assert np.array_equal(fastmod_from_M(a, n), a % np.uint64(n)), n

@@ -52,7 +52,8 @@ __device__ __forceinline__ int jacobi9_group_prof(double* __restrict__ A, double
         for (int c = 0; c < 4; ++c) {
             const double po = dpp_row_d(p, c);
             const int poso = dpp_row(pos, c), klo = dpp_row(kl, c);
-            const bool take = fabs(po) > fabs(p) || (fabs(po) == fabs(p) && poso < pos);
+            // bitwise: no short-circuit branches
+            const bool take = (fabs(po) > fabs(p)) | ((fabs(po) == fabs(p)) & (poso < pos));
             p = take ? po : p;
             pos = take ? poso : pos;
             kl = take ? klo : kl;
@@ -97,10 +98,10 @@ __device__ __forceinline__ int jacobi9_group_prof(double* __restrict__ A, double
         // slots, plus A(k,l) = 0; row l: nb, plus A(l,k) = 0) ----
         const bool aslot = !vslot;
         const double va = fabs(na), vb = fabs(nb);
-        const int rk = refresh_argmax(va, aslot && im > k, im, l);
-        const int ck = refresh_argmax(va, aslot && im < k, im, -1);
-        const int rl = refresh_argmax(vb, aslot && im > l, im, -1);
-        const int cl = refresh_argmax(vb, aslot && im < l, im, k);
+        const int rk = refresh_argmax(va, aslot & (im > k), k, l, l);
+        const int ck = refresh_argmax(va, aslot & (im < k), k, l, -1);
+        const int rl = refresh_argmax(vb, aslot & (im > l), k, l, -1);
+        const int cl = refresh_argmax(vb, aslot & (im < l), k, l, k);
         if (slot == k) {
             if (k < n - 1) indR = rk;
             if (k > 0) indC = ck;

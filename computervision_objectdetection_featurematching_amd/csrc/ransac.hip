@@ -870,7 +870,6 @@ __device__ __forceinline__ unsigned mod_barrett(unsigned a, unsigned m, unsigned
 
 constexpr int kAttemptPerThread = 8;  // window positions per thread (11 draws reduced for 8 attempts)
 
-constexpr int kAttemptRounds = 1;     // 2048-position rounds per block
 constexpr int kAttemptExtra = 4;      // redraws resolved from registers (more: resolve_at)
 
 // getSubset's draw loop for the attempt whose first draw is u[j] (ptsetreg.cpp: redraw while the
@@ -894,62 +893,98 @@ __device__ __forceinline__ int redraw_len(const unsigned (&u)[D], int j) {
     return len;
 }
 
+// The block's 2048 + 15 draws are staged through LDS with coalesced 16-byte loads (a lane's own 15
+// draws at a 32-byte lane stride would touch 16 cache lines per load instruction, 15 times over).
+constexpr int kAttemptSpan = 256 * kAttemptPerThread;  // window positions per block
+
 __global__ __launch_bounds__(256) void ransac_attempt_kernel(const RansacState* __restrict__ st,
                                                              const uint32_t* __restrict__ stream, long long slen,
                                                              uint8_t* __restrict__ flags, int wcap, int bpp, int c1) {
+    constexpr int D = kAttemptPerThread + 3 + kAttemptExtra;
+    constexpr int kStageWords = kAttemptSpan + 16;
+    __shared__ __attribute__((aligned(16))) unsigned sdraw[kStageWords];
     const int p = blockIdx.x / bpp;
     const RansacState S = st[p];
     if (!S.active || S.done || S.fail_iter != -1 || S.produced >= min(c1, S.niters)) return;
     const int wlen = window_len(S, c1, wcap);  // a multiple of 64
-    // stream positions fit 32 bits (the stream is capped at 2^28 draws)
-    const int last = (int)slen - 1;
+    const int boff = (blockIdx.x % bpp) * kAttemptSpan;
+    if (boff >= wlen) return;  // uniform over the block
+    // stream positions fit 32 bits (the stream is capped at 2^28 draws; 64 zero draws pad its end)
+    const int qb = (int)S.stream_pos + boff;
+    const int start = qb & ~3, shift = qb - start;
+    const int nvec = ((int)slen + 64) >> 2;  // 16-byte vectors in the padded stream buffer
+    const uint4* __restrict__ sv = reinterpret_cast<const uint4*>(stream);
+    for (int i = threadIdx.x; i * 4 < kStageWords + 4; i += 256) {
+        const uint4 v = sv[min((start >> 2) + i, nvec - 1)];
+        const unsigned vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const int e = 4 * i + c - shift;
+            if (e >= 0 && e < kStageWords) sdraw[e] = vv[c];
+        }
+    }
+    __syncthreads();
+    const int off = boff + threadIdx.x * kAttemptPerThread;
+    if (off >= wlen) return;
+    const int q0 = qb + threadIdx.x * kAttemptPerThread;
     const unsigned N = (unsigned)S.n, mB = 0xFFFFFFFFu / N;
     const bool big = N > 256 && N < (1u << 24);  // q and n both fit 24 bits
-    constexpr int D = kAttemptPerThread + 3 + kAttemptExtra;
-    for (int r = 0; r < kAttemptRounds; ++r) {
-        const int off = (((blockIdx.x % bpp) * kAttemptRounds + r) * 256 + threadIdx.x) * kAttemptPerThread;
-        if (off >= wlen) break;
-        const int q0 = (int)S.stream_pos + off;
-        // unconditional (clamped) loads, all in flight at once; positions whose 4 draws pass the
-        // stream end are flagged for the walker below, so the clamped values are never used
-        unsigned u[D];
+    unsigned u[D];
+    {
+        const uint4* L = reinterpret_cast<const uint4*>(sdraw + threadIdx.x * kAttemptPerThread);
 #pragma unroll
-        for (int k = 0; k < D; ++k) u[k] = stream[min(q0 + k, last)];
-        if (big) {
+        for (int k4 = 0; k4 < (D + 3) / 4; ++k4) {
+            const uint4 v = L[k4];
+            const unsigned vv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-            for (int k = 0; k < D; ++k) u[k] = mod_barrett<true>(u[k], mB, N);
-        } else {
-#pragma unroll
-            for (int k = 0; k < D; ++k) u[k] = mod_barrett<false>(u[k], mB, N);
+            for (int c = 0; c < 4; ++c)
+                if (4 * k4 + c < D) u[4 * k4 + c] = vv[c];
         }
-        // repeated index among the 4 draws of position j: pairs at distance 1, 2, 3, each tested once
-        constexpr int D0 = kAttemptPerThread + 3;
-        bool d1[D0 - 1], d2[D0 - 2], d3[D0 - 3];
-#pragma unroll
-        for (int k = 0; k < D0 - 1; ++k) d1[k] = u[k] == u[k + 1];
-#pragma unroll
-        for (int k = 0; k < D0 - 2; ++k) d2[k] = u[k] == u[k + 2];
-#pragma unroll
-        for (int k = 0; k < D0 - 3; ++k) d3[k] = u[k] == u[k + 3];
-        uint32_t w[2] = {0, 0};
-#pragma unroll
-        for (int j = 0; j < kAttemptPerThread; ++j) {
-            const bool rep = d1[j] | d1[j + 1] | d1[j + 2] | d2[j] | d2[j + 1] | d3[j];
-            int f = kPassUnknown;
-            if (q0 + j + 4 > (int)slen) {
-                f = kAttemptSerial;
-            } else if (rep) {
-                int len = redraw_len(u, j);
-                if (len == 0 || q0 + j + len > (int)slen) {  // long redraw run or near the stream end
-                    int idx[4];
-                    len = resolve_at(q0 + j, stream, slen, N, S.modM, idx);
-                }
-                f = (len == 0 || len > 67) ? kAttemptSerial : (((len - 4) << 1) | kPassUnknown);
-            }
-            w[j >> 2] |= (uint32_t)f << (8 * (j & 3));
-        }
-        *reinterpret_cast<uint2*>(flags + (long long)p * wcap + off) = make_uint2(w[0], w[1]);
     }
+#ifdef MIM_PROBE_ATTEMPT_LOADONLY  // timing probe only (flags invalid): loads + store, no compute
+    {
+        unsigned x = 0;
+#pragma unroll
+        for (int k = 0; k < D; ++k) x ^= u[k];
+        const unsigned f = x == 0x12345678u ? 0x82808080u : 0x80808080u;  // keeps the loads alive
+        *reinterpret_cast<uint2*>(flags + (long long)p * wcap + off) = make_uint2(f, f);
+        return;
+    }
+#endif
+    if (big) {
+#pragma unroll
+        for (int k = 0; k < D; ++k) u[k] = mod_barrett<true>(u[k], mB, N);
+    } else {
+#pragma unroll
+        for (int k = 0; k < D; ++k) u[k] = mod_barrett<false>(u[k], mB, N);
+    }
+    // repeated index among the 4 draws of position j: pairs at distance 1, 2, 3, each tested once
+    constexpr int D0 = kAttemptPerThread + 3;
+    bool d1[D0 - 1], d2[D0 - 2], d3[D0 - 3];
+#pragma unroll
+    for (int k = 0; k < D0 - 1; ++k) d1[k] = u[k] == u[k + 1];
+#pragma unroll
+    for (int k = 0; k < D0 - 2; ++k) d2[k] = u[k] == u[k + 2];
+#pragma unroll
+    for (int k = 0; k < D0 - 3; ++k) d3[k] = u[k] == u[k + 3];
+    uint32_t w[2] = {0, 0};
+#pragma unroll
+    for (int j = 0; j < kAttemptPerThread; ++j) {
+        const bool rep = d1[j] | d1[j + 1] | d1[j + 2] | d2[j] | d2[j + 1] | d3[j];
+        int f = kPassUnknown;
+        if (q0 + j + 4 > (int)slen) {
+            f = kAttemptSerial;
+        } else if (rep) {
+            int len = redraw_len(u, j);
+            if (len == 0 || q0 + j + len > (int)slen) {  // long redraw run or near the stream end
+                int idx[4];
+                len = resolve_at(q0 + j, stream, slen, N, S.modM, idx);
+            }
+            f = (len == 0 || len > 67) ? kAttemptSerial : (((len - 4) << 1) | kPassUnknown);
+        }
+        w[j >> 2] |= (uint32_t)f << (8 * (j & 3));
+    }
+    *reinterpret_cast<uint2*>(flags + (long long)p * wcap + off) = make_uint2(w[0], w[1]);
 }
 
 __device__ __forceinline__ int wave_excl_prefix_sum(int v) {
@@ -1265,6 +1300,11 @@ __device__ __forceinline__ int chain_seg(const ChainSegs* G, int t) {
 
 // ---- check: checkSubset of every attempt on the walked chain (one thread per attempt) ----
 
+// Each thread checks kCheckPer attempts (block-strided, so every round is one ballot word pair per
+// wave): their stream draws and point gathers are all in flight at once.
+constexpr int kCheckPer = 4;
+constexpr int kCheckSegs = 8;  // segments preloaded per block (a block spans ~4 on average)
+
 __global__ __launch_bounds__(kCheckBlock) void ransac_check_kernel(const ChainSegs* __restrict__ chains,
                                                                    const ProbDev* __restrict__ probs,
                                                                    const float4* __restrict__ pts,
@@ -1274,56 +1314,88 @@ __global__ __launch_bounds__(kCheckBlock) void ransac_check_kernel(const ChainSe
     const int p = blockIdx.x / bpp, lane = threadIdx.x & 63;
     const ChainSegs* G = chains + p;
     const int T = G->T;
-    const int t = (blockIdx.x % bpp) * kCheckBlock + threadIdx.x;
-    if ((blockIdx.x % bpp) * kCheckBlock >= T) return;  // T < 0: nothing this chunk
-    const RansacState S = st[p];
     const int b = blockIdx.x % bpp;
-    // segment data of the block's first 4 segments in one round of (uniform, scalar) loads
+    const int base = b * kCheckBlock * kCheckPer;
+    if (base >= T) return;  // T < 0: nothing this chunk
+    const RansacState S = st[p];
+    // segment data of the block's first kCheckSegs segments in one round of (uniform, scalar) loads
     const int nseg = G->nseg;
-    const int j0 = b < kChainBlk ? G->blk_seg[b] : chain_seg(G, b * kCheckBlock);
-    int segA[5], segS[4], segQ[4];
+    const int bb = base / kCheckBlock;
+    const int j0 = bb < kChainBlk ? G->blk_seg[bb] : chain_seg(G, base);
+    int segA[kCheckSegs + 1], segS[kCheckSegs], segQ[kCheckSegs];
 #pragma unroll
-    for (int k = 0; k < 5; ++k) segA[k] = G->A[min(j0 + k, nseg + 1)];
+    for (int k = 0; k <= kCheckSegs; ++k) segA[k] = G->A[min(j0 + k, nseg + 1)];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < kCheckSegs; ++k) {
         segS[k] = G->seg_s[min(j0 + k, nseg)];
         segQ[k] = G->seg_q[min(j0 + k, max(nseg - 1, 0))];
     }
-    bool pass = false;
-    if (t < T) {
+    const unsigned N = (unsigned)S.n;
+    int q[kCheckPer];
+    bool irr[kCheckPer], valid[kCheckPer];
+#pragma unroll
+    for (int r = 0; r < kCheckPer; ++r) {
+        const int t = base + r * kCheckBlock + threadIdx.x;
+        valid[r] = t < T;
         int k = 0;
 #pragma unroll
-        for (int i = 1; i < 4; ++i) k += (j0 + i <= nseg) && t >= segA[i];
-        int j = j0 + k;
+        for (int i = 1; i < kCheckSegs; ++i) k += (j0 + i <= nseg) && t >= segA[i];
+        int j = j0 + k, pos;
         bool irregular;
-        int pos;
-        if (j < nseg && t >= segA[k + 1]) {  // a block spanning more than 4 segments (rare)
+        if (j < nseg && t >= segA[k + 1]) {  // past the preloaded segments (rare)
             while (j < nseg && t >= G->A[j + 1]) ++j;
             pos = chain_pos(G, j, t, irregular);
         } else {
             irregular = j < nseg && t == segA[k + 1] - 1;
             pos = irregular ? segQ[k] : segS[k] + 4 * (t - segA[k]);
         }
-        const long long q = G->wbase + pos;
-        const unsigned N = (unsigned)S.n;
-        int idx[4];
-        if (!irregular) {
-#pragma unroll
-            for (int k = 0; k < 4; ++k) idx[k] = (int)fastmod(stream[q + k], S.modM, N);
-        } else {
-            resolve_at(q, stream, slen, N, S.modM, idx);  // the walk only listed resolvable ones
-        }
-        const float4* P = pts + probs[p].good_off;
-        const float4 a = P[idx[0]], b = P[idx[1]], c = P[idx[2]], d = P[idx[3]];
-        const float s4[8] = {a.x, a.y, b.x, b.y, c.x, c.y, d.x, d.y};
-        const float t4[8] = {a.z, a.w, b.z, b.w, c.z, c.w, d.z, d.w};
-        pass = check_subset(s4, t4);
+        q[r] = valid[r] ? (int)(G->wbase + pos) : 0;
+        irr[r] = valid[r] && irregular;
     }
-    const unsigned long long m = __ballot(pass);
+    // all regular draws first (one 16-byte load per attempt: consecutive chain attempts are 4 draws
+    // apart, so a wave reads 1 KiB contiguously; dword-aligned vector loads), then the reductions
+    typedef uint4 __attribute__((aligned(4))) uint4a4;
+    unsigned raw[kCheckPer][4];
+#pragma unroll
+    for (int r = 0; r < kCheckPer; ++r) {
+        const uint4 v = *reinterpret_cast<const uint4a4*>(stream + q[r]);
+        raw[r][0] = v.x; raw[r][1] = v.y; raw[r][2] = v.z; raw[r][3] = v.w;
+    }
+    int idx[kCheckPer][4];
+#pragma unroll
+    for (int r = 0; r < kCheckPer; ++r) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) idx[r][k] = valid[r] ? (int)fastmod(raw[r][k], S.modM, N) : 0;
+        if (irr[r]) resolve_at(q[r], stream, slen, N, S.modM, idx[r]);  // the walk only listed resolvable ones
+    }
+    const float4* P = pts + probs[p].good_off;
+    float4 g[kCheckPer][4];
+#pragma unroll
+    for (int r = 0; r < kCheckPer; ++r)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+#ifdef MIM_PROBE_CHECK_NOGATHER  // timing probe only (pass bits invalid): no point gathers
+            const float f = (float)idx[r][k];
+            g[r][k] = make_float4(f, f * 0.5f, f * 0.25f, f * 0.125f + (float)k);
+#else
+            g[r][k] = P[idx[r][k]];
+#endif
+        }
     uint32_t* PB = pass_bits + (long long)p * (wcap / 32);
-    const int w0 = ((blockIdx.x % bpp) * kCheckBlock + (threadIdx.x & ~63)) >> 5;  // 2 words per wave
-    if (lane == 0 && w0 * 32 < T) PB[w0] = (uint32_t)m;
-    if (lane == 32 && (w0 + 1) * 32 < T) PB[w0 + 1] = (uint32_t)(m >> 32);
+#pragma unroll
+    for (int r = 0; r < kCheckPer; ++r) {
+        const float s4[8] = {g[r][0].x, g[r][0].y, g[r][1].x, g[r][1].y, g[r][2].x, g[r][2].y, g[r][3].x, g[r][3].y};
+        const float t4[8] = {g[r][0].z, g[r][0].w, g[r][1].z, g[r][1].w, g[r][2].z, g[r][2].w, g[r][3].z, g[r][3].w};
+#ifdef MIM_PROBE_CHECK_NOSUBSET  // timing probe only: gathers kept, checkSubset replaced
+        const bool pass = valid[r] && (s4[0] + s4[3] + t4[5] + t4[6] > 100.f);
+#else
+        const bool pass = valid[r] && check_subset(s4, t4);
+#endif
+        const unsigned long long m = __ballot(pass);
+        const int w0 = (base + r * kCheckBlock + (threadIdx.x & ~63)) >> 5;  // 2 words per wave
+        if (lane == 0 && w0 * 32 < T) PB[w0] = (uint32_t)m;
+        if (lane == 32 && (w0 + 1) * 32 < T) PB[w0 + 1] = (uint32_t)(m >> 32);
+    }
 }
 
 // ---- count: ranks of the passing attempts, getSubset's failure rule, samples, state ----
@@ -3140,7 +3212,7 @@ void ransac_enqueue(const RansacParams& prm, int n_probs, const ProbDev* probs, 
         // falls back to inline evaluation past the window
         // (a multiple of 64: flags are read as 16-byte vectors, pass bits as 32-bit words)
         const int wcap = (int)(std::min<long long>((long long)(c1 - c0) * 28 + 4096, b.flag_cap / std::max(n_probs, 1)) & ~63LL);
-        const int bppw = (wcap + 256 * kAttemptPerThread * kAttemptRounds - 1) / (256 * kAttemptPerThread * kAttemptRounds);
+        const int bppw = (wcap + kAttemptSpan - 1) / kAttemptSpan;
         ransac_attempt_kernel<<<n_probs * bppw, 256, 0, s>>>(b.state, b.stream, b.stream_len, b.flags, wcap, bppw, c1);
         mark(mark_ctx, "attempt");
         if (use_chain) {
@@ -3151,7 +3223,7 @@ void ransac_enqueue(const RansacParams& prm, int n_probs, const ProbDev* probs, 
             ransac_walk_kernel<<<n_probs, kChainThreads, 0, s>>>(b.state, b.flags, wcap, c1, b.irr, b.irr_cnt,
                                                                  b.irr_blocks, chains);
             mark(mark_ctx, "chain");
-            const int bpp_chk = (wcap / 4 + kCheckBlock) / kCheckBlock;  // T <= wlen / 4 + 1
+            const int bpp_chk = (wcap / 4 + kCheckBlock * kCheckPer) / (kCheckBlock * kCheckPer);  // T <= wlen / 4 + 1
             ransac_check_kernel<<<n_probs * bpp_chk, kCheckBlock, 0, s>>>(chains, probs, pts, b.state, b.stream,
                                                                           b.stream_len, b.pass_bits, wcap, bpp_chk);
             mark(mark_ctx, "check");

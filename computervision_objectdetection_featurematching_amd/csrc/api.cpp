@@ -193,6 +193,7 @@ struct mim_ctx {
     };
     int ev_seq = 0;
     std::vector<Ev> evs;
+    std::vector<hipEvent_t> ev_pool;  // recycled events (creating one per mark costs host time)
     std::map<std::string, double> last_ms;
 };
 
@@ -255,6 +256,7 @@ void mim_ctx_destroy(mim_ctx* c) {
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
     for (auto& e : c->evs) (void)hipEventDestroy(e.e);
+    for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
     for (int g = 0; g < mim_ctx::kMaxGroups; ++g) {
         if (c->sub[g]) (void)hipStreamDestroy(c->sub[g]);
         if (c->ev_knn[g]) (void)hipEventDestroy(c->ev_knn[g]);
@@ -489,7 +491,12 @@ static mim_status build_tables(mim_ctx* c, const mim_problem* problems, int n, i
 static void ev_mark(mim_ctx* c, const char* name) {
     if (!c->timing) return;
     hipEvent_t e;
-    if (hipEventCreate(&e) != hipSuccess) return;
+    if (!c->ev_pool.empty()) {
+        e = c->ev_pool.back();
+        c->ev_pool.pop_back();
+    } else if (hipEventCreate(&e) != hipSuccess) {
+        return;
+    }
     (void)hipEventRecord(e, c->cur);
     if (!strcmp(name, "begin")) ++c->ev_seq;
     c->evs.push_back({name, c->cur, e, c->ev_seq});
@@ -510,7 +517,7 @@ static void ev_collect(mim_ctx* c) {
         }
         prev[e.s] = &e;
     }
-    for (auto& e : c->evs) (void)hipEventDestroy(e.e);
+    for (auto& e : c->evs) c->ev_pool.push_back(e.e);
     c->evs.clear();
 }
 

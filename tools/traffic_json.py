@@ -3,7 +3,7 @@
 usage: python3 tools/traffic_json.py gpurun_out/prof_round profiles/r01_pmc_traffic.json
 Reads pmc_FETCH_SIZE/ and pmc_WRITE_SIZE/ (separate passes of `bench.py --steps 1 --warmup 0`),
 doubles FETCH_SIZE (gfx950 tallies 128-B requests at 64 B: MI355X_MICROARCH.md, HBM section) and sums
-the launches of one step per kernel family ("ransac_bound" = first-chunk VALU kernel + MFMA kernel).
+the launches of one step per kernel family ("ransac_bound" = the MFMA bound kernel of both chunks).
 """
 import collections
 import csv
@@ -12,8 +12,8 @@ import json
 import sys
 
 src, dst = sys.argv[1], sys.argv[2]
-FAMILY = {"knn2_i8_kernel": "knn2_i8_kernel", "ransac_bound_kernel": "ransac_bound",
-          "ransac_bound_mfma_kernel": "ransac_bound"}
+FAMILY = {"knn2_i8_kernel": "knn2_i8_kernel", "ransac_bound_mfma_kernel": "ransac_bound",
+          "ransac_attempt_kernel": "ransac_attempt", "ransac_check_kernel": "ransac_check"}
 per = collections.defaultdict(lambda: {"fetch_size_per_launch": [], "write_size_per_launch": []})
 for counter, key, scale in (("FETCH_SIZE", "fetch_size_per_launch", 2), ("WRITE_SIZE", "write_size_per_launch", 1)):
     for f in sorted(glob.glob(f"{src}/pmc_{counter}/**/*counter_collection.csv", recursive=True)):

@@ -416,8 +416,11 @@ static mim_status build_tables(mim_ctx* c, const mim_problem* problems, int n, i
             return fail(c, MIM_EINVAL, "problem %d: bad set id (%d, %d)", i, qs, ts);
         total_qblocks += (c->sets[qs].d.n + kKnnBlockQ - 1) / kKnnBlockQ;
     }
-    // split the train side until the grid has ~2 blocks per CU
-    const int target = 512;
+    // split the train side until the grid has ~2 blocks per CU (MIM_KNN_TARGET: blocks wanted)
+    static const int target = [] {
+        const char* e = getenv("MIM_KNN_TARGET");
+        return e ? std::max(1, atoi(e)) : 512;
+    }();
     std::vector<std::vector<KnnWork>> per_prob(n);
     for (int i = 0; i < n; ++i) {
         ProbDev& P = c->h_probs[i];

@@ -108,6 +108,8 @@ def main():
     torch.cuda.synchronize()
 
     nf = max(1, args.inflight)
+    if nf > 1:  # the sampler stream helps one batch alone (+5 %), not batches already overlapping
+        os.environ.setdefault("MIM_SAMPLER_STREAM", "0")
     matchers = [Matcher(local) for _ in range(nf)]
     # each context keeps its own non-blocking HIP stream; torch work of a step (the result gather)
     # is ordered on the same stream

@@ -30,7 +30,7 @@ void launch_ratio(const ProbDev* probs, int n_probs, const Top2* parts, float ra
 size_t ransac_chain_bytes();
 void ransac_enqueue(const RansacParams& prm, int n_probs, const ProbDev* probs, const float4* pts,
                     const int* n_good, const RansacBufs& b, uint8_t* masks, mim_result* results, int raw,
-                    hipStream_t s, void (*mark)(void*, const char*), void* mark_ctx, int exact_all);
+                    hipStream_t s, void (*mark)(void*, const char*, hipStream_t), void* mark_ctx, int exact_all);
 }  // namespace mim
 
 using namespace mim;
@@ -183,6 +183,11 @@ struct mim_ctx {
     int n_groups = 1;
     int grp_p0[kMaxGroups + 1] = {}, grp_w0[kMaxGroups + 1] = {};
     hipStream_t cur = nullptr;  // stream the enqueue helpers launch on
+    // sampler stream (RansacBufs::s2): the next chunk's getSubset replay beside this chunk's
+    // selection kernels (MIM_SAMPLER_STREAM=0: one stream)
+    hipStream_t samp = nullptr;
+    hipEvent_t ev_samp_fork = nullptr, ev_samp[2] = {nullptr, nullptr};
+    int samp_on = -1;
     // timing: events per stream, durations summed per kernel name over the streams
     bool timing = false;
     struct Ev {
@@ -263,6 +268,11 @@ void mim_ctx_destroy(mim_ctx* c) {
         if (c->ev_join[g]) (void)hipEventDestroy(c->ev_join[g]);
     }
     if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+    if (c->samp) (void)hipStreamSynchronize(c->samp);
+    if (c->ev_samp_fork) (void)hipEventDestroy(c->ev_samp_fork);
+    for (auto e : c->ev_samp)
+        if (e) (void)hipEventDestroy(e);
+    if (c->samp) (void)hipStreamDestroy(c->samp);
     c->stage.destroy();
     c->prep_stage.destroy();
     c->arena.release();
@@ -656,7 +666,13 @@ mim_status mim_knn2_sets_dev(mim_ctx* c, int32_t query_set, int32_t train_set, i
 // ---------------------------------------------------------------------------------------------
 // RANSAC: RNG stream, workspace, batch entry points
 // ---------------------------------------------------------------------------------------------
-static void mark_cb(void* vc, const char* name) { ev_mark((mim_ctx*)vc, name); }
+static void mark_cb(void* vc, const char* name, hipStream_t st) {
+    mim_ctx* c = (mim_ctx*)vc;
+    const hipStream_t keep = c->cur;
+    c->cur = st;
+    ev_mark(c, name);
+    c->cur = keep;
+}
 
 // cv::RNG((uint64)-1).next() stream (core/include/opencv2/core/operations.hpp). Every
 // findHomography call re-seeds, so one stream serves all problems; generated once per ctx.
@@ -741,6 +757,19 @@ static mim_status ransac_prepare(mim_ctx* c, int n, const mim_params* prm, Ransa
     b.inl = c->rws.inl.as<float4>();
     b.tiles = c->rws.tiles.as<uint4>();
     b.err = c->rws.err.as<int>();
+    if (c->samp_on < 0) {
+        const char* e = getenv("MIM_SAMPLER_STREAM");
+        c->samp_on = (e && e[0] == '0') ? 0 : 1;
+    }
+    if (c->samp_on && !c->samp) {
+        HIPCHK(c, hipStreamCreateWithFlags(&c->samp, hipStreamNonBlocking));
+        HIPCHK(c, hipEventCreateWithFlags(&c->ev_samp_fork, hipEventDisableTiming));
+        for (auto& e : c->ev_samp) HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+    b.s2 = c->samp_on ? c->samp : nullptr;
+    b.ev_fork = c->ev_samp_fork;
+    b.ev_samp[0] = c->ev_samp[0];
+    b.ev_samp[1] = c->ev_samp[1];
     rp = RansacParams{};
     rp.thresh = prm->ransac_thresh > 0 ? prm->ransac_thresh : 3.0;  // findHomography: thresh <= 0 -> 3
     rp.conf = prm->confidence;
@@ -758,6 +787,7 @@ static mim_status ransac_prepare(mim_ctx* c, int n, const mim_params* prm, Ransa
 static mim_status ransac_enqueue_range(mim_ctx* c, int p0, int np, const RansacBufs& b, const RansacParams& rp,
                                        long long flag_per, int raw) {
     RansacBufs g = b;
+    if (c->n_groups > 1) g.s2 = nullptr;  // pipelined groups: one stream per group
     g.state += p0;
     g.flags += (long long)p0 * flag_per;
     g.flag_cap = (long long)np * flag_per;

@@ -131,5 +131,10 @@ struct RansacBufs {
     float4* inl;              // [good_off + k] compressed inliers for the refit (scratch)
     uint4* tiles;             // [good_off / 32 + tile][2][64] f16 MFMA operand tiles of the points
     int* err;                 // device error word (bit0: RNG stream exhausted)
+    // Sampler stream: the getSubset replay of chunk c+1 runs on s2 concurrently with the bound /
+    // candidate / exact / replay kernels of chunk c (null: everything on the caller's stream)
+    hipStream_t s2;
+    hipEvent_t ev_fork;
+    hipEvent_t ev_samp[2];
 };
 }  // namespace mim

@@ -797,6 +797,26 @@ __device__ __forceinline__ int4 decode_sample(int4 s, const uint32_t* __restrict
     return make_int4(idx[0], idx[1], idx[2], idx[3]);
 }
 
+// The sampler kernels (count, sample) and the selection kernels (replay) may run concurrently on
+// two streams (the next chunk's getSubset replay beside this chunk's selection): each stores only
+// the fields it owns.  Reads of the other group's fields may see either value; see DESIGN.md
+// "Sampler stream" for why every outcome is the same.
+__device__ __forceinline__ void store_sampler_state(RansacState* d, const RansacState& S) {
+    d->stream_pos = S.stream_pos;
+    d->produced = S.produced;
+    d->fail_iter = S.fail_iter;
+    d->fail_run = S.fail_run;
+    d->win_base = S.win_base;
+    d->win_len = S.win_len;
+}
+__device__ __forceinline__ void store_select_state(RansacState* d, const RansacState& S) {
+    d->max_good = S.max_good;
+    d->best_iter = S.best_iter;
+    d->niters = S.niters;
+    d->next_iter = S.next_iter;
+    d->done = S.done;
+}
+
 // ------------------------------------------------------------------------------------------------
 // init: per-problem RANSAC state from the ratio-test survivors
 // ------------------------------------------------------------------------------------------------
@@ -1528,7 +1548,7 @@ __global__ __launch_bounds__(kChainThreads) void ransac_count_kernel(RansacState
             S.fail_run = total > 0 ? T - 1 - last_all : S.fail_run + T;
             S.stream_pos = wbase + G->s_end;
         }
-        st[p] = S;
+        store_sampler_state(st + p, S);
     }
 }
 
@@ -1743,7 +1763,7 @@ __global__ __launch_bounds__(64) void ransac_sample_kernel(RansacState* __restri
         S.stream_pos = wbase + rel;
         S.produced = produced;
         S.fail_run = fail_run;
-        st[p] = S;
+        store_sampler_state(st + p, S);
     }
 }
 
@@ -2512,9 +2532,12 @@ __global__ __launch_bounds__(64) void ransac_replay_kernel(RansacState* __restri
         }
     }
     S.next_iter = end;
-    const bool failed = S.fail_iter != -1 && S.produced <= end;
+    // getSubset failed at iteration fail_iter (or the stream ran out: -2) within this chunk's range;
+    // a failure the concurrent sampler finds in the next chunk has fail_iter >= end or is not yet
+    // visible, and only stops the loop where OpenCV stops it too
+    const bool failed = S.fail_iter != -1 && S.fail_iter <= end;
     if (S.niters <= end || failed) S.done = 1;
-    if (lane == 0) st[p] = S;
+    if (lane == 0) store_select_state(st + p, S);
 }
 
 __global__ __launch_bounds__(64) void ransac_select_filtered_kernel(RansacState* __restrict__ st,
@@ -3195,7 +3218,7 @@ size_t ransac_chain_bytes() { return sizeof(ChainSegs); }
 
 void ransac_enqueue(const RansacParams& prm, int n_probs, const ProbDev* probs, const float4* pts,
                     const int* n_good, const RansacBufs& b, uint8_t* masks, mim_result* results, int raw,
-                    hipStream_t s, void (*mark)(void*, const char*), void* mark_ctx, int exact_all) {
+                    hipStream_t s, void (*mark)(void*, const char*, hipStream_t), void* mark_ctx, int exact_all) {
     if (n_probs <= 0) return;
     ransac_init_kernel<<<(n_probs + 255) / 256, 256, 0, s>>>(b.state, n_good, n_probs, prm.max_iters, prm.min_good,
                                                              b.best_h);
@@ -3206,6 +3229,15 @@ void ransac_enqueue(const RansacParams& prm, int n_probs, const ProbDev* probs, 
     int c0 = 0, chunk = 4096;
     const float thr2 = (float)(prm.thresh * prm.thresh);
     if (!exact_all) ransac_tiles_kernel<<<n_probs, 256, 0, s>>>(b.state, probs, pts, b.tiles);
+    // the getSubset replay on the sampler stream when there is one (not in the reference mode)
+    const bool split = b.s2 && !exact_all;
+    hipStream_t ss = split ? b.s2 : s;
+    if (split) {
+        (void)hipEventRecord(b.ev_fork, s);
+        (void)hipStreamWaitEvent(ss, b.ev_fork, 0);
+        mark(mark_ctx, "fork", ss);
+    }
+    int ci = 0;
     while (c0 < max_iters) {
         const int c1 = (int)std::min<long long>((long long)c0 + chunk, max_iters);
         // attempt outcomes for a window of ~28 draws per wanted iteration (pass rate ~1/5), the walk
@@ -3213,38 +3245,44 @@ void ransac_enqueue(const RansacParams& prm, int n_probs, const ProbDev* probs, 
         // (a multiple of 64: flags are read as 16-byte vectors, pass bits as 32-bit words)
         const int wcap = (int)(std::min<long long>((long long)(c1 - c0) * 28 + 4096, b.flag_cap / std::max(n_probs, 1)) & ~63LL);
         const int bppw = (wcap + kAttemptSpan - 1) / kAttemptSpan;
-        ransac_attempt_kernel<<<n_probs * bppw, 256, 0, s>>>(b.state, b.stream, b.stream_len, b.flags, wcap, bppw, c1);
-        mark(mark_ctx, "attempt");
+        ransac_attempt_kernel<<<n_probs * bppw, 256, 0, ss>>>(b.state, b.stream, b.stream_len, b.flags, wcap, bppw, c1);
+        mark(mark_ctx, "attempt", ss);
         if (use_chain) {
             ChainSegs* chains = reinterpret_cast<ChainSegs*>(b.chains);
             const int bpp_irr = (wcap + kIrrBlock - 1) / kIrrBlock;
-            ransac_irr_kernel<<<n_probs * bpp_irr, 256, 0, s>>>(b.state, b.flags, wcap, bpp_irr, c1, b.irr,
+            ransac_irr_kernel<<<n_probs * bpp_irr, 256, 0, ss>>>(b.state, b.flags, wcap, bpp_irr, c1, b.irr,
                                                                b.irr_cnt, b.irr_blocks);
-            ransac_walk_kernel<<<n_probs, kChainThreads, 0, s>>>(b.state, b.flags, wcap, c1, b.irr, b.irr_cnt,
+            ransac_walk_kernel<<<n_probs, kChainThreads, 0, ss>>>(b.state, b.flags, wcap, c1, b.irr, b.irr_cnt,
                                                                  b.irr_blocks, chains);
-            mark(mark_ctx, "chain");
+            mark(mark_ctx, "chain", ss);
             const int bpp_chk = (wcap / 4 + kCheckBlock * kCheckPer) / (kCheckBlock * kCheckPer);  // T <= wlen / 4 + 1
-            ransac_check_kernel<<<n_probs * bpp_chk, kCheckBlock, 0, s>>>(chains, probs, pts, b.state, b.stream,
+            ransac_check_kernel<<<n_probs * bpp_chk, kCheckBlock, 0, ss>>>(chains, probs, pts, b.state, b.stream,
                                                                           b.stream_len, b.pass_bits, wcap, bpp_chk);
-            mark(mark_ctx, "check");
-            ransac_count_kernel<<<n_probs, kChainThreads, 0, s>>>(b.state, probs, chains, b.pass_bits, b.flags, wcap,
+            mark(mark_ctx, "check", ss);
+            ransac_count_kernel<<<n_probs, kChainThreads, 0, ss>>>(b.state, probs, chains, b.pass_bits, b.flags, wcap,
                                                                   b.samples, c1);
-            mark(mark_ctx, "chain");
+            mark(mark_ctx, "chain", ss);
         }
-        ransac_sample_kernel<<<n_probs, 64, 0, s>>>(b.state, probs, pts, b.stream, b.stream_len, b.samples, c1, b.err,
+        ransac_sample_kernel<<<n_probs, 64, 0, ss>>>(b.state, probs, pts, b.stream, b.stream_len, b.samples, c1, b.err,
                                                     b.flags, wcap, use_chain);
-        mark(mark_ctx, "sample");
+        mark(mark_ctx, "sample", ss);
+        if (split) {  // this chunk's selection waits for its samples; the next chunk's sampler does not
+            (void)hipEventRecord(b.ev_samp[ci & 1], ss);
+            (void)hipStreamWaitEvent(s, b.ev_samp[ci & 1], 0);
+            mark(mark_ctx, "join", s);  // span origin of the selection kernels after the wait
+        }
+        ++ci;
         const int bpp256 = (c1 - c0 + 255) / 256;
         if (exact_all) {  // reference mode: every hypothesis through runKernel + computeError
             const int bpp64 = (c1 - c0 + 63) / 64;
             ransac_hypo_kernel<<<n_probs * bpp64, 64, 0, s>>>(b.state, probs, pts, b.samples, b.stream, b.hyp, b.counts, c0, c1,
                                                              bpp64);
-            mark(mark_ctx, "hypo");
+            mark(mark_ctx, "hypo", s);
             ransac_score_kernel<<<n_probs * bpp256, 256, 0, s>>>(b.state, probs, pts, b.hyp, b.counts, c0, c1,
                                                                 bpp256, thr2);
-            mark(mark_ctx, "score");
+            mark(mark_ctx, "score", s);
             ransac_select_kernel<<<n_probs, 64, 0, s>>>(b.state, probs, b.counts, c1, prm.conf);
-            mark(mark_ctx, "select");
+            mark(mark_ctx, "select", s);
         } else {
             if (c0 == 0)
                 ransac_bound_mfma_kernel<true><<<n_probs * bpp256, 256, 0, s>>>(b.state, probs, pts, b.samples, b.stream,
@@ -3252,7 +3290,7 @@ void ransac_enqueue(const RansacParams& prm, int n_probs, const ProbDev* probs, 
             else
                 ransac_bound_mfma_kernel<false><<<n_probs * bpp256, 256, 0, s>>>(b.state, probs, pts, b.samples, b.stream,
                                                                                  b.tiles, b.bounds, c0, c1, bpp256, thr2);
-            mark(mark_ctx, "score");
+            mark(mark_ctx, "score", s);
             if (getenv("MIM_CHECK_BOUNDS")) {  // debug: every bracket against the exact count
                 unsigned long long* dst = nullptr;
                 unsigned long long h[6] = {0, 0, 0, 0, 0, 0};
@@ -3269,7 +3307,7 @@ void ransac_enqueue(const RansacParams& prm, int n_probs, const ProbDev* probs, 
                         "mean_width %.2f tight %llu\n", c0, c1, h[0], h[1], h[2], h[3], h[0] ? (double)h[4] / h[0] : 0.0, h[5]);
             }
             ransac_cand_kernel<<<n_probs, kCandThreads, 0, s>>>(b.state, probs, b.bounds, c1, b.cand, b.ncand);
-            mark(mark_ctx, "cand");
+            mark(mark_ctx, "cand", s);
             if (getenv("MIM_DEBUG_NCAND")) {
                 std::vector<int> h(n_probs);
                 (void)hipMemcpyAsync(h.data(), b.ncand, sizeof(int) * n_probs, hipMemcpyDeviceToHost, s);
@@ -3280,17 +3318,17 @@ void ransac_enqueue(const RansacParams& prm, int n_probs, const ProbDev* probs, 
             }
             ransac_exact_kernel<<<n_probs * kExactWaves, 64, 0, s>>>(b.state, probs, pts, b.samples, b.stream, b.cand,
                                                                    b.ncand, b.bounds, b.cex, b.cH, thr2);
-            mark(mark_ctx, "exact");
+            mark(mark_ctx, "exact", s);
             ransac_replay_kernel<<<n_probs, 64, 0, s>>>(b.state, probs, pts, b.samples, b.stream, b.bounds, b.cand,
                                                         b.ncand, b.cex, b.cH, c1, prm.conf, thr2, b.best_h);
-            mark(mark_ctx, "select");
+            mark(mark_ctx, "select", s);
         }
         c0 = c1;
         chunk = 1 << 30;  // one chunk after the first: every chunk costs a latency-bound exact pass
     }
     ransac_refine_kernel<<<n_probs, kRT, 0, s>>>(b.state, probs, pts, n_good, b.samples, b.stream, b.inl, masks, results, prm,
                                                  raw, b.best_h, exact_all);
-    mark(mark_ctx, "refine");
+    mark(mark_ctx, "refine", s);
 }
 
 }  // namespace mim

@@ -2387,7 +2387,11 @@ __global__ __launch_bounds__(kCandThreads) void ransac_cand_kernel(RansacState* 
 // Exact evaluation of the listed candidates: 4 per wave, each solved by a 16-lane group
 // (cooperative Jacobi), then counted by the whole wave.
 constexpr int kExactGroups = 4;
+#ifdef MIM_PROBE_EXACT_WAVES  // timing probe only (drops candidates past 4 x this per problem)
+constexpr int kExactWaves = MIM_PROBE_EXACT_WAVES;
+#else
 constexpr int kExactWaves = kCandCap / kExactGroups;
+#endif
 
 __global__ __launch_bounds__(64) void ransac_exact_kernel(const RansacState* __restrict__ st,
                                                           const ProbDev* __restrict__ probs,

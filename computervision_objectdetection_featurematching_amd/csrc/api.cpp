@@ -723,9 +723,10 @@ static mim_status ransac_prepare(mim_ctx* c, int n, const mim_params* prm, Ransa
     HIPCHK(c, c->rws.pass_bits.ensure((size_t)flag_cap / 8));
     HIPCHK(c, c->rws.chains.ensure(ransac_chain_bytes() * (size_t)std::max(n, 1)));
     HIPCHK(c, c->rws.best_h.ensure(sizeof(double) * 9 * std::max(n, 1)));
-    const size_t cap = (size_t)std::max(n, 1) * kCandPerProblem;
+    // two candidate lists per problem: chunk 1's (kept when its exact pass is deferred) and chunk 2's
+    const size_t cap = (size_t)std::max(n, 1) * 2 * kCandPerProblem;
     HIPCHK(c, c->rws.cand.ensure(sizeof(int) * cap));
-    HIPCHK(c, c->rws.ncand.ensure(sizeof(int) * std::max(n, 1)));
+    HIPCHK(c, c->rws.ncand.ensure(sizeof(int) * 2 * std::max(n, 1)));
     HIPCHK(c, c->rws.cex.ensure(sizeof(int) * cap));
     HIPCHK(c, c->rws.cH.ensure(sizeof(double) * 9 * cap));
     HIPCHK(c, c->rws.inl.ensure(sizeof(float4) * good_total));
@@ -796,10 +797,10 @@ static mim_status ransac_enqueue_range(mim_ctx* c, int p0, int np, const RansacB
     g.pass_bits += (long long)p0 * flag_per / 32;
     g.chains = static_cast<char*>(b.chains) + (size_t)p0 * ransac_chain_bytes();
     g.best_h += 9LL * p0;
-    g.cand += (long long)p0 * kCandPerProblem;
-    g.ncand += p0;
-    g.cex += (long long)p0 * kCandPerProblem;
-    g.cH += 9LL * p0 * kCandPerProblem;
+    g.cand += (long long)p0 * 2 * kCandPerProblem;
+    g.ncand += 2 * p0;
+    g.cex += (long long)p0 * 2 * kCandPerProblem;
+    g.cH += 9LL * p0 * 2 * kCandPerProblem;
     ransac_enqueue(rp, np, c->probs.as<ProbDev>() + p0, c->pts.as<float4>(), c->n_good.as<int>() + p0, g,
                    c->masks.as<uint8_t>(), c->results.as<mim_result>() + p0, raw, c->cur, mark_cb, c, c->exact_all);
     HIPCHK(c, hipGetLastError());

@@ -89,6 +89,7 @@ struct RansacState {
     int win_len;           // attempts precomputed in that window
     float sa, sb;          // power-of-two scales of the source / destination coordinates (MFMA bound)
     float smax;            // max over points of |x|+|y|+|u|+|v| (MFMA bound margin)
+    int defer;             // chunk 1's exact pass deferred to chunk 2's (no early stop possible in chunk 1)
 };
 
 struct RansacParams {
@@ -115,10 +116,10 @@ struct RansacBufs {
     int* counts;              // [it_off + iter]  inlier count, -1 when runKernel returned 0
     int2* bounds;             // [it_off + iter]  (lower, upper) bound of the count (filtered path)
     double* best_h;           // [problem][9] bestModel of the filtered select (double H of the best sample)
-    int* cand;                // [problem][kCandPerProblem] candidate iterations of the current chunk
-    int* ncand;               // [problem] candidates listed (may exceed the capacity)
-    int* cex;                 // [problem][kCandPerProblem] their exact inlier counts
-    double* cH;               // [problem][kCandPerProblem][9] their exact models
+    int* cand;                // [problem][list 0..1][kCandPerProblem] candidate iterations (list = chunk)
+    int* ncand;               // [problem][list] candidates listed (may exceed the capacity)
+    int* cex;                 // [problem][list][kCandPerProblem] their exact inlier counts
+    double* cH;               // [problem][list][kCandPerProblem][9] their exact models
     uint8_t* flags;           // [problem][window] getSubset attempt outcomes ahead of stream_pos
     long long flag_cap;       // bytes of `flags`
     int* irr;                 // [problem][block][kIrrCap] positions of irregular attempts (chain sampler)

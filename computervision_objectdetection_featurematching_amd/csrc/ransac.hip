@@ -2329,12 +2329,13 @@ constexpr int kCandThreads = 1024;
 __global__ __launch_bounds__(kCandThreads) void ransac_cand_kernel(RansacState* __restrict__ st,
                                                                    const ProbDev* __restrict__ probs,
                                                                    const int2* __restrict__ bounds, int c1,
-                                                                   int* __restrict__ cand, int* __restrict__ ncand) {
+                                                                   int* __restrict__ cand, int* __restrict__ ncand,
+                                                                   int L, int max_iters, double conf) {
     __shared__ int wred[kCandThreads / 64], wred2[kCandThreads / 64];
     const int p = blockIdx.x, tid = threadIdx.x;
     const RansacState S = st[p];
     if (!S.active || S.done) {
-        if (tid == 0) ncand[p] = 0;
+        if (tid == 0) ncand[2 * p + L] = 0;
         return;
     }
     const int2* Bd = bounds + probs[p].it_off;
@@ -2343,17 +2344,24 @@ __global__ __launch_bounds__(kCandThreads) void ransac_cand_kernel(RansacState* 
     const int a = min(t1, t0 + tid * ch), e = min(t1, a + ch);
     // batches of 16 unconditional (clamped) loads: one memory latency per batch, not per iteration
     constexpr int kB = 16;
-    int lmax = INT_MIN;
+    int lmax = INT_MIN, hmax = INT_MIN;
     for (int t = a; t < e; t += kB) {
         int2 v[kB];
 #pragma unroll
         for (int k = 0; k < kB; ++k) v[k] = Bd[min(t + k, e - 1)];
 #pragma unroll
-        for (int k = 0; k < kB; ++k) lmax = t + k < e ? max(lmax, v[k].x) : lmax;
+        for (int k = 0; k < kB; ++k) {
+            lmax = t + k < e ? max(lmax, v[k].x) : lmax;
+            // the deferral heuristic ignores the unbounded [0, n] brackets of screened samples
+            // (deferring is exact either way; a wrong guess only costs chunk-2 work)
+            hmax = (t + k < e && !(v[k].x == 0 && v[k].y == S.n)) ? max(hmax, v[k].y) : hmax;
+        }
     }
     const int init = max(3, max(S.max_good, S.lo_max));
     int all;
     const int run0 = block_excl_max(lmax, init, wred, all);  // bound before this thread's first iteration
+    int hall;
+    block_excl_max(hmax, 0, wred2, hall);
     int cnt = 0, run = run0;
     for (int t = a; t < e; t += kB) {
         int2 v[kB];
@@ -2370,7 +2378,7 @@ __global__ __launch_bounds__(kCandThreads) void ransac_cand_kernel(RansacState* 
     int total;
     int o = block_excl_sum(cnt, wred2, total);
     if (cnt && o < kCandCap) {  // ordered list (beyond the capacity the replay kernel rescans)
-        int* C = cand + (long long)p * kCandCap;
+        int* C = cand + (long long)(2 * p + L) * kCandCap;
         run = run0;
         for (int t = a; t < e && o < kCandCap; ++t) {
             const int2 b = Bd[t];
@@ -2379,8 +2387,27 @@ __global__ __launch_bounds__(kCandThreads) void ransac_cand_kernel(RansacState* 
         }
     }
     if (tid == 0) {
-        ncand[p] = total;
+        ncand[2 * p + L] = total;
         st[p].lo_max = max(S.lo_max, all);
+        // Deferral of chunk 1's exact pass: the candidates of both chunks are evaluated in one pass in
+        // chunk 2 and replayed there in iteration order (one latency-bound exact pass instead of two).
+        // Not after a getSubset failure inside the chunk (the loop ends there) or without a next chunk.
+        if (L == 0) {
+            // defer unless the chunk's lower bounds already prove an early stop inside it (then the
+            // exact pass here saves chunk 2 altogether); a deferral that turns out to stop early only
+            // costs the next chunk's sampling and bounds, never a result
+            const int n = S.n;
+            const bool fail_here = S.fail_iter != -1 && S.fail_iter <= c1;
+            const int lo_best = min(max(max(all, S.max_good), 0), n);
+            const int nit = update_num_iters(conf, (double)(n - lo_best) / n, 4, S.niters);
+#ifdef MIM_EXACT_DEFER  // opt-in: measured -3 % on C3 (the one combined pass has a longer Jacobi tail)
+            st[p].defer = (c1 < max_iters && !fail_here && nit >= c1) ? 1 : 0;
+#else
+            st[p].defer = 0;
+#endif
+            (void)hall;
+            (void)nit;
+        }
     }
 }
 
@@ -2400,20 +2427,27 @@ __global__ __launch_bounds__(64) void ransac_exact_kernel(const RansacState* __r
                                                           const uint32_t* __restrict__ stream,
                                                           const int* __restrict__ cand, const int* __restrict__ ncand,
                                                           const int2* __restrict__ bounds,
-                                                          int* __restrict__ cex, double* __restrict__ cH, float thr2) {
+                                                          int* __restrict__ cex, double* __restrict__ cH, float thr2,
+                                                          int L) {
     __shared__ double sd[kExactGroups * kJ9G];
-    // problem-minor block order: the first (and usually only) busy wave of every problem comes
-    // first and lands on all 8 XCDs (blocks b and b+8 share an XCD under round-robin dispatch)
-    const int np = gridDim.x / kExactWaves;
-    const int p = blockIdx.x % np, w = blockIdx.x / np, lane = threadIdx.x, grp = lane >> 4, slot = lane & 15;
+    // blocks: [list pass][wave][problem]; chunk 1 (L = 0): list 0 of the problems not deferred;
+    // chunk 2 (L = 1): list 1 of every problem, then list 0 of the deferred ones.  Problem-minor
+    // order: the first (and usually only) busy wave of every problem comes first and lands on all 8
+    // XCDs (blocks b and b+8 share an XCD under round-robin dispatch)
+    const int np = gridDim.x / (kExactWaves * (L + 1));
+    const int pass = blockIdx.x / (np * kExactWaves), rem = blockIdx.x % (np * kExactWaves);
+    const int list = L - pass;
+    const int p = rem % np, w = rem / np, lane = threadIdx.x, grp = lane >> 4, slot = lane & 15;
     const RansacState S = st[p];
     if (!S.active || S.done) return;
-    const int nc = min(ncand[p], kCandCap);
+    if (list == 0 && (L == 0) == (S.defer != 0)) return;  // uniform over the block
+    const long long lb = (long long)(2 * p + list) * kCandCap;
+    const int nc = min(ncand[2 * p + list], kCandCap);
     if (w * kExactGroups >= nc) return;  // uniform over the wave
     const bool valid = w * kExactGroups + grp < nc;  // groups past the list only join the counting
     const int k = min(w * kExactGroups + grp, nc - 1);
-    const int t = cand[(long long)p * kCandCap + k];
-    const long long o = (long long)p * kCandCap + k;
+    const int t = cand[lb + k];
+    const long long o = lb + k;
     const int2 bd = bounds[probs[p].it_off + t];
     const bool tight = bd.x == bd.y;  // lo == hi pins the exact count: no eigensolve needed
     double H[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
@@ -2431,7 +2465,7 @@ __global__ __launch_bounds__(64) void ransac_exact_kernel(const RansacState* __r
     }
 #ifdef MIM_REFINE_PROF
     const unsigned long long x1 = clock64();
-    if (p < 3 && lane == 0) printf("[exact] p=%d w=%d nc=%d tight=%d solve %llu\n", p, w, ncand[p], (int)tight, x1 - x0);
+    if (p < 3 && lane == 0) printf("[exact] p=%d w=%d nc=%d tight=%d solve %llu\n", p, w, nc, (int)tight, x1 - x0);
 #endif
     // findInliers of every solved candidate by the whole wave (computeError is per point: the count
     // does not depend on the order)
@@ -2474,17 +2508,25 @@ __global__ __launch_bounds__(64) void ransac_replay_kernel(RansacState* __restri
                                                            const int2* __restrict__ bounds, const int* __restrict__ cand,
                                                            const int* __restrict__ ncand, const int* __restrict__ cex,
                                                            const double* __restrict__ cH, int c1, double conf,
-                                                           float thr2, double* __restrict__ best_h) {
+                                                           float thr2, double* __restrict__ best_h, int L,
+                                                           int c1_prev) {
     __shared__ double sd[kJ9D * 64];
     const int p = blockIdx.x, lane = threadIdx.x;
     RansacState S = st[p];
     if (!S.active || S.done) return;
-    const int end = min(c1, S.produced);
+    if (L == 0 && S.defer) {  // chunk 1's list is replayed with chunk 2's (ransac_cand_kernel)
+        if (lane == 0) st[p].next_iter = min(c1, S.produced);
+        return;
+    }
     const int N = S.n;
-    const int nc = ncand[p];
-    const int* C = cand + (long long)p * kCandCap;
-    const int* E = cex + (long long)p * kCandCap;
-    const double* HH = cH + (long long)p * kCandCap * 9;
+    int end = 0;
+    // lists in iteration order: a deferred chunk 1 (iterations < c1_prev), then this chunk
+    for (int li = (L == 1 && S.defer) ? 0 : L; li <= L; ++li) {
+    end = min(li == L ? c1 : c1_prev, S.produced);
+    const int nc = ncand[2 * p + li];
+    const int* C = cand + (long long)(2 * p + li) * kCandCap;
+    const int* E = cex + (long long)(2 * p + li) * kCandCap;
+    const double* HH = cH + (long long)(2 * p + li) * kCandCap * 9;
     int best_k = -1;  // candidate index whose H becomes bestModel (listed part)
     for (int k0 = 0; k0 < min(nc, kCandCap); k0 += 64) {
         const int k = k0 + lane;
@@ -2535,6 +2577,7 @@ __global__ __launch_bounds__(64) void ransac_replay_kernel(RansacState* __restri
                 for (int i = 0; i < 9; ++i) best_h[(long long)p * 9 + i] = H[i];
         }
     }
+    }  // lists
     S.next_iter = end;
     // getSubset failed at iteration fail_iter (or the stream ran out: -2) within this chunk's range;
     // a failure the concurrent sampler finds in the next chunk has fail_iter >= end or is not yet
@@ -3241,7 +3284,7 @@ void ransac_enqueue(const RansacParams& prm, int n_probs, const ProbDev* probs, 
         (void)hipStreamWaitEvent(ss, b.ev_fork, 0);
         mark(mark_ctx, "fork", ss);
     }
-    int ci = 0;
+    int ci = 0, c1_first = 0;
     while (c0 < max_iters) {
         const int c1 = (int)std::min<long long>((long long)c0 + chunk, max_iters);
         // attempt outcomes for a window of ~28 draws per wanted iteration (pass rate ~1/5), the walk
@@ -3310,23 +3353,29 @@ void ransac_enqueue(const RansacParams& prm, int n_probs, const ProbDev* probs, 
                 fprintf(stderr, "[mim] bound check chunk [%d,%d): checked %llu lo_viol %llu hi_viol %llu valid_mismatch %llu "
                         "mean_width %.2f tight %llu\n", c0, c1, h[0], h[1], h[2], h[3], h[0] ? (double)h[4] / h[0] : 0.0, h[5]);
             }
-            ransac_cand_kernel<<<n_probs, kCandThreads, 0, s>>>(b.state, probs, b.bounds, c1, b.cand, b.ncand);
+            const int L = c0 == 0 ? 0 : 1;  // candidate list of this chunk (at most two chunks)
+            ransac_cand_kernel<<<n_probs, kCandThreads, 0, s>>>(b.state, probs, b.bounds, c1, b.cand, b.ncand, L,
+                                                                max_iters, prm.conf);
             mark(mark_ctx, "cand", s);
             if (getenv("MIM_DEBUG_NCAND")) {
-                std::vector<int> h(n_probs);
-                (void)hipMemcpyAsync(h.data(), b.ncand, sizeof(int) * n_probs, hipMemcpyDeviceToHost, s);
+                std::vector<int> h(2 * n_probs);
+                (void)hipMemcpyAsync(h.data(), b.ncand, sizeof(int) * 2 * n_probs, hipMemcpyDeviceToHost, s);
                 (void)hipStreamSynchronize(s);
                 long long sum = 0; int mx = 0;
-                for (int v : h) { sum += v; mx = std::max(mx, v); }
+                for (int i = 0; i < n_probs; ++i) { sum += h[2 * i + L]; mx = std::max(mx, h[2 * i + L]); }
                 fprintf(stderr, "[mim] chunk [%d,%d): candidates mean %.1f max %d\n", c0, c1, (double)sum / n_probs, mx);
             }
-            ransac_exact_kernel<<<n_probs * kExactWaves, 64, 0, s>>>(b.state, probs, pts, b.samples, b.stream, b.cand,
-                                                                   b.ncand, b.bounds, b.cex, b.cH, thr2);
+            // chunk 2 also evaluates the list of every problem whose chunk-1 pass was deferred
+            ransac_exact_kernel<<<n_probs * kExactWaves * (L + 1), 64, 0, s>>>(b.state, probs, pts, b.samples, b.stream,
+                                                                             b.cand, b.ncand, b.bounds, b.cex, b.cH,
+                                                                             thr2, L);
             mark(mark_ctx, "exact", s);
             ransac_replay_kernel<<<n_probs, 64, 0, s>>>(b.state, probs, pts, b.samples, b.stream, b.bounds, b.cand,
-                                                        b.ncand, b.cex, b.cH, c1, prm.conf, thr2, b.best_h);
+                                                        b.ncand, b.cex, b.cH, c1, prm.conf, thr2, b.best_h, L,
+                                                        c1_first);
             mark(mark_ctx, "select", s);
         }
+        if (c0 == 0) c1_first = c1;
         c0 = c1;
         chunk = 1 << 30;  // one chunk after the first: every chunk costs a latency-bound exact pass
     }

@@ -1251,8 +1251,9 @@ __global__ __launch_bounds__(kChainThreads) void ransac_walk_kernel(const Ransac
             for (;;) {
                 const unsigned long long m = __ballot(q >= s && q < limit && ((q - s) & 3) == 0);
                 if (!m) break;
-                const int k = __builtin_ctzll(m);
-                const int qq = uni(__shfl(q, k)), ff = uni(__shfl(f, k));
+                // wave-uniform lane index: v_readlane (no LDS round trip per walked event)
+                const int k = uni(__builtin_ctzll(m));
+                const int qq = __builtin_amdgcn_readlane(q, k), ff = __builtin_amdgcn_readlane(f, k);
                 if (ff == kAttemptSerial || nseg == kChainSegs) {  // resolved by the walker
                     limit = qq;
                     stop = true;

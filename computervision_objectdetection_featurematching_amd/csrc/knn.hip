@@ -168,18 +168,21 @@ constexpr int kRescan = -2;  // Top2::i2 marker: the split's top-2 needs the exa
 #endif
 constexpr int kEarlyTiles = MIM_KNN_EARLY;
 
-// Threshold on R of a lane in the late tiles.  A row matters iff D < own 2nd best and D <= the
-// other row half's 2nd best (lanes l, l ^ 32 hold the same query; an equal D may still win on the
-// lower index): D <= Dt = min(m2 - 1, other).  D = 2R + p with p in {0,1} gives R <= floor(Dt/2).
+// Threshold on R of a lane in the late tiles.  Lanes l, l ^ 32 hold the same query over disjoint
+// row halves; the union of their two top-2 lists always contains the query's top-2 so far.  A new
+// row can enter that top-2 only if D <= Dc, the 2nd smallest of the pair's four D (an equal D may
+// still win on the lower index), and a row that does enters its own lane's list, so the filter
+// keeps the invariant.  D = 2R + p with p in {0,1} gives R <= floor(Dc/2).
 __device__ __forceinline__ int sel_filter(const LaneSel& s) {
-    const int v = s.m2;
-    const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
-    const int other = (threadIdx.x & 32) ? (int)r[0] : (int)r[1];
-    const int dt = min(s.m2 - 1, other);
-    return dt >> 1;
+    const auto a = __builtin_amdgcn_permlane32_swap(s.m1, s.m1, false, false);
+    const auto b = __builtin_amdgcn_permlane32_swap(s.m2, s.m2, false, false);
+    const bool hi = threadIdx.x & 32;
+    const int o1 = hi ? (int)a[0] : (int)a[1], o2 = hi ? (int)b[0] : (int)b[1];
+    const int dc = min(max(s.m1, o1), min(s.m2, o2));  // 2nd smallest of {m1 <= m2, o1 <= o2}
+    return dc >> 1;
 }
 
-__device__ __forceinline__ int dval(int R, int p) { return (R << 1) + p; }  // v_lshl_add_u32
+__device__ __forceinline__ int dval(int R, int p) { return (R << 1) | p; }  // v_lshl_or_b32
 
 // ------------------------------------------------------------------------------------------------
 // Exact distance kernel.  Block = kKnnWaves waves = kKnnBlockQ queries (each wave: kKnnQT 32-query
@@ -255,7 +258,14 @@ __global__ __launch_bounds__(kThreads, MIM_KNN_OCC) void knn2_i8_kernel(  // OCC
             const int ci = c * kThreads + tid, tt = ci >> 9;
             reinterpret_cast<i32x4*>(base + tt * kLdsTile)[ci & 511] = stg[c];
         }
-        if (tid < kStageNorms) reinterpret_cast<int*>(base + (tid >> 7) * kLdsTile + kTileBytes)[tid & 127] = stgn;
+        if (tid < kStageNorms) {  // wave-uniform: waves 2t, 2t+1 hold tile t's floor(n2/2), n2 & 1
+            int* nb = reinterpret_cast<int*>(base + (tid >> 7) * kLdsTile + kTileBytes);
+            if (!(tid & 64)) nb[tid & 63] = stgn;
+            else {  // the 64 parities as one bit mask (row i = bit i) in words 64, 65
+                const unsigned long long pm = __ballot(stgn & 1);
+                if (lane == 0) *reinterpret_cast<unsigned long long*>(nb + 64) = pm;
+            }
+        }
     };
 
     if (w.tile0 < w.tile1) {
@@ -291,17 +301,16 @@ __global__ __launch_bounds__(kThreads, MIM_KNN_OCC) void knn2_i8_kernel(  // OCC
 #pragma unroll
         for (int u2 = 0; u2 < 2; ++u2) {
             const int row0 = tile * 64 + 32 * u2;
-            const int* tpu = tn + 64 + 32 * u2 + 4 * h;  // n2 & 1
+            const unsigned pw = (unsigned)tn[64 + u2] >> (4 * h);  // bit 8gg + k: n2 & 1 of the lane's row
             i32x16 acc[QT];
             block_mfma(tb, u2, acc);
 #pragma unroll
             for (int gg = 0; gg < 4; ++gg) {
-                const int4 n = *reinterpret_cast<const int4*>(tpu + 8 * gg);
-                const int pv[4] = {n.x, n.y, n.z, n.w};
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
+                    const int pk = (pw >> (8 * gg + k)) & 1;
 #pragma unroll
-                    for (int u = 0; u < QT; ++u) sel_push(st[u], dval(acc[u][4 * gg + k], pv[k]), row0 + k + 8 * gg);
+                    for (int u = 0; u < QT; ++u) sel_push(st[u], dval(acc[u][4 * gg + k], pk), row0 + k + 8 * gg);
                 }
             }
         }
@@ -313,17 +322,19 @@ __global__ __launch_bounds__(kThreads, MIM_KNN_OCC) void knn2_i8_kernel(  // OCC
 #pragma unroll
         for (int u2 = 0; u2 < 2; ++u2) {
             const int row0 = tile * 64 + 32 * u2;
-            const int* tpu = tn + 64 + 32 * u2 + 4 * h;  // n2 & 1
+            const unsigned pw = (unsigned)tn[64 + u2] >> (4 * h);  // bit 8j + k: n2 & 1 of the lane's row
             i32x16 acc[QT];
             block_mfma(tb, u2, acc);
 #ifdef MIM_KNN_NOSEL  // timing probe only: MFMA loop without the selection (results invalid)
 #pragma unroll
             for (int u = 0; u < QT; ++u) {
                 int x = acc[u][0];
+#ifndef MIM_KNN_MFMAONLY  // (MFMAONLY: one accumulator read per column tile, no filter-sized VALU work)
 #pragma unroll
                 for (int g = 1; g < 16; ++g) x ^= acc[u][g];
+#endif
                 st[u].m1 = min(st[u].m1, x);
-                st[u].i1 = min(st[u].i1, x);
+                st[u].i1 = 0;  // a valid row: the indices feed the RANSAC gathers
             }
             continue;
 #endif
@@ -338,23 +349,25 @@ __global__ __launch_bounds__(kThreads, MIM_KNN_OCC) void knn2_i8_kernel(  // OCC
                 mn[u] = min(m, p[15]);
                 hit |= mn[u] <= T[u];
             }
+#ifdef MIM_KNN_NOHIT  // timing probe only (results invalid): the late-tile filter without insertions
+            if (__ballot(hit) != 0) {
+#pragma unroll
+                for (int u = 0; u < QT; ++u) st[u].m2 = min(st[u].m2, mn[u]);
+            }
+            continue;
+#endif
             if (__builtin_expect(__ballot(hit) != 0, 0)) {  // ~1 insertion per wave and half tile
 #pragma unroll
                 for (int u = 0; u < QT; ++u) {
                     if (__ballot(mn[u] <= T[u])) {
+                        // per row: one compare (the ballot) and, if some lane has the row under its
+                        // threshold, an unconditional insertion in every lane (the lane lists stay the
+                        // exact top-2 of the rows pushed, a superset of the filtered ones)
 #pragma unroll
-                        for (int j = 0; j < 4; ++j) {
-                            const i32x16& p = acc[u];
-                            const int gm = min(min(p[4 * j], p[4 * j + 1]), min(p[4 * j + 2], p[4 * j + 3]));
-                            if (__ballot(gm <= T[u])) {
-                                const int4 n = *reinterpret_cast<const int4*>(tpu + 8 * j);
-                                const int pv[4] = {n.x, n.y, n.z, n.w};
-                                if (gm <= T[u]) {
-#pragma unroll
-                                    for (int k = 0; k < 4; ++k)
-                                        sel_push(st[u], dval(p[4 * j + k], pv[k]), row0 + 8 * j + k);
-                                }
-                            }
+                        for (int g = 0; g < 16; ++g) {
+                            if (__ballot(acc[u][g] <= T[u]))
+                                sel_push(st[u], dval(acc[u][g], (pw >> ((g & 3) + 8 * (g >> 2))) & 1),
+                                         row0 + (g & 3) + 8 * (g >> 2));
                         }
                         T[u] = sel_filter(st[u]);
                     }
@@ -383,7 +396,12 @@ __global__ __launch_bounds__(kThreads, MIM_KNN_OCC) void knn2_i8_kernel(  // OCC
         const bool more = stage + kStage < w.tile1;
         if (more) stage_load(stage + kStage);
         const unsigned char* sb = smem + buf * kStage * kLdsTile;
-#pragma unroll
+#ifndef MIM_KNN_LATE_UNROLL
+#define MIM_KNN_LATE_UNROLL 1
+#endif
+        // not unrolled by default: the late tile with its insertion path is ~3 KiB of code, and the
+        // kernel otherwise outgrows the instruction cache
+#pragma unroll MIM_KNN_LATE_UNROLL
         for (int ts = 0; ts < kStage; ++ts)
             if (kStage == 1 || stage + ts < w.tile1) tile_late(sb + ts * kLdsTile, stage + ts);
         if (more) stage_store(buf ^ 1);

@@ -82,3 +82,29 @@ def test_ratio_filter(matcher, oracle):
     gq, gt = matcher.ratio_filter(idx, dist, 0.9)
     np.testing.assert_array_equal(gq, [2])
     np.testing.assert_array_equal(gt, [4])
+
+
+def test_knn_late_tile_ties_across_row_halves(matcher, oracle):
+    # the late-tile filter keeps a row iff D <= the lane pair's 2nd best; duplicates of the query's
+    # nearest rows placed late, in both row halves of a 32-row block (rows 4h..4h+3 of every 8) and
+    # across tiles, must come out in index order
+    rng = np.random.default_rng(23)
+    t = sift_like(rng, 3000)
+    q = sift_like(rng, 40)
+    for j in range(40):
+        pos = np.sort(rng.choice(np.arange(300, 3000), size=5, replace=False))
+        pos[1] = pos[0] + 4 if pos[0] + 4 < pos[2] else pos[1]  # other half of the same 8-row group
+        for p in pos:
+            t[p] = q[j]
+    _check(matcher, oracle, q, t)
+
+
+def test_knn_small_pool_mass_ties(matcher, oracle):
+    # 4,096 train rows drawn from 24 distinct descriptors: every query's best and 2nd best are tied
+    # many times over, in every tile and both row halves
+    rng = np.random.default_rng(29)
+    pool = sift_like(rng, 24)
+    t = pool[rng.integers(0, 24, size=4096)]
+    q = np.concatenate([pool[rng.integers(0, 24, size=100)], sift_like(rng, 100)])
+    gi, _ = _check(matcher, oracle, q, t)
+    assert (gi[:100, 0] < gi[:100, 1]).all()  # equal distance: lower index first

@@ -45,9 +45,15 @@ __device__ __forceinline__ void prep_tile(const float* __restrict__ src, int n, 
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
         const int ci = k * 256 + tid;  // output chunk (16 B) within the tile
+#ifdef MIM_KNN16  // [row block rb 0..3][kstep 0..1][lane]: row 16 rb + (lane & 15), col 64 ks + 16 (lane >> 4)
+        const int rb = ci >> 7, s = (ci >> 6) & 1, lane = ci & 63;
+        const int row = tile * 64 + 16 * rb + (lane & 15);
+        const int col = 64 * s + 16 * (lane >> 4);
+#else
         const int u = ci >> 8, s = (ci >> 6) & 3, lane = ci & 63;
         const int row = tile * 64 + 32 * u + (lane & 31);
         const int col = 32 * s + 16 * (lane >> 5);
+#endif
         uint32_t o[4] = {0, 0, 0, 0};
         if (row < n) {
             const float4* p = reinterpret_cast<const float4*>(src + (size_t)row * kDim + col);
@@ -230,6 +236,12 @@ __global__ __launch_bounds__(kThreads, MIM_KNN_OCC) void knn2_i8_kernel(  // OCC
     }
     LaneSel st[QT];
     int T[QT];  // late-tile thresholds on R
+#ifndef MIM_KNN_EXACT_PAIR
+    // the partner lane's (l ^ 32) m1, m2 as of the last refresh (every stage): between refreshes an
+    // insertion recomputes the threshold from its own fresh pair and these (the partner's values only
+    // decrease, so a stale copy gives a threshold >= the exact one: a superset, no exchange per event)
+    int o1c[QT], o2c[QT];
+#endif
 #pragma unroll
     for (int u = 0; u < QT; ++u) {
         sel_init(st[u]);
@@ -369,7 +381,11 @@ __global__ __launch_bounds__(kThreads, MIM_KNN_OCC) void knn2_i8_kernel(  // OCC
                                 sel_push(st[u], dval(acc[u][g], (pw >> ((g & 3) + 8 * (g >> 2))) & 1),
                                          row0 + (g & 3) + 8 * (g >> 2));
                         }
+#ifdef MIM_KNN_EXACT_PAIR
                         T[u] = sel_filter(st[u]);
+#else
+                        T[u] = min(max(st[u].m1, o1c[u]), min(st[u].m2, o2c[u])) >> 1;
+#endif
                     }
                 }
             }
@@ -389,18 +405,27 @@ __global__ __launch_bounds__(kThreads, MIM_KNN_OCC) void knn2_i8_kernel(  // OCC
         if (more) stage_store(buf ^ 1);
         __syncthreads();
     }
-#pragma unroll
-    for (int u = 0; u < QT; ++u) T[u] = sel_filter(st[u]);
     for (; stage < w.tile1; stage += kStage) {
         const int buf = ((stage - w.tile0) / kStage) & 1;
         const bool more = stage + kStage < w.tile1;
         if (more) stage_load(stage + kStage);
         const unsigned char* sb = smem + buf * kStage * kLdsTile;
+#pragma unroll
+        for (int u = 0; u < QT; ++u) {
+#ifdef MIM_KNN_EXACT_PAIR
+            T[u] = sel_filter(st[u]);
+#else
+            const auto a = __builtin_amdgcn_permlane32_swap(st[u].m1, st[u].m1, false, false);
+            const auto b = __builtin_amdgcn_permlane32_swap(st[u].m2, st[u].m2, false, false);
+            o1c[u] = (tid & 32) ? (int)a[0] : (int)a[1];
+            o2c[u] = (tid & 32) ? (int)b[0] : (int)b[1];
+            T[u] = min(max(st[u].m1, o1c[u]), min(st[u].m2, o2c[u])) >> 1;
+#endif
+        }
 #ifndef MIM_KNN_LATE_UNROLL
 #define MIM_KNN_LATE_UNROLL 1
 #endif
-        // not unrolled by default: the late tile with its insertion path is ~3 KiB of code, and the
-        // kernel otherwise outgrows the instruction cache
+        // rolled by default (unrolling measured no faster; the late tile is ~3 KiB of code)
 #pragma unroll MIM_KNN_LATE_UNROLL
         for (int ts = 0; ts < kStage; ++ts)
             if (kStage == 1 || stage + ts < w.tile1) tile_late(sb + ts * kLdsTile, stage + ts);
@@ -434,6 +459,227 @@ __global__ __launch_bounds__(kThreads, MIM_KNN_OCC) void knn2_i8_kernel(  // OCC
         }
     }
 }
+
+#ifdef MIM_KNN16
+// ------------------------------------------------------------------------------------------------
+// The distance kernel on v_mfma_i32_16x16x64_i8 (MIM_KNN16 build).  In an LDS-fed loop the MI355X
+// holds ~2.15 GHz on this shape against ~1.72 GHz on 32x32x32 (tools/probe/mfma_i8_shape_probe.hip:
+// 4.4 vs 3.5 POPS).  A wave owns one 64-query tile (four 16-query column tiles, q' in 32 VGPRs); per
+// 16-row block rb of a train tile, 2 k-steps x 4 MFMAs; lane l holds query 16 ct + (l & 15) and train
+// rows 16 rb + 4 (l >> 4) + i (i = 0..3), so a query's rows are spread over the 4 lanes l & 15 + 16 g.
+// Same exact integer arithmetic, early/late selection and thresholds as the 32x32 kernel, the
+// threshold over the 4-lane group.
+// ------------------------------------------------------------------------------------------------
+// 2nd smallest of the 4-lane group's eight D (each lane's m1 <= m2), then R <= floor(Dc / 2)
+__device__ __forceinline__ int sel_filter4(const LaneSel& s) {
+    int a1 = s.m1, a2 = s.m2;
+    {
+        const auto x = __builtin_amdgcn_permlane16_swap(a1, a1, false, false);
+        const auto y = __builtin_amdgcn_permlane16_swap(a2, a2, false, false);
+        const bool odd = threadIdx.x & 16;
+        const int b1 = odd ? (int)x[0] : (int)x[1], b2 = odd ? (int)y[0] : (int)y[1];
+        const int n2 = min(max(a1, b1), min(a2, b2));
+        a1 = min(a1, b1);
+        a2 = n2;
+    }
+    {
+        const auto x = __builtin_amdgcn_permlane32_swap(a1, a1, false, false);
+        const auto y = __builtin_amdgcn_permlane32_swap(a2, a2, false, false);
+        const bool hi = threadIdx.x & 32;
+        const int b1 = hi ? (int)x[0] : (int)x[1], b2 = hi ? (int)y[0] : (int)y[1];
+        a2 = min(max(a1, b1), min(a2, b2));
+    }
+    return a2 >> 1;
+}
+
+__global__ __launch_bounds__(kThreads, MIM_KNN_OCC) void knn2_i8_16_kernel(
+    const ProbDev* __restrict__ probs, const KnnWork* __restrict__ works, Top2* __restrict__ parts) {
+    constexpr int CT = 4;  // 16-query column tiles per wave
+    static_assert(32 * kKnnQT == 64, "one 64-query tile per wave");
+    __shared__ __attribute__((aligned(16))) unsigned char smem[2 * kStage * kLdsTile];
+    const KnnWork w = works[blockIdx.x];
+    const ProbDev* P = probs + w.problem;
+    if (*P->q.flags | *P->t.flags) return;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, g = lane >> 4, c16 = lane & 15;
+    const int nq = P->q.n;
+    const uint4* __restrict__ tsrc = reinterpret_cast<const uint4*>(P->t.frag);
+    const int* __restrict__ tnorm = P->t.norm;
+
+    const int qbase = w.q0 + wave * 64;
+    const int qt = qbase >> 6;
+    const int qtc = qt < P->q.n_tiles ? qt : 0;  // rows past the set: tile 0, never written out
+    i32x4 B[CT][2];
+    int qn[CT];
+    {
+        const gi32x4* qsrc = (const gi32x4*)(P->q.frag) + (size_t)qtc * 512;
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) {
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks) B[ct][ks] = ~qsrc[(ct * 2 + ks) * 64 + lane];
+            qn[ct] = ((const gint*)P->q.norm)[(size_t)qtc * kNormWords + 128 + 16 * ct + c16];
+        }
+    }
+    LaneSel st[CT];
+    int T[CT];
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) {
+        sel_init(st[ct]);
+        T[ct] = INT_MAX;
+    }
+
+    i32x4 stg[kStageChunks];
+    int stgn = 0;
+    auto stage_load = [&](int t0) {
+#pragma unroll
+        for (int c = 0; c < kStageChunks; ++c) {
+            const int ci = c * kThreads + tid, tt = ci >> 9;
+            if (kStage == 1 || t0 + tt < w.tile1) stg[c] = ((const gi32x4*)tsrc)[(size_t)t0 * 512 + ci];
+        }
+        if (tid < kStageNorms && (kStage == 1 || t0 + (tid >> 7) < w.tile1))
+            stgn = ((const gint*)tnorm)[(size_t)t0 * kNormWords + (tid >> 7) * kNormWords + (tid & 127)];
+    };
+    auto stage_store = [&](int buf) {
+        unsigned char* base = smem + buf * kStage * kLdsTile;
+#pragma unroll
+        for (int c = 0; c < kStageChunks; ++c) {
+            const int ci = c * kThreads + tid, tt = ci >> 9;
+            reinterpret_cast<i32x4*>(base + tt * kLdsTile)[ci & 511] = stg[c];
+        }
+        if (tid < kStageNorms) {
+            int* nb = reinterpret_cast<int*>(base + (tid >> 7) * kLdsTile + kTileBytes);
+            if (!(tid & 64)) nb[tid & 63] = stgn;
+            else {
+                const unsigned long long pm = __ballot(stgn & 1);
+                if (lane == 0) *reinterpret_cast<unsigned long long*>(nb + 64) = pm;
+            }
+        }
+    };
+    if (w.tile0 < w.tile1) {
+        stage_load(w.tile0);
+        stage_store(0);
+    }
+    __syncthreads();
+    __builtin_amdgcn_s_waitcnt(0);
+
+    // 16-row block rb of a tile: accumulators seeded with floor(n2/2), R = q'.t'' + floor(n2/2)
+    auto block_mfma = [&](const unsigned char* tb, int rb, i32x4 (&acc)[CT]) {
+        const i32x4* A = reinterpret_cast<const i32x4*>(tb);
+        const int4 n = *reinterpret_cast<const int4*>(reinterpret_cast<const int*>(tb + kTileBytes) + 16 * rb + 4 * g);
+        acc[0][0] = n.x; acc[0][1] = n.y; acc[0][2] = n.z; acc[0][3] = n.w;
+#pragma unroll
+        for (int ct = 1; ct < CT; ++ct) acc[ct] = acc[0];
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            const i32x4 a = A[(rb * 2 + ks) * 64 + lane];
+#pragma unroll
+            for (int ct = 0; ct < CT; ++ct) acc[ct] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, B[ct][ks], acc[ct], 0, 0, 0);
+        }
+    };
+    // parity bits of the lane's 4 rows of block rb: bit i
+    auto parity4 = [&](const unsigned char* tb, int rb) {
+        const unsigned wv = reinterpret_cast<const unsigned*>(tb + kTileBytes)[64 + (rb >> 1)];
+        return wv >> (16 * (rb & 1) + 4 * g);
+    };
+    auto tile_early = [&](const unsigned char* tb, int tile) {
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb) {
+            const int row0 = tile * 64 + 16 * rb;
+            const unsigned pw = parity4(tb, rb);
+            i32x4 acc[CT];
+            block_mfma(tb, rb, acc);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int pk = (pw >> i) & 1;
+#pragma unroll
+                for (int ct = 0; ct < CT; ++ct) sel_push(st[ct], dval(acc[ct][i], pk), row0 + i);
+            }
+        }
+    };
+    auto tile_late = [&](const unsigned char* tb, int tile) {
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb) {
+            const int row0 = tile * 64 + 16 * rb;
+            i32x4 acc[CT];
+            block_mfma(tb, rb, acc);
+            int mn[CT];
+            bool hit = false;
+#pragma unroll
+            for (int ct = 0; ct < CT; ++ct) {
+                mn[ct] = min(min(acc[ct][0], acc[ct][1]), min(acc[ct][2], acc[ct][3]));
+                hit |= mn[ct] <= T[ct];
+            }
+            if (__builtin_expect(__ballot(hit) != 0, 0)) {
+                const unsigned pw = parity4(tb, rb);
+#pragma unroll
+                for (int ct = 0; ct < CT; ++ct) {
+                    if (__ballot(mn[ct] <= T[ct])) {
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) {
+                            if (__ballot(acc[ct][i] <= T[ct]))
+                                sel_push(st[ct], dval(acc[ct][i], (pw >> i) & 1), row0 + i);
+                        }
+                        T[ct] = sel_filter4(st[ct]);
+                    }
+                }
+            }
+        }
+    };
+
+    const int tile_e = min(w.tile1, w.tile0 + (kEarlyTiles + kStage - 1) / kStage * kStage);
+    int stage = w.tile0;
+    for (; stage < tile_e; stage += kStage) {
+        const int buf = ((stage - w.tile0) / kStage) & 1;
+        const bool more = stage + kStage < w.tile1;
+        if (more) stage_load(stage + kStage);
+        const unsigned char* sb = smem + buf * kStage * kLdsTile;
+#pragma unroll
+        for (int ts = 0; ts < kStage; ++ts)
+            if (kStage == 1 || stage + ts < w.tile1) tile_early(sb + ts * kLdsTile, stage + ts);
+        if (more) stage_store(buf ^ 1);
+        __syncthreads();
+    }
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) T[ct] = sel_filter4(st[ct]);
+    for (; stage < w.tile1; stage += kStage) {
+        const int buf = ((stage - w.tile0) / kStage) & 1;
+        const bool more = stage + kStage < w.tile1;
+        if (more) stage_load(stage + kStage);
+        const unsigned char* sb = smem + buf * kStage * kLdsTile;
+#pragma unroll 1
+        for (int ts = 0; ts < kStage; ++ts)
+            if (kStage == 1 || stage + ts < w.tile1) tile_late(sb + ts * kLdsTile, stage + ts);
+        if (more) stage_store(buf ^ 1);
+        __syncthreads();
+    }
+
+    // ---- merge the four lanes of each query (disjoint train rows), keys ----
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) {
+        LaneSel m = st[ct];
+        if (m.i1 != INT_MAX) m.i1 += 4 * g;
+        if (m.i2 != INT_MAX) m.i2 += 4 * g;
+#pragma unroll
+        for (int x = 16; x <= 32; x <<= 1) {
+            LaneSel o;
+            o.m1 = __shfl_xor(m.m1, x); o.m2 = __shfl_xor(m.m2, x);
+            o.i1 = __shfl_xor(m.i1, x); o.i2 = __shfl_xor(m.i2, x);
+            m = sel_merge(m, o);
+        }
+        const int q = qbase + 16 * ct + c16;
+        if (g == 0 && q < nq) {
+            const int qq = qn[ct];
+            Top2 t;
+            const int d1 = m.m1 + qq, d2 = m.m2 + qq;
+            t.k1 = m.i1 == INT_MAX ? FLT_MAX : sqrtf((float)d1);
+            t.k2 = m.i2 == INT_MAX ? FLT_MAX : sqrtf((float)d2);
+            t.i1 = m.i1;
+            t.i2 = m.i2;
+            if (t.i2 != INT_MAX && d2 >= 4000000) t.i2 = kRescan;
+            parts[P->part_off + (long long)w.split * P->q_pad + q] = t;
+        }
+    }
+}
+#endif
 
 // ------------------------------------------------------------------------------------------------
 // Exact rescan of the queries the distance kernel marked (kRescan): one wave per query over the
@@ -632,7 +878,11 @@ void launch_prep_batch(const PrepJob* jobs, int njobs, int total_tiles, hipStrea
 // device) and only the matching kernel does the work, so no host round trip is needed.
 void launch_knn(const ProbDev* probs, const KnnWork* works, int n_works, Top2* parts, hipStream_t st) {
     if (n_works <= 0) return;
+#ifdef MIM_KNN16
+    knn2_i8_16_kernel<<<n_works, kThreads, 0, st>>>(probs, works, parts);
+#else
     knn2_i8_kernel<<<n_works, kThreads, 0, st>>>(probs, works, parts);
+#endif
     knn2_rescan_kernel<<<n_works, 256, 0, st>>>(probs, works, parts);
     knn2_f32_kernel<<<n_works, 256, 0, st>>>(probs, works, parts);
 }

@@ -402,7 +402,7 @@ __device__ __forceinline__ int jacobi9_group(double* __restrict__ A, double* __r
             const double po = dpp_row_d(p, c);
             const int poso = dpp_row(pos, c), klo = dpp_row(kl, c);
             // bitwise: no short-circuit branches
-            const bool take = (fabs(po) > fabs(p)) | ((fabs(po) == fabs(p)) & (poso < pos));
+            const bool take = (int)(fabs(po) > fabs(p)) | ((int)(fabs(po) == fabs(p)) & (int)(poso < pos));
             p = take ? po : p;
             pos = take ? poso : pos;
             kl = take ? klo : kl;
@@ -1375,11 +1375,11 @@ __global__ __launch_bounds__(kCheckBlock) void ransac_check_kernel(const ChainSe
     }
     // all regular draws first (one 16-byte load per attempt: consecutive chain attempts are 4 draws
     // apart, so a wave reads 1 KiB contiguously; dword-aligned vector loads), then the reductions
-    typedef uint4 __attribute__((aligned(4))) uint4a4;
+    typedef unsigned uint4a4 __attribute__((ext_vector_type(4), aligned(4)));
     unsigned raw[kCheckPer][4];
 #pragma unroll
     for (int r = 0; r < kCheckPer; ++r) {
-        const uint4 v = *reinterpret_cast<const uint4a4*>(stream + q[r]);
+        const uint4a4 v = *reinterpret_cast<const uint4a4*>(stream + q[r]);  // 4-B aligned 16-B load
         raw[r][0] = v.x; raw[r][1] = v.y; raw[r][2] = v.z; raw[r][3] = v.w;
     }
     int idx[kCheckPer][4];
@@ -2398,7 +2398,9 @@ __global__ __launch_bounds__(kCandThreads) void ransac_cand_kernel(RansacState* 
             // exact pass here saves chunk 2 altogether); a deferral that turns out to stop early only
             // costs the next chunk's sampling and bounds, never a result
             const int n = S.n;
+#ifdef MIM_EXACT_DEFER
             const bool fail_here = S.fail_iter != -1 && S.fail_iter <= c1;
+#endif
             const int lo_best = min(max(max(all, S.max_good), 0), n);
             const int nit = update_num_iters(conf, (double)(n - lo_best) / n, 4, S.niters);
 #ifdef MIM_EXACT_DEFER  // opt-in: measured -3 % on C3 (the one combined pass has a longer Jacobi tail)

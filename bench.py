@@ -55,7 +55,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="c3", choices=["c2", "c3"])
-    ap.add_argument("--cpu-problems", type=int, default=3, help="problems in the CPU-baseline sample (0: skip)")
+    ap.add_argument("--cpu-problems", type=int, default=24,
+                    help="problems in the CPU-baseline sample (~10 s of CPU work; 0: skip)")
     ap.add_argument("--no-timing", action="store_true", help="disable per-kernel HIP events")
     ap.add_argument("--inflight", type=int, default=0,
                     help="scene batches in flight: one library context + HIP stream each, steps assigned "

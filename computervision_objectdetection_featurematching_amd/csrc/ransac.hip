@@ -2065,6 +2065,9 @@ __global__ __launch_bounds__(256) void ransac_bound_mfma_kernel(const RansacStat
     const int p = blockIdx.x / bpp;
     const int tid = threadIdx.x, lane = tid & 63;
     const int it = c0 + (blockIdx.x % bpp) * 256 + tid;
+#ifdef MIM_PROBE_BOUND_CYC  // timing probe: per-wave cycles of the hypothesis setup vs the point loop
+    const long long cyc0 = clock64();
+#endif
     const RansacState S = st[p];
     if (!S.active || S.done) return;  // uniform over the block
     if (c0 + (blockIdx.x % bpp) * 256 >= min(c1, S.produced)) return;  // whole block idle
@@ -2159,6 +2162,9 @@ __global__ __launch_bounds__(256) void ransac_bound_mfma_kernel(const RansacStat
         CL0 = lowh ? CL : CLp; EL0 = lowh ? EL : ELp; CL1 = lowh ? CLp : CL; EL1 = lowh ? ELp : EL;
     }
     const bool wave_counts = __any(count);
+#ifdef MIM_PROBE_BOUND_CYC
+    const long long cyc1 = clock64();
+#endif
     float big = INFINITY;
     asm volatile("" : "+v"(big));
     const uint4* __restrict__ T = tiles + (go >> 5) * 128;
@@ -2218,6 +2224,10 @@ __global__ __launch_bounds__(256) void ransac_bound_mfma_kernel(const RansacStat
         lo = (int)(lowh ? i0 : i1);  // zero-padded rows (ex = ey = W = 0) give m - R_lo = E_lo > 0: never "in"
     }
     if (act) bounds[o] = invalid ? make_int2(-1, -1) : (uncertain ? make_int2(0, n) : make_int2(lo, n - outs));
+#ifdef MIM_PROBE_BOUND_CYC
+    if (!kLo && tid == 0 && blockIdx.x % 61 == 0)
+        printf("BOUNDCYC setup %lld loop %lld n %d\n", cyc1 - cyc0, clock64() - cyc1, n);
+#endif
 }
 
 // exact count of one hypothesis (runKernel + computeError + findInliers, bit-exact)

@@ -2,29 +2,36 @@
 """Benchmark: matches+homographies/sec (10k x 10k SIFT, 50k RANSAC iters) — BASELINE.json metric.
 
 One step = one pass of the hot path (knnMatch k=2 + ratio test + findHomography RANSAC + refine +
-gates, /root/reference/src/TestsDetector.cpp:58-95) over one batch of problems:
-  config c3 (default, BASELINE.json configs[2]): 3 model descriptor sets x 32 scene sets per GPU,
-  10,000 x 10,000 128-D SIFT-like descriptors per problem, RANSAC maxIters 50,000, conf 0.995,
-  8 % geometric inliers among 2,000 planted matches (no early termination: SURVEY.md App. B).
+gates, /root/reference/src/TestsDetector.cpp:58-95) over one batch of problems.  Configs
+(BASELINE.json `configs`; `--config`, default c3):
+  c3  configs[2]: 3 model descriptor sets x 32 scene sets per GPU, 10,000 x 10,000 128-D SIFT-like
+      descriptors per problem, RANSAC maxIters 50,000, conf 0.995, 8 % geometric inliers among 2,000
+      planted matches (no early termination: SURVEY.md App. B).  C4 (configs[3]) is this workload
+      with --gpus 8: every rank owns its own 32 scenes.
+  c2  configs[1]: 1 x 1, 2k x 2k, maxIters 2000.
+  c1  configs[0] surrogate: the reference's own shape, one scene = 29 model views x 5 scales = 145
+      ragged problems (Nq 100-500, Nt 1k-4k, maxIters 2000); the real data needs SIFT.
+  c5  configs[4]: the 50k x 50k dense distance contraction alone (mim_knn2_sets_dev), no RANSAC.
 Inputs (descriptors + keypoints) are resident in HBM before the timed region; each step registers
-the 32 scene sets (i8 fragment layout prep is inside the step) and runs the batch.  Multi-GPU:
-one process per GPU, each rank owns its own 32 scenes (weak scaling, no data-path collective); the
-per-problem result records are all-gathered over RCCL at the end of every step.
-Three scene batches are in flight (--inflight 3): each step runs on one of three library contexts,
-each with its own HIP stream and work buffers, assigned round-robin, so one batch's latency-bound
-RANSAC phases (sampler replay, exact evaluation, refine) overlap the other batches' GPU-filling
-kernels (3 beat 2 by 4-8 %; 4 contexts exceed the box's 4 hardware queues and lose).  With N > 1
-ranks, RCCL's stream takes a hardware queue, so each rank keeps two batches in flight.  Every step
-still does the whole path for its 96 problems; `value` = problems / wall time of the K steps.
+the sets (the i8 layout prep is inside the step) and runs the batch.  Multi-GPU: one process per GPU
+(`--gpus N` launches N ranks through torch.distributed.run when WORLD_SIZE is unset), each rank
+owns its own scenes (weak scaling, no data-path collective); the per-problem result records are
+all-gathered over RCCL at the end of every step.  Three scene batches are in flight on one GPU
+(--inflight).
 
-Prints ONE JSON line on rank 0.  Extra fields: "roofline" (dominant kernel, HIP events on the
-library's stream) and "cpu_baseline" (the oracle/ CPU restatement on this host, bounded sample).
+Prints ONE JSON line on rank 0 with, besides the contract fields: "roofline" (dominant kernel, HIP
+events on the library's stream), "cpu_baseline" (oracle/ restatement on this host's cores, bounded
+sample, with a "parity" check of those problems against the GPU records) and "ranks_seen".
+`--dry-run` exercises the launcher and the gloo/RCCL record gather without a GPU (CPU test).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import statistics
+import subprocess
 import sys
 import time
 
@@ -35,18 +42,22 @@ sys.path.insert(0, ROOT)
 
 PEAK_I8_TOPS = 5000.0       # MI355X dense i8 MFMA = 2x dense bf16 2.5 PF (MI355X_MICROARCH.md, no sparsity)
 PEAK_F32_VALU_TFLOPS = 157.3  # MI355X fp32 vector (VALU) peak
-PEAK_HBM_GBS = 8000.0
 FLOP_PER_POINT_EVAL = 17      # one fp32 reprojection test of a hypothesis on a point
-TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
+H_TOL = 1e-4                  # SURVEY.md 8(c) contract item 4 (the GPU tests hold 1e-7)
 
 
-def pmc_traffic(kernel):
-    """HBM bytes per step of `kernel` from the committed rocprofv3 PMC passes (or None)."""
-    try:
-        with open(TRAFFIC_FILE) as f:
-            return json.load(f)["kernels"][kernel]["hbm_bytes_per_step"]
-    except (OSError, KeyError, ValueError):
-        return None
+def pmc_traffic(kernel, config):
+    """HBM bytes per step of `kernel` from the newest committed rocprofv3 PMC pass (or None)."""
+    for rnd in ("r02", "r01"):
+        try:
+            with open(os.path.join(ROOT, "profiles", f"{rnd}_pmc_traffic.json")) as f:
+                d = json.load(f)
+            if d.get("config", "c3") != config:
+                continue
+            return d["kernels"][kernel]["hbm_bytes_per_step"]
+        except (OSError, KeyError, ValueError):
+            continue
+    return None
 
 
 def parse():
@@ -54,56 +65,234 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--config", default="c3", choices=["c2", "c3"])
-    ap.add_argument("--cpu-problems", type=int, default=24,
-                    help="problems in the CPU-baseline sample (~10 s of CPU work; 0: skip)")
+    ap.add_argument("--config", default="c3", choices=["c1", "c2", "c3", "c5"])
+    ap.add_argument("--cpu-sample", type=int, default=6,
+                    help="problems of the sequential CPU-baseline sample (1 warm-up + the median of the rest; "
+                         "0: skip the CPU baseline)")
+    ap.add_argument("--cpu-rounds", type=int, default=5, help="timed rounds of the parallel CPU row")
     ap.add_argument("--no-timing", action="store_true", help="disable per-kernel HIP events")
     ap.add_argument("--inflight", type=int, default=0,
                     help="scene batches in flight: one library context + HIP stream each, steps assigned "
                          "round-robin, so a batch's latency-bound RANSAC tail overlaps the next batch's kNN "
                          "(0: 3 on one GPU, 2 with RCCL, whose stream takes one of the 4 hardware queues)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="no GPU: launch the ranks, gather fake records over gloo, print the JSON line")
     return ap.parse_args()
 
 
-def cpu_baseline(ds, params, n_probs):
+# ------------------------------------------------------------------------------------------------
+# launcher: N ranks of this script, started before anything touches the GPU
+# ------------------------------------------------------------------------------------------------
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(args) -> int:
+    """`python bench.py --gpus N` without WORLD_SIZE: run N ranks via torch.distributed.run as child
+    processes (this process never initialises the GPU) and return the launcher's exit code."""
+    argv = [a for a in sys.argv[1:]]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__), *argv]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+def dist_env():
+    return (int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1")),
+            int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def dry_run(args):
+    """Launcher + process group + record gather on gloo (CPU): what the N-rank bench does around its
+    GPU work.  Prints the JSON line with n_gpus / ranks_seen so a CPU test can check the launch."""
+    import torch
+    import torch.distributed as dist
+
+    from computervision_objectdetection_featurematching_amd import shard
+    from computervision_objectdetection_featurematching_amd._lib import RESULT_DTYPE
+
+    rank, world, _ = dist_env()
+    if world > 1:
+        dist.init_process_group("gloo")
+    seen = dist.get_world_size() if world > 1 else 1
+    if seen != args.gpus:
+        raise SystemExit(f"rank {rank}: process group has {seen} ranks, --gpus {args.gpus}")
+    rec = np.zeros(4, RESULT_DTYPE)
+    rec["n_good"] = 1000 * rank + np.arange(4)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    g = shard.decode(shard.gather_results(torch.from_numpy(rec.view(np.uint8).copy()), world))
+    el = time.perf_counter() - t0
+    t = torch.tensor([el], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    if rank == 0:
+        assert g.shape == (world, 4) and list(g["n_good"][:, 0]) == [1000 * r for r in range(world)]
+        print(json.dumps({"metric": "dry-run", "value": 0.0, "unit": "problems/s", "n_gpus": world,
+                          "ranks_seen": seen, "steps": 0, "warmup": 0, "ms_per_step": float(t.item()) * 1e3,
+                          "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dry_run": True}),
+              flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+# ------------------------------------------------------------------------------------------------
+# CPU baseline: the oracle (CPU restatement of OpenCV 4.5.4) on this host, plus parity of the sample
+# ------------------------------------------------------------------------------------------------
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def host_cores() -> int:
+    """Host threads for the CPU baseline: the GPU box's CPU share (OMP_NUM_THREADS, 16 per GPU there;
+    nproc shows the whole machine), else every core this process may run on."""
+    aff = len(os.sched_getaffinity(0))
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    return min(aff, int(omp)) if omp.isdigit() and int(omp) > 0 else aff
+
+
+def log(msg):
+    print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
+def _cmp_problem(o, r, det):
+    """First difference between an oracle record and the GPU record/detail of one problem, or None."""
+    gq, gt, gm = det
+    if int(r["n_good"]) != o["n_good"]:
+        return f"n_good {int(r['n_good'])} vs {o['n_good']}"
+    if not (np.array_equal(gq, o["good_q"]) and np.array_equal(gt, o["good_t"])):
+        return "good-match lists"
+    if int(r["status"]) != o["status"] or int(r["n_inl"]) != o["n_inl"] or int(r["iters"]) != o["iters"]:
+        return f"status/n_inl/iters {(int(r['status']), int(r['n_inl']), int(r['iters']))} vs " \
+               f"{(o['status'], o['n_inl'], o['iters'])}"
+    if len(o["mask"]) and not np.array_equal(gm, o["mask"]):
+        return "inlier mask"
+    Ho = o["H"]
+    if np.any(Ho != 0) and np.max(np.abs(r["H"].reshape(3, 3) - Ho) / (np.abs(Ho) + 1e-3)) > H_TOL:
+        return "H"
+    return None
+
+
+def cpu_baseline_problems(ds, cfg, gpu_res, gpu_detail, n_sample, rounds):
+    """Reference-style leg: problems one after another, kNN on all host cores (OpenCV parallel_for_),
+    RANSAC single-threaded (cv::findHomography); 1 warm-up problem, value = 1 / median of the others.
+    Parallel leg ("best effort"): one problem per core at once (ctypes releases the GIL), 1 warm-up
+    round + `rounds` timed rounds, median.  Every oracle record is compared with the GPU's."""
+    from concurrent.futures import ThreadPoolExecutor
+
     from oracle import oracle as O
     O.build()
-    threads = min(16, len(os.sched_getaffinity(0)))
-    prm = O.default_params(max_iters=params["max_iters"])
-    probs = ds.problems[:n_probs]
-    t_knn = t_all = 0.0
-    for (m, s) in probs:
+    cores = host_cores()
+    prm = O.default_params(max_iters=cfg["max_iters"])
+    P = ds.problems
+    checked, mismatches = {}, []
+
+    def run(i, threads):
+        m, s = P[i]
+        o = O.match_problem(ds.model_desc[m], ds.model_kp[m], ds.scene_desc[s], ds.scene_kp[s], prm, threads)
+        if i not in checked:
+            d = _cmp_problem(o, gpu_res[i], gpu_detail(i))
+            checked[i] = d
+            if d:
+                mismatches.append((i, d))
+        return o
+
+    ids = [(7 * k) % len(P) for k in range(max(n_sample, 2))]
+    times = []
+    for i in ids:
         t0 = time.perf_counter()
-        O.match_problem(ds.model_desc[m], ds.model_kp[m], ds.scene_desc[s], ds.scene_kp[s], prm, threads)
-        t_all += time.perf_counter() - t0
-    return {"value": len(probs) / t_all, "unit": "problems/s", "cores": threads, "kind": "port",
-            "sample": f"{len(probs)} problems of the same workload (10k x 10k knn on {threads} threads like "
-                      f"OpenCV parallel_for_, RANSAC single-threaded as cv::findHomography), "
-                      f"{t_all:.1f} s total, oracle/mim_oracle.c -O3 -ffp-contract=off"}
+        run(i, cores)
+        times.append(time.perf_counter() - t0)
+        log(f"cpu baseline: problem {i} {times[-1]:.2f} s")
+    seq = 1.0 / statistics.median(times[1:])
+    par_times = []
+    with ThreadPoolExecutor(cores) as ex:
+        for rnd in range(rounds + 1):
+            batch = [(rnd * cores + k) % len(P) for k in range(cores)]
+            t0 = time.perf_counter()
+            list(ex.map(lambda i: run(i, 1), batch))
+            if rnd:
+                par_times.append(time.perf_counter() - t0)
+            log(f"cpu baseline: parallel round {rnd} {time.perf_counter() - t0:.2f} s")
+    par = cores / statistics.median(par_times)
+    return {"value": round(seq, 4), "unit": "problems/s", "cores": cores, "kind": "port",
+            "cpu_model": cpu_model(),
+            "sample": f"{len(ids)} problems of the same workload one after another (1 warm-up, median of "
+                      f"{len(ids) - 1}): kNN on {cores} threads like OpenCV parallel_for_, RANSAC single-threaded "
+                      f"as cv::findHomography; oracle/mim_oracle.c -O3 -ffp-contract=off",
+            "parallel": {"value": round(par, 4), "unit": "problems/s", "cores": cores,
+                         "sample": f"{cores} problems at once, one per core (kNN and RANSAC single-threaded), "
+                                   f"1 warm-up + {rounds} rounds, median"},
+            "parity": {"checked": len(checked), "mismatch": len(mismatches),
+                       "first": mismatches[0] if mismatches else None}}
 
 
+def cpu_baseline_knn(q, t, idx_gpu, dist_gpu, n_rows):
+    """C5: the oracle's batchDistance(K=2) restatement on all host cores over n_rows query rows of the
+    50k set against the full 50k train set (1 warm-up + median of 5), bit-compared with the GPU rows."""
+    from oracle import oracle as O
+    O.build()
+    cores = host_cores()
+    rows = np.linspace(0, q.shape[0] - 1, n_rows).astype(np.int64)
+    times = []
+    mism = 0
+    for r in range(6):
+        sub = rows[r::6] if r else rows[:max(1, n_rows // 6)]
+        t0 = time.perf_counter()
+        i_o, d_o = O.knn2(q[sub], t, cores)
+        times.append((time.perf_counter() - t0) / len(sub))
+        mism += int(np.sum(np.any(i_o != idx_gpu[sub], axis=1) | np.any(d_o.view(np.int32) != dist_gpu[sub].view(np.int32),
+                                                                        axis=1)))
+    per_row = statistics.median(times[1:])
+    ops = 2.0 * t.shape[0] * 128
+    return {"value": round(ops / per_row / 1e9, 3), "unit": "GOP/s (distance)", "cores": cores, "kind": "port",
+            "cpu_model": cpu_model(),
+            "sample": f"{n_rows} query rows x {t.shape[0]} train rows in 6 slices (1 warm-up, median of 5) on "
+                      f"{cores} threads, oracle batchDistance restatement",
+            "problems_per_s_equiv": round(1.0 / (per_row * q.shape[0]), 6),
+            "parity": {"checked": int(n_rows + max(1, n_rows // 6)), "mismatch": mism}}
+
+
+# ------------------------------------------------------------------------------------------------
 def main():
     args = parse()
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))  # children only: this process never touches the GPU
+    if args.dry_run:
+        return dry_run(args)
+    rank, world, local = dist_env()
     import torch
     import torch.distributed as dist
 
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    ranks_seen = dist.get_world_size() if world > 1 else 1
+    if ranks_seen != args.gpus:
+        raise SystemExit(f"rank {rank}: {ranks_seen} ranks in the process group, --gpus {args.gpus}")
     dev = torch.device("cuda", local)
 
     from computervision_objectdetection_featurematching_amd import Matcher, build, default_params, shard
     from computervision_objectdetection_featurematching_amd._lib import RESULT_DTYPE
-    from computervision_objectdetection_featurematching_amd.synthetic import CONFIGS, SEED_BASE, make_dataset
+    from computervision_objectdetection_featurematching_amd.synthetic import CONFIGS, SEED_BASE, make_config_dataset
 
     build.build()
     cfg = CONFIGS[args.config]
-    # every rank: the same 3 models, its own scenes (seeded by rank)
-    ds = make_dataset(cfg["n_models"], cfg["n_scenes"], cfg["nq"], cfg["nt"], cfg["n_plant"],
-                      seed=SEED_BASE + 1000 * rank)
+    knn_only = bool(cfg.get("knn_only"))
+    # every rank: the same models, its own scenes (seeded by rank)
+    ds = make_config_dataset(args.config, seed=SEED_BASE + 1000 * rank)
     n_probs = len(ds.problems)
     mdesc = [torch.from_numpy(d).to(dev) for d in ds.model_desc]
     mkp = [torch.from_numpy(k).to(dev) for k in ds.model_kp]
@@ -111,16 +300,18 @@ def main():
     skp = [torch.from_numpy(k).to(dev) for k in ds.scene_kp]
     torch.cuda.synchronize()
 
-    nf = args.inflight if args.inflight > 0 else (3 if world == 1 else 2)
+    nf = args.inflight if args.inflight > 0 else (1 if knn_only else (3 if world == 1 else 2))
     if nf > 1:  # the sampler stream helps one batch alone (+5 %), not batches already overlapping
         os.environ.setdefault("MIM_SAMPLER_STREAM", "0")
     matchers = [Matcher(local) for _ in range(nf)]
     # each context keeps its own non-blocking HIP stream; torch work of a step (the result gather)
     # is ordered on the same stream
     streams = [torch.cuda.ExternalStream(mm.stream_handle(), device=dev) for mm in matchers]
-    prm = default_params(max_iters=cfg["max_iters"])
+    prm = default_params(max_iters=max(cfg["max_iters"], 1))
     mine = [torch.empty(n_probs * RESULT_DTYPE.itemsize, dtype=torch.uint8, device=dev) for _ in range(nf)]
-    gathered = [None]
+    nq0 = int(ds.model_desc[0].shape[0])
+    knn_idx = torch.empty((nq0, 2), dtype=torch.int32, device=dev)
+    knn_dist = torch.empty((nq0, 2), dtype=torch.float32, device=dev)
     counter = [0]
 
     def step():
@@ -131,17 +322,21 @@ def main():
             m.clear_sets()
             q_ids = [m.add_set(d, kp) for d, kp in zip(mdesc, mkp)]
             t_ids = [m.add_set(d, kp) for d, kp in zip(sdesc, skp)]
+            if knn_only:  # C5: the distance contraction + top-2 alone
+                m.knn_sets_dev(q_ids[0], t_ids[0], knn_idx, knn_dist)
+                return
             m.match_batch_async([(q_ids[a], t_ids[b]) for a, b in ds.problems], prm)
             m.batch_results_copy_to(mine[k])
-            gathered[0] = shard.gather_results(mine[k], world)  # RCCL all-gather of the result records
+            shard.gather_results(mine[k], world)  # RCCL all-gather of the result records
 
     for mm in matchers:
         mm.set_timing(False)
     for _ in range(max(args.warmup, nf if args.warmup > 0 else 0)):
         step()
     torch.cuda.synchronize()
-    # parity spot check of the warm-up output (not timed)
-    res = matchers[0].batch_results(n_probs)
+    # the warm-up output: records (and, for the CPU parity sample, good lists + masks) of context 0
+    m0 = matchers[0]
+    res = None if knn_only else m0.batch_results(n_probs)
 
     for mm in matchers:
         mm.set_timing(not args.no_timing)
@@ -151,26 +346,28 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step()  # no host wait inside the loop: steps queue back to back on the stream
+        step()  # no host wait inside the loop: steps queue back to back on the streams
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
+    names = ("knn", "ratio") if knn_only else ("knn", "ratio", "attempt", "chain", "check", "sample", "hypo", "score",
+                                               "cand", "exact", "select", "refine")
     if not args.no_timing:
         for mm in matchers:
-            mm.batch_results(n_probs)  # collects the HIP events of every timed step (outside the timed region)
-        for k in ("knn", "ratio", "attempt", "chain", "check", "sample", "hypo", "score", "cand", "exact", "select",
-                  "refine"):
+            if knn_only:
+                mm.synchronize()
+            mm.batch_results(0)  # collects the HIP events of every timed step (outside the timed region)
+        for k in names:
             kern[k] = sum(max(mm.kernel_ms(k), 0.0) for mm in matchers)
     # the same kernels without a concurrent batch (one context, steps back to back; not part of `value`)
     iso = {}
     if not args.no_timing and nf > 1:
-        m0 = matchers[0]
         for _ in range(args.steps):
             counter[0] = 0  # always context 0
             step()
         torch.cuda.synchronize()
-        m0.batch_results(n_probs)
+        m0.batch_results(0)
         iso = {k: max(m0.kernel_ms(k), 0.0) / max(args.steps, 1) for k in kern}
     if world > 1:
         t = torch.tensor([el], dtype=torch.float64, device=dev)
@@ -180,30 +377,33 @@ def main():
     value = total / el
 
     if rank == 0:
-        knn_flops = 2.0 * cfg["nq"] * cfg["nt"] * 128 * n_probs
-        knn_bytes = (4 * 128 * (cfg["nq"] + cfg["nt"]) + 16 * cfg["nq"]) * n_probs
-        # bound kernel: every produced iteration's hypothesis is tested on every good match
-        point_evals = float(np.sum(res["iters"].astype(np.float64) * res["n_good"]))
+        nq_all = np.array([d.shape[0] for d in ds.model_desc])
+        nt_all = np.array([d.shape[0] for d in ds.scene_desc])
+        pq = np.array([nq_all[m] for m, _ in ds.problems], np.float64)
+        pt = np.array([nt_all[s] for _, s in ds.problems], np.float64)
+        knn_flops = float(np.sum(2.0 * pq * pt * 128))
+        knn_bytes = float(np.sum(4 * 128 * (pq + pt) + 16 * pq))
+        point_evals = 0.0 if knn_only else float(np.sum(res["iters"].astype(np.float64) * res["n_good"]))
         steps = max(args.steps, 1)
         kavg = {k: v / steps for k, v in kern.items()}
         dom = max(kavg, key=kavg.get) if kavg else None
         rooflines = {}
         if kavg.get("knn", 0) > 0:
             ach = knn_flops / (kavg["knn"] * 1e-3) / 1e12
-            t = pmc_traffic("knn2_i8_kernel")
             rooflines["knn"] = {"kernel": "knn2_i8 (distance GEMM on i8 MFMA, exact integer, + top-2 selection), "
-                                          "1 launch/step; flops = 2*Nq*Nt*128 integer ops, peak = dense i8",
+                                          "1 launch/step; ops = 2*Nq*Nt*128 integer ops, peak = dense i8",
                                 "bound": "mfma",
                                 "achieved": round(ach, 2), "peak": PEAK_I8_TOPS, "unit": "TFLOP/s",
-                                "frac": round(ach / PEAK_I8_TOPS, 4), "traffic": t,
+                                "frac": round(ach / PEAK_I8_TOPS, 4),
+                                "traffic": pmc_traffic("knn2_i8_kernel", args.config),
                                 "algorithmic_bytes": knn_bytes,
                                 "achieved_hbm_GBs": round(knn_bytes / (kavg["knn"] * 1e-3) / 1e9, 1)}
         if kavg.get("score", 0) > 0:
             ach = FLOP_PER_POINT_EVAL * point_evals / (kavg["score"] * 1e-3) / 1e12
-            t = pmc_traffic("ransac_bound")
             rooflines["score"] = {"kernel": "ransac_bound (closed-form hypotheses, bounded inlier counts), 2 launches/step",
                                   "bound": "valu", "achieved": round(ach, 2), "peak": PEAK_F32_VALU_TFLOPS,
-                                  "unit": "TFLOP/s", "frac": round(ach / PEAK_F32_VALU_TFLOPS, 4), "traffic": t,
+                                  "unit": "TFLOP/s", "frac": round(ach / PEAK_F32_VALU_TFLOPS, 4),
+                                  "traffic": pmc_traffic("ransac_bound", args.config),
                                   "point_evals_per_step": point_evals,
                                   "hypothesis_point_evals_per_s": round(point_evals / (kavg["score"] * 1e-3), 1)}
         roof = None
@@ -212,7 +412,7 @@ def main():
             roof = dict(rooflines[key])
             roof["dominant_kernel_by_time"] = dom
             roof["kernel_ms_per_step"] = {k: round(v, 3) for k, v in kavg.items()}
-            if iso:  # per-kernel times of one batch alone (no overlap with the other in-flight batch)
+            if iso:  # per-kernel times of one batch alone (no overlap with the other in-flight batches)
                 roof["isolated_kernel_ms_per_step"] = {k: round(v, 3) for k, v in iso.items()}
                 for key2, r in rooflines.items():
                     t_iso = iso.get(key2, 0)
@@ -221,25 +421,46 @@ def main():
                         r["isolated_frac"] = round(r["isolated_achieved"] / r["peak"], 4)
                 roof.update({k: v for k, v in rooflines[key].items() if k.startswith("isolated")})
             roof["others"] = {k: v for k, v in rooflines.items() if k != key}
-        accepted = int((res["status"] == 0).sum())
+        metric = {"c3": "matches+homographies/sec (10k x 10k SIFT, 50k RANSAC iters)",
+                  "c2": "matches+homographies/sec (2k x 2k SIFT, 2k RANSAC iters)",
+                  "c1": "matches+homographies/sec (C1 surrogate: 29 views x 5 scales, ragged 100-500 x 1k-4k, "
+                        "2k RANSAC iters)",
+                  "c5": "knnMatch(k=2) problems/sec (50k x 50k SIFT dense distance contraction)"}[args.config]
+        if cfg.get("ragged"):
+            workload = (f"c1: {len(ds.model_desc)} model views (Nq {nq_all.min()}-{nq_all.max()}) x {len(ds.scene_desc)} "
+                        f"scene scales (Nt {nt_all.min()}-{nt_all.max()}) per GPU, maxIters {cfg['max_iters']}")
+        elif knn_only:
+            workload = f"c5: {cfg['nq']} x {cfg['nt']} descriptors, distance + top-2 only"
+        else:
+            workload = (f"{args.config}: {cfg['n_models']} models x {cfg['n_scenes']} scenes per GPU, "
+                        f"{cfg['nq']}x{cfg['nt']} descriptors, maxIters {cfg['max_iters']}")
         out = {
-            "metric": "matches+homographies/sec (10k x 10k SIFT, 50k RANSAC iters)" if args.config == "c3"
-            else "matches+homographies/sec (2k x 2k SIFT, 2k RANSAC iters)",
-            "value": round(value, 3), "unit": "problems/s", "n_gpus": world, "steps": args.steps,
+            "metric": metric, "value": round(value, 3), "unit": "problems/s", "n_gpus": world,
+            "ranks_seen": ranks_seen, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(1e3 * el / args.steps, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None,
-            "dtype": "i8-MFMA exact-int distances (i32 acc), fp64 DLT/Jacobi, fp32 reprojection",
-            "data": "synthetic SIFT-like integer descriptors (seeded), planted 8% geometric inliers",
-            "config": {"workload": f"{args.config}: {cfg['n_models']} models x {cfg['n_scenes']} scenes per GPU, "
-                                   f"{cfg['nq']}x{cfg['nt']} descriptors, maxIters {cfg['max_iters']}",
-                       "problems_per_gpu": n_probs, "global_batch": world * n_probs, "parallelism": f"dp{world}",
-                       "batches_in_flight": nf},
-            "accepted_problems_rank0": accepted,
+            "dtype": "i8-MFMA exact-int distances (i32 acc)" + ("" if knn_only else
+                                                               ", fp64 DLT/Jacobi, fp32 reprojection"),
+            "data": "synthetic SIFT-like integer descriptors (seeded)" + ("" if knn_only else
+                                                                        ", planted geometric inliers"),
+            "config": {"workload": workload, "problems_per_gpu": n_probs, "global_batch": world * n_probs,
+                       "parallelism": f"dp{world}", "batches_in_flight": nf},
         }
+        if res is not None:
+            out["accepted_problems_rank0"] = int((res["status"] == 0).sum())
+            out["stream_short_rank0"] = int((res["status"] == 5).sum())
         if roof:
             out["roofline"] = roof
-        if args.cpu_problems > 0:
-            out["cpu_baseline"] = cpu_baseline(ds, cfg, args.cpu_problems)
+        if args.cpu_sample > 0:
+            if knn_only:
+                m0.synchronize()
+                out["cpu_baseline"] = cpu_baseline_knn(ds.model_desc[0], ds.scene_desc[0], knn_idx.cpu().numpy(),
+                                                       knn_dist.cpu().numpy(), 96 * args.cpu_sample)
+            else:
+                def detail(i):
+                    return m0.problem_detail(i, int(res["n_good"][i]))
+                out["cpu_baseline"] = cpu_baseline_problems(ds, cfg, res, detail, args.cpu_sample, args.cpu_rounds)
+            out["parity"] = out["cpu_baseline"]["parity"]
         print(json.dumps(out), flush=True)
     for mm in matchers:
         mm.close()

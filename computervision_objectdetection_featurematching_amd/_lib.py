@@ -10,7 +10,8 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 SO_PATH = os.environ.get("MIM_LIB") or os.path.join(_HERE, "lib", "libmim.so")  # MIM_LIB: variant builds
 
 MIM_OK, MIM_EINVAL, MIM_ENOMODEL, MIM_EDEVICE, MIM_ENOMEM, MIM_ERANGE = range(6)
-STATUS_NAMES = {0: "accepted", 1: "few_good", 2: "empty_H", 3: "few_inliers", 4: "bad_det"}
+STATUS_NAMES = {0: "accepted", 1: "few_good", 2: "empty_H", 3: "few_inliers", 4: "bad_det", 5: "stream_short"}
+MIM_STREAM_SHORT = 5
 
 # every symbol include/mim.h declares (checked by tests/test_abi.py)
 EXPORTS = [
@@ -50,30 +51,6 @@ assert RESULT_DTYPE.itemsize == C.sizeof(Result)
 _lib = None
 
 
-class _Lazy:
-    """Attribute setter that tolerates symbols a partial build does not export yet."""
-
-    def __init__(self, cdll):
-        object.__setattr__(self, "_cdll", cdll)
-
-    def __getattr__(self, name):
-        cd = object.__getattribute__(self, "_cdll")
-        if hasattr(cd, name):
-            return getattr(cd, name)
-        return _Missing(name)
-
-
-class _Missing:
-    def __init__(self, name):
-        self.__dict__["name"] = name
-
-    def __setattr__(self, k, v):
-        pass
-
-    def __call__(self, *a, **k):
-        raise MimError(-1, f"{self.name} is not exported by this libmim.so build")
-
-
 def load():
     global _lib
     if _lib is not None:
@@ -81,7 +58,11 @@ def load():
     if not os.path.exists(SO_PATH):
         raise ImportError(f"{SO_PATH} is missing: run `python -m computervision_objectdetection_featurematching_amd.build`"
                           " (there is no CPU fallback)")
-    L = _Lazy(C.CDLL(SO_PATH))
+    try:  # one HIP runtime per process: libmim.so binds libamdhip64.so.7 by soname, and torch's own copy
+        import torch  # noqa: F401  (ROCm wheel) fails to initialise if the system one was loaded first
+    except ImportError:
+        pass
+    L = C.CDLL(SO_PATH)
     vp, i32, f32p, f64p, u8p, i32p = C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p
     L.mim_version.restype = C.c_char_p
     L.mim_default_params.argtypes = [C.POINTER(Params)]

@@ -28,6 +28,8 @@ void launch_ratio(const ProbDev* probs, int n_probs, const Top2* parts, float ra
                   int32_t* good_t, float4* pts, int* n_good, int32_t* knn_idx, float* knn_dist,
                   hipStream_t st);
 size_t ransac_chain_bytes();
+void launch_rng_stream(const unsigned long long* seg_state, uint32_t* out, long long len, int seg, int n_seg,
+                       hipStream_t s);
 void ransac_enqueue(const RansacParams& prm, int n_probs, const ProbDev* probs, const float4* pts,
                     const int* n_good, const RansacBufs& b, uint8_t* masks, mim_result* results, int raw,
                     hipStream_t s, void (*mark)(void*, const char*, hipStream_t), void* mark_ctx, int exact_all);
@@ -169,6 +171,15 @@ struct mim_ctx {
     PinnedStage prep_stage;
     DevBuf prep_jobs;
     int last_n = 0;
+    // the last mim_batch_run, kept so that mim_batch_results can re-run it on a longer RNG stream
+    // (possible while its sets are intact: sets_gen unchanged since the batch)
+    std::vector<mim_problem> last_problems;
+    mim_params last_params{};
+    long long sets_gen = 0, last_gen = -1;
+    // MIM_CAND_CAP: candidate-list capacity override (test knob for the replay's overflow rescan)
+    int cand_cap = 0;
+    // MIM_STREAM_DRAWS: initial RNG stream length (test knob for the grow-and-re-run path)
+    long long stream_draws = 0;
     // MIM_RANSAC_EXACT=1: evaluate every hypothesis exactly (reference mode for cross-checks)
     int exact_all = 0;
     // Pipelined batches: mim_batch_run splits the problems into groups, each on its own stream,
@@ -252,6 +263,10 @@ mim_status mim_ctx_create(int device, mim_ctx** out) {
     c->cur = c->own;
     const char* ex = getenv("MIM_RANSAC_EXACT");
     c->exact_all = (ex && ex[0] == '1') ? 1 : 0;
+    const char* cc = getenv("MIM_CAND_CAP");
+    c->cand_cap = cc ? std::max(1, atoi(cc)) : 0;
+    const char* sd = getenv("MIM_STREAM_DRAWS");
+    c->stream_draws = sd ? std::max(4096LL, atoll(sd)) : 0;
     *out = c;
     return MIM_OK;
 }
@@ -318,8 +333,6 @@ static mim_status set_create_locked(mim_ctx* c, const float* desc, const float* 
                                     int32_t on_device, int32_t* set_id) {
     if (!set_id || n < 0 || (n > 0 && (!desc || !kp))) return fail(c, MIM_EINVAL, "set_create: bad arguments");
     if (dim != kDim) return fail(c, MIM_EINVAL, "set_create: dim must be %d (got %d)", kDim, dim);
-    if (n >= (1 << 18))  // BFMatcher::knnMatchImpl asserts trainDescCollection rows < 1<<18 (IMGIDX_SHIFT)
-        return fail(c, MIM_EINVAL, "set_create: n=%d exceeds OpenCV's 2^18 train-row limit", n);
     HIPCHK(c, hipSetDevice(c->device));
     SetRec r{};
     r.d.n = n;
@@ -398,6 +411,7 @@ mim_status mim_sets_clear(mim_ctx* c) {
     c->pend.clear();
     c->pend_set.clear();
     c->arena.rewind();
+    ++c->sets_gen;
     return MIM_OK;
 }
 
@@ -424,6 +438,9 @@ static mim_status build_tables(mim_ctx* c, const mim_problem* problems, int n, i
         const int qs = problems[i].query_set, ts = problems[i].train_set;
         if (qs < 0 || qs >= (int)c->sets.size() || ts < 0 || ts >= (int)c->sets.size())
             return fail(c, MIM_EINVAL, "problem %d: bad set id (%d, %d)", i, qs, ts);
+        if (c->sets[ts].d.n >= (1 << 18))  // BFMatcher::knnMatchImpl: train rows < 1 << 18 (IMGIDX_SHIFT)
+            return fail(c, MIM_EINVAL, "problem %d: train set of %d rows exceeds OpenCV's 2^18 limit", i,
+                        c->sets[ts].d.n);
         total_qblocks += (c->sets[qs].d.n + kKnnBlockQ - 1) / kKnnBlockQ;
     }
     // split the train side until the grid has ~2 blocks per CU (MIM_KNN_TARGET: blocks wanted)
@@ -587,6 +604,8 @@ mim_status mim_knn2_l2(mim_ctx* c, const float* q, int32_t nq, const float* t, i
     HIPCHK(c, hipStreamSynchronize(c->stream));
     ev_collect(c);
     c->sets.resize(base);  // arena space is reclaimed at the next mim_sets_clear
+    c->last_n = 0;         // no RANSAC records: the previous batch's are invalidated (mim.h)
+    c->last_gen = -1;
     return MIM_OK;
 }
 
@@ -638,6 +657,7 @@ mim_status mim_ratio_filter(mim_ctx* c, const int32_t* idx, const float* dist, i
     }
     *n_good = ng;
     c->last_n = 0;
+    c->last_gen = -1;
     return MIM_OK;
 }
 
@@ -658,6 +678,8 @@ mim_status mim_knn2_sets_dev(mim_ctx* c, int32_t query_set, int32_t train_set, i
                  c->good_t.as<int32_t>(), c->pts.as<float4>(), c->n_good.as<int>(), idx_dev, dist_dev, c->stream);
     HIPCHK(c, hipGetLastError());
     ev_mark(c, "ratio");
+    c->last_n = 0;  // no RANSAC records (mim.h)
+    c->last_gen = -1;
     return MIM_OK;
 }
 
@@ -674,25 +696,61 @@ static void mark_cb(void* vc, const char* name, hipStream_t st) {
     c->cur = keep;
 }
 
-// cv::RNG((uint64)-1).next() stream (core/include/opencv2/core/operations.hpp). Every
-// findHomography call re-seeds, so one stream serves all problems; generated once per ctx.
+// cv::RNG((uint64)-1).next() stream (core/include/opencv2/core/operations.hpp).  Every
+// findHomography call re-seeds, so one stream serves all problems of a ctx.  Generated on the
+// device: the MWC state s' = (u32)s * a + (s >> 32) (a = 4164903690) is, from the second state on,
+// the Lehmer sequence s_{n+1} = a * s_n mod (a * 2^32 - 1), so each 4096-draw segment starts from
+// a * ... jump-ahead computed here in 128-bit arithmetic and the device expands the segments.
+constexpr long long kStreamMin = 1LL << 23, kStreamCap = 1LL << 30;  // draws (the cap: 4 GiB)
+constexpr int kStreamSeg = 4096;
+
+static inline unsigned long long mwc_next(unsigned long long s) {
+    return (unsigned long long)(uint32_t)s * 4164903690ULL + (s >> 32);
+}
+static inline unsigned long long mulmod(unsigned long long x, unsigned long long y, unsigned long long m) {
+    return (unsigned long long)(((unsigned __int128)x * y) % m);
+}
+
 static mim_status ensure_stream(mim_ctx* c, long long need) {
     if (c->rws.stream_len >= need) return MIM_OK;
-    long long len = std::max<long long>(need, 1LL << 23);
-    if (len > (1LL << 28)) return fail(c, MIM_ERANGE, "RNG stream of %lld draws exceeds the 2^28 cap", len);
-    std::vector<uint32_t> h((size_t)len);
-    uint64_t st = 0xffffffffffffffffULL;
-    for (long long i = 0; i < len; ++i) {
-        st = (uint64_t)(uint32_t)st * 4164903690U + (uint32_t)(st >> 32);
-        h[(size_t)i] = (uint32_t)st;
+    long long len = std::max(need, kStreamMin);
+    if (c->stream_draws && c->rws.stream_len == 0) len = c->stream_draws;  // test knob: first stream only
+    if (len > kStreamCap) return fail(c, MIM_ERANGE, "RNG stream of %lld draws exceeds the 2^30 cap", len);
+    len = (len + kStreamSeg - 1) / kStreamSeg * kStreamSeg;
+    const int n_seg = (int)(len / kStreamSeg);
+    const unsigned long long a = 4164903690ULL, m = a * 4294967296ULL - 1;
+    std::vector<unsigned long long> seg((size_t)n_seg);
+    const unsigned long long s0 = mwc_next(~0ULL), s1 = mwc_next(s0);
+    // a^(kStreamSeg) and a^(kStreamSeg - 1) mod m
+    unsigned long long J = 1, Jm1 = 1;
+    for (int k = 0; k < kStreamSeg; ++k) {
+        Jm1 = J;
+        J = mulmod(J, a, m);
     }
+    seg[0] = s0;
+    if (n_seg > 1) seg[1] = mulmod(Jm1, s1, m);  // s_{4096} = a^4095 s_1
+    for (int i = 2; i < n_seg; ++i) seg[(size_t)i] = mulmod(seg[(size_t)i - 1], J, m);
     HIPCHK(c, hipStreamSynchronize(c->stream));
     // 64 zero draws of padding: the draw prefetches of resolve_at may read up to 7 past the end
     HIPCHK(c, c->rws.stream.ensure(sizeof(uint32_t) * (len + 64)));
-    HIPCHK(c, hipMemcpy(c->rws.stream.p, h.data(), sizeof(uint32_t) * len, hipMemcpyHostToDevice));
-    HIPCHK(c, hipMemset((uint32_t*)c->rws.stream.p + len, 0, sizeof(uint32_t) * 64));
+    DevBuf segs;
+    HIPCHK(c, segs.ensure(sizeof(unsigned long long) * n_seg));
+    HIPCHK(c, hipMemcpy(segs.p, seg.data(), sizeof(unsigned long long) * n_seg, hipMemcpyHostToDevice));
+    launch_rng_stream(segs.as<unsigned long long>(), c->rws.stream.as<uint32_t>(), len, kStreamSeg, n_seg,
+                      c->stream);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipMemsetAsync((uint32_t*)c->rws.stream.p + len, 0, sizeof(uint32_t) * 64, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    segs.release();
     c->rws.stream_len = len;
     return MIM_OK;
+}
+
+// Longer stream after a batch ran out (status MIM_STREAM_SHORT): x8, up to the cap.
+static mim_status grow_stream(mim_ctx* c) {
+    if (c->rws.stream_len >= kStreamCap)
+        return fail(c, MIM_ERANGE, "RANSAC consumed the whole RNG stream (%lld draws, the cap)", c->rws.stream_len);
+    return ensure_stream(c, std::min(kStreamCap, c->rws.stream_len * 8));
 }
 
 // Buffers and parameters of one RANSAC batch over n problems (allocation only: call before any
@@ -780,6 +838,7 @@ static mim_status ransac_prepare(mim_ctx* c, int n, const mim_params* prm, Ransa
     rp.min_inliers = prm->min_inliers;
     rp.det_lo = prm->det_lo;
     rp.det_hi = prm->det_hi;
+    rp.cand_cap = c->cand_cap;
     return MIM_OK;
 }
 
@@ -836,15 +895,15 @@ static mim_status check_params(mim_ctx* c, const mim_params* p) {
 
 extern "C" {
 
-mim_status mim_batch_run(mim_ctx* c, const mim_problem* problems, int32_t n, const mim_params* params) {
-    if (!c) return MIM_EINVAL;
-    if (n < 0 || (n > 0 && !problems)) return fail(c, MIM_EINVAL, "batch_run: bad arguments");
-    mim_status s = check_params(c, params);
-    if (s != MIM_OK) return s;
-    std::lock_guard<std::mutex> lk(c->mu);
+}  // extern "C"
+
+static mim_status batch_run_locked(mim_ctx* c, const mim_problem* problems, int32_t n, const mim_params* params) {
     HIPCHK(c, hipSetDevice(c->device));
+    c->last_problems.assign(problems, problems + n);
+    c->last_params = *params;
+    c->last_gen = c->sets_gen;
     if (n == 0) { c->last_n = 0; return MIM_OK; }
-    s = build_tables(c, problems, n, std::max(params->max_iters, 1), pick_groups(n));
+    mim_status s = build_tables(c, problems, n, std::max(params->max_iters, 1), pick_groups(n));
     if (s != MIM_OK) return s;
     RansacBufs b;
     RansacParams rp;
@@ -884,17 +943,50 @@ mim_status mim_batch_run(mim_ctx* c, const mim_problem* problems, int32_t n, con
     return MIM_OK;
 }
 
+// Waits for the last batch; if a problem ran out of RNG draws (status MIM_STREAM_SHORT: OpenCV's
+// loop consumed more than the stream holds), grows the stream and re-runs the batch, which is
+// possible while its sets are intact.  `res` receives the final records.
+static mim_status finish_batch_locked(mim_ctx* c, std::vector<mim_result>& res) {
+    for (;;) {
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        ev_collect(c);
+        res.resize((size_t)c->last_n);
+        if (c->last_n > 0)
+            HIPCHK(c, hipMemcpy(res.data(), c->results.p, sizeof(mim_result) * c->last_n, hipMemcpyDeviceToHost));
+        bool short_ = false;
+        for (const mim_result& r : res) short_ |= r.status == MIM_STREAM_SHORT;
+        if (!short_) return MIM_OK;
+        if (c->last_gen != c->sets_gen || c->last_problems.size() != res.size())
+            return fail(c, MIM_ERANGE, "a problem ran out of RNG draws (%lld) and its sets were cleared: re-run the "
+                                       "batch", c->rws.stream_len);
+        mim_status s = grow_stream(c);
+        if (s != MIM_OK) return s;
+        const std::vector<mim_problem> probs = c->last_problems;
+        const mim_params prm = c->last_params;
+        s = batch_run_locked(c, probs.data(), (int32_t)probs.size(), &prm);
+        if (s != MIM_OK) return s;
+    }
+}
+
+extern "C" {
+
+mim_status mim_batch_run(mim_ctx* c, const mim_problem* problems, int32_t n, const mim_params* params) {
+    if (!c) return MIM_EINVAL;
+    if (n < 0 || (n > 0 && !problems)) return fail(c, MIM_EINVAL, "batch_run: bad arguments");
+    mim_status s = check_params(c, params);
+    if (s != MIM_OK) return s;
+    std::lock_guard<std::mutex> lk(c->mu);
+    return batch_run_locked(c, problems, n, params);
+}
+
 mim_status mim_batch_results(mim_ctx* c, mim_result* out) {
     if (!c) return MIM_EINVAL;
     std::lock_guard<std::mutex> lk(c->mu);
     HIPCHK(c, hipSetDevice(c->device));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    ev_collect(c);
-    if (c->last_n > 0 && out)
-        HIPCHK(c, hipMemcpy(out, c->results.p, sizeof(mim_result) * c->last_n, hipMemcpyDeviceToHost));
-    int err = 0;
-    if (c->rws.err.p) HIPCHK(c, hipMemcpy(&err, c->rws.err.p, sizeof(int), hipMemcpyDeviceToHost));
-    if (err & 1) return fail(c, MIM_ERANGE, "RANSAC consumed the whole RNG stream (%lld draws)", c->rws.stream_len);
+    std::vector<mim_result> res;
+    mim_status s = finish_batch_locked(c, res);
+    if (s != MIM_OK) return s;
+    if (out && !res.empty()) memcpy(out, res.data(), sizeof(mim_result) * res.size());
     return MIM_OK;
 }
 
@@ -959,19 +1051,23 @@ mim_status mim_find_homography(mim_ctx* c, const float* src, const float* dst, i
     HIPCHK(c, hipMemcpy(c->probs.p, &P, sizeof P, hipMemcpyHostToDevice));
     c->h_probs.assign(1, P);
     c->h_good_off.assign(1, 0);
-    c->last_n = 1;
-    c->cur = c->stream;
-    ev_mark(c, "begin");
-    s = ransac_locked(c, 1, &prm, 1);
-    if (s != MIM_OK) return s;
+    c->last_n = 1;  // mim_batch_results returns this call's record (mim.h)
+    c->last_gen = -1;
+    c->last_problems.clear();
     mim_result r;
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    ev_collect(c);
-    HIPCHK(c, hipMemcpy(&r, c->results.p, sizeof r, hipMemcpyDeviceToHost));
+    for (;;) {  // a run out of RNG draws is re-run on a longer stream
+        c->cur = c->stream;
+        ev_mark(c, "begin");
+        s = ransac_locked(c, 1, &prm, 1);
+        if (s != MIM_OK) return s;
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        ev_collect(c);
+        HIPCHK(c, hipMemcpy(&r, c->results.p, sizeof r, hipMemcpyDeviceToHost));
+        if (r.status != MIM_STREAM_SHORT) break;
+        s = grow_stream(c);
+        if (s != MIM_OK) return s;
+    }
     HIPCHK(c, hipMemcpy(mask, c->masks.p, n, hipMemcpyDeviceToHost));
-    int err = 0;
-    HIPCHK(c, hipMemcpy(&err, c->rws.err.p, sizeof(int), hipMemcpyDeviceToHost));
-    if (err & 1) return fail(c, MIM_ERANGE, "RANSAC consumed the whole RNG stream");
     if (r.status == MIM_EMPTY_H) {
         for (int i = 0; i < 9; ++i) H[i] = 0;
         memset(mask, 0, n);

@@ -99,6 +99,7 @@ struct RansacParams {
     float ratio;
     int min_good, min_inliers;
     double det_lo, det_hi;
+    int cand_cap;    // candidate-list capacity per problem and chunk (0: kCandPerProblem)
 };
 
 }  // namespace mim

@@ -961,16 +961,6 @@ __global__ __launch_bounds__(256) void ransac_attempt_kernel(const RansacState* 
                 if (4 * k4 + c < D) u[4 * k4 + c] = vv[c];
         }
     }
-#ifdef MIM_PROBE_ATTEMPT_LOADONLY  // timing probe only (flags invalid): loads + store, no compute
-    {
-        unsigned x = 0;
-#pragma unroll
-        for (int k = 0; k < D; ++k) x ^= u[k];
-        const unsigned f = x == 0x12345678u ? 0x82808080u : 0x80808080u;  // keeps the loads alive
-        *reinterpret_cast<uint2*>(flags + (long long)p * wcap + off) = make_uint2(f, f);
-        return;
-    }
-#endif
     if (big) {
 #pragma unroll
         for (int k = 0; k < D; ++k) u[k] = mod_barrett<true>(u[k], mB, N);
@@ -1395,23 +1385,14 @@ __global__ __launch_bounds__(kCheckBlock) void ransac_check_kernel(const ChainSe
     for (int r = 0; r < kCheckPer; ++r)
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-#ifdef MIM_PROBE_CHECK_NOGATHER  // timing probe only (pass bits invalid): no point gathers
-            const float f = (float)idx[r][k];
-            g[r][k] = make_float4(f, f * 0.5f, f * 0.25f, f * 0.125f + (float)k);
-#else
             g[r][k] = P[idx[r][k]];
-#endif
         }
     uint32_t* PB = pass_bits + (long long)p * (wcap / 32);
 #pragma unroll
     for (int r = 0; r < kCheckPer; ++r) {
         const float s4[8] = {g[r][0].x, g[r][0].y, g[r][1].x, g[r][1].y, g[r][2].x, g[r][2].y, g[r][3].x, g[r][3].y};
         const float t4[8] = {g[r][0].z, g[r][0].w, g[r][1].z, g[r][1].w, g[r][2].z, g[r][2].w, g[r][3].z, g[r][3].w};
-#ifdef MIM_PROBE_CHECK_NOSUBSET  // timing probe only: gathers kept, checkSubset replaced
-        const bool pass = valid[r] && (s4[0] + s4[3] + t4[5] + t4[6] > 100.f);
-#else
         const bool pass = valid[r] && check_subset(s4, t4);
-#endif
         const unsigned long long m = __ballot(pass);
         const int w0 = (base + r * kCheckBlock + (threadIdx.x & ~63)) >> 5;  // 2 words per wave
         if (lane == 0 && w0 * 32 < T) PB[w0] = (uint32_t)m;
@@ -1591,22 +1572,9 @@ __global__ __launch_bounds__(64) void ransac_sample_kernel(RansacState* __restri
     long long lb = -(1LL << 40);
     int produced = S.produced, fail_run = S.fail_run;
     bool stop_all = false;
-#ifdef MIM_SAMPLER_PROF
-    const unsigned long long t_start = wall_clock64();
-    int n_round = 0, n_sub = 0, n_fill = 0, n_unk = 0;
-    unsigned long long tp[6] = {0, 0, 0, 0, 0, 0}, tc = clock64();
-#define PROF_T(k) { const unsigned long long t_ = clock64(); tp[k] += t_ - tc; tc = t_; }
-    const int produced0 = produced;
-#define PROF_INC(x) ++x
-#else
-#define PROF_INC(x)
-#define PROF_T(k)
-#endif
     while (!stop_all && produced < target) {
-        PROF_INC(n_round);
         const long long wb = rel & ~15LL;
         if (wb < lb || wb + 1024 > lb + kFlagWin) {  // refill the LDS window at wb
-            PROF_INC(n_fill);
             lb = wb;
             __syncthreads();
 #pragma unroll 4
@@ -1636,8 +1604,6 @@ __global__ __launch_bounds__(64) void ransac_sample_kernel(RansacState* __restri
         const uint32_t wd[4] = {w.x, w.y, w.z, w.w};
         long long s = rel;  // chain position inside [wb, wb + 1024)
         while (s < wb + 1024) {
-            PROF_INC(n_sub);
-            PROF_T(0);
             const int rho = (int)(s - wb) & 3;
             const int a0 = (int)(s - wb) >> 2;  // first attempt of this sub-round (a = 4 lane + i)
             int f[4];
@@ -1646,8 +1612,7 @@ __global__ __launch_bounds__(64) void ransac_sample_kernel(RansacState* __restri
             for (int i = 0; i < 4; ++i) {
                 const int a = 4 * lane + i;
                 int fi = (int)((wd[i] >> (8 * rho)) & 0xFF);
-                if (a >= a0 && fi == kFlagUnknown) PROF_INC(n_unk);
-                // outside the window, or checkSubset not evaluated yet (kPassUnknown): evaluate here
+                                // outside the window, or checkSubset not evaluated yet (kPassUnknown): evaluate here
                 if (a >= a0 && (fi == kFlagUnknown || (fi != kAttemptSerial && (fi & kPassUnknown))))
                     fi = attempt_flag(wbase + wb + 4LL * a + rho, stream, slen, N, M, P);
                 f[i] = fi;
@@ -1656,7 +1621,6 @@ __global__ __launch_bounds__(64) void ransac_sample_kernel(RansacState* __restri
                 Pm[i] = __ballot(a >= a0 && !irr && (fi & 1));
             }
             // first attempt whose length is not 4 draws (or must be resolved here)
-            PROF_T(1);
             int afc = 256;
 #pragma unroll
             for (int i = 0; i < 4; ++i)
@@ -1693,7 +1657,6 @@ __global__ __launch_bounds__(64) void ransac_sample_kernel(RansacState* __restri
                 for (int i = 0; i < 4; ++i) Pm[i] &= (i < e) ? (below | (1ull << L)) : below;
                 if (fcpass) Pm[e] |= 1ull << L;
             }
-            PROF_T(2);
             const int end = afc < 256 ? afc + 1 : 256;  // attempts a0 .. end-1 are walked
             int tot = 0, a_p = BIG, a_lp = -1;
 #pragma unroll
@@ -1722,7 +1685,6 @@ __global__ __launch_bounds__(64) void ransac_sample_kernel(RansacState* __restri
                 for (int i = 0; i < 4; ++i)
                     if (((hb >> i) & 1) && --k == 0) at = 4 * Lh + i;
             }
-            PROF_T(3);
             const int fails_before = (a_p < BIG ? a_p : end) - a0;
             const int af = fail_run + fails_before >= 10000 ? a0 + (10000 - fail_run - 1) : BIG;  // 10000th failure
             int stop = end - 1, got = tot;
@@ -1737,7 +1699,6 @@ __global__ __launch_bounds__(64) void ransac_sample_kernel(RansacState* __restri
                     out[produced + rank] = make_int4((int)(wbase + wb + 4LL * a + rho), (a == afc && fcres) ? -2 : -1, 0, 0);
                 }
             }
-            PROF_T(4);
             produced += got;
             fail_run = hit_t ? 0 : (hit_f ? 10000 : (tot > 0 ? stop - a_lp : fail_run + (end - a0)));
             s = uni64(stop == afc ? endfc : wb + 4LL * (stop + 1) + rho);
@@ -1750,16 +1711,6 @@ __global__ __launch_bounds__(64) void ransac_sample_kernel(RansacState* __restri
         }
         rel = uni64(s);
     }
-#ifdef MIM_SAMPLER_PROF
-    if (lane == 0 && p < 3)
-        printf("[sampler] p=%d c1=%d produced %d->%d draws %lld rounds %d sub %d fills %d unknown %d wlen %d time %.1f us\n",
-               p, c1, produced0, produced, rel, n_round, n_sub, n_fill, n_unk, wlen,
-               (double)(wall_clock64() - t_start) / 100.0);
-    if (lane == 0 && p < 3)
-        printf("[sampler] p=%d cycles: outer %llu ballots %llu afc %llu count %llu store %llu\n", p, tp[0], tp[1], tp[2],
-               tp[3], tp[4]);
-#endif
-#undef PROF_INC
     if (lane == 0) {
         S.stream_pos = wbase + rel;
         S.produced = produced;
@@ -2065,9 +2016,6 @@ __global__ __launch_bounds__(256) void ransac_bound_mfma_kernel(const RansacStat
     const int p = blockIdx.x / bpp;
     const int tid = threadIdx.x, lane = tid & 63;
     const int it = c0 + (blockIdx.x % bpp) * 256 + tid;
-#ifdef MIM_PROBE_BOUND_CYC  // timing probe: per-wave cycles of the hypothesis setup vs the point loop
-    const long long cyc0 = clock64();
-#endif
     const RansacState S = st[p];
     if (!S.active || S.done) return;  // uniform over the block
     if (c0 + (blockIdx.x % bpp) * 256 >= min(c1, S.produced)) return;  // whole block idle
@@ -2162,9 +2110,6 @@ __global__ __launch_bounds__(256) void ransac_bound_mfma_kernel(const RansacStat
         CL0 = lowh ? CL : CLp; EL0 = lowh ? EL : ELp; CL1 = lowh ? CLp : CL; EL1 = lowh ? ELp : EL;
     }
     const bool wave_counts = __any(count);
-#ifdef MIM_PROBE_BOUND_CYC
-    const long long cyc1 = clock64();
-#endif
     float big = INFINITY;
     asm volatile("" : "+v"(big));
     const uint4* __restrict__ T = tiles + (go >> 5) * 128;
@@ -2224,10 +2169,6 @@ __global__ __launch_bounds__(256) void ransac_bound_mfma_kernel(const RansacStat
         lo = (int)(lowh ? i0 : i1);  // zero-padded rows (ex = ey = W = 0) give m - R_lo = E_lo > 0: never "in"
     }
     if (act) bounds[o] = invalid ? make_int2(-1, -1) : (uncertain ? make_int2(0, n) : make_int2(lo, n - outs));
-#ifdef MIM_PROBE_BOUND_CYC
-    if (!kLo && tid == 0 && blockIdx.x % 61 == 0)
-        printf("BOUNDCYC setup %lld loop %lld n %d\n", cyc1 - cyc0, clock64() - cyc1, n);
-#endif
 }
 
 // exact count of one hypothesis (runKernel + computeError + findInliers, bit-exact)
@@ -2235,13 +2176,7 @@ __device__ int exact_count(const float4* __restrict__ P, int n, int4 s4, double*
     const float4 a = P[s4.x], b = P[s4.y], c = P[s4.z], d = P[s4.w];
     const float M[8] = {a.x, a.y, b.x, b.y, c.x, c.y, d.x, d.y};
     const float m[8] = {a.z, a.w, b.z, b.w, c.z, c.w, d.z, d.w};
-#ifdef MIM_REFINE_PROF
-    const unsigned long long e0 = clock64();
-#endif
     if (!run_kernel4<64>(M, m, D, H)) return -1;
-#ifdef MIM_REFINE_PROF
-    const unsigned long long e1 = clock64();
-#endif
     float Hf[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) Hf[i] = (float)H[i];
@@ -2250,9 +2185,6 @@ __device__ int exact_count(const float4* __restrict__ P, int n, int4 s4, double*
         const float4 q = P[i];
         cnt += reproj_err(Hf, q.x, q.y, q.z, q.w) <= thr2;
     }
-#ifdef MIM_REFINE_PROF
-    if (blockIdx.x < 3) printf("[exact] block %d lane %d: kernel4 %llu count %llu (n=%d)\n", blockIdx.x, (int)threadIdx.x, e1 - e0, clock64() - e1, n);
-#endif
     return cnt;
 }
 
@@ -2314,18 +2246,6 @@ __global__ __launch_bounds__(64) void ransac_bound_check_kernel(const RansacStat
     }
 }
 
-__device__ __forceinline__ int wave_excl_prefix_max(int v) {
-    const int lane = threadIdx.x & 63;
-    int incl = v;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const int o = __shfl_up(incl, off);
-        if (lane >= off) incl = max(incl, o);
-    }
-    const int ex = __shfl_up(incl, 1);
-    return lane == 0 ? INT_MIN : ex;
-}
-
 // Split form of the filtered select (default): candidates of every problem are listed first,
 // evaluated exactly by a GPU-wide grid (one lane each), then replayed in order per problem.
 constexpr int kCandWaves = 16;                 // exact-evaluation waves per problem and chunk
@@ -2341,7 +2261,7 @@ __global__ __launch_bounds__(kCandThreads) void ransac_cand_kernel(RansacState* 
                                                                    const ProbDev* __restrict__ probs,
                                                                    const int2* __restrict__ bounds, int c1,
                                                                    int* __restrict__ cand, int* __restrict__ ncand,
-                                                                   int L, int max_iters, double conf) {
+                                                                   int L, int cap) {
     __shared__ int wred[kCandThreads / 64], wred2[kCandThreads / 64];
     const int p = blockIdx.x, tid = threadIdx.x;
     const RansacState S = st[p];
@@ -2355,7 +2275,7 @@ __global__ __launch_bounds__(kCandThreads) void ransac_cand_kernel(RansacState* 
     const int a = min(t1, t0 + tid * ch), e = min(t1, a + ch);
     // batches of 16 unconditional (clamped) loads: one memory latency per batch, not per iteration
     constexpr int kB = 16;
-    int lmax = INT_MIN, hmax = INT_MIN;
+    int lmax = INT_MIN;
     for (int t = a; t < e; t += kB) {
         int2 v[kB];
 #pragma unroll
@@ -2363,16 +2283,11 @@ __global__ __launch_bounds__(kCandThreads) void ransac_cand_kernel(RansacState* 
 #pragma unroll
         for (int k = 0; k < kB; ++k) {
             lmax = t + k < e ? max(lmax, v[k].x) : lmax;
-            // the deferral heuristic ignores the unbounded [0, n] brackets of screened samples
-            // (deferring is exact either way; a wrong guess only costs chunk-2 work)
-            hmax = (t + k < e && !(v[k].x == 0 && v[k].y == S.n)) ? max(hmax, v[k].y) : hmax;
         }
     }
     const int init = max(3, max(S.max_good, S.lo_max));
     int all;
     const int run0 = block_excl_max(lmax, init, wred, all);  // bound before this thread's first iteration
-    int hall;
-    block_excl_max(hmax, 0, wred2, hall);
     int cnt = 0, run = run0;
     for (int t = a; t < e; t += kB) {
         int2 v[kB];
@@ -2388,10 +2303,10 @@ __global__ __launch_bounds__(kCandThreads) void ransac_cand_kernel(RansacState* 
     }
     int total;
     int o = block_excl_sum(cnt, wred2, total);
-    if (cnt && o < kCandCap) {  // ordered list (beyond the capacity the replay kernel rescans)
+    if (cnt && o < cap) {  // ordered list (beyond the capacity the replay kernel rescans)
         int* C = cand + (long long)(2 * p + L) * kCandCap;
         run = run0;
-        for (int t = a; t < e && o < kCandCap; ++t) {
+        for (int t = a; t < e && o < cap; ++t) {
             const int2 b = Bd[t];
             if (b.y > run) C[o++] = t;
             run = max(run, b.x);
@@ -2400,38 +2315,16 @@ __global__ __launch_bounds__(kCandThreads) void ransac_cand_kernel(RansacState* 
     if (tid == 0) {
         ncand[2 * p + L] = total;
         st[p].lo_max = max(S.lo_max, all);
-        // Deferral of chunk 1's exact pass: the candidates of both chunks are evaluated in one pass in
-        // chunk 2 and replayed there in iteration order (one latency-bound exact pass instead of two).
-        // Not after a getSubset failure inside the chunk (the loop ends there) or without a next chunk.
-        if (L == 0) {
-            // defer unless the chunk's lower bounds already prove an early stop inside it (then the
-            // exact pass here saves chunk 2 altogether); a deferral that turns out to stop early only
-            // costs the next chunk's sampling and bounds, never a result
-            const int n = S.n;
-#ifdef MIM_EXACT_DEFER
-            const bool fail_here = S.fail_iter != -1 && S.fail_iter <= c1;
-#endif
-            const int lo_best = min(max(max(all, S.max_good), 0), n);
-            const int nit = update_num_iters(conf, (double)(n - lo_best) / n, 4, S.niters);
-#ifdef MIM_EXACT_DEFER  // opt-in: measured -3 % on C3 (the one combined pass has a longer Jacobi tail)
-            st[p].defer = (c1 < max_iters && !fail_here && nit >= c1) ? 1 : 0;
-#else
-            st[p].defer = 0;
-#endif
-            (void)hall;
-            (void)nit;
-        }
+        // chunk 1's exact pass is never deferred into chunk 2's (measured -3 % on C3: the combined
+        // pass has a longer Jacobi tail); the replay/exact kernels still accept a deferred list
+        if (L == 0) st[p].defer = 0;
     }
 }
 
 // Exact evaluation of the listed candidates: 4 per wave, each solved by a 16-lane group
 // (cooperative Jacobi), then counted by the whole wave.
 constexpr int kExactGroups = 4;
-#ifdef MIM_PROBE_EXACT_WAVES  // timing probe only (drops candidates past 4 x this per problem)
-constexpr int kExactWaves = MIM_PROBE_EXACT_WAVES;
-#else
 constexpr int kExactWaves = kCandCap / kExactGroups;
-#endif
 
 __global__ __launch_bounds__(64) void ransac_exact_kernel(const RansacState* __restrict__ st,
                                                           const ProbDev* __restrict__ probs,
@@ -2441,7 +2334,7 @@ __global__ __launch_bounds__(64) void ransac_exact_kernel(const RansacState* __r
                                                           const int* __restrict__ cand, const int* __restrict__ ncand,
                                                           const int2* __restrict__ bounds,
                                                           int* __restrict__ cex, double* __restrict__ cH, float thr2,
-                                                          int L) {
+                                                          int L, int cap) {
     __shared__ double sd[kExactGroups * kJ9G];
     // blocks: [list pass][wave][problem]; chunk 1 (L = 0): list 0 of the problems not deferred;
     // chunk 2 (L = 1): list 1 of every problem, then list 0 of the deferred ones.  Problem-minor
@@ -2455,7 +2348,7 @@ __global__ __launch_bounds__(64) void ransac_exact_kernel(const RansacState* __r
     if (!S.active || S.done) return;
     if (list == 0 && (L == 0) == (S.defer != 0)) return;  // uniform over the block
     const long long lb = (long long)(2 * p + list) * kCandCap;
-    const int nc = min(ncand[2 * p + list], kCandCap);
+    const int nc = min(ncand[2 * p + list], cap);
     if (w * kExactGroups >= nc) return;  // uniform over the wave
     const bool valid = w * kExactGroups + grp < nc;  // groups past the list only join the counting
     const int k = min(w * kExactGroups + grp, nc - 1);
@@ -2466,9 +2359,6 @@ __global__ __launch_bounds__(64) void ransac_exact_kernel(const RansacState* __r
     double H[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
     int ok = 0;
     const float4* __restrict__ P = pts + probs[p].good_off;
-#ifdef MIM_REFINE_PROF
-    const unsigned long long x0 = clock64();
-#endif
     if (valid && !tight) {  // uniform over the group
         const int4 s4 = decode_sample(samples[probs[p].it_off + t], stream, (unsigned)S.n, S.modM);
         const float4 a = P[s4.x], b = P[s4.y], c = P[s4.z], d = P[s4.w];
@@ -2476,10 +2366,6 @@ __global__ __launch_bounds__(64) void ransac_exact_kernel(const RansacState* __r
         const float m[8] = {a.z, a.w, b.z, b.w, c.z, c.w, d.z, d.w};
         ok = run_kernel4_group(M, m, sd + grp * kJ9G, H);
     }
-#ifdef MIM_REFINE_PROF
-    const unsigned long long x1 = clock64();
-    if (p < 3 && lane == 0) printf("[exact] p=%d w=%d nc=%d tight=%d solve %llu\n", p, w, nc, (int)tight, x1 - x0);
-#endif
     // findInliers of every solved candidate by the whole wave (computeError is per point: the count
     // does not depend on the order)
     float Hf[8];
@@ -2522,7 +2408,7 @@ __global__ __launch_bounds__(64) void ransac_replay_kernel(RansacState* __restri
                                                            const int* __restrict__ ncand, const int* __restrict__ cex,
                                                            const double* __restrict__ cH, int c1, double conf,
                                                            float thr2, double* __restrict__ best_h, int L,
-                                                           int c1_prev) {
+                                                           int c1_prev, int cap) {
     __shared__ double sd[kJ9D * 64];
     const int p = blockIdx.x, lane = threadIdx.x;
     RansacState S = st[p];
@@ -2541,9 +2427,9 @@ __global__ __launch_bounds__(64) void ransac_replay_kernel(RansacState* __restri
     const int* E = cex + (long long)(2 * p + li) * kCandCap;
     const double* HH = cH + (long long)(2 * p + li) * kCandCap * 9;
     int best_k = -1;  // candidate index whose H becomes bestModel (listed part)
-    for (int k0 = 0; k0 < min(nc, kCandCap); k0 += 64) {
+    for (int k0 = 0; k0 < min(nc, cap); k0 += 64) {
         const int k = k0 + lane;
-        const bool in = k < min(nc, kCandCap);
+        const bool in = k < min(nc, cap);
         const int t = in ? C[k] : INT_MAX;
         const int ex = in ? E[k] : -1;
         for (;;) {
@@ -2558,13 +2444,13 @@ __global__ __launch_bounds__(64) void ransac_replay_kernel(RansacState* __restri
         }
     }
     if (best_k >= 0 && lane < 9) best_h[(long long)p * 9 + lane] = HH[(long long)best_k * 9 + lane];
-    if (nc > kCandCap) {
+    if (nc > cap) {
         // overflow (very many candidates): rescan the iterations after the last listed one and
         // evaluate their candidates here, 64 at a time, with the running exact best
         const int2* Bd = bounds + probs[p].it_off;
         const float4* __restrict__ P = pts + probs[p].good_off;
         const int4* Sm = samples + probs[p].it_off;
-        const int start = C[kCandCap - 1] + 1;
+        const int start = C[cap - 1] + 1;
         for (int base = start; base < end && base < S.niters; base += 64) {
             const int t = base + lane;
             const bool valid = t < end;
@@ -2598,78 +2484,6 @@ __global__ __launch_bounds__(64) void ransac_replay_kernel(RansacState* __restri
     const bool failed = S.fail_iter != -1 && S.fail_iter <= end;
     if (S.niters <= end || failed) S.done = 1;
     if (lane == 0) store_select_state(st + p, S);
-}
-
-__global__ __launch_bounds__(64) void ransac_select_filtered_kernel(RansacState* __restrict__ st,
-                                                                    const ProbDev* __restrict__ probs,
-                                                                    const float4* __restrict__ pts,
-                                                                    const int4* __restrict__ samples,
-                                                                    const uint32_t* __restrict__ stream,
-                                                                    const int2* __restrict__ bounds, int c1,
-                                                                    double conf, float thr2,
-                                                                    double* __restrict__ best_h) {
-    __shared__ double sd[kJ9D * 64];
-    __shared__ int cand[64];
-    const int p = blockIdx.x, lane = threadIdx.x;
-    RansacState S = st[p];
-    if (!S.active || S.done) return;
-    const int2* Bd = bounds + probs[p].it_off;
-    const int4* Sm = samples + probs[p].it_off;
-    const float4* __restrict__ P = pts + probs[p].good_off;
-    const int end = min(c1, S.produced);
-    const int N = S.n;
-    int ncand = 0;
-    // exact evaluation of the queued candidates, then their replay in iteration order
-    auto flush = [&]() {
-        if (ncand == 0) return;
-        const int t = lane < ncand ? cand[lane] : INT_MAX;
-        int ex = -1;
-        double H[9];
-        if (lane < ncand && t < S.niters)
-            ex = exact_count(P, N, decode_sample(Sm[t], stream, (unsigned)N, S.modM), sd + lane, thr2, H);
-        int fbest = -1;
-        for (;;) {
-            const int thr = max(S.max_good, 3);
-            const unsigned long long m = __ballot(t < S.niters && ex > thr);
-            if (!m) break;
-            const int f = __ffsll((long long)m) - 1;
-            const int cf = __shfl(ex, f);
-            S.max_good = cf;
-            S.best_iter = __shfl(t, f);
-            S.niters = update_num_iters(conf, (double)(N - cf) / N, 4, S.niters);
-            fbest = f;
-        }
-        if (fbest >= 0 && lane == fbest) {  // keep bestModel: the refine kernel starts from it
-#pragma unroll
-            for (int i = 0; i < 9; ++i) best_h[(long long)p * 9 + i] = H[i];
-        }
-        ncand = 0;
-        __syncthreads();
-    };
-    for (int base = S.next_iter; base < end && base < S.niters; base += 64) {
-        const int t = base + lane;
-        const bool valid = t < end;
-        const int2 b = valid ? Bd[t] : make_int2(-1, -1);
-        const int lb = max(max(3, max(S.max_good, S.lo_max)), wave_excl_prefix_max(b.x));
-        const bool c = valid && t < S.niters && b.y > lb;
-        int wmax = b.x;
-#pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) wmax = max(wmax, __shfl_xor(wmax, off));
-        S.lo_max = max(S.lo_max, wmax);
-        const unsigned long long cm = __ballot(c);
-        const int nc = __popcll(cm);
-        if (nc == 0) continue;
-        if (ncand + nc > 64) flush();
-        const int pos = __builtin_amdgcn_mbcnt_hi((uint32_t)(cm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)cm, 0));
-        if (c) cand[ncand + pos] = t;
-        ncand += nc;
-        __syncthreads();
-    }
-    flush();
-    S.next_iter = end;
-    const bool failed = S.fail_iter != -1 && S.produced <= end;
-    if (S.niters <= end || failed) S.done = 1;
-    if (lane == 0) st[p] = S;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -2985,13 +2799,6 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                                                             int raw, const double* __restrict__ best_h, int exact_all) {
     __shared__ RefineShared sh;
     const int p = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-#ifdef MIM_REFINE_PROF
-    unsigned long long rt[8] = {0, 0, 0, 0, 0, 0, 0, 0}, rc = clock64();
-    int rp_recompute = 0, rp_chol_fail = 0;
-#define RPROF(k) { const unsigned long long t_ = clock64(); rt[k] += t_ - rc; rc = t_; }
-#else
-#define RPROF(k)
-#endif
     const RansacState S = st[p];
     const int ng = n_good_arr[p];
     const long long go = probs[p].good_off;
@@ -3035,9 +2842,6 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                 for (int i = 0; i < 9; ++i) sh.Hb[i] = best_h[(long long)p * 9 + i];  // from the exact pass
             } else if (tid < 16 && (exact_all || best_h[(long long)p * 9 + 8] == 0.0)) {
                 // bestModel = runKernel(sample[best_iter]), bit-identical, by one 16-lane group
-#ifdef MIM_REFINE_PROF
-                rp_recompute = 1;
-#endif
                 const int4 s4 = decode_sample(samples[probs[p].it_off + S.best_iter], stream, (unsigned)S.n, S.modM);
                 const float4 a = P[s4.x], b = P[s4.y], c = P[s4.z], d = P[s4.w];
                 const float M[8] = {a.x, a.y, b.x, b.y, c.x, c.y, d.x, d.y};
@@ -3048,7 +2852,6 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                     for (int i = 0; i < 9; ++i) sh.Hb[i] = Hl[i];
             }
             __syncthreads();
-            RPROF(0);
             float Hf[8];
             for (int i = 0; i < 8; ++i) Hf[i] = (float)sh.Hb[i];
             const float thr2 = (float)(prm.thresh * prm.thresh);
@@ -3077,7 +2880,6 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
             }
             if (tid == 0) sh.n_inl = base;
             __syncthreads();
-            RPROF(1);
             const int k = sh.n_inl;
             if (k > 0) {
                 // ---- refit: runKernel over all inliers (parallel sums; contract is |dH| <= 1e-4) ----
@@ -3114,7 +2916,6 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                             for (int kk = j; kk < 9; kk++, ++e) lt[e] += Lx[j] * Lx[kk] + Ly[j] * Ly[kk];
                     }
                     block_sum<45>(lt, sh.red);
-                    RPROF(2);
                     const double invHnorm[9] = {1. / smx, 0, cmx, 0, 1. / smy, cmy, 0, 0, 1};
                     const double Hnorm2[9] = {sMx, 0, -cMx * sMx, 0, sMy, -cMy * sMy, 0, 0, 1};
                     if (tid == 0) {
@@ -3148,7 +2949,6 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                 // ---- LMSolverImpl (levmarq.cpp) on H8 = H[0..7], maxIters 10, eps FLT_EPSILON ----
                 if (tid < 8) sh.x[tid] = sh.H[tid];
                 __syncthreads();
-                RPROF(3);
                 double x[8];
                 for (int i = 0; i < 8; ++i) x[i] = sh.x[i];
                 double A[64], v[8], Sv, rinf;
@@ -3166,9 +2966,6 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                         for (int i = 0; i < 64; ++i) Ap[i] = sh.A[i];
                         for (int i = 0; i < 8; ++i) Ap[9 * i] += sh.lambda * sh.D[i];
                         if (!solve_chol8(Ap, sh.v, sh.d)) {
-#ifdef MIM_REFINE_PROF
-                            ++rp_chol_fail;
-#endif
                             solve_eig8(Ap, sh.v, sh.d, sh.J9);
                         }
                         double dinf = 0;
@@ -3234,12 +3031,6 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                 }
                 if (tid < 8) sh.H[tid] = sh.x[tid];
                 __syncthreads();
-                RPROF(4);
-#ifdef MIM_REFINE_PROF
-                if (tid == 0)
-                    printf("[refine] p=%d recompute %d: best %llu mask %llu sums %llu refit %llu LM %llu (iters %d chol_fail %d) k=%d invit %d\n",
-                           p, rp_recompute, rt[0], rt[1], rt[2], rt[3], rt[4], iter, rp_chol_fail, k, sh.flag);
-#endif
             } else if (tid == 0) {
                 for (int i = 0; i < 9; ++i) sh.H[i] = sh.Hb[i];
             }
@@ -3253,7 +3044,8 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
     if (tid != 0) return;
     res.n_inl = ok ? sh.n_inl : 0;
     if (!ok) {
-        res.status = MIM_EMPTY_H;
+        // the RNG stream ran out before the loop ended: the host grows it and re-runs the batch
+        res.status = (S.active && S.fail_iter == -2) ? MIM_STREAM_SHORT : MIM_EMPTY_H;
     } else {
         for (int i = 0; i < 9; ++i) res.H[i] = sh.H[i];
         const double* H = sh.H;
@@ -3275,6 +3067,28 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
 // host orchestration (called by api.cpp with the ctx mutex held)
 // ------------------------------------------------------------------------------------------------
 size_t ransac_chain_bytes() { return sizeof(ChainSegs); }
+
+// cv::RNG((uint64)-1).next() stream (core/include/opencv2/core/operations.hpp): thread i expands
+// segment i from its start state (computed on the host by jump-ahead) with the MWC recurrence
+// state = (u32)state * 4164903690 + (state >> 32), emitting the low 32 bits.
+__global__ __launch_bounds__(256) void rng_stream_kernel(const unsigned long long* __restrict__ seg_state,
+                                                         uint32_t* __restrict__ out, long long len, int seg,
+                                                         int n_seg) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_seg) return;
+    unsigned long long st = seg_state[i];
+    const long long p0 = (long long)i * seg;
+    const int m = (int)min((long long)seg, len - p0);
+    for (int k = 0; k < m; ++k) {
+        out[p0 + k] = (uint32_t)st;
+        st = (unsigned long long)(uint32_t)st * 4164903690ull + (st >> 32);
+    }
+}
+
+void launch_rng_stream(const unsigned long long* seg_state, uint32_t* out, long long len, int seg, int n_seg,
+                       hipStream_t s) {
+    rng_stream_kernel<<<(n_seg + 255) / 256, 256, 0, s>>>(seg_state, out, len, seg, n_seg);
+}
 
 void ransac_enqueue(const RansacParams& prm, int n_probs, const ProbDev* probs, const float4* pts,
                     const int* n_good, const RansacBufs& b, uint8_t* masks, mim_result* results, int raw,
@@ -3298,6 +3112,9 @@ void ransac_enqueue(const RansacParams& prm, int n_probs, const ProbDev* probs, 
         mark(mark_ctx, "fork", ss);
     }
     int ci = 0, c1_first = 0;
+    // listed candidates per problem and chunk (MIM_CAND_CAP < 1024: test knob forcing the replay's
+    // overflow rescan)
+    const int cap = prm.cand_cap > 0 ? std::min(prm.cand_cap, kCandCap) : kCandCap;
     while (c0 < max_iters) {
         const int c1 = (int)std::min<long long>((long long)c0 + chunk, max_iters);
         // attempt outcomes for a window of ~28 draws per wanted iteration (pass rate ~1/5), the walk
@@ -3368,7 +3185,7 @@ void ransac_enqueue(const RansacParams& prm, int n_probs, const ProbDev* probs, 
             }
             const int L = c0 == 0 ? 0 : 1;  // candidate list of this chunk (at most two chunks)
             ransac_cand_kernel<<<n_probs, kCandThreads, 0, s>>>(b.state, probs, b.bounds, c1, b.cand, b.ncand, L,
-                                                                max_iters, prm.conf);
+                                                                cap);
             mark(mark_ctx, "cand", s);
             if (getenv("MIM_DEBUG_NCAND")) {
                 std::vector<int> h(2 * n_probs);
@@ -3381,11 +3198,11 @@ void ransac_enqueue(const RansacParams& prm, int n_probs, const ProbDev* probs, 
             // chunk 2 also evaluates the list of every problem whose chunk-1 pass was deferred
             ransac_exact_kernel<<<n_probs * kExactWaves * (L + 1), 64, 0, s>>>(b.state, probs, pts, b.samples, b.stream,
                                                                              b.cand, b.ncand, b.bounds, b.cex, b.cH,
-                                                                             thr2, L);
+                                                                             thr2, L, cap);
             mark(mark_ctx, "exact", s);
             ransac_replay_kernel<<<n_probs, 64, 0, s>>>(b.state, probs, pts, b.samples, b.stream, b.bounds, b.cand,
                                                         b.ncand, b.cex, b.cH, c1, prm.conf, thr2, b.best_h, L,
-                                                        c1_first);
+                                                        c1_first, cap);
             mark(mark_ctx, "select", s);
         }
         if (c0 == 0) c1_first = c1;

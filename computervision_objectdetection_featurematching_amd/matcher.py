@@ -47,8 +47,13 @@ class Matcher:
         if st != _lib.MIM_OK:
             raise MimError(st, f"mim_ctx_create(device={device}) failed (no HIP device?)")
         self.device = device
+        self._borrowed = []  # device tensors the registered sets read until clear_sets (mim.h)
+        self._retired = []   # (event on the matcher stream, tensors) kept alive until the event completes
 
     def close(self):
+        if self._ctx and (self._borrowed or self._retired):
+            self.L.mim_synchronize(self._ctx)
+        self._borrowed, self._retired = [], []
         if self._ctx:
             self.L.mim_ctx_destroy(self._ctx)
             self._ctx = C.c_void_p()
@@ -79,11 +84,33 @@ class Matcher:
 
     # ---- descriptor sets ------------------------------------------------------------------
     def add_set(self, desc, kp) -> int:
-        """Register one ObjectModel view / scene scale.  numpy (host) or torch (device) arrays."""
+        """Register one ObjectModel view / scene scale.  numpy (host) or torch (device) arrays.
+
+        Device tensors are borrowed, not copied (mim.h): they must be float32, contiguous, shaped
+        (n, 128) and (n, 2), on this matcher's device; the matcher keeps them alive until
+        clear_sets() and orders its stream after the stream that is current when they are added."""
         on_dev = int(hasattr(desc, "is_cuda") and desc.is_cuda)
         if not on_dev:
             desc = np.ascontiguousarray(desc, np.float32).reshape(-1, DIM)
             kp = np.ascontiguousarray(kp, np.float32).reshape(-1, 2)
+        else:
+            import torch
+            if not (hasattr(kp, "is_cuda") and kp.is_cuda):
+                raise ValueError("add_set: keypoints must be on the device when the descriptors are")
+            for name, t, cols in (("descriptors", desc, DIM), ("keypoints", kp, 2)):
+                if t.dtype != torch.float32 or not t.is_contiguous() or t.dim() != 2 or t.shape[1] != cols:
+                    raise ValueError(f"add_set: {name} must be a contiguous float32 (n, {cols}) tensor, got "
+                                     f"{t.dtype} {tuple(t.shape)} contiguous={t.is_contiguous()}")
+                if t.device.index != self.device:
+                    raise ValueError(f"add_set: {name} on {t.device}, matcher on cuda:{self.device}")
+            if kp.shape[0] != desc.shape[0]:
+                raise ValueError("add_set: descriptor and keypoint row counts differ")
+            # the producer stream's work (the tensors' contents) before anything on the matcher's stream
+            mine = torch.cuda.ExternalStream(self.stream_handle(), device=desc.device)
+            cur = torch.cuda.current_stream(desc.device)
+            if cur.cuda_stream != mine.cuda_stream:
+                mine.wait_stream(cur)
+            self._borrowed += [desc, kp]
         n = int(desc.shape[0])
         sid = C.c_int32()
         self._check(self.L.mim_set_create(self._ctx, C.c_void_p(_lib.ptr(desc)), C.c_void_p(_lib.ptr(kp)), n,
@@ -92,6 +119,16 @@ class Matcher:
 
     def clear_sets(self):
         self._check(self.L.mim_sets_clear(self._ctx))
+        # the cleared sets' tensors stay referenced until the work already enqueued on the matcher's
+        # stream (their last readers) has completed: an event per clear, polled at the next clears
+        # (not record_stream: the allocator would later record events on this stream after close())
+        self._retired = [(ev, ts) for ev, ts in self._retired if not ev.query()]
+        if self._borrowed:
+            import torch
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.ExternalStream(self.stream_handle(), device=self._borrowed[0].device))
+            self._retired.append((ev, self._borrowed))
+        self._borrowed = []
 
     # ---- primitives -----------------------------------------------------------------------
     def knn_match_arrays(self, query, train):
@@ -150,8 +187,10 @@ class Matcher:
         return len(problems)
 
     def batch_results(self, n: int) -> np.ndarray:
+        """Waits for the last batch and returns its n records (n must be the batch's problem count;
+        n = 0 only waits and collects the kernel timings)."""
         out = np.zeros(n, RESULT_DTYPE)
-        self._check(self.L.mim_batch_results(self._ctx, C.c_void_p(out.ctypes.data)))
+        self._check(self.L.mim_batch_results(self._ctx, C.c_void_p(out.ctypes.data if n else 0)))
         return out
 
     def batch_results_copy_to(self, dst_dev):

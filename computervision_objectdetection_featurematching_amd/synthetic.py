@@ -108,9 +108,72 @@ def make_dataset(n_models: int, n_scenes: int, nq: int, nt: int, n_plant: int,
     return Dataset(model_desc, model_kp, scene_desc, scene_kp, H_true, plant_pos, n_plant, n_inl)
 
 
-# Configs of BASELINE.json (C1 is the reference's own real-data case; its surrogate shapes are
-# SURVEY.md §8(d)).
+def make_ragged_dataset(nqs, nts, scene_plant_frac: float = 0.5, inlier_frac: float = 0.5,
+                        seed: int = SEED_BASE) -> Dataset:
+    """Ragged problem shapes of the reference's own run (SURVEY.md §8(d) C1 surrogate): model views of
+    ``nqs[v]`` rows (an ObjectModel's masked SIFT views, ~100-500 keypoints) against scaled scenes of
+    ``nts[s]`` rows (~1k-4k).  A fraction ``scene_plant_frac`` of every scene's rows are noisy copies
+    of view rows, split evenly over the views (``n_plant[v, s]`` rows of view v), of which
+    ``inlier_frac`` sit at H_true(v, s) of the view keypoint: every problem has a few to a few dozen
+    good matches and stops early or runs its 2000 iterations, as real detections do."""
+    nv, ns = len(nqs), len(nts)
+    mrng = np.random.default_rng(seed)
+    model_desc = [sift_like(mrng, int(n)) for n in nqs]
+    model_kp = [np.c_[mrng.uniform(0, IMG_W, int(n)), mrng.uniform(0, IMG_H, int(n))].astype(np.float32)
+                for n in nqs]
+    n_plant = np.zeros((nv, ns), np.int64)
+    H_true = np.zeros((nv, ns, 3, 3))
+    plant_pos = np.full((nv, ns, max(int(n) for n in nqs)), -1, np.int64)
+    scene_desc, scene_kp = [], []
+    for s in range(ns):
+        nt = int(nts[s])
+        srng = np.random.default_rng(seed + 1 + s)
+        d = sift_like(srng, nt)
+        kp = np.c_[srng.uniform(0, IMG_W, nt), srng.uniform(0, IMG_H, nt)].astype(np.float32)
+        per_view = int(scene_plant_frac * nt) // nv
+        free = srng.permutation(nt)
+        used = 0
+        for v in range(nv):
+            k = min(per_view, int(nqs[v]))
+            rows = srng.choice(int(nqs[v]), size=k, replace=False)
+            pos = free[used:used + k]
+            used += k
+            d[pos] = perturb(srng, model_desc[v][rows])
+            H = random_homography(srng)
+            H_true[v, s] = H
+            ninl = int(round(inlier_frac * k))
+            inl = srng.choice(k, size=ninl, replace=False)
+            proj = apply_h(H, model_kp[v][rows[inl]])
+            kp[pos[inl]] = proj + srng.uniform(-0.5, 0.5, size=proj.shape).astype(np.float32)
+            n_plant[v, s] = k
+            plant_pos[v, s, :k] = pos
+        scene_desc.append(d)
+        scene_kp.append(kp)
+    return Dataset(model_desc, model_kp, scene_desc, scene_kp, H_true, plant_pos, n_plant, -1)
+
+
+def c1_shapes(seed: int = SEED_BASE):
+    """C1 surrogate shapes: sugar_box's 29 model views x the 5 scales of one scene
+    (TestsDetector.cpp:58,99) = 145 problems, Nq in [100, 500], Nt in [1000, 4000]."""
+    rng = np.random.default_rng(seed ^ 0xC1)
+    nqs = rng.integers(100, 501, size=29)
+    nts = np.sort(rng.integers(1000, 4001, size=5))  # scales 0.7 .. 1.3: more keypoints when larger
+    return nqs, nts
+
+
+def make_config_dataset(name: str, seed: int = SEED_BASE) -> Dataset:
+    cfg = CONFIGS[name]
+    if cfg.get("ragged"):
+        nqs, nts = c1_shapes(seed)
+        return make_ragged_dataset(nqs, nts, seed=seed)
+    return make_dataset(cfg["n_models"], cfg["n_scenes"], cfg["nq"], cfg["nt"], cfg["n_plant"], seed=seed)
+
+
+# Configs of BASELINE.json: C1 is the reference's own real-data case (no SIFT here: its surrogate
+# shapes, SURVEY.md §8(d)); C4 is C3's workload sharded over 8 GPUs; C5 is the distance kernel alone.
 CONFIGS = {
+    "c1": dict(ragged=True, n_models=29, n_scenes=5, nq=500, nt=4000, max_iters=2000),
     "c2": dict(n_models=1, n_scenes=1, nq=2000, nt=2000, n_plant=400, max_iters=2000),
     "c3": dict(n_models=3, n_scenes=32, nq=10000, nt=10000, n_plant=2000, max_iters=50000),
+    "c5": dict(n_models=1, n_scenes=1, nq=50000, nt=50000, n_plant=0, max_iters=0, knn_only=True),
 }

@@ -4,8 +4,9 @@
  * Drop-in boundary for the reference's hot path.  The reference has no plugin/FFI layer: the path
  * is two direct OpenCV calls inside detectObjects (/root/reference/src/TestsDetector.cpp:60,78) plus
  * the glue around them (:62-94).  Each entry point below names the reference interface it replaces.
- * The C++ drop-in adapter that keeps ObjectModel / detectObjects is in
- * computervision_objectdetection_featurematching_amd/host/ (see INTEGRATION.md).
+ * include/mim.hpp is the OpenCV-free C++ layer over this ABI; the cv::Mat-typed drop-in adapter
+ * that keeps ObjectModel / processAllModelsImages / detectObjects is adapter/ (built only with
+ * OpenCV).
  *
  * Conventions
  *   - POD only, no C++ exceptions cross this boundary; every call returns mim_status.
@@ -13,8 +14,9 @@
  *   - One ctx = one GPU + one HIP stream; calls on one ctx are serialised by an internal mutex.
  *   - `_dev`/batch calls are asynchronous on the ctx stream; mim_synchronize() waits.
  *   - Descriptors must be CV_32F rows of dim 128 (SIFT).  Integer-valued rows in [0,255] (what
- *     OpenCV SIFT emits) take the exact bf16-MFMA path; anything else takes the exact-order fp32
- *     path.  Either way indices and distances are bit-identical to the CPU restatement in oracle/.
+ *     OpenCV SIFT emits) take the exact-integer i8-MFMA path (v_mfma_i32_32x32x32_i8); any other
+ *     rows take the fp32 path in OpenCV's SSE summation order.  Either way indices and distances
+ *     are bit-identical to the CPU restatement in oracle/.
  */
 #ifndef MIM_H
 #define MIM_H
@@ -41,7 +43,11 @@ enum {
     MIM_FEW_GOOD = 1,     /* goodMatches.size() < MIN_INLIERS            (:74) */
     MIM_EMPTY_H = 2,      /* findHomography returned an empty matrix      (:79) */
     MIM_FEW_INLIERS = 3,  /* countNonZero(inlierMask) < MIN_INLIERS       (:81) */
-    MIM_BAD_DET = 4       /* |det H| outside [0.1f, 10.0f]                (:84) */
+    MIM_BAD_DET = 4,      /* |det H| outside [0.1f, 10.0f]                (:84) */
+    MIM_STREAM_SHORT = 5  /* RANSAC needed more RNG draws than the ctx's stream holds: not a result.
+                             mim_batch_results / mim_find_homography grow the stream and re-run, so
+                             it is only seen in records read on the device (mim_batch_results_dev /
+                             _copy) before that */
 };
 
 /* Thresholds of detectObjects (TestsDetector.cpp:21-25) + findHomography defaults. */
@@ -85,14 +91,22 @@ mim_status mim_synchronize(struct mim_ctx* ctx);
 
 /* ---- descriptor sets: ObjectModel views and scene scales -------------------------------------
  * Registers n descriptors (n x dim float32, row stride dim) and their keypoints (n x 2 float32,
- * KeyPoint::pt).  on_device != 0: both pointers are device pointers (read asynchronously on the
- * ctx stream, must stay valid until mim_synchronize); else host pointers (copied).  The set is
- * converted once into the device layout the kernels stream (DESIGN.md "Data layout in HBM"). */
+ * KeyPoint::pt).  on_device == 0: host pointers, copied before the call returns.  on_device != 0:
+ * device pointers that the set BORROWS: they are read on the ctx stream by later batch calls (the
+ * layout prep, the ratio kernel's keypoint gather, the fp32 and rescan kernels), so they must stay
+ * valid and unmodified until mim_sets_clear() / mim_ctx_destroy(), and their producer must be
+ * ordered before the ctx stream (the Python Matcher holds the tensors and waits on the producing
+ * stream).  The set is converted once into the device layout the kernels stream (DESIGN.md "Data
+ * layout in HBM").  Any row count is accepted; a set used as the TRAIN side of a problem must have
+ * fewer than 2^18 rows (BFMatcher::knnMatchImpl's assertion), checked at mim_batch_run. */
 mim_status mim_set_create(struct mim_ctx* ctx, const float* desc, const float* kp_xy, int32_t n,
                           int32_t dim, int32_t on_device, int32_t* set_id);
 mim_status mim_sets_clear(struct mim_ctx* ctx);
 
-/* ---- primitive ops, host buffers, synchronous ------------------------------------------------ */
+/* ---- primitive ops, host buffers, synchronous ------------------------------------------------
+ * Each primitive call replaces the ctx's "last batch": after mim_knn2_l2 / mim_ratio_filter /
+ * mim_knn2_sets_dev there are no records (mim_batch_results returns none), after
+ * mim_find_homography there is that call's one record. */
 /* ≙ BFMatcher(NORM_L2).knnMatch(q, t, matches, 2)            TestsDetector.cpp:36,60
  * idx[2i+k] = trainIdx of the k-th match of query i (-1 if absent), dist[2i+k] = DMatch::distance. */
 mim_status mim_knn2_l2(struct mim_ctx* ctx, const float* q, int32_t nq, const float* t, int32_t nt,
@@ -113,7 +127,10 @@ mim_status mim_find_homography(struct mim_ctx* ctx, const float* src_xy, const f
  * without waiting.  Results stay on the device until fetched. */
 mim_status mim_batch_run(struct mim_ctx* ctx, const mim_problem* problems, int32_t n,
                          const mim_params* params);
-/* Waits, then copies the n mim_result records to host memory. */
+/* Waits, then copies the n mim_result records to host memory.  A problem that ran out of RNG
+ * draws (MIM_STREAM_SHORT) makes the ctx grow its stream (x8, up to 2^30 draws) and re-run the
+ * batch first; that needs the batch's sets intact (no mim_sets_clear since mim_batch_run), else
+ * MIM_ERANGE. */
 mim_status mim_batch_results(struct mim_ctx* ctx, mim_result* out);
 /* Device pointer to the n mim_result records of the last batch (valid until the next batch). */
 const mim_result* mim_batch_results_dev(struct mim_ctx* ctx);
@@ -131,8 +148,10 @@ mim_status mim_knn2_sets_dev(struct mim_ctx* ctx, int32_t query_set, int32_t tra
                              int32_t* idx_dev, float* dist_dev);
 
 /* ---- introspection for benches / profiles ----------------------------------------------------- */
-/* Per-kernel device time (ms) of the last batch, measured with HIP events on the ctx stream.
- * names: "knn", "ratio", "sample", "hypo", "score", "select", "refine".  Returns -1 if unknown. */
+/* Per-kernel device time (ms) summed over the batches since the last result fetch, measured with
+ * HIP events on the stream each kernel ran on.  names: "knn", "ratio", "attempt", "chain",
+ * "check", "sample", "score" (the bound kernel; "hypo"/"score"/"select" in the MIM_RANSAC_EXACT
+ * reference mode), "cand", "exact", "select" (the replay), "refine".  Returns -1 if unknown. */
 double mim_last_kernel_ms(struct mim_ctx* ctx, const char* name);
 mim_status mim_set_timing(struct mim_ctx* ctx, int32_t enable);
 

@@ -1,0 +1,49 @@
+"""CPU tests of bench.py's multi-rank launch (`--gpus N` without WORLD_SIZE spawns N ranks through
+torch.distributed.run before anything touches a GPU) with the gloo dry-run mode, and of the CPU
+baseline's record comparison."""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(args):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(GLOO_SOCKET_IFNAME="lo", OMP_NUM_THREADS="1")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], env=env, capture_output=True,
+                       text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    return json.loads(lines[0])
+
+
+def test_launcher_spawns_two_ranks():
+    d = _run(["--gpus", "2", "--dry-run"])
+    assert d["n_gpus"] == 2 and d["ranks_seen"] == 2 and d["dry_run"]
+
+
+def test_single_rank_dry_run():
+    d = _run(["--dry-run"])
+    assert d["n_gpus"] == 1 and d["ranks_seen"] == 1
+
+
+def test_cpu_parity_compare_detects_differences():
+    sys.path.insert(0, ROOT)
+    import bench
+    from computervision_objectdetection_featurematching_amd._lib import RESULT_DTYPE
+    o = dict(n_good=5, n_inl=4, status=0, iters=7, H=np.eye(3), mask=np.array([1, 1, 0, 1, 1], np.uint8),
+             good_q=np.arange(5, dtype=np.int32), good_t=np.arange(5, dtype=np.int32) + 10)
+    r = np.zeros(1, RESULT_DTYPE)[0]
+    r["n_good"], r["n_inl"], r["status"], r["iters"] = 5, 4, 0, 7
+    r["H"] = np.eye(3).ravel()
+    det = (o["good_q"].copy(), o["good_t"].copy(), o["mask"].copy())
+    assert bench._cmp_problem(o, r, det) is None
+    det2 = (det[0], det[1], np.array([1, 1, 1, 1, 1], np.uint8))
+    assert bench._cmp_problem(o, r, det2) == "inlier mask"
+    r["H"][0] = 1.01
+    assert bench._cmp_problem(o, r, det) == "H"

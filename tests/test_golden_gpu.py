@@ -1,0 +1,57 @@
+"""GPU path against the committed golden fixtures (tests/golden/golden_v2.npz, made by
+tests/golden/make_golden.py from the CPU restatement): the HIP kernels must reproduce the stored
+outputs, so parity does not depend on the oracle build of the GPU box.
+
+Reference call sites: /root/reference/src/TestsDetector.cpp:60 (knnMatch k=2), :66-72 (ratio test),
+:78 (findHomography RANSAC 5.0), :74-94 (the per-view loop and its gates).
+"""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+G = np.load(os.path.join(os.path.dirname(__file__), "golden", "golden_v2.npz"))
+
+
+def test_golden_knn_and_ratio(matcher):
+    idx, dist = matcher.knn_match_arrays(G["knn_q"], G["knn_t"])
+    np.testing.assert_array_equal(idx, G["knn_idx"])
+    np.testing.assert_array_equal(dist.view(np.int32), G["knn_dist"].view(np.int32))
+    q, t = matcher.ratio_filter(idx, dist, 0.9)
+    assert len(G["ratio_q"]) >= 30
+    np.testing.assert_array_equal(q, G["ratio_q"])
+    np.testing.assert_array_equal(t, G["ratio_t"])
+
+
+@pytest.mark.parametrize("name", list("abc"))
+def test_golden_find_homography(matcher, name):
+    H, mask = matcher.find_homography(G[f"rs_{name}_src"], G[f"rs_{name}_dst"], 5.0, int(G[f"rs_{name}_iters_max"]),
+                                      0.995)
+    assert (H is not None) == bool(G[f"rs_{name}_ok"])
+    np.testing.assert_array_equal(mask, G[f"rs_{name}_mask"])
+    r = matcher.batch_results(1)[0]  # the call's record: RANSAC iteration count of OpenCV's loop
+    assert int(r["iters"]) == int(G[f"rs_{name}_iters"])
+    if H is not None:
+        Ho = G[f"rs_{name}_H"]
+        assert np.max(np.abs(H - Ho) / (np.abs(Ho) + 1e-3)) < 1e-7
+
+
+def test_golden_problems(matcher):
+    from computervision_objectdetection_featurematching_amd import default_params
+    matcher.clear_sets()
+    q = matcher.add_set(G["pb_qd"], G["pb_qk"])
+    ts = [matcher.add_set(G[f"pb{s}_td"], G[f"pb{s}_tk"]) for s in range(2)]
+    res = matcher.match_batch([(q, t) for t in ts], default_params(max_iters=2000))
+    for s in range(2):
+        r = res[s]
+        assert int(r["n_good"]) == int(G[f"pb{s}_n_good"])
+        assert (int(r["status"]), int(r["n_inl"]), int(r["iters"])) == \
+            (int(G[f"pb{s}_status"]), int(G[f"pb{s}_n_inl"]), int(G[f"pb{s}_iters"]))
+        gq, gt, gm = matcher.problem_detail(s, int(r["n_good"]))
+        np.testing.assert_array_equal(gq, G[f"pb{s}_good_q"])
+        np.testing.assert_array_equal(gt, G[f"pb{s}_good_t"])
+        np.testing.assert_array_equal(gm, G[f"pb{s}_mask"])
+        Ho = G[f"pb{s}_H"]
+        assert np.max(np.abs(r["H"].reshape(3, 3) - Ho) / (np.abs(Ho) + 1e-3)) < 1e-7
+    matcher.clear_sets()

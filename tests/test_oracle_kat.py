@@ -123,10 +123,14 @@ def test_ratio_strict(oracle):
 def test_golden_fixture_regenerates(oracle):
     # the committed goldens equal what the restatement computes today
     import os
-    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "golden_v1.npz"))
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "golden_v2.npz"))
     idx, dist = oracle.knn2(g["knn_q"], g["knn_t"], 1)
     np.testing.assert_array_equal(idx, g["knn_idx"])
     np.testing.assert_array_equal(dist, g["knn_dist"])
+    gq, gt = oracle.ratio_filter(idx, dist, 0.9)
+    assert len(g["ratio_q"]) >= 30  # the planted rows survive the ratio test
+    np.testing.assert_array_equal(gq, g["ratio_q"])
+    np.testing.assert_array_equal(gt, g["ratio_t"])
     for name in "abc":
         r = oracle.ransac(g[f"rs_{name}_src"], g[f"rs_{name}_dst"], 5.0, 0.995, int(g[f"rs_{name}_iters_max"]))
         np.testing.assert_array_equal(r["mask"], g[f"rs_{name}_mask"])

@@ -3,6 +3,6 @@ set -e
 cd $GRAFT_REPO_ROOT
 for i in 1 2; do
   for v in ${VARS}; do
-    MIM_LIB=$PWD/computervision_objectdetection_featurematching_amd/lib/variants/libmim_$v.so timeout -k 10 200 python3 bench.py --cpu-problems 0 ${ARGS:---steps 10} > gpurun_out/ab_${v}_$i.log 2>&1
+    MIM_LIB=$PWD/computervision_objectdetection_featurematching_amd/lib/variants/libmim_$v.so timeout -k 10 200 python3 bench.py --cpu-sample 0 ${ARGS:---steps 10} > gpurun_out/ab_${v}_$i.log 2>&1
   done
 done

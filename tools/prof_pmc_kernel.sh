@@ -12,6 +12,6 @@ for C in $PASSES; do
   i=$((i+1))
   IFS=' '
   timeout -k 10 400 rocprofv3 --pmc $C --kernel-trace --output-format csv --kernel-include-regex "$K" \
-     -d gpurun_out/pmck/p$i -o run -- python3 bench.py --steps 1 --warmup 0 --cpu-problems 0 --no-timing > gpurun_out/pmck/p$i.log 2>&1
+     -d gpurun_out/pmck/p$i -o run -- python3 bench.py --steps 1 --warmup 0 --cpu-sample 0 --no-timing > gpurun_out/pmck/p$i.log 2>&1
   IFS='|'
 done

@@ -2,4 +2,4 @@ set -e
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 mkdir -p gpurun_out/prof
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof/trace -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --cpu-problems 0 > gpurun_out/prof/bench_trace.log 2>&1
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof/trace -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --cpu-sample 0 > gpurun_out/prof/bench_trace.log 2>&1

@@ -27,6 +27,8 @@ void launch_knn(const ProbDev* probs, const KnnWork* works, int n_works, Top2* p
 void launch_ratio(const ProbDev* probs, int n_probs, const Top2* parts, float ratio, int32_t* good_q,
                   int32_t* good_t, float4* pts, int* n_good, int32_t* knn_idx, float* knn_dist,
                   hipStream_t st);
+void launch_knn_emit(const ProbDev* probs, int nq, const Top2* parts, int32_t* knn_idx, float* knn_dist,
+                     hipStream_t st);
 size_t ransac_chain_bytes();
 void launch_rng_stream(const unsigned long long* seg_state, uint32_t* out, long long len, int seg, int n_seg,
                        hipStream_t s);
@@ -674,8 +676,7 @@ mim_status mim_knn2_sets_dev(mim_ctx* c, int32_t query_set, int32_t train_set, i
     launch_knn(c->probs.as<ProbDev>(), c->works.as<KnnWork>(), c->n_works, c->parts.as<Top2>(), c->stream);
     HIPCHK(c, hipGetLastError());
     ev_mark(c, "knn");
-    launch_ratio(c->probs.as<ProbDev>(), 1, c->parts.as<Top2>(), 0.9f, c->good_q.as<int32_t>(),
-                 c->good_t.as<int32_t>(), c->pts.as<float4>(), c->n_good.as<int>(), idx_dev, dist_dev, c->stream);
+    launch_knn_emit(c->probs.as<ProbDev>(), c->h_probs[0].q.n, c->parts.as<Top2>(), idx_dev, dist_dev, c->stream);
     HIPCHK(c, hipGetLastError());
     ev_mark(c, "ratio");
     c->last_n = 0;  // no RANSAC records (mim.h)

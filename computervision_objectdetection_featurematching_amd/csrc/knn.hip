@@ -868,6 +868,26 @@ __global__ __launch_bounds__(1024) void ratio_compact_kernel(const ProbDev* __re
 }
 
 // ------------------------------------------------------------------------------------------------
+// knnMatch rows alone (mim_knn2_l2 / mim_knn2_sets_dev): merge the train splits of every query of
+// one problem, one thread per query over the whole grid (no ratio test, no compaction).
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void knn_emit_kernel(const ProbDev* __restrict__ probs,
+                                                      const Top2* __restrict__ parts,
+                                                      int32_t* __restrict__ knn_idx, float* __restrict__ knn_dist) {
+    const ProbDev* P = probs;
+    const int q = blockIdx.x * 256 + threadIdx.x;
+    if (q >= P->q.n) return;
+    T2 m{FLT_MAX, INT_MAX, FLT_MAX, INT_MAX};
+    for (int sp = 0; sp < P->nsplit; ++sp) {
+        const Top2 t = parts[P->part_off + (long long)sp * P->q_pad + q];
+        m = top2_merge(m, t.k1, t.i1);
+        m = top2_merge(m, t.k2, t.i2);
+    }
+    reinterpret_cast<int2*>(knn_idx)[q] = make_int2(m.i1 == INT_MAX ? -1 : m.i1, m.i2 == INT_MAX ? -1 : m.i2);
+    reinterpret_cast<float2*>(knn_dist)[q] = make_float2(m.k1, m.k2);
+}
+
+// ------------------------------------------------------------------------------------------------
 // host-side launchers (called from api.cpp)
 // ------------------------------------------------------------------------------------------------
 void launch_prep_batch(const PrepJob* jobs, int njobs, int total_tiles, hipStream_t st) {
@@ -885,6 +905,11 @@ void launch_knn(const ProbDev* probs, const KnnWork* works, int n_works, Top2* p
 #endif
     knn2_rescan_kernel<<<n_works, 256, 0, st>>>(probs, works, parts);
     knn2_f32_kernel<<<n_works, 256, 0, st>>>(probs, works, parts);
+}
+
+void launch_knn_emit(const ProbDev* probs, int nq, const Top2* parts, int32_t* knn_idx, float* knn_dist,
+                     hipStream_t st) {
+    if (nq > 0) knn_emit_kernel<<<(nq + 255) / 256, 256, 0, st>>>(probs, parts, knn_idx, knn_dist);
 }
 
 void launch_ratio(const ProbDev* probs, int n_probs, const Top2* parts, float ratio, int32_t* good_q,

@@ -107,7 +107,7 @@ struct RansacParams {
 namespace mim {
 constexpr int kCandPerProblem = 1024;  // listed exact-evaluation candidates per problem and chunk
 constexpr int kIrrBlock = 16384;       // attempt positions per irregular-list block
-constexpr int kIrrCap = 512;           // listed irregular attempts per block
+constexpr int kIrrCap = 4096;          // listed irregular attempts per block (25 %: n >= ~25 points fit)
 
 // Device buffers of one RANSAC batch (owned by the ctx in api.cpp).
 struct RansacBufs {

@@ -1102,7 +1102,8 @@ __global__ __launch_bounds__(256) void ransac_irr_kernel(const RansacState* __re
 }
 
 constexpr int kChainThreads = 1024;
-constexpr int kChainEntries = 8192;                 // irregular attempts staged in LDS
+constexpr int kChainEntries = 8192;                 // irregular attempts staged in LDS per piece
+constexpr int kIrrBlocksMax = 512;                  // list blocks per window (7.3M positions max)
 constexpr int kChainSegs = 4 * kChainThreads - 2;   // runs (segments) walked per chunk
 constexpr int kNoEvent = INT_MAX;
 
@@ -1127,10 +1128,10 @@ struct ChainSegs {
 struct ChainWalkShared {
     int q[kChainEntries];
     uint8_t f[kChainEntries];
-    int boff[kIrrCap + 1];
+    int boff[kIrrBlocksMax + 1];
     int wred[kChainThreads / 64];
     int wred2[kChainThreads / 64];
-    int n_entries, limit, nseg, tail;
+    int n_entries, limit, nseg, tail, cut, stop;
 };
 
 __device__ __forceinline__ int block_excl_sum(int v, int* wred, int& total) {
@@ -1202,68 +1203,79 @@ __global__ __launch_bounds__(kChainThreads) void ransac_walk_kernel(const Ransac
     }
     const int wlen = window_len(S, c1, wcap);
     const uint8_t* F = flags + (long long)p * wcap;
-    const int nb = min((wlen + kIrrBlock - 1) / kIrrBlock, kIrrCap);  // boff has kIrrCap + 1 slots
-    // blocks up to the first overflowing one, at most kChainEntries entries
+    const int nb = min((wlen + kIrrBlock - 1) / kIrrBlock, kIrrBlocksMax);
+    // the listed blocks up to the first overflowing one (more than kIrrCap irregular positions)
     {
         const int cnt = tid < nb ? irr_cnt[(long long)p * irr_blocks + tid] : 0;
         const int bad = tid < nb && cnt < 0 ? tid : INT_MAX;
         int total;
         const int off = block_excl_sum(max(cnt, 0), sh.wred, total);
-        const int over = tid < nb && off + max(cnt, 0) > kChainEntries ? tid : INT_MAX;
-        const int cut = min(min(block_min(bad, sh.wred2), block_min(over, sh.wred)), nb);
+        const int cut = min(block_min(bad, sh.wred2), nb);
         if (tid <= nb) sh.boff[tid] = tid < nb ? off : 0;
         __syncthreads();
         if (tid == 0) {
+            sh.cut = cut;
             sh.n_entries = cut > 0 ? sh.boff[cut - 1] + irr_cnt[(long long)p * irr_blocks + cut - 1] : 0;
             sh.limit = min(wlen, cut * kIrrBlock);
+            sh.stop = 0;
         }
         __syncthreads();
-        for (int e = tid; e < sh.n_entries; e += kChainThreads) {
+    }
+    // the entries stream through LDS in pieces of kChainEntries; wave 0 walks each piece, keeping its
+    // chain position across pieces (entries are in ascending position order)
+    int s = 0, nwalk = 0, limit = sh.limit;
+    const int E = sh.n_entries, cut = sh.cut;
+    for (int eb = 0; eb < E; eb += kChainEntries) {
+        const int ee = min(E, eb + kChainEntries);
+        for (int e = eb + tid; e < ee; e += kChainThreads) {
             int lo = 0, hi = cut - 1;
             while (lo < hi) {
                 const int mid = (lo + hi + 1) >> 1;
                 if (sh.boff[mid] <= e) lo = mid; else hi = mid - 1;
             }
             const int q = irr[((long long)p * irr_blocks + lo) * kIrrCap + (e - sh.boff[lo])];
-            sh.q[e] = q;
-            sh.f[e] = F[q];
+            sh.q[e - eb] = q;
+            sh.f[e - eb] = F[q];
         }
         __syncthreads();
+        if (tid < 64) {
+            bool stop = false;
+            for (int e0 = eb; e0 < ee && !stop; e0 += 64) {
+                const int e = e0 + lane;
+                const int q = e < ee ? sh.q[e - eb] : INT_MAX;
+                const int f = e < ee ? (int)sh.f[e - eb] : 0;
+                for (;;) {
+                    const unsigned long long m = __ballot(q >= s && q < limit && ((q - s) & 3) == 0);
+                    if (!m) break;
+                    // wave-uniform lane index: v_readlane (no LDS round trip per walked event)
+                    const int k = uni(__builtin_ctzll(m));
+                    const int qq = __builtin_amdgcn_readlane(q, k), ff = __builtin_amdgcn_readlane(f, k);
+                    if (ff == kAttemptSerial || nwalk == kChainSegs) {  // resolved by the walker
+                        limit = qq;
+                        stop = true;
+                        break;
+                    }
+                    if (lane == 0) {
+                        G->seg_s[nwalk] = s;
+                        G->seg_q[nwalk] = qq;
+                        G->seg_f[nwalk] = (uint8_t)ff;
+                    }
+                    ++nwalk;
+                    s = uni(qq + 4 + ((ff & 0x7F) >> 1));
+                }
+            }
+            if (lane == 0 && stop) sh.stop = 1;
+        }
+        __syncthreads();
+        if (sh.stop) break;
     }
     if (tid < 64) {
-        int s = 0, nseg = 0, limit = sh.limit;
-        const int E = sh.n_entries;
-        bool stop = false;
-        for (int e0 = 0; e0 < E && !stop; e0 += 64) {
-            const int e = e0 + lane;
-            const int q = e < E ? sh.q[e] : INT_MAX;
-            const int f = e < E ? (int)sh.f[e] : 0;
-            for (;;) {
-                const unsigned long long m = __ballot(q >= s && q < limit && ((q - s) & 3) == 0);
-                if (!m) break;
-                // wave-uniform lane index: v_readlane (no LDS round trip per walked event)
-                const int k = uni(__builtin_ctzll(m));
-                const int qq = __builtin_amdgcn_readlane(q, k), ff = __builtin_amdgcn_readlane(f, k);
-                if (ff == kAttemptSerial || nseg == kChainSegs) {  // resolved by the walker
-                    limit = qq;
-                    stop = true;
-                    break;
-                }
-                if (lane == 0) {
-                    G->seg_s[nseg] = s;
-                    G->seg_q[nseg] = qq;
-                    G->seg_f[nseg] = (uint8_t)ff;
-                }
-                ++nseg;
-                s = uni(qq + 4 + ((ff & 0x7F) >> 1));
-            }
-        }
         if (lane == 0) {
             const int tail = s < limit ? (limit - s + 3) >> 2 : 0;
-            G->seg_s[nseg] = s;
-            sh.nseg = nseg;
+            G->seg_s[nwalk] = s;
+            sh.nseg = nwalk;
             sh.tail = tail;
-            G->nseg = nseg;
+            G->nseg = nwalk;
             G->tail = tail;
             G->s_end = s + 4 * tail;
             G->wbase = S.stream_pos;

@@ -35,8 +35,9 @@ typedef const __attribute__((address_space(1))) int gint;
 // row = 32u + (lane & 31), col = 32s + 16(lane >> 5) + j — the per-lane operand of
 // v_mfma_i32_32x32x32_i8 (query and train use the same k order, so the product is k-order free);
 // one 1 KiB wave load = one fragment, fully coalesced.
-// Norm block per tile (kNormWords): [64] floor(n2/2), [64] n2 & 1 (the train side, staged to LDS),
-// [64] c (the query side); padded rows floor(n2/2) = 2^30 - 1, n2 & 1 = 1, so D = INT_MAX.
+// Norm block per tile (kNormWords): [64] floor(n2/2), [2] the 64 values n2 & 1 as a bit mask + [62]
+// zero (the train side, staged to LDS as is), [64] c (the query side); padded rows floor(n2/2) =
+// 2^30 - 1, n2 & 1 = 1, so D = INT_MAX.
 // ------------------------------------------------------------------------------------------------
 __device__ __forceinline__ void prep_tile(const float* __restrict__ src, int n, int8_t* __restrict__ frag,
                                           int* __restrict__ norm, int* __restrict__ flags, int tile) {
@@ -83,7 +84,9 @@ __device__ __forceinline__ void prep_tile(const float* __restrict__ src, int n, 
         }
         int* nb = norm + (size_t)tile * kNormWords;
         nb[tid] = row < n ? n2 >> 1 : (1 << 30) - 1;
-        nb[64 + tid] = row < n ? n2 & 1 : 1;
+        // the 64 parities as one bit mask (row i = bit i) in words 64, 65; words 66..127 zero
+        const unsigned long long pm = __ballot(row < n ? n2 & 1 : 1);  // tid < 64: wave 0, all lanes
+        nb[64 + tid] = tid < 2 ? (int)(uint32_t)(pm >> (32 * tid)) : 0;
         nb[128 + tid] = n2 + 2 * sum;
     }
     if (__any(bad) && (tid & 63) == 0) atomicOr(flags, 1);
@@ -193,17 +196,15 @@ __device__ __forceinline__ int dval(int R, int p) { return (R << 1) | p; }  // v
 // ------------------------------------------------------------------------------------------------
 // Exact distance kernel.  Block = kKnnWaves waves = kKnnBlockQ queries (each wave: kKnnQT 32-query
 // MFMA column tiles, their q' fragments held in VGPRs for the whole sweep).  Train rows stream
-// HBM -> registers -> LDS in stages of kKnnStage 64-row tiles (double buffer, one barrier per
-// stage); per tile a wave reads the 8 KiB of fragments as 8 conflict-free ds_read_b128 and issues
-// 8 kKnnQT i8 MFMAs.
+// HBM -> LDS by LDS-DMA in stages of kKnnStage 64-row tiles (double buffer, one barrier per stage);
+// per tile a wave reads the 8 KiB of fragments as 8 conflict-free ds_read_b128 and issues 8 kKnnQT
+// i8 MFMAs.
 // ------------------------------------------------------------------------------------------------
 constexpr int kLdsTile = kTileBytes + 512;  // fragments + the train half of the norm block
 constexpr int kStage = kKnnStage;
 constexpr int kThreads = 64 * kKnnWaves;
 constexpr int kStageChunks = kStage * kTileBytes / 16 / kThreads;  // 16-B fragment chunks per thread
-constexpr int kStageNorms = kStage * 128;                           // norm words per stage
 static_assert(kStageChunks * 16 * kThreads == kStage * kTileBytes, "stage split");
-static_assert(kStageNorms <= kThreads, "one norm word per thread");
 
 #ifndef MIM_KNN_OCC
 #define MIM_KNN_OCC 4
@@ -248,46 +249,40 @@ __global__ __launch_bounds__(kThreads, MIM_KNN_OCC) void knn2_i8_kernel(  // OCC
         T[u] = INT_MAX;
     }
 
-    // ---- staging: HBM -> registers (issued before the stage's compute) -> LDS (after it), double
-    // buffered.  (LDS DMA would make the compiler wait for the next stage's DMA before every LDS
-    // read of the current one: it cannot tell the buffers apart.)  LDS stage layout: kStage x
-    // [8 KiB fragments | 512 B norms]; tiles past the work item's range are not loaded.
-    i32x4 stg[kStageChunks];
-    int stgn = 0;
-    auto stage_load = [&](int t0) {
-#pragma unroll
-        for (int c = 0; c < kStageChunks; ++c) {
-            const int ci = c * kThreads + tid, tt = ci >> 9;
-            if (kStage == 1 || t0 + tt < w.tile1) stg[c] = ((const gi32x4*)tsrc)[(size_t)t0 * 512 + ci];
-        }
-        if (tid < kStageNorms && (kStage == 1 || t0 + (tid >> 7) < w.tile1))
-            stgn = ((const gint*)tnorm)[(size_t)t0 * kNormWords + (tid >> 7) * kNormWords + (tid & 127)];
-    };
-    auto stage_store = [&](int buf) {
+    // ---- staging: LDS-DMA (global_load_lds_dwordx4 / _dword), double buffered, one barrier per
+    // stage of kStage 64-row tiles.  One wave-instruction writes 64 lanes x size contiguous bytes at a
+    // wave-uniform LDS base, which the fragment-major tile already is; the norm half of the tile's
+    // norm block (floor(n2/2), parity mask) is two 256-B pieces.  No staging VGPRs, no ds_write pass.
+    // LDS stage layout: kStage x [8 KiB fragments | 512 B norms]; tiles past the work item's range
+    // are not loaded.  (Every LDS read is an ext-vector or int access of the one smem array: with the
+    // seeds read as a struct type the waitcnt pass could not tell them from the DMA's target and
+    // waited for the next stage's DMA before each tile.)
+    const int wv = __builtin_amdgcn_readfirstlane(wave);
+    auto stage_dma = [&](int t0, int buf) {
         unsigned char* base = smem + buf * kStage * kLdsTile;
 #pragma unroll
         for (int c = 0; c < kStageChunks; ++c) {
-            const int ci = c * kThreads + tid, tt = ci >> 9;
-            reinterpret_cast<i32x4*>(base + tt * kLdsTile)[ci & 511] = stg[c];
+            const int cw = c * kThreads + wv * 64, tt = cw >> 9;  // the wave's first chunk: uniform
+            if (kStage == 1 || t0 + tt < w.tile1)
+                __builtin_amdgcn_global_load_lds((const void*)(tsrc + (size_t)t0 * 512 + cw + lane),
+                                                 (__attribute__((address_space(3))) void*)(base + tt * kLdsTile + (cw & 511) * 16),
+                                                 16, 0, 0);
         }
-        if (tid < kStageNorms) {  // wave-uniform: waves 2t, 2t+1 hold tile t's floor(n2/2), n2 & 1
-            int* nb = reinterpret_cast<int*>(base + (tid >> 7) * kLdsTile + kTileBytes);
-            if (!(tid & 64)) nb[tid & 63] = stgn;
-            else {  // the 64 parities as one bit mask (row i = bit i) in words 64, 65
-                const unsigned long long pm = __ballot(stgn & 1);
-                if (lane == 0) *reinterpret_cast<unsigned long long*>(nb + 64) = pm;
-            }
+#pragma unroll
+        for (int p = wv; p < 2 * kStage; p += kKnnWaves) {  // piece p: tile p >> 1, norm words 64 (p & 1) ..
+            const int tt = p >> 1;
+            if (kStage == 1 || t0 + tt < w.tile1)
+                __builtin_amdgcn_global_load_lds((const void*)(tnorm + (size_t)(t0 + tt) * kNormWords + 64 * (p & 1) + lane),
+                                                 (__attribute__((address_space(3))) void*)(base + tt * kLdsTile + kTileBytes + 256 * (p & 1)),
+                                                 4, 0, 0);
         }
     };
 
-    if (w.tile0 < w.tile1) {
-        stage_load(w.tile0);
-        stage_store(0);
-    }
-    __syncthreads();
+    if (w.tile0 < w.tile1) stage_dma(w.tile0, 0);
     // retire every prologue load (q' fragments included) here: with one still pending at the loop
-    // entry the waitcnt pass keeps a vmcnt(0) in the loop, i.e. waits for the next stage's loads
+    // entry the waitcnt pass keeps a vmcnt(0) in the loop
     __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
 
     // the 32x32 block u2 of a tile: accumulators start at floor(n2/2) (LDS), R = q'.t'' + floor(n2/2)
     auto block_mfma = [&](const unsigned char* tb, int u2, i32x16 (&acc)[QT]) {
@@ -295,7 +290,7 @@ __global__ __launch_bounds__(kThreads, MIM_KNN_OCC) void knn2_i8_kernel(  // OCC
         const int* tnu = reinterpret_cast<const int*>(tb + kTileBytes) + 32 * u2 + 4 * h;
 #pragma unroll
         for (int gg = 0; gg < 4; ++gg) {
-            const int4 n = *reinterpret_cast<const int4*>(tnu + 8 * gg);
+            const i32x4 n = *reinterpret_cast<const i32x4*>(tnu + 8 * gg);
             acc[0][4 * gg + 0] = n.x; acc[0][4 * gg + 1] = n.y; acc[0][4 * gg + 2] = n.z; acc[0][4 * gg + 3] = n.w;
         }
 #pragma unroll
@@ -337,6 +332,9 @@ __global__ __launch_bounds__(kThreads, MIM_KNN_OCC) void knn2_i8_kernel(  // OCC
             const unsigned pw = (unsigned)tn[64 + u2] >> (4 * h);  // bit 8j + k: n2 & 1 of the lane's row
             i32x16 acc[QT];
             block_mfma(tb, u2, acc);
+            // the parity word is read with the seeds (its LDS latency hidden behind the MFMAs), not
+            // inside the rare insertion path where the compiler would sink it: one LDS round trip per event
+            asm volatile("" ::"v"(pw));
 #ifdef MIM_KNN_NOSEL  // timing probe only: MFMA loop without the selection (results invalid)
 #pragma unroll
             for (int u = 0; u < QT; ++u) {
@@ -375,9 +373,15 @@ __global__ __launch_bounds__(kThreads, MIM_KNN_OCC) void knn2_i8_kernel(  // OCC
                         // per row: one compare (the ballot) and, if some lane has the row under its
                         // threshold, an unconditional insertion in every lane (the lane lists stay the
                         // exact top-2 of the rows pushed, a superset of the filtered ones)
+                        // the 16 row ballots first (independent compares into SGPR pairs, no VALU ->
+                        // VCC -> branch dependency per row), then a not-taken scalar test per row: the
+                        // insertion code sits out of line
+                        unsigned long long hm[16];
+#pragma unroll
+                        for (int g = 0; g < 16; ++g) hm[g] = __ballot(acc[u][g] <= T[u]);
 #pragma unroll
                         for (int g = 0; g < 16; ++g) {
-                            if (__ballot(acc[u][g] <= T[u]))
+                            if (__builtin_expect(hm[g] != 0, 0))
                                 sel_push(st[u], dval(acc[u][g], (pw >> ((g & 3) + 8 * (g >> 2))) & 1),
                                          row0 + (g & 3) + 8 * (g >> 2));
                         }
@@ -397,18 +401,18 @@ __global__ __launch_bounds__(kThreads, MIM_KNN_OCC) void knn2_i8_kernel(  // OCC
     for (; stage < tile_e; stage += kStage) {
         const int buf = ((stage - w.tile0) / kStage) & 1;
         const bool more = stage + kStage < w.tile1;
-        if (more) stage_load(stage + kStage);
+        if (more) stage_dma(stage + kStage, buf ^ 1);
         const unsigned char* sb = smem + buf * kStage * kLdsTile;
 #pragma unroll
         for (int ts = 0; ts < kStage; ++ts)
             if (kStage == 1 || stage + ts < w.tile1) tile_early(sb + ts * kLdsTile, stage + ts);
-        if (more) stage_store(buf ^ 1);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA into the next buffer landed
         __syncthreads();
     }
     for (; stage < w.tile1; stage += kStage) {
         const int buf = ((stage - w.tile0) / kStage) & 1;
         const bool more = stage + kStage < w.tile1;
-        if (more) stage_load(stage + kStage);
+        if (more) stage_dma(stage + kStage, buf ^ 1);
         const unsigned char* sb = smem + buf * kStage * kLdsTile;
 #pragma unroll
         for (int u = 0; u < QT; ++u) {
@@ -429,7 +433,7 @@ __global__ __launch_bounds__(kThreads, MIM_KNN_OCC) void knn2_i8_kernel(  // OCC
 #pragma unroll MIM_KNN_LATE_UNROLL
         for (int ts = 0; ts < kStage; ++ts)
             if (kStage == 1 || stage + ts < w.tile1) tile_late(sb + ts * kLdsTile, stage + ts);
-        if (more) stage_store(buf ^ 1);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA into the next buffer landed
         __syncthreads();
     }
 
@@ -527,58 +531,48 @@ __global__ __launch_bounds__(kThreads, MIM_KNN_OCC) void knn2_i8_16_kernel(
         T[ct] = INT_MAX;
     }
 
-    i32x4 stg[kStageChunks];
-    int stgn = 0;
-    auto stage_load = [&](int t0) {
-#pragma unroll
-        for (int c = 0; c < kStageChunks; ++c) {
-            const int ci = c * kThreads + tid, tt = ci >> 9;
-            if (kStage == 1 || t0 + tt < w.tile1) stg[c] = ((const gi32x4*)tsrc)[(size_t)t0 * 512 + ci];
-        }
-        if (tid < kStageNorms && (kStage == 1 || t0 + (tid >> 7) < w.tile1))
-            stgn = ((const gint*)tnorm)[(size_t)t0 * kNormWords + (tid >> 7) * kNormWords + (tid & 127)];
-    };
-    auto stage_store = [&](int buf) {
+    // LDS-DMA staging, as in knn2_i8_kernel: fragments and the norm half of every tile of a stage
+    const int wv = __builtin_amdgcn_readfirstlane(wave);
+    auto stage_dma = [&](int t0, int buf) {
         unsigned char* base = smem + buf * kStage * kLdsTile;
 #pragma unroll
         for (int c = 0; c < kStageChunks; ++c) {
-            const int ci = c * kThreads + tid, tt = ci >> 9;
-            reinterpret_cast<i32x4*>(base + tt * kLdsTile)[ci & 511] = stg[c];
+            const int cw = c * kThreads + wv * 64, tt = cw >> 9;
+            if (kStage == 1 || t0 + tt < w.tile1)
+                __builtin_amdgcn_global_load_lds((const void*)(tsrc + (size_t)t0 * 512 + cw + lane),
+                                                 (__attribute__((address_space(3))) void*)(base + tt * kLdsTile + (cw & 511) * 16),
+                                                 16, 0, 0);
         }
-        if (tid < kStageNorms) {
-            int* nb = reinterpret_cast<int*>(base + (tid >> 7) * kLdsTile + kTileBytes);
-            if (!(tid & 64)) nb[tid & 63] = stgn;
-            else {
-                const unsigned long long pm = __ballot(stgn & 1);
-                if (lane == 0) *reinterpret_cast<unsigned long long*>(nb + 64) = pm;
-            }
+#pragma unroll
+        for (int p = wv; p < 2 * kStage; p += kKnnWaves) {
+            const int tt = p >> 1;
+            if (kStage == 1 || t0 + tt < w.tile1)
+                __builtin_amdgcn_global_load_lds((const void*)(tnorm + (size_t)(t0 + tt) * kNormWords + 64 * (p & 1) + lane),
+                                                 (__attribute__((address_space(3))) void*)(base + tt * kLdsTile + kTileBytes + 256 * (p & 1)),
+                                                 4, 0, 0);
         }
     };
-    if (w.tile0 < w.tile1) {
-        stage_load(w.tile0);
-        stage_store(0);
-    }
+    if (w.tile0 < w.tile1) stage_dma(w.tile0, 0);
+    __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
     __builtin_amdgcn_s_waitcnt(0);
 
     // 16-row block rb of a tile: accumulators seeded with floor(n2/2), R = q'.t'' + floor(n2/2)
     auto block_mfma = [&](const unsigned char* tb, int rb, i32x4 (&acc)[CT]) {
         const i32x4* A = reinterpret_cast<const i32x4*>(tb);
-        const int4 n = *reinterpret_cast<const int4*>(reinterpret_cast<const int*>(tb + kTileBytes) + 16 * rb + 4 * g);
-        acc[0][0] = n.x; acc[0][1] = n.y; acc[0][2] = n.z; acc[0][3] = n.w;
-#pragma unroll
-        for (int ct = 1; ct < CT; ++ct) acc[ct] = acc[0];
+        const i32x4 n = *reinterpret_cast<const i32x4*>(reinterpret_cast<const int*>(tb + kTileBytes) + 16 * rb + 4 * g);
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
             const i32x4 a = A[(rb * 2 + ks) * 64 + lane];
 #pragma unroll
-            for (int ct = 0; ct < CT; ++ct) acc[ct] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, B[ct][ks], acc[ct], 0, 0, 0);
+            for (int ct = 0; ct < CT; ++ct)
+                acc[ct] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, B[ct][ks], ks ? acc[ct] : n, 0, 0, 0);
         }
     };
     // parity bits of the lane's 4 rows of block rb: bit i
     auto parity4 = [&](const unsigned char* tb, int rb) {
-        const unsigned wv = reinterpret_cast<const unsigned*>(tb + kTileBytes)[64 + (rb >> 1)];
-        return wv >> (16 * (rb & 1) + 4 * g);
+        const unsigned wvp = reinterpret_cast<const unsigned*>(tb + kTileBytes)[64 + (rb >> 1)];
+        return wvp >> (16 * (rb & 1) + 4 * g);
     };
     auto tile_early = [&](const unsigned char* tb, int tile) {
 #pragma unroll
@@ -599,8 +593,10 @@ __global__ __launch_bounds__(kThreads, MIM_KNN_OCC) void knn2_i8_16_kernel(
 #pragma unroll
         for (int rb = 0; rb < 4; ++rb) {
             const int row0 = tile * 64 + 16 * rb;
+            const unsigned pw = parity4(tb, rb);
             i32x4 acc[CT];
             block_mfma(tb, rb, acc);
+            asm volatile("" ::"v"(pw));  // read with the seeds, not inside the rare insertion path
             int mn[CT];
             bool hit = false;
 #pragma unroll
@@ -609,15 +605,16 @@ __global__ __launch_bounds__(kThreads, MIM_KNN_OCC) void knn2_i8_16_kernel(
                 hit |= mn[ct] <= T[ct];
             }
             if (__builtin_expect(__ballot(hit) != 0, 0)) {
-                const unsigned pw = parity4(tb, rb);
 #pragma unroll
                 for (int ct = 0; ct < CT; ++ct) {
                     if (__ballot(mn[ct] <= T[ct])) {
+                        unsigned long long hm[4];
 #pragma unroll
-                        for (int i = 0; i < 4; ++i) {
-                            if (__ballot(acc[ct][i] <= T[ct]))
+                        for (int i = 0; i < 4; ++i) hm[i] = __ballot(acc[ct][i] <= T[ct]);
+#pragma unroll
+                        for (int i = 0; i < 4; ++i)
+                            if (__builtin_expect(hm[i] != 0, 0))
                                 sel_push(st[ct], dval(acc[ct][i], (pw >> i) & 1), row0 + i);
-                        }
                         T[ct] = sel_filter4(st[ct]);
                     }
                 }
@@ -630,12 +627,12 @@ __global__ __launch_bounds__(kThreads, MIM_KNN_OCC) void knn2_i8_16_kernel(
     for (; stage < tile_e; stage += kStage) {
         const int buf = ((stage - w.tile0) / kStage) & 1;
         const bool more = stage + kStage < w.tile1;
-        if (more) stage_load(stage + kStage);
+        if (more) stage_dma(stage + kStage, buf ^ 1);
         const unsigned char* sb = smem + buf * kStage * kLdsTile;
 #pragma unroll
         for (int ts = 0; ts < kStage; ++ts)
             if (kStage == 1 || stage + ts < w.tile1) tile_early(sb + ts * kLdsTile, stage + ts);
-        if (more) stage_store(buf ^ 1);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
     }
 #pragma unroll
@@ -643,12 +640,12 @@ __global__ __launch_bounds__(kThreads, MIM_KNN_OCC) void knn2_i8_16_kernel(
     for (; stage < w.tile1; stage += kStage) {
         const int buf = ((stage - w.tile0) / kStage) & 1;
         const bool more = stage + kStage < w.tile1;
-        if (more) stage_load(stage + kStage);
+        if (more) stage_dma(stage + kStage, buf ^ 1);
         const unsigned char* sb = smem + buf * kStage * kLdsTile;
 #pragma unroll 1
         for (int ts = 0; ts < kStage; ++ts)
             if (kStage == 1 || stage + ts < w.tile1) tile_late(sb + ts * kLdsTile, stage + ts);
-        if (more) stage_store(buf ^ 1);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
     }
 

@@ -422,6 +422,48 @@ static int get_subset(const float* M, const float* m, int count, float* ms1, flo
     return 0;
 }
 
+/* Study knob (tools/eigen_gap.py), off by default: OpenCV built HAVE_EIGEN solves runKernel's 9x9
+ * eigenproblem with Eigen's SelfAdjointEigenSolver instead of JacobiImpl_, so its minimal-sample models
+ * can differ from this restatement's in the last bits.  With ulps > 0 every minimal-sample model of
+ * orc_ransac gets each of h0..h7 moved by a pseudo-random k in [-ulps, ulps] ulp (splitmix64 of seed,
+ * iteration, element), to measure how often such a difference changes the RANSAC outcome. */
+static int g_perturb_ulps = 0;
+static uint64_t g_perturb_seed = 0;
+
+void orc_set_model_perturbation(int ulps, uint64_t seed) {
+    g_perturb_ulps = ulps;
+    g_perturb_seed = seed;
+}
+
+static uint64_t splitmix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ULL;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBULL;
+    return x ^ (x >> 31);
+}
+
+/* Study knob: record every iteration's inlier count (-1: runKernel rejected the sample) */
+static int* g_count_trace = NULL;
+static int g_count_cap = 0;
+
+void orc_set_count_trace(int* counts, int cap) {
+    g_count_trace = counts;
+    g_count_cap = counts ? cap : 0;
+}
+
+static void perturb_model(double H[9], int iter) {
+    for (int i = 0; i < 8; ++i) {
+        const uint64_t r = splitmix64(g_perturb_seed ^ ((uint64_t)iter << 8) ^ (uint64_t)i);
+        const int64_t k = (int64_t)(r % (uint64_t)(2 * (int64_t)g_perturb_ulps + 1)) - g_perturb_ulps;
+        if (k > -8 && k < 8) {  /* exact ulp steps */
+            for (int64_t j = k; j > 0; --j) H[i] = nextafter(H[i], INFINITY);
+            for (int64_t j = k; j < 0; ++j) H[i] = nextafter(H[i], -INFINITY);
+        } else {  /* large levels: k times the element's ulp */
+            H[i] += (double)k * (nextafter(H[i], INFINITY) - H[i]);
+        }
+    }
+}
+
 /* RANSACPointSetRegistrator::run (calib3d/src/ptsetreg.cpp) */
 int orc_ransac(const float* M, const float* m, int count, double thresh, double conf, int max_iters,
                double Hbest[9], uint8_t* bestMask, int* n_iters, int* best_iter,
@@ -451,8 +493,13 @@ int orc_ransac(const float* M, const float* m, int count, double thresh, double 
             }
             break;
         }
-        if (orc_run_kernel(ms1, ms2, 4, model) <= 0) continue;
+        if (orc_run_kernel(ms1, ms2, 4, model) <= 0) {
+            if (iter < g_count_cap) g_count_trace[iter] = -1;
+            continue;
+        }
+        if (g_perturb_ulps > 0) perturb_model(model, iter);
         int goodCount = find_inliers(M, m, count, model, err, mask, thresh);
+        if (iter < g_count_cap) g_count_trace[iter] = goodCount;
         if (goodCount > (maxGoodCount > 3 ? maxGoodCount : 3)) {
             memcpy(bestMask, mask, (size_t)count);
             memcpy(Hbest, model, sizeof model);

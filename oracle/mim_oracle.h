@@ -82,6 +82,13 @@ typedef struct {
     double det;
 } orc_result;
 
+/* Study knob, off by default (tools/eigen_gap.py): perturb every minimal-sample model of orc_ransac by
+ * up to +-ulps ulp per element, modelling an OpenCV whose cv::eigen is Eigen's solver. */
+void orc_set_model_perturbation(int ulps, uint64_t seed);
+/* Study knob: orc_ransac writes each iteration's inlier count (-1 = degenerate sample) to counts[iter]
+ * for iter < cap; NULL turns it off.  Not thread-safe (one process per study worker). */
+void orc_set_count_trace(int* counts, int cap);
+
 void orc_default_params(orc_params* p);
 /* Full per-problem path.  mask_out (optional) receives n_good bytes. good_q/good_t optional
  * (n_q ints each) receive the ratio-test survivors. knn_threads as in orc_knn2_l2. */

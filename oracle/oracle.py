@@ -59,6 +59,8 @@ def lib():
                                  C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int64)]
         L.orc_find_homography.argtypes = [f32p, f32p, C.c_int, C.c_double, C.c_int, C.c_double, f64p, u8p]
         L.orc_default_params.argtypes = [C.POINTER(Params)]
+        L.orc_set_model_perturbation.argtypes = [C.c_int, C.c_uint64]
+        L.orc_set_count_trace.argtypes = [C.c_void_p, C.c_int]
         L.orc_match_problem.argtypes = [f32p, f32p, C.c_int, f32p, f32p, C.c_int, C.c_int,
                                         C.POINTER(Params), C.c_int, C.POINTER(Result),
                                         C.c_void_p, C.c_void_p, C.c_void_p]
@@ -131,6 +133,22 @@ def ransac(src, dst, thresh=5.0, conf=0.995, max_iters=2000):
                           n, thresh, conf, max_iters, H, mask, C.byref(it), C.byref(bi), C.byref(used))
     return dict(ok=ok, H=H.reshape(3, 3), mask=mask[:n], iters=it.value, best_iter=bi.value,
                 stream_used=used.value)
+
+
+def set_model_perturbation(ulps: int, seed: int = 0):
+    """Study knob (tools/eigen_gap.py): +-ulps ulp on every minimal-sample model; 0 = off."""
+    lib().orc_set_model_perturbation(int(ulps), int(seed) & 0xFFFFFFFFFFFFFFFF)
+
+
+def ransac_counts(src, dst, thresh=5.0, conf=0.995, max_iters=2000):
+    """orc_ransac with the per-iteration inlier counts (study knob): (result dict, counts[:iters])."""
+    counts = np.full(max(max_iters, 1), -2, np.int32)
+    lib().orc_set_count_trace(counts.ctypes.data, len(counts))
+    try:
+        r = ransac(src, dst, thresh, conf, max_iters)
+    finally:
+        lib().orc_set_count_trace(None, 0)
+    return r, counts[:r["iters"]]
 
 
 def find_homography(src, dst, thresh=5.0, max_iters=2000, conf=0.995):

@@ -1924,12 +1924,20 @@ typedef float f16acc __attribute__((ext_vector_type(16)));
 constexpr float kMfmaErr = 0x1p-15f;
 constexpr int kTileChunk = 16;  // 32-point tiles per LDS stage of the MFMA bound kernel (32 KiB)
 
+// hi + lo = a to 2^-22 relative, with hi = (f16)a and lo = (f16)(a - hi) taken from the SAME value a.
+// `a` is pinned in a register first: given split_f16(u * x), the compiler otherwise forms
+// hi = v_fma_mixlo_f16(u, x, 0) (the exact product rounded once to f16) next to a - hi from the fp32
+// product; where the fp32 product is an f16 rounding tie the two hi differ by one f16 ulp and hi + lo
+// is off by 2^-11 relative (found by tests/test_bounds_corpus_gpu.py: a missed upper bound).
 __device__ __forceinline__ void split_f16(float a, _Float16& hi, _Float16& lo) {
+    asm volatile("" : "+v"(a));
     hi = (_Float16)a;
     lo = (_Float16)(a - (float)hi);  // a - hi is exact in fp32
 }
 __device__ __forceinline__ void split_f16(double a, _Float16& hi, _Float16& lo) {
-    hi = (_Float16)(float)a;
+    float af = (float)a;
+    asm volatile("" : "+v"(af));
+    hi = (_Float16)af;
     lo = (_Float16)(float)(a - (double)(float)hi);
 }
 
@@ -2070,6 +2078,12 @@ __global__ __launch_bounds__(256) void ransac_bound_mfma_kernel(const RansacStat
     const double aw = (fabs(Hd[6]) + fabs(Hd[7])) * mx + 1.0;
     const float A = (float)(gam * (ax + (mu + 6.0) * aw) * S.sb * sc * (1.0 + 1e-6));
     const float E = (1.f + C) * kMfmaErr * (1.f + 1e-6f) + A;
+#ifdef MIM_BOUND_DEBUG_IT
+    if (act && it == MIM_BOUND_DEBUG_IT)
+        printf("[mim] hyp it=%d e=%d sa=%g sb=%g C=%.9g A=%.9g E=%.9g eta=%g eta_model=%g count=%d h'=%.9g %.9g %.9g %.9g %.9g %.9g %.9g %.9g %.9g\n",
+               it, e, (double)S.sa, (double)S.sb, (double)C, (double)A, (double)E, (double)eta, eta_model, (int)count,
+               h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], h[8]);
+#endif
     float CL = 0.f, EL = 0.f;
     if (kLo) {
         float tl = thr2 - fmaf(1e-7f * S.smax, S.smax, 0.5f);
@@ -2121,6 +2135,13 @@ __global__ __launch_bounds__(256) void ransac_bound_mfma_kernel(const RansacStat
         const float CLp = __shfl_xor(CL, 32), ELp = __shfl_xor(EL, 32);
         CL0 = lowh ? CL : CLp; EL0 = lowh ? EL : ELp; CL1 = lowh ? CLp : CL; EL1 = lowh ? ELp : EL;
     }
+#ifdef MIM_BOUND_DEBUG_IT
+    if (act && it == MIM_BOUND_DEBUG_IT)
+        printf("[mim] frag it=%d lane=%d fy=%g %g %g %g %g %g %g %g fn=%g %g %g %g %g %g %g %g b0y=%g %g %g %g %g %g %g %g\n", it, lane,
+               (double)fy[0], (double)fy[1], (double)fy[2], (double)fy[3], (double)fy[4], (double)fy[5], (double)fy[6], (double)fy[7],
+               (double)fn[0], (double)fn[1], (double)fn[2], (double)fn[3], (double)fn[4], (double)fn[5], (double)fn[6], (double)fn[7],
+               (double)b0y[0], (double)b0y[1], (double)b0y[2], (double)b0y[3], (double)b0y[4], (double)b0y[5], (double)b0y[6], (double)b0y[7]);
+#endif
     const bool wave_counts = __any(count);
     float big = INFINITY;
     asm volatile("" : "+v"(big));
@@ -2136,6 +2157,13 @@ __global__ __launch_bounds__(256) void ransac_bound_mfma_kernel(const RansacStat
         for (int t = 0; t < tc; ++t) {
             const h8v ax = __builtin_bit_cast(h8v, lt[t * 128 + lane]);
             const h8v ay = __builtin_bit_cast(h8v, lt[t * 128 + 64 + lane]);
+#ifdef MIM_BOUND_DEBUG_IT
+            if (((t0 + t) * 32 + (lane & 31)) == MIM_BOUND_DEBUG_PT && (blockIdx.x % bpp) == (MIM_BOUND_DEBUG_IT - c0) / 256 &&
+                (tid >> 6) == ((MIM_BOUND_DEBUG_IT - c0) % 256) / 64)
+                printf("[mim] tile pt=%d lane=%d ax=%g %g %g %g %g %g %g %g ay=%g %g %g %g %g %g %g %g\n", MIM_BOUND_DEBUG_PT, lane,
+                       (double)ax[0], (double)ax[1], (double)ax[2], (double)ax[3], (double)ax[4], (double)ax[5], (double)ax[6], (double)ax[7],
+                       (double)ay[0], (double)ay[1], (double)ay[2], (double)ay[3], (double)ay[4], (double)ay[5], (double)ay[6], (double)ay[7]);
+#endif
             const f16acc zc = {};
             const f16acc ex0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ax, b0x, zc, 0, 0, 0);
             const f16acc ey0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ay, b0y, zc, 0, 0, 0);
@@ -2155,6 +2183,20 @@ __global__ __launch_bounds__(256) void ransac_bound_mfma_kernel(const RansacStat
                 const float d1 = fmaf(C1, fabsf(w1[r]), E1) - m1;
                 bits0 = __builtin_amdgcn_alignbit(bits0, __float_as_uint(d0), 31);
                 bits1 = __builtin_amdgcn_alignbit(bits1, __float_as_uint(d1), 31);
+#ifdef MIM_BOUND_DEBUG_IT  // debug build: the box test of one (iteration, point)
+                {
+                    const int row = (t0 + t) * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                    const int itb = c0 + (blockIdx.x % bpp) * 256 + (tid & ~63);  // the wave's first iteration
+                    for (int cb = 0; cb < 2; ++cb) {
+                        const int itc = itb + 32 * cb + (lane & 31);
+                        if (itc == MIM_BOUND_DEBUG_IT && row == MIM_BOUND_DEBUG_PT)
+                            printf("[mim] box it=%d pt=%d ex=%.9g ey=%.9g W=%.9g C=%.9g E=%.9g d=%.9g\n", itc, row,
+                                   (double)(cb ? ex1[r] : ex0[r]), (double)(cb ? ey1[r] : ey0[r]),
+                                   (double)(cb ? w1[r] : w0[r]), (double)(cb ? C1 : C0), (double)(cb ? E1 : E0),
+                                   (double)(cb ? d1 : d0));
+                    }
+                }
+#endif
                 if (kLo) {  // sign bit of max(|ex|, |ey|, (|ex| + |ey|) / sqrt 2) - R_lo: set when surely in
                     const float o0 = __builtin_amdgcn_fmed3f(m0, (fabsf(ex0[r]) + fabsf(ey0[r])) * 0.70710677f, big);
                     const float o1 = __builtin_amdgcn_fmed3f(m1, (fabsf(ex1[r]) + fabsf(ey1[r])) * 0.70710677f, big);
@@ -2236,8 +2278,9 @@ __global__ __launch_bounds__(64) void ransac_bound_check_kernel(const RansacStat
                              inv, unc, eta, eta_m);
             double dmax = 0;
             for (int i = 0; i < 8; ++i) dmax = fmax(dmax, fabs(Hd[i] - H[i]) / (fabs(H[i]) + 1e-12));
-            printf("[mim] bound violation p=%d it=%d exact=%d lo=%d hi=%d eta=%g uncertain=%d max_rel_dH=%g\n", p, it,
-                   ex, b.x, b.y, (double)eta, (int)unc, dmax);
+            const int4 s4v = decode_sample(samples[o], stream, (unsigned)S.n, S.modM);
+            printf("[mim] bound violation p=%d it=%d exact=%d lo=%d hi=%d eta=%g uncertain=%d max_rel_dH=%g sample %d %d %d %d\n",
+                   p, it, ex, b.x, b.y, (double)eta, (int)unc, dmax, s4v.x, s4v.y, s4v.z, s4v.w);
             float Hf[8], Hb[8];
             for (int i = 0; i < 8; ++i) { Hf[i] = (float)H[i]; Hb[i] = (float)Hd[i]; }
             const float4* P = pts + probs[p].good_off;
@@ -2248,9 +2291,10 @@ __global__ __launch_bounds__(64) void ransac_bound_check_kernel(const RansacStat
                 const float exx = fmaf(-q.z, W, fmaf(Hb[0], q.x, fmaf(Hb[1], q.y, Hb[2])));
                 const float eyy = fmaf(-q.w, W, fmaf(Hb[3], q.x, fmaf(Hb[4], q.y, Hb[5])));
                 const float eb = fmaf(exx, exx, eyy * eyy) / (W * W);
-                if ((err <= thr2) != (eb <= thr2) || fabsf(err - eb) > 0.1f)
-                    printf("[mim]   pt %d (%g %g -> %g %g) exact err %.6g bound-form err %.6g W %g\n", i, q.x, q.y, q.z, q.w,
-                           (double)err, (double)eb, (double)W);
+                if (err <= thr2 || (err <= thr2) != (eb <= thr2))
+                    printf("[mim]   pt %d (%g %g -> %g %g) exact err %.6g bound-form err %.6g W %g sa %g sb %g smax %g\n", i,
+                           q.x, q.y, q.z, q.w, (double)err, (double)eb, (double)W, (double)S.sa, (double)S.sb,
+                           (double)S.smax);
             }
         }
         atomicAdd(stats + 4, (unsigned long long)(b.y - b.x));

@@ -21,12 +21,9 @@
 #include <vector>
 
 #include "mim.h"
+#include "mim_types.hpp"
 
 namespace mim {
-
-struct Point2f {
-    float x, y;
-};
 
 // One view of an ObjectModel: n keypoints (KeyPoint::pt) + n x 128 CV_32F descriptors.
 struct View {

@@ -60,3 +60,23 @@ def test_struct_layouts():
     assert ctypes.sizeof(_lib.Params) == 56
     assert ctypes.sizeof(_lib.Result) == 96
     assert ctypes.sizeof(_lib.Problem) == 8
+
+
+def test_cmake_drop_in_builds(tmp_path):
+    """The CMake target the reference's pipeline links configures and builds the same
+    library for gfx950, exporting every mim.h symbol."""
+    import shutil
+    import subprocess
+    cmake = shutil.which("cmake")
+    if cmake is None or not os.path.exists("/opt/rocm/llvm/bin/clang++"):
+        pytest.skip("cmake / ROCm clang not available")
+    b = tmp_path / "build"
+    gen = ["-G", "Ninja"] if shutil.which("ninja") else []
+    subprocess.run([cmake, "-S", ROOT, "-B", str(b), *gen, "-DCMAKE_HIP_COMPILER=/opt/rocm/llvm/bin/clang++",
+                    "-DCMAKE_PREFIX_PATH=/opt/rocm"], check=True, capture_output=True, timeout=300)
+    subprocess.run([cmake, "--build", str(b), "-j", "8"], check=True, capture_output=True, timeout=900)
+    so = b / "libmim.so"
+    assert so.exists() and b"gfx950" in so.read_bytes()
+    lib = ctypes.CDLL(str(so))
+    missing = [s for s in _header_symbols() if not hasattr(lib, s)]
+    assert not missing, missing

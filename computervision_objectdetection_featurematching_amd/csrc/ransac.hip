@@ -2151,7 +2151,17 @@ __global__ __launch_bounds__(256) void ransac_bound_mfma_kernel(const RansacStat
     for (int t0 = 0; t0 < nt; t0 += kTileChunk) {
         const int tc = min(kTileChunk, nt - t0);
         __syncthreads();
+#ifdef MIM_BOUND_REGSTAGE
         for (int i = tid; i < tc * 128; i += 256) lt[i] = T[(long long)t0 * 128 + i];
+#else
+        // LDS-DMA: every 1-KiB piece of the chunk in flight at once (a register round trip per 16-B
+        // chunk waited for each load before its ds_write: one full load latency per piece)
+        const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+        for (int i0 = wv * 64; i0 < tc * 128; i0 += 256)
+            __builtin_amdgcn_global_load_lds((const void*)(T + (long long)t0 * 128 + i0 + lane),
+                                             (__attribute__((address_space(3))) void*)(lt + i0), 16, 0, 0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
         __syncthreads();
         if (!wave_counts) continue;
         for (int t = 0; t < tc; ++t) {

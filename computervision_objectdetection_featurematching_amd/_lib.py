@@ -19,7 +19,7 @@ EXPORTS = [
     "mim_ctx_set_stream", "mim_ctx_get_stream", "mim_synchronize", "mim_set_create", "mim_sets_clear", "mim_knn2_l2",
     "mim_ratio_filter", "mim_find_homography", "mim_batch_run", "mim_batch_results",
     "mim_batch_results_dev", "mim_batch_results_copy", "mim_batch_problem_detail", "mim_knn2_sets_dev", "mim_last_kernel_ms",
-    "mim_set_timing",
+    "mim_set_timing", "mim_sift_detect_compute", "mim_resize_linear_u8",
 ]
 
 
@@ -90,9 +90,13 @@ def load():
     L.mim_last_kernel_ms.argtypes = [vp, C.c_char_p]
     L.mim_last_kernel_ms.restype = C.c_double
     L.mim_set_timing.argtypes = [vp, i32]
+    L.mim_sift_detect_compute.argtypes = [vp, u8p, i32, i32, C.c_int64, u8p, C.c_int64, i32, vp, f32p,
+                                          C.POINTER(C.c_int32)]
+    L.mim_resize_linear_u8.argtypes = [vp, u8p, i32, i32, C.c_int64, u8p, i32, i32, C.c_double, C.c_double]
     for name in ("mim_ctx_create", "mim_ctx_set_stream", "mim_synchronize", "mim_set_create", "mim_sets_clear",
                  "mim_knn2_l2", "mim_ratio_filter", "mim_find_homography", "mim_batch_run", "mim_batch_results",
-                 "mim_batch_problem_detail", "mim_knn2_sets_dev", "mim_set_timing"):
+                 "mim_batch_problem_detail", "mim_knn2_sets_dev", "mim_set_timing",
+                 "mim_sift_detect_compute", "mim_resize_linear_u8"):
         getattr(L, name).restype = C.c_int32
     _lib = L
     return L

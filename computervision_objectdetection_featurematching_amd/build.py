@@ -9,7 +9,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIBDIR = os.path.join(HERE, "lib")
 SO = os.path.join(LIBDIR, "libmim.so")
-SOURCES = ["knn.hip", "ransac.hip", "api.cpp"]
+SOURCES = ["knn.hip", "ransac.hip", "sift.hip", "api.cpp"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 # -ffp-contract=off: the RANSAC/DLT arithmetic must not be FMA-contracted (OpenCV's calib3d
 # x86-64 build has no FMA), see DESIGN.md "Floating-point contract".

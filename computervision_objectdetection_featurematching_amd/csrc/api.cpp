@@ -213,6 +213,7 @@ struct mim_ctx {
     std::vector<Ev> evs;
     std::vector<hipEvent_t> ev_pool;  // recycled events (creating one per mark costs host time)
     std::map<std::string, double> last_ms;
+    mim::SiftWs* sift = nullptr;  // SIFT pyramid / candidate / descriptor workspace (first use)
 };
 
 static mim_status fail(mim_ctx* c, mim_status code, const char* fmt, ...) {
@@ -290,6 +291,7 @@ void mim_ctx_destroy(mim_ctx* c) {
     for (auto e : c->ev_samp)
         if (e) (void)hipEventDestroy(e);
     if (c->samp) (void)hipStreamDestroy(c->samp);
+    mim::sift_ws_destroy(c->sift);
     c->stage.destroy();
     c->prep_stage.destroy();
     c->arena.release();
@@ -681,6 +683,39 @@ mim_status mim_knn2_sets_dev(mim_ctx* c, int32_t query_set, int32_t train_set, i
     ev_mark(c, "ratio");
     c->last_n = 0;  // no RANSAC records (mim.h)
     c->last_gen = -1;
+    return MIM_OK;
+}
+
+mim_status mim_sift_detect_compute(mim_ctx* c, const uint8_t* gray, int32_t rows, int32_t cols, int64_t step,
+                                   const uint8_t* mask, int64_t mask_step, int32_t max_kp, mim_keypoint* kps,
+                                   float* desc, int32_t* n_kp) {
+    if (!c) return MIM_EINVAL;
+    if (!gray || !n_kp || rows <= 0 || cols <= 0 || step < cols || max_kp < 0 || (max_kp > 0 && (!kps || !desc)) ||
+        (mask && mask_step < cols))
+        return fail(c, MIM_EINVAL, "sift_detect_compute: bad arguments");
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIPCHK(c, hipSetDevice(c->device));
+    if (!c->sift) c->sift = mim::sift_ws_create();
+    int n = 0;
+    const int r = mim::sift_detect_compute(c->sift, c->stream, gray, rows, cols, step, mask, mask_step, max_kp, kps,
+                                           desc, &n, c->err);
+    *n_kp = n;
+    if (r == -1) return MIM_EDEVICE;
+    if (r == -2) return MIM_ERANGE;
+    return MIM_OK;
+}
+
+mim_status mim_resize_linear_u8(mim_ctx* c, const uint8_t* src, int32_t rows, int32_t cols, int64_t step,
+                                uint8_t* dst, int32_t drows, int32_t dcols, double fx, double fy) {
+    if (!c) return MIM_EINVAL;
+    if (!src || !dst || rows <= 0 || cols <= 0 || step < cols || drows <= 0 || dcols <= 0 || fx < 0 || fy < 0 ||
+        (fx > 0) != (fy > 0))
+        return fail(c, MIM_EINVAL, "resize_linear_u8: bad arguments");
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIPCHK(c, hipSetDevice(c->device));
+    if (!c->sift) c->sift = mim::sift_ws_create();
+    if (mim::sift_resize_u8(c->sift, c->stream, src, rows, cols, step, dst, drows, dcols, fx, fy, c->err) != 0)
+        return MIM_EDEVICE;
     return MIM_OK;
 }
 

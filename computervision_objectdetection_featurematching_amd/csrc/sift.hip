@@ -1,0 +1,649 @@
+// sift.hip — SIFT::detectAndCompute (OpenCV 4.5.4 defaults) and resize(INTER_LINEAR, 8U) on gfx950.
+//
+// Replaces the feature extraction around the matcher: the model views (/root/reference/src/
+// ModelsDetector.cpp:75, with mask) and every scene scale (TestsDetector.cpp:102 resize, :106
+// detectAndCompute), SIFT::create() defaults (main.cpp:17): 3 octave layers, contrast 0.04, edge 10,
+// sigma 1.6, first octave -1 (the image doubled), CV_32F descriptors of 0..255 integers.
+//
+// One launch per stage, every pixel / candidate / keypoint its own thread:
+//   up2       u8 -> float, x2 INTER_LINEAR (createInitialImage)
+//   blur_row  Gaussian row pass, taps in order          } GaussianBlur(CV_32F, BORDER_REFLECT_101):
+//   blur_col  Gaussian column pass, symmetric pairs     } OpenCV's RowFilter / SymmColumnFilter sums
+//   down2     next octave's first layer (INTER_NEAREST, every 2nd pixel)
+//   dog       difference of adjacent layers, all 5 of an octave in one launch
+//   extrema   26-neighbour test + threshold over layers 1..3, candidates appended
+//   refine    adjustLocalExtrema (<= 5 Newton steps, Cramer 3x3 solve), contrast + edge tests,
+//             calcOrientationHist (36 bins, smoothed), one keypoint per peak >= 80 % of the maximum
+//   (host)    KeyPointsFilter::removeDuplicatedSorted, the 1/2 rescale of octave -1, the mask filter
+//   descr     calcSIFTDescriptor: 4x4x8 trilinear histogram in LDS (per thread, pixel order),
+//             wrap, clamp at 0.2 of the norm, x 512 / norm, saturate to 0..255
+// The histograms accumulate in the reference's pixel order (one thread per keypoint), so the results
+// are the CPU restatement's (oracle/sift_oracle.c) bit for bit up to the rare last-bit difference of
+// a double-precision exp/sin/cos/pow rounded to float (both sides use those, see sift_oracle.h).
+#include "mim_internal.h"
+
+#include <float.h>
+#include <limits.h>
+
+#include <algorithm>
+#include <cmath>
+#include <string>
+#include <vector>
+
+namespace mim {
+
+namespace {
+
+constexpr int kNOL = 3;
+constexpr int kBorder = 5;
+constexpr int kOriBins = 36;
+constexpr int kDW = 4, kDB = 8;
+constexpr int kHistLen = (kDW + 2) * (kDW + 2) * (kDB + 2);  // 360
+constexpr int kDescrThreads = 32;                             // threads (keypoints) per descriptor block
+
+__device__ __forceinline__ int reflect101(int p, int len) {
+    if (len == 1) return 0;
+    while (p < 0 || p >= len) p = p < 0 ? -p : 2 * len - 2 - p;
+    return p;
+}
+
+__device__ __forceinline__ int cv_round(float v) { return __float2int_rn(v); }  // ties to even
+__device__ __forceinline__ int cv_round_d(double v) { return __double2int_rn(v); }
+
+struct LinCoef {
+    int s;
+    float a0, a1;
+};
+
+// resize(INTER_LINEAR) source offset and weights of destination index d (resize.cpp)
+__device__ __forceinline__ LinCoef lin_coef(int d, int ssize, double scale, bool clamp) {
+    float f = (float)((d + 0.5) * scale - 0.5);
+    int s = (int)floor(f);
+    f -= s;
+    if (clamp) {
+        if (s < 0) f = 0, s = 0;
+        if (s >= ssize - 1) f = 0, s = ssize - 1;
+    }
+    return LinCoef{s, 1.f - f, f};
+}
+
+__global__ void up2_kernel(const uint8_t* __restrict__ src, int rows, int cols, float* __restrict__ dst) {
+    const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
+    const int dr = rows * 2, dc = cols * 2;
+    if (x >= dc) return;
+    const LinCoef cx = lin_coef(x, cols, (double)cols / dc, true), cy = lin_coef(y, rows, (double)rows / dr, false);
+    float h[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        int sy = cy.s + k;
+        sy = sy < 0 ? 0 : (sy >= rows ? rows - 1 : sy);
+        const uint8_t* S = src + (size_t)sy * cols;
+        h[k] = cx.s + 1 < cols ? (float)S[cx.s] * cx.a0 + (float)S[cx.s + 1] * cx.a1 : (float)S[cx.s];
+    }
+    dst[(size_t)y * dc + x] = h[0] * cy.a0 + h[1] * cy.a1;
+}
+
+// resize(INTER_LINEAR) of CV_8UC1: fixed-point weights (x 2048); the vertical pass as OpenCV's
+// 128-bit vector path for columns < (dcols / 16) * 16, the exact rounding shift for the rest
+__global__ void resize_u8_kernel(const uint8_t* __restrict__ src, int rows, int cols, uint8_t* __restrict__ dst,
+                                 int drows, int dcols, double sx, double sy) {
+    const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
+    if (x >= dcols) return;
+    const LinCoef cx = lin_coef(x, cols, sx, true), cy = lin_coef(y, rows, sy, false);
+    const int a0 = cv_round(cx.a0 * 2048.f), a1 = cv_round(cx.a1 * 2048.f);
+    const int b0 = (short)cv_round(cy.a0 * 2048.f), b1 = (short)cv_round(cy.a1 * 2048.f);
+    int h[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        int sy = cy.s + k;
+        sy = sy < 0 ? 0 : (sy >= rows ? rows - 1 : sy);
+        const uint8_t* S = src + (size_t)sy * cols;
+        h[k] = cx.s + 1 < cols ? S[cx.s] * a0 + S[cx.s + 1] * a1 : S[cx.s] * 2048;
+    }
+    int v;
+    if (x < dcols / 16 * 16) {
+        const int p0 = (int)(short)(h[0] >> 4), p1 = (int)(short)(h[1] >> 4);
+        v = (((p0 * b0) >> 16) + ((p1 * b1) >> 16) + 2) >> 2;
+    } else {
+        v = (h[0] * b0 + h[1] * b1 + (1 << 21)) >> 22;
+    }
+    dst[(size_t)y * dcols + x] = (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v));
+}
+
+struct Taps {
+    float k[64];
+    int n;
+};
+
+__global__ void blur_row_kernel(const float* __restrict__ src, float* __restrict__ dst, int rows, int cols, Taps t) {
+    const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
+    if (x >= cols) return;
+    const float* S = src + (size_t)y * cols;
+    const int a = t.n / 2;
+    float acc = t.k[0] * S[reflect101(x - a, cols)];
+    for (int i = 1; i < t.n; ++i) acc += t.k[i] * S[reflect101(x - a + i, cols)];
+    dst[(size_t)y * cols + x] = acc;
+}
+
+__global__ void blur_col_kernel(const float* __restrict__ src, float* __restrict__ dst, int rows, int cols, Taps t) {
+    const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
+    if (x >= cols) return;
+    const int a = t.n / 2;
+    float acc = t.k[a] * src[(size_t)y * cols + x] + 0.f;
+    for (int i = 1; i <= a; ++i)
+        acc += t.k[a + i] * (src[(size_t)reflect101(y + i, rows) * cols + x] + src[(size_t)reflect101(y - i, rows) * cols + x]);
+    dst[(size_t)y * cols + x] = acc;
+}
+
+__global__ void down2_kernel(const float* __restrict__ src, int scols, float* __restrict__ dst, int rows, int cols) {
+    const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
+    if (x >= cols) return;
+    dst[(size_t)y * cols + x] = src[(size_t)(2 * y) * scols + 2 * x];
+}
+
+// the 5 DoG layers of one octave: dog[i] = gauss[i + 1] - gauss[i]
+__global__ void dog_kernel(const float* __restrict__ gauss, float* __restrict__ dog, size_t plane) {
+    const size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int i = blockIdx.y;
+    if (p >= plane) return;
+    dog[i * plane + p] = gauss[(i + 1) * plane + p] - gauss[i * plane + p];
+}
+
+struct Cand {
+    int o, layer, r, c;
+};
+
+// findScaleSpaceExtrema's pixel test over layers 1..3 of one octave (blockIdx.z = layer - 1)
+__global__ void extrema_kernel(const float* __restrict__ dog, int rows, int cols, int octave, int threshold,
+                               Cand* __restrict__ cand, int* __restrict__ n_cand, int cap) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x + kBorder, r = blockIdx.y + kBorder, layer = blockIdx.z + 1;
+    if (c >= cols - kBorder || r >= rows - kBorder) return;
+    const size_t plane = (size_t)rows * cols;
+    const float* cur = dog + layer * plane;
+    const float val = cur[(size_t)r * cols + c];
+    if (!(fabsf(val) > (float)threshold)) return;
+    bool ext = true;
+    for (int dz = -1; dz <= 1 && ext; ++dz) {
+        const float* L = cur + dz * (long long)plane;
+        for (int dy = -1; dy <= 1 && ext; ++dy)
+            for (int dx = -1; dx <= 1; ++dx) {
+                if (dz == 0 && dy == 0 && dx == 0) continue;
+                const float nb = L[(size_t)(r + dy) * cols + c + dx];
+                if (val > 0 ? !(val >= nb) : !(val <= nb)) {
+                    ext = false;
+                    break;
+                }
+            }
+    }
+    if (!ext) return;
+    const int k = atomicAdd(n_cand, 1);
+    if (k < cap) cand[k] = Cand{octave, layer, r, c};
+}
+
+struct Layer {
+    const float* p;
+    int rows, cols;
+};
+
+struct Pyr {
+    Layer gauss[16][kNOL + 3];
+    Layer dog[16][kNOL + 2];
+};
+
+#define AT(L, r, c) ((L).p[(size_t)(r) * (L).cols + (c)])
+
+// OpenCV fastAtan2 (degrees)
+__device__ __forceinline__ float fast_atan2(float y, float x) {
+    const float p1 = 0.9997878412794807f * (float)(180 / M_PI), p3 = -0.3258083974640975f * (float)(180 / M_PI);
+    const float p5 = 0.1555786518463281f * (float)(180 / M_PI), p7 = -0.04432655554792128f * (float)(180 / M_PI);
+    const float ax = fabsf(x), ay = fabsf(y);
+    float a, c, c2;
+    if (ax >= ay) {
+        c = ay / (ax + (float)DBL_EPSILON);
+        c2 = c * c;
+        a = (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+    } else {
+        c = ax / (ay + (float)DBL_EPSILON);
+        c2 = c * c;
+        a = 90.f - (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+    }
+    if (x < 0) a = 180.f - a;
+    if (y < 0) a = 360.f - a;
+    return a;
+}
+
+// Matx33f::solve(DECOMP_LU) for 3x3: Cramer with the float determinant
+__device__ __forceinline__ bool solve3(const float* H, const float* b, float* x) {
+    float d = H[0] * (H[4] * H[8] - H[7] * H[5]) - H[1] * (H[3] * H[8] - H[6] * H[5]) + H[2] * (H[3] * H[7] - H[6] * H[4]);
+    if (d == 0) return false;
+    d = 1 / d;
+    x[0] = d * (b[0] * (H[4] * H[8] - H[5] * H[7]) - H[1] * (b[1] * H[8] - H[5] * b[2]) + H[2] * (b[1] * H[7] - H[4] * b[2]));
+    x[1] = d * (H[0] * (b[1] * H[8] - H[5] * b[2]) - b[0] * (H[3] * H[8] - H[5] * H[6]) + H[2] * (H[3] * b[2] - b[1] * H[6]));
+    x[2] = d * (H[0] * (H[4] * b[2] - b[1] * H[7]) - H[1] * (H[3] * b[2] - b[1] * H[6]) + b[0] * (H[3] * H[7] - H[4] * H[6]));
+    return true;
+}
+
+// adjustLocalExtrema + calcOrientationHist + the peak loop of findScaleSpaceExtrema, one thread per
+// candidate; keypoints in the doubled image's coordinates (octave field packed as OpenCV's)
+__global__ void refine_kernel(const Pyr* __restrict__ pyr, const Cand* __restrict__ cand, const int* __restrict__ n_cand,
+                              int cap, mim_keypoint* __restrict__ kp, int* __restrict__ n_kp, int kp_cap) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= min(*n_cand, cap)) return;
+    const float kSigma = 1.6f, kContrast = 0.04f, kEdge = 10.f;
+    const float img_scale = 1.f / 255, deriv_scale = img_scale * 0.5f, second_deriv_scale = img_scale;
+    const float cross_deriv_scale = img_scale * 0.25f;
+    const Cand cd = cand[t];
+    const int octv = cd.o;
+    int layer = cd.layer, r = cd.r, c = cd.c;
+    float xi = 0, xr = 0, xc = 0, contr = 0;
+    int i = 0;
+    for (; i < 5; i++) {
+        const Layer im = pyr->dog[octv][layer], pv = pyr->dog[octv][layer - 1], nx = pyr->dog[octv][layer + 1];
+        const float dD[3] = {(AT(im, r, c + 1) - AT(im, r, c - 1)) * deriv_scale,
+                             (AT(im, r + 1, c) - AT(im, r - 1, c)) * deriv_scale,
+                             (AT(nx, r, c) - AT(pv, r, c)) * deriv_scale};
+        const float v2 = AT(im, r, c) * 2;
+        const float dxx = (AT(im, r, c + 1) + AT(im, r, c - 1) - v2) * second_deriv_scale;
+        const float dyy = (AT(im, r + 1, c) + AT(im, r - 1, c) - v2) * second_deriv_scale;
+        const float dss = (AT(nx, r, c) + AT(pv, r, c) - v2) * second_deriv_scale;
+        const float dxy = (AT(im, r + 1, c + 1) - AT(im, r + 1, c - 1) - AT(im, r - 1, c + 1) + AT(im, r - 1, c - 1)) * cross_deriv_scale;
+        const float dxs = (AT(nx, r, c + 1) - AT(nx, r, c - 1) - AT(pv, r, c + 1) + AT(pv, r, c - 1)) * cross_deriv_scale;
+        const float dys = (AT(nx, r + 1, c) - AT(nx, r - 1, c) - AT(pv, r + 1, c) + AT(pv, r - 1, c)) * cross_deriv_scale;
+        const float H[9] = {dxx, dxy, dxs, dxy, dyy, dys, dxs, dys, dss};
+        float X[3] = {0, 0, 0};
+        if (!solve3(H, dD, X)) X[0] = X[1] = X[2] = 0;
+        xi = -X[2];
+        xr = -X[1];
+        xc = -X[0];
+        if (fabsf(xi) < 0.5f && fabsf(xr) < 0.5f && fabsf(xc) < 0.5f) break;
+        if (fabsf(xi) > (float)(INT_MAX / 3) || fabsf(xr) > (float)(INT_MAX / 3) || fabsf(xc) > (float)(INT_MAX / 3)) return;
+        c += cv_round(xc);
+        r += cv_round(xr);
+        layer += cv_round(xi);
+        if (layer < 1 || layer > kNOL || c < kBorder || c >= im.cols - kBorder || r < kBorder || r >= im.rows - kBorder) return;
+    }
+    if (i >= 5) return;
+    {
+        const Layer im = pyr->dog[octv][layer], pv = pyr->dog[octv][layer - 1], nx = pyr->dog[octv][layer + 1];
+        const float dD[3] = {(AT(im, r, c + 1) - AT(im, r, c - 1)) * deriv_scale,
+                             (AT(im, r + 1, c) - AT(im, r - 1, c)) * deriv_scale,
+                             (AT(nx, r, c) - AT(pv, r, c)) * deriv_scale};
+        const float tt = dD[0] * xc + dD[1] * xr + dD[2] * xi;
+        contr = AT(im, r, c) * img_scale + tt * 0.5f;
+        if (fabsf(contr) * kNOL < kContrast) return;
+        const float v2 = AT(im, r, c) * 2.f;
+        const float dxx = (AT(im, r, c + 1) + AT(im, r, c - 1) - v2) * second_deriv_scale;
+        const float dyy = (AT(im, r + 1, c) + AT(im, r - 1, c) - v2) * second_deriv_scale;
+        const float dxy = (AT(im, r + 1, c + 1) - AT(im, r + 1, c - 1) - AT(im, r - 1, c + 1) + AT(im, r - 1, c - 1)) * cross_deriv_scale;
+        const float tr = dxx + dyy, det = dxx * dyy - dxy * dxy;
+        if (det <= 0 || tr * tr * kEdge >= (kEdge + 1) * (kEdge + 1) * det) return;
+    }
+    mim_keypoint k;
+    k.x = (c + xc) * (1 << octv);
+    k.y = (r + xr) * (1 << octv);
+    k.octave = octv + (layer << 8) + (cv_round_d((xi + 0.5) * 255) << 16);
+    k.size = kSigma * (float)pow(2.0, (double)((layer + xi) / kNOL)) * (1 << octv) * 2;
+    k.response = fabsf(contr);
+    k.angle = 0;
+
+    // calcOrientationHist on the Gaussian layer, pixel order
+    const Layer g = pyr->gauss[octv][layer];
+    const float scl_octv = k.size * 0.5f / (1 << octv);
+    const int radius = cv_round(4.5f * scl_octv);
+    const float sigma = 1.5f * scl_octv;
+    const float expf_scale = -1.f / (2.f * sigma * sigma);
+    float th[kOriBins + 4];
+    for (int b = 0; b < kOriBins + 4; ++b) th[b] = 0.f;
+    for (int ii = -radius; ii <= radius; ii++) {
+        const int y = r + ii;
+        if (y <= 0 || y >= g.rows - 1) continue;
+        for (int j = -radius; j <= radius; j++) {
+            const int x = c + j;
+            if (x <= 0 || x >= g.cols - 1) continue;
+            const float dx = AT(g, y, x + 1) - AT(g, y, x - 1);
+            const float dy = AT(g, y - 1, x) - AT(g, y + 1, x);
+            const float w = (float)exp((double)((float)(ii * ii + j * j) * expf_scale));
+            const float ori = fast_atan2(dy, dx);
+            const float mag = sqrtf(dx * dx + dy * dy);
+            int bin = cv_round((kOriBins / 360.f) * ori);
+            if (bin >= kOriBins) bin -= kOriBins;
+            if (bin < 0) bin += kOriBins;
+            th[bin + 2] += w * mag;
+        }
+    }
+    th[1] = th[kOriBins + 1];
+    th[0] = th[kOriBins];
+    th[kOriBins + 2] = th[2];
+    th[kOriBins + 3] = th[3];
+    float hist[kOriBins];
+    float mx = 0;
+    for (int b = 0; b < kOriBins; b++) {
+        hist[b] = (th[b] + th[b + 4]) * (1.f / 16.f) + (th[b + 1] + th[b + 3]) * (4.f / 16.f) + th[b + 2] * (6.f / 16.f);
+        mx = b == 0 ? hist[0] : fmaxf(mx, hist[b]);
+    }
+    const float mag_thr = mx * 0.8f;
+    for (int j = 0; j < kOriBins; j++) {
+        const int l = j > 0 ? j - 1 : kOriBins - 1, r2 = j < kOriBins - 1 ? j + 1 : 0;
+        if (hist[j] > hist[l] && hist[j] > hist[r2] && hist[j] >= mag_thr) {
+            float bin = j + 0.5f * (hist[l] - hist[r2]) / (hist[l] - 2 * hist[j] + hist[r2]);
+            bin = bin < 0 ? kOriBins + bin : (bin >= kOriBins ? bin - kOriBins : bin);
+            k.angle = 360.f - (float)((360.f / kOriBins) * bin);
+            if (fabsf(k.angle - 360.f) < FLT_EPSILON) k.angle = 0.f;
+            const int slot = atomicAdd(n_kp, 1);
+            if (slot < kp_cap) kp[slot] = k;
+        }
+    }
+}
+
+// calcSIFTDescriptor, one thread per keypoint, its 360-bin histogram in LDS; keypoints in input
+// coordinates (after the 1/2 rescale), octave field as OpenCV packs it
+__global__ __launch_bounds__(kDescrThreads) void descr_kernel(const Pyr* __restrict__ pyr, const mim_keypoint* __restrict__ kp,
+                                                              int n, float* __restrict__ desc) {
+    __shared__ float hbuf[kDescrThreads * kHistLen];
+    const int t = blockIdx.x * kDescrThreads + threadIdx.x;
+    if (t >= n) return;
+    float* hist = hbuf + threadIdx.x * kHistLen;
+    const mim_keypoint p = kp[t];
+    int octave = p.octave & 255;
+    const int layer = (p.octave >> 8) & 255;
+    octave = octave < 128 ? octave : (-128 | octave);
+    const float scale = octave >= 0 ? 1.f / (1 << octave) : (float)(1 << -octave);
+    const float size = p.size * scale;
+    const Layer im = pyr->gauss[octave + 1][layer];
+    float ori = 360.f - p.angle;
+    if (fabsf(ori - 360.f) < FLT_EPSILON) ori = 0.f;
+    const float scl = size * 0.5f;
+    const int px = cv_round(p.x * scale), py = cv_round(p.y * scale);
+    float cos_t = (float)cos((double)(ori * (float)(M_PI / 180))), sin_t = (float)sin((double)(ori * (float)(M_PI / 180)));
+    const float bins_per_rad = kDB / 360.f, exp_scale = -1.f / (kDW * kDW * 0.5f);
+    const float hist_width = 3.f * scl;
+    int radius = cv_round(hist_width * 1.4142135623730951f * (kDW + 1) * 0.5f);
+    const int rmax = (int)sqrt((double)im.cols * im.cols + (double)im.rows * im.rows);
+    if (radius > rmax) radius = rmax;
+    cos_t /= hist_width;
+    sin_t /= hist_width;
+    for (int b = 0; b < kHistLen; ++b) hist[b] = 0.f;
+    for (int i = -radius; i <= radius; i++)
+        for (int j = -radius; j <= radius; j++) {
+            const float c_rot = j * cos_t - i * sin_t, r_rot = j * sin_t + i * cos_t;
+            float rbin = r_rot + kDW / 2 - 0.5f, cbin = c_rot + kDW / 2 - 0.5f;
+            const int r = py + i, c = px + j;
+            if (!(rbin > -1 && rbin < kDW && cbin > -1 && cbin < kDW && r > 0 && r < im.rows - 1 && c > 0 && c < im.cols - 1))
+                continue;
+            const float dx = AT(im, r, c + 1) - AT(im, r, c - 1), dy = AT(im, r - 1, c) - AT(im, r + 1, c);
+            const float w = (float)exp((double)((c_rot * c_rot + r_rot * r_rot) * exp_scale));
+            const float o = fast_atan2(dy, dx), m = sqrtf(dx * dx + dy * dy);
+            float obin = (o - ori) * bins_per_rad;
+            const float mag = m * w;
+            const int r0 = (int)floorf(rbin), c0 = (int)floorf(cbin);
+            int o0 = (int)floorf(obin);
+            rbin -= r0;
+            cbin -= c0;
+            obin -= o0;
+            if (o0 < 0) o0 += kDB;
+            if (o0 >= kDB) o0 -= kDB;
+            const float v_r1 = mag * rbin, v_r0 = mag - v_r1;
+            const float v_rc11 = v_r1 * cbin, v_rc10 = v_r1 - v_rc11, v_rc01 = v_r0 * cbin, v_rc00 = v_r0 - v_rc01;
+            const float v_rco111 = v_rc11 * obin, v_rco110 = v_rc11 - v_rco111, v_rco101 = v_rc10 * obin, v_rco100 = v_rc10 - v_rco101;
+            const float v_rco011 = v_rc01 * obin, v_rco010 = v_rc01 - v_rco011, v_rco001 = v_rc00 * obin, v_rco000 = v_rc00 - v_rco001;
+            const int idx = ((r0 + 1) * (kDW + 2) + c0 + 1) * (kDB + 2) + o0;
+            hist[idx] += v_rco000;
+            hist[idx + 1] += v_rco001;
+            hist[idx + (kDB + 2)] += v_rco010;
+            hist[idx + (kDB + 3)] += v_rco011;
+            hist[idx + (kDW + 2) * (kDB + 2)] += v_rco100;
+            hist[idx + (kDW + 2) * (kDB + 2) + 1] += v_rco101;
+            hist[idx + (kDW + 3) * (kDB + 2)] += v_rco110;
+            hist[idx + (kDW + 3) * (kDB + 2) + 1] += v_rco111;
+        }
+    float* out = desc + (size_t)t * 128;
+    float nrm2 = 0;
+    for (int i = 0; i < kDW; i++)
+        for (int j = 0; j < kDW; j++) {
+            const int idx = ((i + 1) * (kDW + 2) + (j + 1)) * (kDB + 2);
+            hist[idx] += hist[idx + kDB];
+            hist[idx + 1] += hist[idx + kDB + 1];
+        }
+    for (int i = 0; i < kDW; i++)
+        for (int j = 0; j < kDW; j++)
+            for (int k = 0; k < kDB; k++) {
+                const float v = hist[((i + 1) * (kDW + 2) + (j + 1)) * (kDB + 2) + k];
+                nrm2 += v * v;
+            }
+    const float thr = sqrtf(nrm2) * 0.2f;
+    nrm2 = 0;
+    for (int i = 0; i < kDW; i++)
+        for (int j = 0; j < kDW; j++)
+            for (int k = 0; k < kDB; k++) {
+                float& v = hist[((i + 1) * (kDW + 2) + (j + 1)) * (kDB + 2) + k];
+                v = fminf(v, thr);
+                nrm2 += v * v;
+            }
+    nrm2 = 512.f / fmaxf(sqrtf(nrm2), FLT_EPSILON);
+    for (int i = 0; i < kDW; i++)
+        for (int j = 0; j < kDW; j++)
+            for (int k = 0; k < kDB; k++) {
+                const int v = cv_round(hist[((i + 1) * (kDW + 2) + (j + 1)) * (kDB + 2) + k] * nrm2);
+                out[(i * kDW + j) * kDB + k] = (float)(v < 0 ? 0 : (v > 255 ? 255 : v));
+            }
+}
+
+// ---- host ---------------------------------------------------------------------------------------
+
+int gauss_taps(double sigma, Taps& t) {
+    const int n = (int)lrint(sigma * 4 * 2 + 1) | 1;
+    if (n > 64) return -1;
+    const double scale2X = -0.5 / (sigma * sigma);
+    double sum = 0;
+    for (int i = 0; i < n; ++i) {
+        const double x = i - (n - 1) * 0.5;
+        t.k[i] = (float)exp(scale2X * x * x);
+        sum += t.k[i];
+    }
+    sum = 1. / sum;
+    for (int i = 0; i < n; ++i) t.k[i] = (float)(t.k[i] * sum);
+    t.n = n;
+    return n;
+}
+
+bool kp_greater(const mim_keypoint& a, const mim_keypoint& b) {  // KeypointGreater
+    if (a.x != b.x) return a.x > b.x;
+    if (a.y != b.y) return a.y > b.y;
+    if (a.size != b.size) return a.size > b.size;
+    if (a.angle != b.angle) return a.angle > b.angle;
+    if (a.response != b.response) return a.response > b.response;
+    return a.octave > b.octave;
+}
+
+}  // namespace
+
+struct SiftWs {
+    void* img = nullptr;   size_t img_cap = 0;
+    void* pyr = nullptr;   size_t pyr_cap = 0;
+    void* tmp = nullptr;   size_t tmp_cap = 0;
+    void* aux = nullptr;   size_t aux_cap = 0;  // candidates, keypoints, counters, Pyr table
+    void* desc = nullptr;  size_t desc_cap = 0;
+};
+
+static hipError_t grow(void*& p, size_t& cap, size_t need) {
+    if (need <= cap) return hipSuccess;
+    if (p) {
+        hipError_t e = hipFree(p);
+        if (e != hipSuccess) return e;
+        p = nullptr;
+        cap = 0;
+    }
+    const size_t want = need + need / 4;
+    hipError_t e = hipMalloc(&p, want);
+    if (e == hipSuccess) cap = want;
+    return e;
+}
+
+SiftWs* sift_ws_create() { return new SiftWs(); }
+
+void sift_ws_destroy(SiftWs* w) {
+    if (!w) return;
+    for (void* p : {w->img, w->pyr, w->tmp, w->aux, w->desc})
+        if (p) (void)hipFree(p);
+    delete w;
+}
+
+#define SCHK(x)                                              \
+    do {                                                     \
+        hipError_t e_ = (x);                                 \
+        if (e_ != hipSuccess) {                              \
+            err = std::string(#x) + ": " + hipGetErrorString(e_); \
+            return -1;                                       \
+        }                                                    \
+    } while (0)
+
+int sift_resize_u8(SiftWs* w, hipStream_t st, const uint8_t* src, int rows, int cols, long long step, uint8_t* dst,
+                   int drows, int dcols, double fx, double fy, std::string& err) {
+    const size_t sb = (size_t)rows * cols, db = (size_t)drows * dcols;
+    SCHK(grow(w->img, w->img_cap, sb + db));
+    uint8_t* ds = (uint8_t*)w->img;
+    uint8_t* dd = ds + sb;
+    SCHK(hipMemcpy2DAsync(ds, cols, src, step, cols, rows, hipMemcpyHostToDevice, st));
+    resize_u8_kernel<<<dim3((dcols + 255) / 256, drows), 256, 0, st>>>(ds, rows, cols, dd, drows, dcols, 1. / (fx > 0 ? fx : (double)dcols / cols),
+                                                                     1. / (fy > 0 ? fy : (double)drows / rows));
+    SCHK(hipGetLastError());
+    SCHK(hipMemcpyAsync(dst, dd, db, hipMemcpyDeviceToHost, st));
+    SCHK(hipStreamSynchronize(st));
+    return 0;
+}
+
+int sift_detect_compute(SiftWs* w, hipStream_t st, const uint8_t* img, int rows, int cols, long long step,
+                        const uint8_t* mask, long long mstep, int max_kp, mim_keypoint* kps, float* desc, int* n_out,
+                        std::string& err) {
+    *n_out = 0;
+    const int R = rows * 2, C = cols * 2;
+    const int n_oct = (int)lrint(log((double)std::min(R, C)) / log(2.) - 2) + 1;
+    if (n_oct < 1 || n_oct > 16) {
+        err = "image too small or too large for SIFT";
+        return -2;
+    }
+    // pyramid layout: per octave 6 Gaussian + 5 DoG planes
+    std::vector<int> orows(n_oct), ocols(n_oct);
+    std::vector<size_t> goff(n_oct), doff(n_oct);
+    size_t total = 0;
+    for (int o = 0; o < n_oct; ++o) {
+        orows[o] = o == 0 ? R : orows[o - 1] / 2;
+        ocols[o] = o == 0 ? C : ocols[o - 1] / 2;
+        const size_t plane = (size_t)orows[o] * ocols[o];
+        goff[o] = total;
+        total += plane * (kNOL + 3);
+        doff[o] = total;
+        total += plane * (kNOL + 2);
+    }
+    const size_t img_bytes = (size_t)rows * cols;
+    SCHK(grow(w->img, w->img_cap, img_bytes));
+    SCHK(grow(w->pyr, w->pyr_cap, total * sizeof(float)));
+    SCHK(grow(w->tmp, w->tmp_cap, (size_t)R * C * sizeof(float) * 2));
+    float* P = (float*)w->pyr;
+    float* T0 = (float*)w->tmp;
+    float* T1 = T0 + (size_t)R * C;
+    SCHK(hipMemcpy2DAsync(w->img, cols, img, step, cols, rows, hipMemcpyHostToDevice, st));
+
+    auto blur = [&](const float* s, float* d, int rr, int cc, double sigma) -> bool {
+        Taps t;
+        if (gauss_taps(sigma, t) < 0) return false;
+        const dim3 g((cc + 255) / 256, rr);
+        blur_row_kernel<<<g, 256, 0, st>>>(s, T1, rr, cc, t);
+        blur_col_kernel<<<g, 256, 0, st>>>(T1, d, rr, cc, t);
+        return true;
+    };
+    // createInitialImage
+    up2_kernel<<<dim3((C + 255) / 256, R), 256, 0, st>>>((const uint8_t*)w->img, rows, cols, T0);
+    const float sig_diff = sqrtf(std::max(1.6f * 1.6f - 0.5f * 0.5f * 4, 0.01f));
+    if (!blur(T0, P + goff[0], R, C, sig_diff)) { err = "kernel size"; return -2; }
+    // buildGaussianPyramid + DoG
+    double sig[kNOL + 3];
+    sig[0] = 1.6;
+    const double kk = pow(2., 1. / kNOL);
+    for (int i = 1; i < kNOL + 3; i++) {
+        const double sp = pow(kk, (double)(i - 1)) * 1.6, stt = sp * kk;
+        sig[i] = sqrt(stt * stt - sp * sp);
+    }
+    for (int o = 0; o < n_oct; ++o) {
+        const size_t plane = (size_t)orows[o] * ocols[o];
+        float* G = P + goff[o];
+        if (o > 0)
+            down2_kernel<<<dim3((ocols[o] + 255) / 256, orows[o]), 256, 0, st>>>(P + goff[o - 1] + kNOL * (size_t)orows[o - 1] * ocols[o - 1],
+                                                                                ocols[o - 1], G, orows[o], ocols[o]);
+        for (int i = 1; i < kNOL + 3; ++i)
+            if (!blur(G + (i - 1) * plane, G + i * plane, orows[o], ocols[o], sig[i])) { err = "kernel size"; return -2; }
+        dog_kernel<<<dim3((unsigned)((plane + 255) / 256), kNOL + 2), 256, 0, st>>>(G, P + doff[o], plane);
+    }
+    SCHK(hipGetLastError());
+    // layer table
+    Pyr h_pyr{};
+    for (int o = 0; o < n_oct; ++o) {
+        const size_t plane = (size_t)orows[o] * ocols[o];
+        for (int i = 0; i < kNOL + 3; ++i) h_pyr.gauss[o][i] = Layer{P + goff[o] + i * plane, orows[o], ocols[o]};
+        for (int i = 0; i < kNOL + 2; ++i) h_pyr.dog[o][i] = Layer{P + doff[o] + i * plane, orows[o], ocols[o]};
+    }
+    const int cand_cap = 1 << 20, kp_cap = 1 << 19;
+    const size_t aux_bytes = sizeof(Pyr) + 256 + sizeof(Cand) * cand_cap + sizeof(mim_keypoint) * kp_cap;
+    SCHK(grow(w->aux, w->aux_cap, aux_bytes));
+    char* A = (char*)w->aux;
+    Pyr* d_pyr = (Pyr*)A;
+    int* d_cnt = (int*)(A + sizeof(Pyr));  // [0] candidates, [1] keypoints
+    Cand* d_cand = (Cand*)(A + sizeof(Pyr) + 256);
+    mim_keypoint* d_kp = (mim_keypoint*)(d_cand + cand_cap);
+    SCHK(hipMemcpyAsync(d_pyr, &h_pyr, sizeof(Pyr), hipMemcpyHostToDevice, st));
+    SCHK(hipMemsetAsync(d_cnt, 0, 2 * sizeof(int), st));
+    const int threshold = (int)floor(0.5 * 0.04 / kNOL * 255);
+    for (int o = 0; o < n_oct; ++o) {
+        if (orows[o] <= 2 * kBorder || ocols[o] <= 2 * kBorder) continue;
+        extrema_kernel<<<dim3((ocols[o] - 2 * kBorder + 127) / 128, orows[o] - 2 * kBorder, kNOL), 128, 0, st>>>(
+            P + doff[o], orows[o], ocols[o], o, threshold, d_cand, d_cnt, cand_cap);
+    }
+    int h_cnt[2] = {0, 0};
+    SCHK(hipMemcpyAsync(h_cnt, d_cnt, sizeof(int), hipMemcpyDeviceToHost, st));
+    SCHK(hipStreamSynchronize(st));
+    if (h_cnt[0] > cand_cap) { err = "more than 2^20 SIFT candidates"; return -2; }
+    if (h_cnt[0] > 0) refine_kernel<<<(h_cnt[0] + 127) / 128, 128, 0, st>>>(d_pyr, d_cand, d_cnt, cand_cap, d_kp, d_cnt + 1, kp_cap);
+    SCHK(hipGetLastError());
+    SCHK(hipMemcpyAsync(h_cnt + 1, d_cnt + 1, sizeof(int), hipMemcpyDeviceToHost, st));
+    SCHK(hipStreamSynchronize(st));
+    if (h_cnt[1] > kp_cap) { err = "more than 2^19 SIFT keypoints"; return -2; }
+    std::vector<mim_keypoint> k(h_cnt[1]);
+    if (!k.empty()) SCHK(hipMemcpyAsync(k.data(), d_kp, sizeof(mim_keypoint) * k.size(), hipMemcpyDeviceToHost, st));
+    SCHK(hipStreamSynchronize(st));
+    // removeDuplicatedSorted, the octave -1 rescale, runByPixelsMask (features2d keypoint.cpp, sift)
+    std::sort(k.begin(), k.end(), kp_greater);
+    size_t m = 0;
+    for (size_t j = 0; j < k.size(); ++j) {
+        if (m > 0 && k[m - 1].x == k[j].x && k[m - 1].y == k[j].y && k[m - 1].size == k[j].size && k[m - 1].angle == k[j].angle)
+            continue;
+        k[m++] = k[j];
+    }
+    k.resize(m);
+    for (auto& p : k) {
+        p.octave = (p.octave & ~255) | ((p.octave - 1) & 255);
+        p.x *= 0.5f;
+        p.y *= 0.5f;
+        p.size *= 0.5f;
+    }
+    if (mask) {
+        m = 0;
+        for (size_t j = 0; j < k.size(); ++j) {
+            const int yy = (int)(k[j].y + 0.5f), xx = (int)(k[j].x + 0.5f);
+            if (mask[(size_t)yy * mstep + xx] != 0) k[m++] = k[j];
+        }
+        k.resize(m);
+    }
+    *n_out = (int)k.size();
+    const int n = std::min((int)k.size(), max_kp);
+    if (n <= 0) return 0;
+    SCHK(hipMemcpyAsync(d_kp, k.data(), sizeof(mim_keypoint) * n, hipMemcpyHostToDevice, st));
+    SCHK(grow(w->desc, w->desc_cap, sizeof(float) * 128 * (size_t)n));
+    descr_kernel<<<(n + kDescrThreads - 1) / kDescrThreads, kDescrThreads, 0, st>>>(d_pyr, d_kp, n, (float*)w->desc);
+    SCHK(hipGetLastError());
+    SCHK(hipMemcpyAsync(desc, w->desc, sizeof(float) * 128 * (size_t)n, hipMemcpyDeviceToHost, st));
+    SCHK(hipStreamSynchronize(st));
+    std::copy(k.begin(), k.begin() + n, kps);
+    return 0;
+}
+
+}  // namespace mim

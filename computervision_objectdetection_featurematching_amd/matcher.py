@@ -5,6 +5,9 @@ Reference call sites (/root/reference/src/TestsDetector.cpp):
   :66-72   ratio test `m[0].distance < 0.9f * m[1].distance`           -> Matcher.ratio_filter
   :78      findHomography(objPts, scenePts, RANSAC, 5.0, inlierMask)   -> Matcher.find_homography
   :58-95   the per-view loop with its gates (:74, :79, :81, :84)       -> Matcher.match_batch
+  :102     resize(scene, scaled, Size(), s, s) (INTER_LINEAR)          -> Matcher.resize_linear
+  :106     sift->detectAndCompute(scaled, noArray(), kps, desc)        -> Matcher.sift_detect_compute
+  (ModelsDetector.cpp:75, the model views with their masks: the same call with a mask)
 Argument meaning and error behaviour follow OpenCV: an empty query gives no rows, n < 4 points
 raise (CV_Error StsVecLengthErr), a failed RANSAC returns an empty H (None) and a zero mask.
 """
@@ -19,6 +22,9 @@ from . import _lib
 from ._lib import MimError, Params, Problem, RESULT_DTYPE
 
 DIM = 128
+# cv::KeyPoint without class_id (mim_keypoint in include/mim.h)
+KEYPOINT_DTYPE = np.dtype([("x", np.float32), ("y", np.float32), ("size", np.float32), ("angle", np.float32),
+                           ("response", np.float32), ("octave", np.int32)])
 
 
 def default_params(**kw) -> Params:
@@ -149,6 +155,51 @@ class Matcher:
         idx, dist = self.knn_match_arrays(query, train)
         return [[DMatch(i, int(idx[i, j]), 0, float(dist[i, j])) for j in range(2) if idx[i, j] >= 0]
                 for i in range(idx.shape[0])]
+
+    # ---- feature extraction either side of the matcher (ModelsDetector.cpp:75, TestsDetector.cpp:102,106)
+    def sift_detect_compute(self, gray, mask=None, max_kp: int = 1 << 18):
+        """SIFT::create()->detectAndCompute(gray, mask, kps, desc) on the GPU.
+
+        gray / mask: CV_8UC1 arrays (rows, cols).  Returns (keypoints as a KEYPOINT_DTYPE array,
+        descriptors (n, 128) float32).  More than max_kp keypoints raises (no silent truncation)."""
+        g = np.ascontiguousarray(gray, np.uint8)
+        if g.ndim != 2:
+            raise ValueError("sift_detect_compute: a single-channel image is required")
+        m = None
+        if mask is not None:
+            m = np.ascontiguousarray(mask, np.uint8)
+            if m.shape != g.shape:
+                raise ValueError("sift_detect_compute: mask must have the image's size")
+        kps = np.zeros(max(max_kp, 1), KEYPOINT_DTYPE)
+        desc = np.zeros((max(max_kp, 1), DIM), np.float32)
+        n = C.c_int32()
+        self._check(self.L.mim_sift_detect_compute(
+            self._ctx, C.c_void_p(g.ctypes.data), g.shape[0], g.shape[1], g.strides[0],
+            None if m is None else C.c_void_p(m.ctypes.data), 0 if m is None else m.strides[0], max_kp,
+            C.c_void_p(kps.ctypes.data), C.c_void_p(desc.ctypes.data), C.byref(n)))
+        if n.value > max_kp:
+            raise ValueError(f"sift_detect_compute: {n.value} keypoints > max_kp={max_kp}")
+        return kps[:n.value].copy(), desc[:n.value].copy()
+
+    def resize_linear(self, src, dsize=None, fx: float = 0.0, fy: float = 0.0):
+        """cv::resize(src, dst, dsize, fx, fy, INTER_LINEAR) of a CV_8UC1 image.
+
+        dsize = (width, height), or None with fx (and fy, default fx) > 0 as the reference calls it:
+        resize(scene, scaled, Size(), scale, scale) with a float scale (TestsDetector.cpp:99-102)."""
+        s = np.ascontiguousarray(src, np.uint8)
+        if dsize is None:
+            if not fx > 0:
+                raise ValueError("resize_linear: dsize or fx > 0 required")
+            fx = float(np.float32(fx))
+            fy = float(np.float32(fy)) if fy else fx
+            dcols, drows = int(np.rint(s.shape[1] * fx)), int(np.rint(s.shape[0] * fy))
+        else:
+            dcols, drows = int(dsize[0]), int(dsize[1])
+            fx = fy = 0.0
+        dst = np.zeros((max(drows, 1), max(dcols, 1)), np.uint8)
+        self._check(self.L.mim_resize_linear_u8(self._ctx, C.c_void_p(s.ctypes.data), s.shape[0], s.shape[1],
+                                                s.strides[0], C.c_void_p(dst.ctypes.data), drows, dcols, fx, fy))
+        return dst
 
     def ratio_filter(self, idx, dist, ratio: float = 0.9):
         idx = np.ascontiguousarray(idx, np.int32)

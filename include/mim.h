@@ -147,6 +147,31 @@ mim_status mim_batch_problem_detail(struct mim_ctx* ctx, int32_t i, int32_t* q_i
 mim_status mim_knn2_sets_dev(struct mim_ctx* ctx, int32_t query_set, int32_t train_set,
                              int32_t* idx_dev, float* dist_dev);
 
+/* ---- feature extraction either side of the matcher ---------------------------
+ * cv::KeyPoint without class_id; octave packed as OpenCV packs it (octave & 255 | layer << 8 |
+ * sub-layer << 16, octave -1 for the doubled image). */
+typedef struct {
+    float x, y, size, angle, response;
+    int32_t octave;
+} mim_keypoint;
+
+/* SIFT::create()->detectAndCompute(gray, mask, kps, desc) with the reference's defaults
+ * (main.cpp:17; called at ModelsDetector.cpp:75 with the model mask and at TestsDetector.cpp:106
+ * with an empty mask).  gray: host CV_8UC1 rows x cols, row stride `step` bytes; mask: NULL or host
+ * CV_8UC1 of the same size, stride mask_step.  Writes min(found, max_kp) keypoints (OpenCV's order:
+ * KeypointGreater after removeDuplicatedSorted, then the mask filter) and their 128-float
+ * descriptors (row-major); *n_kp = keypoints found (may exceed max_kp).  Synchronous. */
+mim_status mim_sift_detect_compute(struct mim_ctx* ctx, const uint8_t* gray, int32_t rows, int32_t cols,
+                                   int64_t step, const uint8_t* mask, int64_t mask_step, int32_t max_kp,
+                                   mim_keypoint* kps, float* desc, int32_t* n_kp);
+
+/* cv::resize(src, dst, dsize, fx, fy, INTER_LINEAR) of a CV_8UC1 image (TestsDetector.cpp:102, the
+ * scene scales).  fx, fy > 0: resize(src, dst, Size(), fx, fy) — the caller passes
+ * drows = cvRound(rows * fy), dcols = cvRound(cols * fx) and OpenCV's coefficients use 1/fx, 1/fy;
+ * fx = fy = 0: dsize given.  src stride `step` bytes, dst dense drows x dcols.  Synchronous. */
+mim_status mim_resize_linear_u8(struct mim_ctx* ctx, const uint8_t* src, int32_t rows, int32_t cols, int64_t step,
+                                uint8_t* dst, int32_t drows, int32_t dcols, double fx, double fy);
+
 /* ---- introspection for benches / profiles ----------------------------------------------------- */
 /* Per-kernel device time (ms) summed over the batches since the last result fetch, measured with
  * HIP events on the stream each kernel ran on.  names: "knn", "ratio", "attempt", "chain",

@@ -64,6 +64,11 @@ def lib():
         L.orc_match_problem.argtypes = [f32p, f32p, C.c_int, f32p, f32p, C.c_int, C.c_int,
                                         C.POINTER(Params), C.c_int, C.POINTER(Result),
                                         C.c_void_p, C.c_void_p, C.c_void_p]
+        L.orc_resize_linear_u8.argtypes = [u8p, C.c_int, C.c_int, u8p, C.c_int, C.c_int, C.c_double, C.c_double]
+        L.orc_sift_detect_compute.argtypes = [u8p, C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
+        L.orc_sift_detect_compute.restype = C.c_int
+        L.orc_fast_atan2.argtypes = [C.c_float, C.c_float]
+        L.orc_fast_atan2.restype = C.c_float
         _lib = L
     return _lib
 
@@ -186,3 +191,45 @@ def match_problem(qd, qk, td, tk, params: Params | None = None, threads: int = 0
                 H=np.array(res.H[:]).reshape(3, 3), det=res.det,
                 mask=mask[:ng] if ng >= params.min_good else np.zeros(0, np.uint8),
                 good_q=gq[:ng], good_t=gt[:ng])
+
+
+# ---- SIFT / resize (sift_oracle.h; ModelsDetector.cpp:75, TestsDetector.cpp:102,106) ----------
+KEYPOINT_DTYPE = np.dtype([("x", np.float32), ("y", np.float32), ("size", np.float32), ("angle", np.float32),
+                           ("response", np.float32), ("octave", np.int32)])
+
+
+def resize_dsize(rows: int, cols: int, fx: float, fy: float):
+    """dsize of resize(src, dst, Size(), fx, fy): saturate_cast<int>(cols * fx) (round half even)."""
+    return int(np.rint(cols * float(fx))), int(np.rint(rows * float(fy)))
+
+
+def resize_linear_u8(src: np.ndarray, dsize=None, fx: float = 0.0, fy: float = 0.0) -> np.ndarray:
+    """cv::resize(src, dst, dsize, fx, fy, INTER_LINEAR) of a CV_8UC1 image; dsize = (width, height) or
+    None with fx, fy > 0 (float factors as the reference passes them, TestsDetector.cpp:99-102)."""
+    src = np.ascontiguousarray(src, np.uint8)
+    if dsize is None:
+        fx = float(np.float32(fx))
+        fy = float(np.float32(fy)) if fy else fx
+        dsize = resize_dsize(src.shape[0], src.shape[1], fx, fy)
+    else:
+        fx = fy = 0.0
+    dcols, drows = dsize
+    dst = np.zeros((drows, dcols), np.uint8)
+    lib().orc_resize_linear_u8(src, src.shape[0], src.shape[1], dst, drows, dcols, fx, fy)
+    return dst
+
+
+def sift_detect_compute(gray: np.ndarray, mask: np.ndarray | None = None, max_kp: int = 1 << 20):
+    """SIFT::create()->detectAndCompute(gray, mask): (keypoints [KEYPOINT_DTYPE], descriptors (n,128) f32)."""
+    gray = np.ascontiguousarray(gray, np.uint8)
+    m = None if mask is None else np.ascontiguousarray(mask, np.uint8)
+    kps = np.zeros(max_kp, KEYPOINT_DTYPE)
+    desc = np.zeros((max_kp, 128), np.float32)
+    n = lib().orc_sift_detect_compute(gray, gray.shape[0], gray.shape[1], None if m is None else m.ctypes.data,
+                                      max_kp, kps.ctypes.data, desc.ctypes.data)
+    n = min(n, max_kp)
+    return kps[:n].copy(), desc[:n].copy()
+
+
+def fast_atan2(y: float, x: float) -> float:
+    return float(lib().orc_fast_atan2(y, x))

@@ -12,6 +12,10 @@ gates, /root/reference/src/TestsDetector.cpp:58-95) over one batch of problems. 
   c1  configs[0] surrogate: the reference's own shape, one scene = 29 model views x 5 scales = 145
       ragged problems (Nq 100-500, Nt 1k-4k, maxIters 2000); the real data needs SIFT.
   c5  configs[4]: the 50k x 50k dense distance contraction alone (mim_knn2_sets_dev), no RANSAC.
+  c1img  configs[0] on the reference's own images (tests/golden/c1_sugar_box.npz): the sugar_box model
+      (29 views, SIFT computed once before the timed region as processAllModelsImages does) against one
+      test view per step through detectObjects: 5 x (resize + SIFT) on the GPU, the 145 problems as one
+      device batch, clustering and boxes on the host (pipeline.detect_objects).
 Inputs (descriptors + keypoints) are resident in HBM before the timed region; each step registers
 the sets (the i8 layout prep is inside the step) and runs the batch.  Multi-GPU: one process per GPU
 (`--gpus N` launches N ranks through torch.distributed.run when WORLD_SIZE is unset), each rank
@@ -65,7 +69,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--config", default="c3", choices=["c1", "c2", "c3", "c5"])
+    ap.add_argument("--config", default="c3", choices=["c1", "c1img", "c2", "c3", "c5"])
     ap.add_argument("--cpu-sample", type=int, default=6,
                     help="problems of the sequential CPU-baseline sample (1 warm-up + the median of the rest; "
                          "0: skip the CPU baseline)")
@@ -266,6 +270,99 @@ def cpu_baseline_knn(q, t, idx_gpu, dist_gpu, n_rows):
 
 
 # ------------------------------------------------------------------------------------------------
+def run_c1img(args, rank, world, local):
+    """configs[0] on the reference's images, one scene per step (see the module docstring)."""
+    import torch
+    import torch.distributed as dist
+
+    from computervision_objectdetection_featurematching_amd import Matcher, build
+    from computervision_objectdetection_featurematching_amd.pipeline import SCALES, detect_objects, process_model_views
+
+    build.build()
+    with np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "tests", "golden", "c1_sugar_box.npz")) as z:
+        d = {k: z[k] for k in z.files if not k.startswith("exp/")}
+    names = sorted(k[5:] for k in d if k.startswith("view/"))
+    scenes = sorted(k[6:] for k in d if k.startswith("scene/"))
+    m = Matcher(local)
+    model = process_model_views(m, "004_sugar_box", [(d[f"view/{n}"], d[f"mask/{n}"]) for n in names])
+    sid = scenes[rank % len(scenes)]
+    scene = d[f"scene/{sid}"]
+    n_probs = len(SCALES) * len(names)
+    for _ in range(max(args.warmup, 1)):
+        run = detect_objects(m, scene, [model], keep=True)
+    m.set_timing(not args.no_timing)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        dets = detect_objects(m, scene, [model])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=torch.device("cuda", local))
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    # SIFT of one 640x480 image alone (the step's dominant stage), timed separately
+    ts = []
+    for _ in range(5):
+        t1 = time.perf_counter()
+        m.sift_detect_compute(scene)
+        ts.append(time.perf_counter() - t1)
+    if rank == 0:
+        out = {"metric": "matches+homographies/sec (configs[0]: sugar_box model vs one test view, reference images, "
+                         "SIFT + match + RANSAC + boxes)",
+               "value": round(world * n_probs * args.steps / el, 3), "unit": "problems/s", "n_gpus": world,
+               "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * el / args.steps, 3),
+               "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+               "dtype": "f32 SIFT (OpenCV order), i8-MFMA exact-int distances, fp64 DLT/LM, fp32 reprojection",
+               "data": "reference images: 29 sugar_box model views + masks, test view " + sid,
+               "config": {"workload": f"c1img: detectObjects of one 640x480 scene against {len(names)} views x "
+                                      f"{len(SCALES)} scales = {n_probs} problems per step per GPU",
+                          "problems_per_gpu": n_probs, "global_batch": world * n_probs, "parallelism": f"dp{world}"},
+               "scenes_per_s": round(world * args.steps / el, 3),
+               "sift_640x480_ms": round(1e3 * statistics.median(ts), 3),
+               "detections_rank0": [list(b) for b, _ in dets],
+               "accepted_problems_rank0": int((run.results["status"] == 0).sum())}
+        if args.cpu_sample > 0:
+            out["cpu_baseline"] = cpu_baseline_c1img(scene, model, run, names)
+            out["parity"] = out["cpu_baseline"]["parity"]
+        print(json.dumps(out), flush=True)
+    m.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline_c1img(scene, model, run, names):
+    """The oracle pipeline for the same scene, one core: resize + SIFT per scale, then the 145
+    problems (kNN + ratio + RANSAC + refine) one after another; every record compared with the GPU's."""
+    from oracle import oracle as O
+    from computervision_objectdetection_featurematching_amd.pipeline import SCALES
+    O.build()
+    t0 = time.perf_counter()
+    res, mism = [], 0
+    for si, s in enumerate(SCALES):
+        sk, sd = O.sift_detect_compute(O.resize_linear_u8(scene, fx=s))
+        sxy = np.stack([sk["x"], sk["y"]], 1)
+        for vi in range(len(names)):
+            k, dd = model.keypoints[vi], model.descriptors[vi]
+            o = O.match_problem(dd, np.stack([k["x"], k["y"]], 1), sd, sxy, threads=1)
+            g = run.results[si * len(names) + vi]
+            same = (o["n_good"], o["n_inl"], o["status"], o["iters"]) == (int(g["n_good"]), int(g["n_inl"]),
+                                                                         int(g["status"]), int(g["iters"]))
+            same = same and (o["status"] not in (0, 3, 4) or np.array_equal(o["H"].reshape(9), g["H"]))
+            mism += not same
+            res.append(o)
+    el = time.perf_counter() - t0
+    n = len(res)
+    return {"value": round(n / el, 4), "unit": "problems/s", "cores": 1, "kind": "port", "cpu_model": cpu_model(),
+            "sample": f"one scene: 5 x (resize + SIFT) + {n} problems, oracle/sift_oracle.c + oracle/mim_oracle.c "
+                      f"single-threaded (-O3 -ffp-contract=off), {el:.1f} s",
+            "parity": {"checked": n, "mismatch": mism}}
+
+
 def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -273,6 +370,13 @@ def main():
     if args.dry_run:
         return dry_run(args)
     rank, world, local = dist_env()
+    if args.config == "c1img":
+        import torch
+        import torch.distributed as dist
+        if world > 1:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        return run_c1img(args, rank, world, local)
     import torch
     import torch.distributed as dist
 

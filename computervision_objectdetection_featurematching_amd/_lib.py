@@ -20,6 +20,7 @@ EXPORTS = [
     "mim_ratio_filter", "mim_find_homography", "mim_batch_run", "mim_batch_results",
     "mim_batch_results_dev", "mim_batch_results_copy", "mim_batch_problem_detail", "mim_knn2_sets_dev", "mim_last_kernel_ms",
     "mim_set_timing", "mim_sift_detect_compute", "mim_resize_linear_u8",
+    "mim_default_box_params", "mim_detect_boxes",
 ]
 
 
@@ -38,6 +39,15 @@ class Params(C.Structure):
 class Result(C.Structure):
     _fields_ = [("n_good", C.c_int32), ("n_inl", C.c_int32), ("status", C.c_int32),
                 ("iters", C.c_int32), ("H", C.c_double * 9), ("det", C.c_double)]
+
+
+class BoxParams(C.Structure):
+    _fields_ = [("cluster_distance", C.c_float), ("min_points_per_cluster", C.c_int32),
+                ("box_merge_distance", C.c_float), ("min_box_area", C.c_int32), ("dynamic_margin", C.c_float)]
+
+
+class Rect(C.Structure):
+    _fields_ = [("x", C.c_int32), ("y", C.c_int32), ("width", C.c_int32), ("height", C.c_int32)]
 
 
 class Problem(C.Structure):
@@ -93,10 +103,12 @@ def load():
     L.mim_sift_detect_compute.argtypes = [vp, u8p, i32, i32, C.c_int64, u8p, C.c_int64, i32, vp, f32p,
                                           C.POINTER(C.c_int32)]
     L.mim_resize_linear_u8.argtypes = [vp, u8p, i32, i32, C.c_int64, u8p, i32, i32, C.c_double, C.c_double]
+    L.mim_default_box_params.argtypes = [C.POINTER(BoxParams)]
+    L.mim_detect_boxes.argtypes = [f32p, i32, C.POINTER(BoxParams), C.POINTER(Rect), i32, C.POINTER(C.c_int32)]
     for name in ("mim_ctx_create", "mim_ctx_set_stream", "mim_synchronize", "mim_set_create", "mim_sets_clear",
                  "mim_knn2_l2", "mim_ratio_filter", "mim_find_homography", "mim_batch_run", "mim_batch_results",
                  "mim_batch_problem_detail", "mim_knn2_sets_dev", "mim_set_timing",
-                 "mim_sift_detect_compute", "mim_resize_linear_u8"):
+                 "mim_sift_detect_compute", "mim_resize_linear_u8", "mim_detect_boxes"):
         getattr(L, name).restype = C.c_int32
     _lib = L
     return L

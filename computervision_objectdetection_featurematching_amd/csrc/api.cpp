@@ -19,6 +19,7 @@
 #include <vector>
 
 #include "../../include/mim.h"
+#include "../../include/mim_detect.hpp"
 #include "mim_internal.h"
 
 namespace mim {
@@ -683,6 +684,40 @@ mim_status mim_knn2_sets_dev(mim_ctx* c, int32_t query_set, int32_t train_set, i
     ev_mark(c, "ratio");
     c->last_n = 0;  // no RANSAC records (mim.h)
     c->last_gen = -1;
+    return MIM_OK;
+}
+
+void mim_default_box_params(mim_box_params* p) {
+    const mim::BoxParams d;
+    p->cluster_distance = d.cluster_distance;
+    p->min_points_per_cluster = d.min_points_per_cluster;
+    p->box_merge_distance = d.box_merge_distance;
+    p->min_box_area = d.min_box_area;
+    p->dynamic_margin = d.dynamic_margin;
+}
+
+mim_status mim_detect_boxes(const float* pts_xy, int32_t n, const mim_box_params* bp, mim_rect* boxes, int32_t cap,
+                            int32_t* n_boxes) {
+    if (n < 0 || (n > 0 && !pts_xy) || !n_boxes || cap < 0 || (cap > 0 && !boxes)) return MIM_EINVAL;
+    mim::BoxParams p;
+    if (bp) {
+        p.cluster_distance = bp->cluster_distance;
+        p.min_points_per_cluster = bp->min_points_per_cluster;
+        p.box_merge_distance = bp->box_merge_distance;
+        p.min_box_area = bp->min_box_area;
+        p.dynamic_margin = bp->dynamic_margin;
+    }
+    try {
+        std::vector<mim::Point2f> pts(n);
+        for (int32_t i = 0; i < n; ++i) pts[i] = {pts_xy[2 * i], pts_xy[2 * i + 1]};
+        mim::Detections dets;
+        mim::boxes_for_model(pts, "", dets, p);
+        *n_boxes = (int32_t)dets.size();
+        for (int32_t i = 0; i < std::min(cap, *n_boxes); ++i)
+            boxes[i] = mim_rect{dets[i].first.x, dets[i].first.y, dets[i].first.width, dets[i].first.height};
+    } catch (const std::bad_alloc&) {
+        return MIM_ENOMEM;
+    }
     return MIM_OK;
 }
 

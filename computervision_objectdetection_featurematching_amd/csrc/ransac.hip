@@ -586,102 +586,6 @@ __device__ void dlt_finish_group(const double* lt, double* D, const double* invH
     for (int i = 0; i < 9; ++i) H[i] = H0[i] * sc;
 }
 
-// Refit eigenvector by inverse iteration (one lane).  The refit's runKernel over all inliers needs
-// H only to the findHomography contract (LM refines it next; the RANSAC mask is already final), so
-// instead of the ~140-rotation Jacobi, the eigenvector of the smallest eigenvalue of LtL comes from
-// inverse iteration on the Cholesky factor of LtL + delta I (delta = 1e-10 trace: same eigenvectors,
-// positive definite), started from the RANSAC best model in the refit's normalized coordinates.
-// Returns false (caller falls back to the Jacobi) when the factorisation fails, the iteration does not
-// settle within 8 steps, or the Rayleigh residual |A x - (x'Ax) x| exceeds 1e-9 trace.
-__device__ bool refit_inverse_iteration(const double* lt, const double* x0, double* x) {
-    double a[9][9], L[9][9];
-    {
-        int e = 0;
-#pragma unroll
-        for (int j = 0; j < 9; ++j)
-#pragma unroll
-            for (int k = j; k < 9; ++k, ++e) a[j][k] = a[k][j] = lt[e];
-    }
-    double tr = 0;
-#pragma unroll
-    for (int i = 0; i < 9; ++i) tr += a[i][i];
-    if (!(tr > 0) || !isfinite(tr)) return false;
-    const double delta = 1e-10 * tr;
-#pragma unroll
-    for (int j = 0; j < 9; ++j) {
-        double s = a[j][j] + delta;
-#pragma unroll
-        for (int k = 0; k < j; ++k) s -= L[j][k] * L[j][k];
-        if (!(s > 0.5 * delta)) return false;
-        const double d = sqrt(s), id = 1.0 / d;
-        L[j][j] = d;
-#pragma unroll
-        for (int i = j + 1; i < 9; ++i) {
-            double t = a[i][j];
-#pragma unroll
-            for (int k = 0; k < j; ++k) t -= L[i][k] * L[j][k];
-            L[i][j] = t * id;
-        }
-    }
-    double v[9], nrm = 0;
-#pragma unroll
-    for (int i = 0; i < 9; ++i) nrm += x0[i] * x0[i];
-    if (!(nrm > 0) || !isfinite(nrm)) return false;
-    nrm = 1.0 / sqrt(nrm);
-#pragma unroll
-    for (int i = 0; i < 9; ++i) v[i] = x0[i] * nrm;
-    bool settled = false;
-    for (int it = 0; it < 8 && !settled; ++it) {
-        double y[9], z[9];
-#pragma unroll
-        for (int i = 0; i < 9; ++i) {
-            double t = v[i];
-#pragma unroll
-            for (int k = 0; k < i; ++k) t -= L[i][k] * y[k];
-            y[i] = t / L[i][i];
-        }
-#pragma unroll
-        for (int i = 8; i >= 0; --i) {
-            double t = y[i];
-#pragma unroll
-            for (int k = i + 1; k < 9; ++k) t -= L[k][i] * z[k];
-            z[i] = t / L[i][i];
-        }
-        double zn = 0, dot = 0;
-#pragma unroll
-        for (int i = 0; i < 9; ++i) {
-            zn += z[i] * z[i];
-            dot += z[i] * v[i];
-        }
-        if (!(zn > 0) || !isfinite(zn)) return false;
-        zn = (dot < 0 ? -1.0 : 1.0) / sqrt(zn);
-        double dmax = 0;
-#pragma unroll
-        for (int i = 0; i < 9; ++i) {
-            const double w = z[i] * zn;
-            dmax = fmax(dmax, fabs(w - v[i]));
-            v[i] = w;
-        }
-        settled = it >= 1 && dmax < 1e-15;
-    }
-    double Av[9], rq = 0;
-#pragma unroll
-    for (int i = 0; i < 9; ++i) {
-        double t = 0;
-#pragma unroll
-        for (int k = 0; k < 9; ++k) t += a[i][k] * v[k];
-        Av[i] = t;
-        rq += v[i] * t;
-    }
-    double res = 0;
-#pragma unroll
-    for (int i = 0; i < 9; ++i) res = fmax(res, fabs(Av[i] - rq * v[i]));
-    if (!(res <= 1e-9 * tr)) return false;
-#pragma unroll
-    for (int i = 0; i < 9; ++i) x[i] = v[i];
-    return true;
-}
-
 // ------------------------------------------------------------------------------------------------
 // checkSubset (fundam.cpp haveCollinearPoints + the Marquez-Neila orientation test), fp64
 // ------------------------------------------------------------------------------------------------
@@ -2641,46 +2545,119 @@ __device__ __forceinline__ void refine_point(const double* h, double Mx, double 
     }
 }
 
-// A = J^T J (upper, 36), v = J^T r (8), S = |r|^2, rinf = |r|_inf over the inliers
-__device__ void lm_normal(const float4* __restrict__ X, int n, const double* h, double* red, double* A, double* v,
-                          double& S, double& rinf) {
-    double acc[45];
-#pragma unroll
-    for (int k = 0; k < 45; ++k) acc[k] = 0;
-    double mx = 0;
-    for (int i = threadIdx.x; i < n; i += kRT) {
-        const float4 q = X[i];
-        double ex, ey, Jx[8], Jy[8];
-        refine_point(h, q.x, q.y, q.z, q.w, ex, ey, Jx, Jy);
-        int e = 0;
-#pragma unroll
-        for (int a = 0; a < 8; ++a)
-#pragma unroll
-            for (int b = a; b < 8; ++b, ++e) acc[e] += Jx[a] * Jx[b] + Jy[a] * Jy[b];
-#pragma unroll
-        for (int a = 0; a < 8; ++a) acc[36 + a] += Jx[a] * ex + Jy[a] * ey;
-        acc[44] += ex * ex + ey * ey;
-        mx = fmax(mx, fmax(fabs(ex), fabs(ey)));
+// ---- LM sums in OpenCV's order ------------------------------------------------------------------
+// HomographyRefineCallback::compute fills r (2k rows) and J (2k x 8) row by row; LMSolverImpl forms
+// A = J^T J and v = J^T r (mulTransposed / gemm: each entry one sequential sum over the rows) and
+// S = |r|^2 (norm(r, NORM_L2SQR): sequential).  The per-point quantities (ww, xi, yi, residuals) are
+// computed by all threads into an LDS chunk; each of 45 lanes then owns one sum (36 A entries, 8 v
+// entries, S) and adds the chunk's rows in order: the same operations in the same order as the oracle
+// (lm_refine / normal_eq in oracle/mim_oracle.c), so the refined H is bit-identical, also for the
+// near-degenerate inlier sets of real data (duplicated keypoints) where a reordered sum moves the
+// LM path far (tests/test_pipeline_gpu.py).
+constexpr int kLmChunk = 512;
+struct LmStage {
+    double Mx[kLmChunk], My[kLmChunk], ww[kLmChunk], xi[kLmChunk], yi[kLmChunk], ex[kLmChunk], ey[kLmChunk];
+};
+
+// J row entries of point i: x-row Jx(a), y-row Jy(a) (HomographyRefineCallback::compute)
+__device__ __forceinline__ double jx_of(int a, double Mx, double My, double ww, double xi) {
+    switch (a) {
+        case 0: return Mx * ww;
+        case 1: return My * ww;
+        case 2: return ww;
+        case 6: return -Mx * ww * xi;
+        case 7: return -My * ww * xi;
+        default: return 0.;
     }
-    block_sum<45>(acc, red);
-    rinf = block_max(mx, red);
-    int e = 0;
-    for (int a = 0; a < 8; ++a)
-        for (int b = a; b < 8; ++b, ++e) A[a * 8 + b] = A[b * 8 + a] = acc[e];
-    for (int a = 0; a < 8; ++a) v[a] = acc[36 + a];
-    S = acc[44];
+}
+__device__ __forceinline__ double jy_of(int a, double Mx, double My, double ww, double yi) {
+    switch (a) {
+        case 3: return Mx * ww;
+        case 4: return My * ww;
+        case 5: return ww;
+        case 6: return -Mx * ww * yi;
+        case 7: return -My * ww * yi;
+        default: return 0.;
+    }
 }
 
-__device__ double lm_cost(const float4* __restrict__ X, int n, const double* h, double* red) {
-    double acc[1] = {0};
+// stage points [c0, c0 + n) of X under model h into L; returns this thread's max |residual|
+__device__ double lm_stage(const float4* __restrict__ X, int c0, int n, const double* h, LmStage& L) {
+    double mx = 0;
     for (int i = threadIdx.x; i < n; i += kRT) {
-        const float4 q = X[i];
-        double ex, ey;
-        refine_point(h, q.x, q.y, q.z, q.w, ex, ey, nullptr, nullptr);
-        acc[0] += ex * ex + ey * ey;
+        const float4 q = X[c0 + i];
+        const double Mx = q.x, My = q.y;
+        double ww = h[6] * Mx + h[7] * My + 1.;
+        ww = fabs(ww) > DBL_EPSILON ? 1. / ww : 0;
+        const double xi = (h[0] * Mx + h[1] * My + h[2]) * ww;
+        const double yi = (h[3] * Mx + h[4] * My + h[5]) * ww;
+        const double ex = xi - (double)q.z, ey = yi - (double)q.w;
+        L.Mx[i] = Mx; L.My[i] = My; L.ww[i] = ww; L.xi[i] = xi; L.yi[i] = yi; L.ex[i] = ex; L.ey[i] = ey;
+        mx = fmax(mx, fmax(fabs(ex), fabs(ey)));
     }
-    block_sum<1>(acc, red);
-    return acc[0];
+    return mx;
+}
+
+// A = J^T J (full 8x8), v = J^T r, S = |r|^2, rinf = |r|_inf: out[0..35] A upper, [36..43] v, [44] S
+__device__ void lm_normal(const float4* __restrict__ X, int n, const double* h, LmStage& L, double* red,
+                          double* out, double& rinf) {
+    const int e = threadIdx.x;
+    int a = 0, b = 0;
+    if (e < 36) {  // (a, b), b >= a, row-major upper triangle
+        int r = e;
+        while (r >= 8 - a) { r -= 8 - a; ++a; }
+        b = a + r;
+    } else if (e < 44) {
+        a = e - 36;
+    }
+    double acc = 0, mx = 0;
+    for (int c0 = 0; c0 < n; c0 += kLmChunk) {
+        const int m = min(kLmChunk, n - c0);
+        __syncthreads();
+        mx = fmax(mx, lm_stage(X, c0, m, h, L));
+        __syncthreads();
+        if (e < 36) {
+            for (int i = 0; i < m; ++i) {
+                const double Mx = L.Mx[i], My = L.My[i], ww = L.ww[i];
+                acc += jx_of(a, Mx, My, ww, L.xi[i]) * jx_of(b, Mx, My, ww, L.xi[i]);
+                acc += jy_of(a, Mx, My, ww, L.yi[i]) * jy_of(b, Mx, My, ww, L.yi[i]);
+            }
+        } else if (e < 44) {
+            for (int i = 0; i < m; ++i) {
+                const double Mx = L.Mx[i], My = L.My[i], ww = L.ww[i];
+                acc += jx_of(a, Mx, My, ww, L.xi[i]) * L.ex[i];
+                acc += jy_of(a, Mx, My, ww, L.yi[i]) * L.ey[i];
+            }
+        } else if (e == 44) {
+            for (int i = 0; i < m; ++i) {
+                acc += L.ex[i] * L.ex[i];
+                acc += L.ey[i] * L.ey[i];
+            }
+        }
+    }
+    if (e < 45) out[e] = acc;
+    rinf = block_max(mx, red);  // max is order-free; block_max synchronises
+}
+
+// S(h) = |r(h)|^2, sequential over the rows
+__device__ double lm_cost(const float4* __restrict__ X, int n, const double* h, LmStage& L, double* red) {
+    double acc = 0;
+    for (int c0 = 0; c0 < n; c0 += kLmChunk) {
+        const int m = min(kLmChunk, n - c0);
+        __syncthreads();
+        lm_stage(X, c0, m, h, L);
+        __syncthreads();
+        if (threadIdx.x == 0)
+            for (int i = 0; i < m; ++i) {
+                acc += L.ex[i] * L.ex[i];
+                acc += L.ey[i] * L.ey[i];
+            }
+    }
+    if (threadIdx.x == 0) red[0] = acc;
+    __syncthreads();
+    const double r = red[0];
+    __syncthreads();
+    return r;
 }
 
 // Jacobi of an 8x8 symmetric matrix (single thread, stride-1 scratch); w sorted descending,
@@ -2721,110 +2698,8 @@ __device__ void solve_eig8(const double* Ap, const double* b, double* x, double*
     }
 }
 
-// LM step solve.  cv::solve(DECOMP_EIG) applies the pseudo-inverse with eigenvalues below
-// 2*DBL_EPSILON*trace dropped; for the positive-definite systems of a refit on >= 4 points in
-// general position no eigenvalue is dropped and the solution equals the Cholesky one to rounding
-// (the LM contract is |dH| <= 1e-4).  Ill-conditioned systems fall back to the Jacobi path.
-__device__ bool solve_chol8(const double* A, const double* b, double* x) {
-    // symmetric diagonal scaling first (unit diagonal): J^T J of a homography spans ~1e13
-    double sc[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        if (!(A[9 * i] > 0)) return false;
-        sc[i] = 1.0 / sqrt(A[9 * i]);
-    }
-    double L[8][8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        double sjj = 1.0;
-#pragma unroll
-        for (int k = 0; k < j; ++k) sjj -= L[j][k] * L[j][k];
-        if (!(sjj > 1e-10)) return false;
-        const double ljj = sqrt(sjj);
-        L[j][j] = ljj;
-#pragma unroll
-        for (int i = j + 1; i < 8; ++i) {
-            double sij = A[8 * i + j] * sc[i] * sc[j];
-#pragma unroll
-            for (int k = 0; k < j; ++k) sij -= L[i][k] * L[j][k];
-            L[i][j] = sij / ljj;
-        }
-    }
-    double y[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        double si = b[i] * sc[i];
-#pragma unroll
-        for (int k = 0; k < i; ++k) si -= L[i][k] * y[k];
-        y[i] = si / L[i][i];
-    }
-    double z[8];
-#pragma unroll
-    for (int i = 7; i >= 0; --i) {
-        double si = y[i];
-#pragma unroll
-        for (int k = i + 1; k < 8; ++k) si -= L[k][i] * z[k];
-        z[i] = si / L[i][i];
-    }
-#pragma unroll
-    for (int i = 0; i < 8; ++i) x[i] = z[i] * sc[i];
-    return true;
-}
-
-// max |diag(A^-1)| through the scaled Cholesky factor (A = S^-1 L L^T S^-1, S = diag(A)^-1/2):
-// diag(A^-1)_i = S_i^2 * sum_k (L^-1)_{k,i}^2.  For the positive-definite LM normal matrices this is
-// the pseudo-inverse of cv::invert(DECOMP_EIG) to rounding (contract |dH| <= 1e-4); returns false
-// when the factorisation is not safe, and the caller falls back to the eigen path.
-__device__ bool inv_diag_max_chol8(const double* A, double& maxval) {
-    double sc[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        if (!(A[9 * i] > 0)) return false;
-        sc[i] = 1.0 / sqrt(A[9 * i]);
-    }
-    double L[8][8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        double sjj = 1.0;
-#pragma unroll
-        for (int k = 0; k < j; ++k) sjj -= L[j][k] * L[j][k];
-        if (!(sjj > 1e-10)) return false;
-        const double ljj = sqrt(sjj);
-        L[j][j] = ljj;
-#pragma unroll
-        for (int i = j + 1; i < 8; ++i) {
-            double sij = A[8 * i + j] * sc[i] * sc[j];
-#pragma unroll
-            for (int k = 0; k < j; ++k) sij -= L[i][k] * L[j][k];
-            L[i][j] = sij / ljj;
-        }
-    }
-    double Li[8][8];  // L^-1 (lower)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        Li[j][j] = 1.0 / L[j][j];
-#pragma unroll
-        for (int i = j + 1; i < 8; ++i) {
-            double s = 0;
-#pragma unroll
-            for (int k = j; k < i; ++k) s += L[i][k] * Li[k][j];
-            Li[i][j] = -s / L[i][i];
-        }
-    }
-    maxval = DBL_EPSILON;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        double d = 0;
-#pragma unroll
-        for (int k = i; k < 8; ++k) d += Li[k][i] * Li[k][i];
-        maxval = fmax(maxval, fabs(d * sc[i] * sc[i]));
-    }
-    return true;
-}
-
+// invert(A, Ai, DECOMP_EIG), max |Ai(i,i)| (LMSolverImpl's lambda restart)
 __device__ double inv_diag_max8(const double* A, double* J) {
-    double mv;
-    if (inv_diag_max_chol8(A, mv)) return mv;
     double w[8], V[64];
     eig8(A, J, w, V);
     double threshold = 0;
@@ -2845,6 +2720,8 @@ __device__ double inv_diag_max8(const double* A, double* J) {
 struct RefineShared {
     double red[4 * 45];
     double lt[45];
+    double nrm[45];       // LM sums: A upper (36), v (8), S
+    LmStage lm;
     double norm[8];       // cm, cM, sm, sM (x,y each)
     double H[9], Hb[9];
     double A[64], v[8], D[8], x[8], xd[8], d[8];
@@ -2901,7 +2778,10 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
         res.iters = 0;
     } else {
         ok = S.max_good > 0 && S.fail_iter != -2;
-        res.iters = (S.fail_iter >= 0 && S.fail_iter < S.niters) ? S.fail_iter : S.niters;
+        // the loop counter at exit: niters, or best_iter + 1 when the last update dropped niters to or
+        // below the iteration that found the best model (RANSACPointSetRegistrator::run's `for`)
+        const int stop = max(S.niters, S.best_iter + 1);
+        res.iters = (S.fail_iter >= 0 && S.fail_iter < stop) ? S.fail_iter : stop;
         if (ok) {
             // bestModel = runKernel(sample[best_iter]) (bit-identical to the hypo kernel's)
             if (tid == 0 && !exact_all && best_h[(long long)p * 9 + 8] != 0.0) {
@@ -2948,63 +2828,58 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
             __syncthreads();
             const int k = sh.n_inl;
             if (k > 0) {
-                // ---- refit: runKernel over all inliers (parallel sums; contract is |dH| <= 1e-4) ----
-                double c4[4] = {0, 0, 0, 0};
-                for (int i = tid; i < k; i += kRT) {
-                    const float4 q = X[i];
-                    c4[0] += q.z; c4[1] += q.w; c4[2] += q.x; c4[3] += q.y;  // cm (scene), cM (object)
-                }
-                block_sum<4>(c4, sh.red);
-                const double cmx = c4[0] / k, cmy = c4[1] / k, cMx = c4[2] / k, cMy = c4[3] / k;
-                double s4[4] = {0, 0, 0, 0};
-                for (int i = tid; i < k; i += kRT) {
-                    const float4 q = X[i];
-                    s4[0] += fabs(q.z - cmx); s4[1] += fabs(q.w - cmy);
-                    s4[2] += fabs(q.x - cMx); s4[3] += fabs(q.y - cMy);
-                }
-                block_sum<4>(s4, sh.red);
-                const bool degenerate = fabs(s4[0]) < DBL_EPSILON || fabs(s4[1]) < DBL_EPSILON ||
-                                        fabs(s4[2]) < DBL_EPSILON || fabs(s4[3]) < DBL_EPSILON;
-                if (!degenerate) {
-                    const double smx = k / s4[0], smy = k / s4[1], sMx = k / s4[2], sMy = k / s4[3];
-                    double lt[45];
-                    for (int e = 0; e < 45; ++e) lt[e] = 0;
-                    for (int i = tid; i < k; i += kRT) {
+                // ---- refit: runKernel over all inliers, OpenCV's sequential sums (fundam.cpp) ----
+                if (tid < 4) {  // centroids cm (scene), cM (object): one sequential sum each
+                    double c = 0;
+                    for (int i = 0; i < k; ++i) {
                         const float4 q = X[i];
-                        const double x = (q.z - cmx) * smx, y = (q.w - cmy) * smy;
-                        const double Xx = (q.x - cMx) * sMx, Yy = (q.y - cMy) * sMy;
-                        const double Lx[9] = {Xx, Yy, 1, 0, 0, 0, -x * Xx, -x * Yy, -x};
-                        const double Ly[9] = {0, 0, 0, Xx, Yy, 1, -y * Xx, -y * Yy, -y};
-                        int e = 0;
-#pragma unroll
-                        for (int j = 0; j < 9; j++)
-#pragma unroll
-                            for (int kk = j; kk < 9; kk++, ++e) lt[e] += Lx[j] * Lx[kk] + Ly[j] * Ly[kk];
+                        c += tid == 0 ? q.z : tid == 1 ? q.w : tid == 2 ? q.x : q.y;
                     }
-                    block_sum<45>(lt, sh.red);
-                    const double invHnorm[9] = {1. / smx, 0, cmx, 0, 1. / smy, cmy, 0, 0, 1};
-                    const double Hnorm2[9] = {sMx, 0, -cMx * sMx, 0, sMy, -cMy * sMy, 0, 0, 1};
-                    if (tid == 0) {
-                        // start: bestModel in the normalized coordinates of the refit,
-                        // H0 = Hnorm_dst Hb Hnorm2^-1 (runKernel maps H = invHnorm H0 Hnorm2)
-                        const double Nd[9] = {smx, 0, -cmx * smx, 0, smy, -cmy * smy, 0, 0, 1};
-                        const double N2i[9] = {1. / sMx, 0, cMx, 0, 1. / sMy, cMy, 0, 0, 1};
-                        double T1[9], H0[9], ev[9];
-                        mat3_mul(Nd, sh.Hb, T1);
-                        mat3_mul(T1, N2i, H0);
-                        sh.flag = refit_inverse_iteration(lt, H0, ev) ? 1 : 0;
-                        if (sh.flag) {
-                            double Ht[9], Hn[9];
-                            mat3_mul(invHnorm, ev, Ht);
-                            mat3_mul(Ht, Hnorm2, Hn);
-                            const double sc = 1. / Hn[8];
-                            for (int i = 0; i < 9; ++i) sh.H[i] = Hn[i] * sc;
+                    sh.norm[tid] = c / k;
+                }
+                __syncthreads();
+                if (tid < 4) {  // mean absolute deviations
+                    const double c = sh.norm[tid];
+                    double sd = 0;
+                    for (int i = 0; i < k; ++i) {
+                        const float4 q = X[i];
+                        sd += fabs((tid == 0 ? q.z : tid == 1 ? q.w : tid == 2 ? q.x : q.y) - c);
+                    }
+                    sh.norm[4 + tid] = sd;
+                }
+                __syncthreads();
+                const double cmx = sh.norm[0], cmy = sh.norm[1], cMx = sh.norm[2], cMy = sh.norm[3];
+                const bool degenerate = fabs(sh.norm[4]) < DBL_EPSILON || fabs(sh.norm[5]) < DBL_EPSILON ||
+                                        fabs(sh.norm[6]) < DBL_EPSILON || fabs(sh.norm[7]) < DBL_EPSILON;
+                if (!degenerate) {
+                    const double smx = k / sh.norm[4], smy = k / sh.norm[5], sMx = k / sh.norm[6], sMy = k / sh.norm[7];
+                    if (tid < 45) {  // LtL entry (j, kk), kk >= j: one sequential sum over the inliers
+                        int j = 0, r = tid;
+                        while (r >= 9 - j) { r -= 9 - j; ++j; }
+                        const int kk = j + r;
+                        double acc = 0;
+                        for (int i = 0; i < k; ++i) {
+                            const float4 q = X[i];
+                            const double x = (q.z - cmx) * smx, y = (q.w - cmy) * smy;
+                            const double Xx = (q.x - cMx) * sMx, Yy = (q.y - cMy) * sMy;
+                            const double Lx[9] = {Xx, Yy, 1, 0, 0, 0, -x * Xx, -x * Yy, -x};
+                            const double Ly[9] = {0, 0, 0, Xx, Yy, 1, -y * Xx, -y * Yy, -y};
+                            double lxj = 0, lxk = 0, lyj = 0, lyk = 0;
+#pragma unroll
+                            for (int t = 0; t < 9; ++t) {
+                                lxj = t == j ? Lx[t] : lxj; lxk = t == kk ? Lx[t] : lxk;
+                                lyj = t == j ? Ly[t] : lyj; lyk = t == kk ? Ly[t] : lyk;
+                            }
+                            acc += lxj * lxk + lyj * lyk;
                         }
+                        sh.lt[tid] = acc;
                     }
                     __syncthreads();
-                    if (!sh.flag && tid < 16) {  // fallback: the Jacobi of runKernel, one 16-lane group
+                    const double invHnorm[9] = {1. / smx, 0, cmx, 0, 1. / smy, cmy, 0, 0, 1};
+                    const double Hnorm2[9] = {sMx, 0, -cMx * sMx, 0, sMy, -cMy * sMy, 0, 0, 1};
+                    if (tid < 16) {  // the Jacobi of runKernel, one 16-lane group (bit-identical)
                         double Hl[9];
-                        dlt_finish_group(lt, sh.J9, invHnorm, Hnorm2, Hl);
+                        dlt_finish_group(sh.lt, sh.J9, invHnorm, Hnorm2, Hl);
                         if (tid == 0)
                             for (int i = 0; i < 9; ++i) sh.H[i] = Hl[i];
                     }
@@ -3017,12 +2892,14 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                 __syncthreads();
                 double x[8];
                 for (int i = 0; i < 8; ++i) x[i] = sh.x[i];
-                double A[64], v[8], Sv, rinf;
-                lm_normal(X, k, x, sh.red, A, v, Sv, rinf);
+                double rinf;
+                lm_normal(X, k, x, sh.lm, sh.red, sh.nrm, rinf);
                 if (tid == 0) {
-                    for (int i = 0; i < 64; ++i) sh.A[i] = A[i];
-                    for (int i = 0; i < 8; ++i) { sh.v[i] = v[i]; sh.D[i] = A[9 * i]; }
-                    sh.S = Sv; sh.rinf = rinf; sh.lambda = 1; sh.lc = 0.75;
+                    int e = 0;
+                    for (int a = 0; a < 8; ++a)
+                        for (int b = a; b < 8; ++b, ++e) sh.A[a * 8 + b] = sh.A[b * 8 + a] = sh.nrm[e];
+                    for (int i = 0; i < 8; ++i) { sh.v[i] = sh.nrm[36 + i]; sh.D[i] = sh.A[9 * i]; }
+                    sh.S = sh.nrm[44]; sh.rinf = rinf; sh.lambda = 1; sh.lc = 0.75;
                 }
                 __syncthreads();
                 int iter = 0;
@@ -3031,9 +2908,7 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                         double Ap[64];
                         for (int i = 0; i < 64; ++i) Ap[i] = sh.A[i];
                         for (int i = 0; i < 8; ++i) Ap[9 * i] += sh.lambda * sh.D[i];
-                        if (!solve_chol8(Ap, sh.v, sh.d)) {
-                            solve_eig8(Ap, sh.v, sh.d, sh.J9);
-                        }
+                        solve_eig8(Ap, sh.v, sh.d, sh.J9);
                         double dinf = 0;
                         for (int i = 0; i < 8; ++i) {
                             sh.xd[i] = sh.x[i] - sh.d[i];
@@ -3044,7 +2919,7 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                     __syncthreads();
                     double xd[8];
                     for (int i = 0; i < 8; ++i) xd[i] = sh.xd[i];
-                    const double Sd = lm_cost(X, k, xd, sh.red);
+                    const double Sd = lm_cost(X, k, xd, sh.lm, sh.red);
                     if (tid == 0) {
                         const double Rlo = 0.25, Rhi = 0.75;
                         double temp_d[8];
@@ -3080,11 +2955,12 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                     __syncthreads();
                     if (sh.accept) {
                         for (int i = 0; i < 8; ++i) x[i] = sh.x[i];
-                        double S2;
-                        lm_normal(X, k, x, sh.red, A, v, S2, rinf);
+                        lm_normal(X, k, x, sh.lm, sh.red, sh.nrm, rinf);
                         if (tid == 0) {
-                            for (int i = 0; i < 64; ++i) sh.A[i] = A[i];
-                            for (int i = 0; i < 8; ++i) sh.v[i] = v[i];
+                            int e = 0;
+                            for (int a = 0; a < 8; ++a)
+                                for (int b = a; b < 8; ++b, ++e) sh.A[a * 8 + b] = sh.A[b * 8 + a] = sh.nrm[e];
+                            for (int i = 0; i < 8; ++i) sh.v[i] = sh.nrm[36 + i];
                             sh.rinf = rinf;
                         }
                     }
@@ -3226,6 +3102,15 @@ void ransac_enqueue(const RansacParams& prm, int n_probs, const ProbDev* probs, 
             mark(mark_ctx, "score", s);
             ransac_select_kernel<<<n_probs, 64, 0, s>>>(b.state, probs, b.counts, c1, prm.conf);
             mark(mark_ctx, "select", s);
+            if (getenv("MIM_DEBUG_TRACE") && n_probs == 1) {  // debug: problem 0's samples and exact counts
+                std::vector<int> hc(c1 - c0);
+                std::vector<int4> hs(c1 - c0);
+                (void)hipMemcpyAsync(hc.data(), b.counts + c0, sizeof(int) * (c1 - c0), hipMemcpyDeviceToHost, s);
+                (void)hipMemcpyAsync(hs.data(), b.samples + c0, sizeof(int4) * (c1 - c0), hipMemcpyDeviceToHost, s);
+                (void)hipStreamSynchronize(s);
+                for (int i = 0; i < c1 - c0; ++i)
+                    fprintf(stderr, "[trace] %d %d %d %d %d %d\n", c0 + i, hc[i], hs[i].x, hs[i].y, hs[i].z, hs[i].w);
+            }
         } else {
             if (c0 == 0)
                 ransac_bound_mfma_kernel<true><<<n_probs * bpp256, 256, 0, s>>>(b.state, probs, pts, b.samples, b.stream,

@@ -1,0 +1,134 @@
+"""The reference's detection pipeline on libmim, OpenCV-free: models, detectObjects, results, metrics.
+
+Mirrors (names, argument meaning, outputs):
+  ObjectModel                       include/objectModel.hpp:11-16  (name, images, keypoints, descriptors)
+  process_model_views               ModelsDetector.cpp:46-80  one object: detectAndCompute(view, mask) per view
+  detect_objects                    TestsDetector.cpp:32-251  scene -> [(Rect, model name)]
+  save_detections                   utils.cpp:12-20
+Every compute stage runs in libmim: resize and SIFT on the GPU (mim_resize_linear_u8,
+mim_sift_detect_compute), the (model, scale, view) problems as ONE device batch (knnMatch k=2 + ratio
++ findHomography RANSAC + gates, mim_batch_run), the boxes in the library's host stage
+(mim_detect_boxes = include/mim_detect.hpp).  Images are CV_8UC1 arrays: the grayscale conversion of
+preprocessImage (preprocessing.cpp:11) is the caller's (cv::imread(..., IMREAD_GRAYSCALE) or
+cvtColor), as is file decoding.
+
+Differences from the reference, all without effect on the result:
+  - the scene is resized and SIFT-described once per scale, not once per (model, scale)
+    (TestsDetector.cpp:99-107 inside the model loop recomputes the same keypoints per model);
+  - view order: the reference iterates an unordered_map filled in directory order
+    (ModelsDetector.cpp:29-45), which is filesystem-dependent; here the caller's order is used (the
+    clustering's float sums depend on point order, so compare runs with the same view order).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import _lib
+from ._lib import BoxParams, Rect
+from .matcher import DIM, Matcher, default_params
+
+SCALES = (0.7, 0.85, 1.0, 1.15, 1.3)  # TestsDetector.cpp:99
+
+
+@dataclass
+class ObjectModel:  # objectModel.hpp:11-16
+    name: str
+    images: list = field(default_factory=list)
+    keypoints: list = field(default_factory=list)    # KEYPOINT_DTYPE arrays
+    descriptors: list = field(default_factory=list)  # (n, 128) float32
+
+
+def default_box_params(**kw) -> BoxParams:
+    p = BoxParams()
+    _lib.load().mim_default_box_params(C.byref(p))
+    for k, v in kw.items():
+        setattr(p, k, v)
+    return p
+
+
+def process_model_views(matcher: Matcher, name: str, views) -> ObjectModel:
+    """ModelsDetector.cpp:46-80 for one object: views = [(gray, mask or None), ...]."""
+    m = ObjectModel(name)
+    for gray, mask in views:
+        k, d = matcher.sift_detect_compute(gray, mask)
+        m.images.append(gray)
+        m.keypoints.append(k)
+        m.descriptors.append(d)
+    return m
+
+
+def detect_boxes(points: np.ndarray, bp: BoxParams | None = None) -> list[tuple[int, int, int, int]]:
+    """TestsDetector.cpp:111-248 for one model's allUnfilteredScenePts -> [(x, y, w, h)]."""
+    L = _lib.load()
+    pts = np.ascontiguousarray(points, np.float32).reshape(-1, 2)
+    bp = bp or default_box_params()
+    cap = max(16, len(pts) // 8 + 1)
+    out = (Rect * cap)()
+    n = C.c_int32()
+    st = L.mim_detect_boxes(C.c_void_p(pts.ctypes.data), len(pts), C.byref(bp), out, cap, C.byref(n))
+    if st != 0:
+        raise _lib.MimError(st, "mim_detect_boxes failed")
+    return [(out[i].x, out[i].y, out[i].width, out[i].height) for i in range(n.value)]
+
+
+@dataclass
+class SceneRun:
+    """detect_objects' intermediate products (for tests and benches)."""
+    scene_kp: list      # per scale: KEYPOINT_DTYPE
+    scene_desc: list    # per scale: (n, 128) float32
+    results: np.ndarray  # RESULT_DTYPE per problem, problems in (model, scale, view) order
+    points: list        # per model: allUnfilteredScenePts (n, 2) float32
+    detections: list    # [((x, y, w, h), name)]
+
+
+def detect_objects(matcher: Matcher, scene_gray, models: list[ObjectModel], scales=SCALES, params=None,
+                   box_params: BoxParams | None = None, keep: bool = False):
+    """detectObjects(scene, models, detector) (TestsDetector.cpp:32-251) on a grayscale scene.
+
+    Returns [((x, y, w, h), name)], or the SceneRun when keep=True."""
+    params = params or default_params()
+    scene_kp, scene_desc = [], []
+    for s in scales:  # :99-107
+        scaled = matcher.resize_linear(scene_gray, fx=s)
+        k, d = matcher.sift_detect_compute(scaled)
+        scene_kp.append(k)
+        scene_desc.append(d)
+    matcher.clear_sets()
+    view_ids = [[matcher.add_set(d, np.stack([k["x"], k["y"]], 1)) for k, d in zip(m.keypoints, m.descriptors)]
+                for m in models]
+    scene_ids = [matcher.add_set(d, np.stack([k["x"], k["y"]], 1)) for k, d in zip(scene_kp, scene_desc)]
+    tags = [(mi, si, vi) for mi in range(len(models)) for si in range(len(scales)) for vi in range(len(view_ids[mi]))]
+    res = matcher.match_batch([(view_ids[mi][vi], scene_ids[si]) for mi, si, vi in tags], params)
+    pts = [[] for _ in models]
+    for i, (mi, si, vi) in enumerate(tags):
+        r = res[i]
+        if r["status"] != 0:  # :74, :79, :81, :84
+            continue
+        q, t, mask = matcher.problem_detail(i, int(r["n_good"]))
+        k = scene_kp[si][t[mask.astype(bool)]]
+        p = np.stack([k["x"], k["y"]], 1).astype(np.float32)
+        s = np.float32(scales[si])
+        if s != np.float32(1.0):  # scalePoints (:48-55): pt /= scale in float
+            p = p / s
+        pts[mi].append(p)
+    points = [np.concatenate(p).astype(np.float32) if p else np.zeros((0, 2), np.float32) for p in pts]
+    dets = []
+    for mi, m in enumerate(models):  # :111-248, model order
+        dets += [(b, m.name) for b in detect_boxes(points[mi], box_params)]
+    if keep:
+        return SceneRun(scene_kp, scene_desc, res, points, dets)
+    return dets
+
+
+def save_detections(path: str, detections) -> None:
+    """utils.cpp:12-20: one "<name> x0 y0 x1 y1" line per detection."""
+    with open(path, "w") as f:
+        for (x, y, w, h), name in detections:
+            f.write(f"{name} {x} {y} {x + w} {y + h}\n")
+
+
+__all__ = ["ObjectModel", "SCALES", "SceneRun", "default_box_params", "detect_boxes", "detect_objects",
+           "process_model_views", "save_detections", "DIM"]

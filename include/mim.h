@@ -172,6 +172,27 @@ mim_status mim_sift_detect_compute(struct mim_ctx* ctx, const uint8_t* gray, int
 mim_status mim_resize_linear_u8(struct mim_ctx* ctx, const uint8_t* src, int32_t rows, int32_t cols, int64_t step,
                                 uint8_t* dst, int32_t drows, int32_t dcols, double fx, double fy);
 
+/* ---- host stage after the matcher: clustering, margins, merge, area gate (TestsDetector.cpp:111-248)
+ * Host code (include/mim_detect.hpp), no ctx, no device.  Thresholds: TestsDetector.cpp:26-30. */
+typedef struct {
+    float cluster_distance;          /* CLUSTER_DISTANCE_THRESHOLD 20.0f */
+    int32_t min_points_per_cluster;  /* MIN_POINTS_PER_CLUSTER 18 */
+    float box_merge_distance;        /* BOX_MERGE_DISTANCE 250.0f */
+    int32_t min_box_area;            /* MIN_BOX_AREA 2500 */
+    float dynamic_margin;            /* DYNAMIC_MARGIN 1.0f */
+} mim_box_params;
+
+typedef struct {
+    int32_t x, y, width, height; /* cv::Rect */
+} mim_rect;
+
+void mim_default_box_params(mim_box_params* p);
+/* One model's boxes from its allUnfilteredScenePts (n x 2 float32, the inlier scene points of every
+ * accepted (view, scale) problem in the reference's order): writes the merged boxes that pass the
+ * area gate, in the reference's order, at most `cap` of them; *n_boxes = their number. */
+mim_status mim_detect_boxes(const float* pts_xy, int32_t n, const mim_box_params* bp, mim_rect* boxes, int32_t cap,
+                            int32_t* n_boxes);
+
 /* ---- introspection for benches / profiles ----------------------------------------------------- */
 /* Per-kernel device time (ms) summed over the batches since the last result fetch, measured with
  * HIP events on the stream each kernel ran on.  names: "knn", "ratio", "attempt", "chain",

@@ -340,12 +340,13 @@ __device__ __forceinline__ unsigned group_bits(unsigned long long m) {
 // values, in increasing index order) plus, optionally, a zero entry at index `zi` (-1: none).
 // The index of the first maximal slot j is recomputed from j (the (j-9)-th index outside {k, l})
 // instead of being fetched from that lane: no LDS round trip.
+template <int n>
 __device__ __forceinline__ int refresh_argmax(double val, bool cand, int k, int l, int zi) {
     const double mx = row_max(cand ? val : -1.0);
     const unsigned m = group_bits(__ballot(cand & (val == mx)));
     int first = INT_MAX;
     if (m) {
-        int im = __builtin_ctz(m) - 9;
+        int im = __builtin_ctz(m) - n;
         im += im >= k;
         im += im >= l;
         first = im;
@@ -355,10 +356,13 @@ __device__ __forceinline__ int refresh_argmax(double val, bool cand, int k, int 
 }
 
 // A/W/V: this group's LDS state (A packed strict upper, W diagonal) written by the caller.
-// Returns, in every slot, the row of V holding the eigenvector of the smallest eigenvalue after
-// OpenCV's descending selection sort.
-__device__ __forceinline__ int jacobi9_group(double* __restrict__ A, double* __restrict__ W, double* __restrict__ V) {
-    constexpr int n = 9;
+// n = 9 (runKernel's LtL) uses all 16 slots (9 V pairs + 7 A pairs), n = 8 (LMSolverImpl's normal
+// matrix) 14 of them.  Outputs, in every slot, Ws = the eigenvalues in OpenCV's descending
+// selection-sort order and perm[i] = the row of V holding the i-th of them.
+template <int n>
+__device__ __forceinline__ void jacobi_group(double* __restrict__ A, double* __restrict__ W, double* __restrict__ V,
+                                             double (&Ws)[n], int (&perm)[n]) {
+    static_assert(2 * n - 2 <= 16, "one rotation's pairs must fit the 16 slots");
     const int slot = threadIdx.x & 15;
     const double eps = DBL_EPSILON;
     for (int e = slot; e < n * n; e += 16) V[e] = (e % (n + 1) == 0) ? 1.0 : 0.0;
@@ -414,8 +418,9 @@ __device__ __forceinline__ int jacobi9_group(double* __restrict__ A, double* __r
         if (im >= k) ++im;
         if (im >= l) ++im;
         const bool vslot = slot < n;
-        const int ia = vslot ? k * n + slot : pk_any<n>(im, k);
-        const int ib = vslot ? l * n + slot : pk_any<n>(im, l);
+        const bool idle = slot >= 2 * n - 2;  // n = 8: slots 14, 15
+        const int ia = vslot ? k * n + slot : (idle ? 0 : pk_any<n>(im, k));
+        const int ib = vslot ? l * n + slot : (idle ? 0 : pk_any<n>(im, l));
         double* base = vslot ? V : A;
         const double a0 = base[ia], b0 = base[ib];
         const double wk = W[k], wl = W[l];
@@ -429,8 +434,10 @@ __device__ __forceinline__ int jacobi9_group(double* __restrict__ A, double* __r
         t = y < 0 ? -t : t;
         const double na = a0 * c - b0 * s;
         const double nb = a0 * s + b0 * c;
-        base[ia] = na;
-        base[ib] = nb;
+        if (!idle) {
+            base[ia] = na;
+            base[ib] = nb;
+        }
         if (slot == 0) {
             A[pk<n>(k, l)] = 0;
             W[k] = wk - t;
@@ -441,12 +448,12 @@ __device__ __forceinline__ int jacobi9_group(double* __restrict__ A, double* __r
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         // ---- refresh the cached maxima of rows/columns k and l (row k: A(k,i) = na of the A
         // slots, plus A(k,l) = 0; row l: nb, plus A(l,k) = 0) ----
-        const bool aslot = !vslot;
+        const bool aslot = !vslot && !idle;
         const double va = fabs(na), vb = fabs(nb);
-        const int rk = refresh_argmax(va, aslot & (im > k), k, l, l);
-        const int ck = refresh_argmax(va, aslot & (im < k), k, l, -1);
-        const int rl = refresh_argmax(vb, aslot & (im > l), k, l, -1);
-        const int cl = refresh_argmax(vb, aslot & (im < l), k, l, k);
+        const int rk = refresh_argmax<n>(va, aslot & (im > k), k, l, l);
+        const int ck = refresh_argmax<n>(va, aslot & (im < k), k, l, -1);
+        const int rl = refresh_argmax<n>(vb, aslot & (im > l), k, l, -1);
+        const int cl = refresh_argmax<n>(vb, aslot & (im < l), k, l, k);
         if (slot == k) {
             if (k < n - 1) indR = rk;
             if (k > 0) indC = ck;
@@ -457,8 +464,6 @@ __device__ __forceinline__ int jacobi9_group(double* __restrict__ A, double* __r
         }
     }
     // ---- OpenCV's selection sort (descending), tracked as a permutation ----
-    double Ws[n];
-    int perm[n];
 #pragma unroll
     for (int i = 0; i < n; i++) {
         Ws[i] = W[i];
@@ -486,7 +491,14 @@ __device__ __forceinline__ int jacobi9_group(double* __restrict__ A, double* __r
         Ws[k] = wm;
         perm[k] = pm;
     }
-    return perm[n - 1];
+}
+
+// runKernel's 9x9: the row of V holding the eigenvector of the smallest eigenvalue
+__device__ __forceinline__ int jacobi9_group(double* __restrict__ A, double* __restrict__ W, double* __restrict__ V) {
+    double Ws[9];
+    int perm[9];
+    jacobi_group<9>(A, W, V, Ws, perm);
+    return perm[8];
 }
 
 // normalized-DLT accumulation of runKernel for `count` points, entry e of LtL (upper incl. the
@@ -2554,35 +2566,15 @@ __device__ __forceinline__ void refine_point(const double* h, double Mx, double 
 // (lm_refine / normal_eq in oracle/mim_oracle.c), so the refined H is bit-identical, also for the
 // near-degenerate inlier sets of real data (duplicated keypoints) where a reordered sum moves the
 // LM path far (tests/test_pipeline_gpu.py).
-constexpr int kLmChunk = 512;
+constexpr int kLmChunk = 64;
+constexpr int kLmRow = 9;  // J row (8 entries) + the residual, per x / y row of a point
 struct LmStage {
-    double Mx[kLmChunk], My[kLmChunk], ww[kLmChunk], xi[kLmChunk], yi[kLmChunk], ex[kLmChunk], ey[kLmChunk];
+    double rx[kLmChunk * kLmRow], ry[kLmChunk * kLmRow];  // [point][Jx(0..7), r_x] and [point][Jy, r_y]
 };
 
-// J row entries of point i: x-row Jx(a), y-row Jy(a) (HomographyRefineCallback::compute)
-__device__ __forceinline__ double jx_of(int a, double Mx, double My, double ww, double xi) {
-    switch (a) {
-        case 0: return Mx * ww;
-        case 1: return My * ww;
-        case 2: return ww;
-        case 6: return -Mx * ww * xi;
-        case 7: return -My * ww * xi;
-        default: return 0.;
-    }
-}
-__device__ __forceinline__ double jy_of(int a, double Mx, double My, double ww, double yi) {
-    switch (a) {
-        case 3: return Mx * ww;
-        case 4: return My * ww;
-        case 5: return ww;
-        case 6: return -Mx * ww * yi;
-        case 7: return -My * ww * yi;
-        default: return 0.;
-    }
-}
-
-// stage points [c0, c0 + n) of X under model h into L; returns this thread's max |residual|
-__device__ double lm_stage(const float4* __restrict__ X, int c0, int n, const double* h, LmStage& L) {
+// stage points [c0, c0 + n) of X under model h into L (J rows only when `jac`); returns this
+// thread's max |residual|
+__device__ double lm_stage(const float4* __restrict__ X, int c0, int n, const double* h, LmStage& L, bool jac) {
     double mx = 0;
     for (int i = threadIdx.x; i < n; i += kRT) {
         const float4 q = X[c0 + i];
@@ -2592,18 +2584,30 @@ __device__ double lm_stage(const float4* __restrict__ X, int c0, int n, const do
         const double xi = (h[0] * Mx + h[1] * My + h[2]) * ww;
         const double yi = (h[3] * Mx + h[4] * My + h[5]) * ww;
         const double ex = xi - (double)q.z, ey = yi - (double)q.w;
-        L.Mx[i] = Mx; L.My[i] = My; L.ww[i] = ww; L.xi[i] = xi; L.yi[i] = yi; L.ex[i] = ex; L.ey[i] = ey;
+        double* x = L.rx + i * kLmRow;
+        double* y = L.ry + i * kLmRow;
+        if (jac) {  // HomographyRefineCallback::compute's J rows
+            x[0] = Mx * ww; x[1] = My * ww; x[2] = ww; x[3] = x[4] = x[5] = 0.;
+            x[6] = -Mx * ww * xi; x[7] = -My * ww * xi;
+            y[0] = y[1] = y[2] = 0.; y[3] = Mx * ww; y[4] = My * ww; y[5] = ww;
+            y[6] = -Mx * ww * yi; y[7] = -My * ww * yi;
+        }
+        x[8] = ex;
+        y[8] = ey;
         mx = fmax(mx, fmax(fabs(ex), fabs(ey)));
     }
     return mx;
 }
 
-// A = J^T J (full 8x8), v = J^T r, S = |r|^2, rinf = |r|_inf: out[0..35] A upper, [36..43] v, [44] S
+// A = J^T J, v = J^T r, S = |r|^2 as the 45 entries (a, b), a <= b <= 8, of [J r]^T [J r] (column 8
+// = r): out[e] in the packing order A upper (36), v (8), S; each entry one lane's sequential sum over
+// the rows (x row, then y row, point by point).  rinf = |r|_inf.
 __device__ void lm_normal(const float4* __restrict__ X, int n, const double* h, LmStage& L, double* red,
                           double* out, double& rinf) {
     const int e = threadIdx.x;
-    int a = 0, b = 0;
-    if (e < 36) {  // (a, b), b >= a, row-major upper triangle
+    int a = 8, b = 8;  // e == 44: S
+    if (e < 36) {      // (a, b), b >= a, row-major upper triangle of A
+        a = 0;
         int r = e;
         while (r >= 8 - a) { r -= 8 - a; ++a; }
         b = a + r;
@@ -2614,24 +2618,15 @@ __device__ void lm_normal(const float4* __restrict__ X, int n, const double* h, 
     for (int c0 = 0; c0 < n; c0 += kLmChunk) {
         const int m = min(kLmChunk, n - c0);
         __syncthreads();
-        mx = fmax(mx, lm_stage(X, c0, m, h, L));
+        mx = fmax(mx, lm_stage(X, c0, m, h, L, true));
         __syncthreads();
-        if (e < 36) {
+        if (e < 45) {
+#pragma unroll 4
             for (int i = 0; i < m; ++i) {
-                const double Mx = L.Mx[i], My = L.My[i], ww = L.ww[i];
-                acc += jx_of(a, Mx, My, ww, L.xi[i]) * jx_of(b, Mx, My, ww, L.xi[i]);
-                acc += jy_of(a, Mx, My, ww, L.yi[i]) * jy_of(b, Mx, My, ww, L.yi[i]);
-            }
-        } else if (e < 44) {
-            for (int i = 0; i < m; ++i) {
-                const double Mx = L.Mx[i], My = L.My[i], ww = L.ww[i];
-                acc += jx_of(a, Mx, My, ww, L.xi[i]) * L.ex[i];
-                acc += jy_of(a, Mx, My, ww, L.yi[i]) * L.ey[i];
-            }
-        } else if (e == 44) {
-            for (int i = 0; i < m; ++i) {
-                acc += L.ex[i] * L.ex[i];
-                acc += L.ey[i] * L.ey[i];
+                const double* x = L.rx + i * kLmRow;
+                const double* y = L.ry + i * kLmRow;
+                acc += x[a] * x[b];
+                acc += y[a] * y[b];
             }
         }
     }
@@ -2645,12 +2640,14 @@ __device__ double lm_cost(const float4* __restrict__ X, int n, const double* h, 
     for (int c0 = 0; c0 < n; c0 += kLmChunk) {
         const int m = min(kLmChunk, n - c0);
         __syncthreads();
-        lm_stage(X, c0, m, h, L);
+        lm_stage(X, c0, m, h, L, false);
         __syncthreads();
         if (threadIdx.x == 0)
+#pragma unroll 8
             for (int i = 0; i < m; ++i) {
-                acc += L.ex[i] * L.ex[i];
-                acc += L.ey[i] * L.ey[i];
+                const double ex = L.rx[i * kLmRow + 8], ey = L.ry[i * kLmRow + 8];
+                acc += ex * ex;
+                acc += ey * ey;
             }
     }
     if (threadIdx.x == 0) red[0] = acc;
@@ -2660,57 +2657,74 @@ __device__ double lm_cost(const float4* __restrict__ X, int n, const double* h, 
     return r;
 }
 
-// Jacobi of an 8x8 symmetric matrix (single thread, stride-1 scratch); w sorted descending,
-// V rows in the matching order (OpenCV's sorted layout)
-__device__ void eig8(const double* Ain, double* J, double* w, double* V) {
+// eig8 by a 16-lane group (jacobi_group<8>, bit-identical to OpenCV's JacobiImpl_): the state lives in
+// J (A packed upper | W | V); every slot gets the sorted eigenvalues Ws and perm (row of V of each)
+__device__ __forceinline__ void eig8_group(const double* Ain, double* J, double (&Ws)[8], int (&perm)[8]) {
+    const int slot = threadIdx.x & 15;
     double* A = J;
     double* W = J + 28;
     double* VV = J + 36;
-    for (int i = 0; i < 8; ++i) {
-        W[i] = Ain[9 * i];
-        for (int j = i + 1; j < 8; ++j) A[pk<8>(i, j)] = Ain[8 * i + j];
+    for (int e = slot; e < 64; e += 16) {
+        const int i = e >> 3, j = e & 7;
+        if (i == j) W[i] = Ain[e];
+        else if (j > i) A[pk<8>(i, j)] = Ain[e];
     }
-    double Ws[8];
-    int perm[8];
-    jacobi_fast<8, 1>(A, W, VV, Ws, perm);
-    for (int i = 0; i < 8; ++i) {
-        w[i] = Ws[i];
-        for (int j = 0; j < 8; ++j) V[8 * i + j] = VV[perm[i] * 8 + j];
-    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    jacobi_group<8>(A, W, VV, Ws, perm);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// solve(Ap, v, d, DECOMP_EIG) = Jacobi + SVBkSb(eps = 2 DBL_EPSILON)
-__device__ void solve_eig8(const double* Ap, const double* b, double* x, double* J) {
-    double w[8], V[64];
-    eig8(Ap, J, w, V);
+// solve(Ap, v, d, DECOMP_EIG) = Jacobi + SVBkSb(eps = 2 DBL_EPSILON) (Ap, b in LDS); called by a
+// 16-lane group, every slot gets x
+__device__ void solve_eig8(const double* Ap, const double* b, double (&x)[8], double* J) {
+    double w[8];
+    int perm[8];
+    eig8_group(Ap, J, w, perm);
+    const double* V = J + 36;
     double threshold = 0;
+#pragma unroll
     for (int i = 0; i < 8; i++) threshold += w[i];
     threshold *= DBL_EPSILON * 2;
+#pragma unroll
     for (int j = 0; j < 8; j++) x[j] = 0;
+#pragma unroll
     for (int i = 0; i < 8; i++) {
         double wi = w[i];
         if (fabs(wi) <= threshold) continue;
         wi = 1 / wi;
+        const double* Vi = V + perm[i] * 8;
         double s = 0;
-        for (int j = 0; j < 8; j++) s += V[8 * i + j] * b[j];
+#pragma unroll
+        for (int j = 0; j < 8; j++) s += Vi[j] * b[j];
         s *= wi;
-        for (int j = 0; j < 8; j++) x[j] = x[j] + s * V[8 * i + j];
+#pragma unroll
+        for (int j = 0; j < 8; j++) x[j] = x[j] + s * Vi[j];
     }
 }
 
-// invert(A, Ai, DECOMP_EIG), max |Ai(i,i)| (LMSolverImpl's lambda restart)
+// invert(A, Ai, DECOMP_EIG), max |Ai(i,i)| (LMSolverImpl's lambda restart); 16-lane group
 __device__ double inv_diag_max8(const double* A, double* J) {
-    double w[8], V[64];
-    eig8(A, J, w, V);
+    double w[8];
+    int perm[8];
+    eig8_group(A, J, w, perm);
+    const double* V = J + 36;
     double threshold = 0;
+#pragma unroll
     for (int i = 0; i < 8; i++) threshold += w[i];
     threshold *= DBL_EPSILON * 2;
     double maxval = DBL_EPSILON;
+#pragma unroll
     for (int c = 0; c < 8; ++c) {
         double diag = 0;
+#pragma unroll
         for (int i = 0; i < 8; i++) {
             if (fabs(w[i]) <= threshold) continue;
-            diag += V[8 * i + c] * V[8 * i + c] / w[i];
+            const double v = V[perm[i] * 8 + c];
+            diag += v * v / w[i];
         }
         maxval = fmax(maxval, fabs(diag));
     }
@@ -2724,7 +2738,7 @@ struct RefineShared {
     LmStage lm;
     double norm[8];       // cm, cM, sm, sM (x,y each)
     double H[9], Hb[9];
-    double A[64], v[8], D[8], x[8], xd[8], d[8];
+    double A[64], Ap[64], v[8], D[8], x[8], xd[8], d[8];
     double S, Sd, rinf, dinf, lambda, lc;
     double J9[kJ9D];
     int flag, n_inl, proceed, accept;
@@ -2783,6 +2797,9 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
         const int stop = max(S.niters, S.best_iter + 1);
         res.iters = (S.fail_iter >= 0 && S.fail_iter < stop) ? S.fail_iter : stop;
         if (ok) {
+#ifdef MIM_REFINE_PROF
+            const long long tp0 = clock64();
+#endif
             // bestModel = runKernel(sample[best_iter]) (bit-identical to the hypo kernel's)
             if (tid == 0 && !exact_all && best_h[(long long)p * 9 + 8] != 0.0) {
                 for (int i = 0; i < 9; ++i) sh.Hb[i] = best_h[(long long)p * 9 + i];  // from the exact pass
@@ -2828,9 +2845,13 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
             __syncthreads();
             const int k = sh.n_inl;
             if (k > 0) {
+#ifdef MIM_REFINE_PROF
+                const long long tp1 = clock64();
+#endif
                 // ---- refit: runKernel over all inliers, OpenCV's sequential sums (fundam.cpp) ----
                 if (tid < 4) {  // centroids cm (scene), cM (object): one sequential sum each
                     double c = 0;
+#pragma unroll 8
                     for (int i = 0; i < k; ++i) {
                         const float4 q = X[i];
                         c += tid == 0 ? q.z : tid == 1 ? q.w : tid == 2 ? q.x : q.y;
@@ -2841,6 +2862,7 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                 if (tid < 4) {  // mean absolute deviations
                     const double c = sh.norm[tid];
                     double sd = 0;
+#pragma unroll 8
                     for (int i = 0; i < k; ++i) {
                         const float4 q = X[i];
                         sd += fabs((tid == 0 ? q.z : tid == 1 ? q.w : tid == 2 ? q.x : q.y) - c);
@@ -2849,6 +2871,9 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                 }
                 __syncthreads();
                 const double cmx = sh.norm[0], cmy = sh.norm[1], cMx = sh.norm[2], cMy = sh.norm[3];
+#ifdef MIM_REFINE_PROF
+                const long long tq1 = clock64();
+#endif
                 const bool degenerate = fabs(sh.norm[4]) < DBL_EPSILON || fabs(sh.norm[5]) < DBL_EPSILON ||
                                         fabs(sh.norm[6]) < DBL_EPSILON || fabs(sh.norm[7]) < DBL_EPSILON;
                 if (!degenerate) {
@@ -2858,6 +2883,7 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                         while (r >= 9 - j) { r -= 9 - j; ++j; }
                         const int kk = j + r;
                         double acc = 0;
+#pragma unroll 4
                         for (int i = 0; i < k; ++i) {
                             const float4 q = X[i];
                             const double x = (q.z - cmx) * smx, y = (q.w - cmy) * smy;
@@ -2875,6 +2901,10 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                         sh.lt[tid] = acc;
                     }
                     __syncthreads();
+#ifdef MIM_REFINE_PROF
+                    const long long tq2 = clock64();
+                    if (tid == 0 && p < 2) printf("[refit] p=%d centroid=%lld ltl=%lld\n", p, tq1 - tp1, tq2 - tq1);
+#endif
                     const double invHnorm[9] = {1. / smx, 0, cmx, 0, 1. / smy, cmy, 0, 0, 1};
                     const double Hnorm2[9] = {sMx, 0, -cMx * sMx, 0, sMy, -cMy * sMy, 0, 0, 1};
                     if (tid < 16) {  // the Jacobi of runKernel, one 16-lane group (bit-identical)
@@ -2887,6 +2917,9 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                     for (int i = 0; i < 9; ++i) sh.H[i] = sh.Hb[i];  // runKernel returned 0: H kept
                 }
                 __syncthreads();
+#ifdef MIM_REFINE_PROF
+                const long long tp2 = clock64();
+#endif
                 // ---- LMSolverImpl (levmarq.cpp) on H8 = H[0..7], maxIters 10, eps FLT_EPSILON ----
                 if (tid < 8) sh.x[tid] = sh.H[tid];
                 __syncthreads();
@@ -2903,25 +2936,41 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                 }
                 __syncthreads();
                 int iter = 0;
+#ifdef MIM_REFINE_PROF
+                long long tsolve = 0, tcost = 0, tupd = 0, tnorm = 0, tl0 = clock64();
+#endif
                 for (;;) {
-                    if (tid == 0) {
-                        double Ap[64];
-                        for (int i = 0; i < 64; ++i) Ap[i] = sh.A[i];
-                        for (int i = 0; i < 8; ++i) Ap[9 * i] += sh.lambda * sh.D[i];
-                        solve_eig8(Ap, sh.v, sh.d, sh.J9);
-                        double dinf = 0;
-                        for (int i = 0; i < 8; ++i) {
-                            sh.xd[i] = sh.x[i] - sh.d[i];
-                            dinf = fmax(dinf, fabs(sh.d[i]));
+                    if (tid < 16) {  // the step solve on one 16-lane group (group Jacobi)
+                        for (int i = tid; i < 64; i += 16) sh.Ap[i] = (i % 9) == 0 ? sh.A[i] + sh.lambda * sh.D[i / 9] : sh.A[i];
+                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                        __builtin_amdgcn_wave_barrier();
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                        double dl[8];
+                        solve_eig8(sh.Ap, sh.v, dl, sh.J9);
+                        if (tid == 0) {
+                            double dinf = 0;
+                            for (int i = 0; i < 8; ++i) {
+                                sh.d[i] = dl[i];
+                                sh.xd[i] = sh.x[i] - dl[i];
+                                dinf = fmax(dinf, fabs(dl[i]));
+                            }
+                            sh.dinf = dinf;
                         }
-                        sh.dinf = dinf;
                     }
                     __syncthreads();
+#ifdef MIM_REFINE_PROF
+                    const long long tl1 = clock64(); tsolve += tl1 - tl0;
+#endif
                     double xd[8];
                     for (int i = 0; i < 8; ++i) xd[i] = sh.xd[i];
                     const double Sd = lm_cost(X, k, xd, sh.lm, sh.red);
-                    if (tid == 0) {
+#ifdef MIM_REFINE_PROF
+                    const long long tl2 = clock64(); tcost += tl2 - tl1;
+#endif
+                    if (tid < 16) {  // every slot evaluates the same update; slot 0 stores it
                         const double Rlo = 0.25, Rhi = 0.75;
+                        double lambda = sh.lambda, lc = sh.lc;
+                        const double Scur = sh.S;
                         double temp_d[8];
                         for (int i = 0; i < 8; ++i) {
                             double s = 0;
@@ -2930,29 +2979,36 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                         }
                         double dS = 0;
                         for (int i = 0; i < 8; ++i) dS += sh.d[i] * temp_d[i];
-                        const double R = (sh.S - Sd) / (fabs(dS) > DBL_EPSILON ? dS : 1);
+                        const double R = (Scur - Sd) / (fabs(dS) > DBL_EPSILON ? dS : 1);
                         if (R > Rhi) {
-                            sh.lambda *= 0.5;
-                            if (sh.lambda < sh.lc) sh.lambda = 0;
+                            lambda *= 0.5;
+                            if (lambda < lc) lambda = 0;
                         } else if (R < Rlo) {
                             double t = 0;
                             for (int i = 0; i < 8; ++i) t += sh.d[i] * sh.v[i];
-                            double nu = (Sd - sh.S) / (fabs(t) > DBL_EPSILON ? t : 1) + 2;
+                            double nu = (Sd - Scur) / (fabs(t) > DBL_EPSILON ? t : 1) + 2;
                             nu = fmin(fmax(nu, 2.), 10.);
-                            if (sh.lambda == 0) {
+                            if (lambda == 0) {
                                 const double maxval = inv_diag_max8(sh.A, sh.J9);
-                                sh.lambda = sh.lc = 1. / maxval;
+                                lambda = lc = 1. / maxval;
                                 nu *= 0.5;
                             }
-                            sh.lambda *= nu;
+                            lambda *= nu;
                         }
-                        sh.accept = Sd < sh.S;
-                        if (sh.accept) {
-                            sh.S = Sd;
-                            for (int i = 0; i < 8; ++i) sh.x[i] = sh.xd[i];
+                        if (tid == 0) {
+                            sh.lambda = lambda;
+                            sh.lc = lc;
+                            sh.accept = Sd < Scur;
+                            if (sh.accept) {
+                                sh.S = Sd;
+                                for (int i = 0; i < 8; ++i) sh.x[i] = sh.xd[i];
+                            }
                         }
                     }
                     __syncthreads();
+#ifdef MIM_REFINE_PROF
+                    const long long tl3 = clock64(); tupd += tl3 - tl2;
+#endif
                     if (sh.accept) {
                         for (int i = 0; i < 8; ++i) x[i] = sh.x[i];
                         lm_normal(X, k, x, sh.lm, sh.red, sh.nrm, rinf);
@@ -2964,6 +3020,9 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                             sh.rinf = rinf;
                         }
                     }
+#ifdef MIM_REFINE_PROF
+                    tl0 = clock64(); tnorm += tl0 - tl3;
+#endif
                     ++iter;
                     if (tid == 0) sh.proceed = iter < 10 && sh.dinf >= FLT_EPSILON && sh.rinf >= FLT_EPSILON;
                     __syncthreads();
@@ -2971,6 +3030,11 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                     __syncthreads();
                     if (!proceed) break;
                 }
+#ifdef MIM_REFINE_PROF
+                if (tid == 0 && p < 4)
+                    printf("[refine] p=%d ng=%d k=%d lm_iters=%d compact=%lld refit=%lld lm=%lld solve=%lld cost=%lld upd=%lld norm=%lld\n",
+                           p, ng, k, iter, tp1 - tp0, tp2 - tp1, (long long)clock64() - tp2, tsolve, tcost, tupd, tnorm);
+#endif
                 if (tid < 8) sh.H[tid] = sh.x[tid];
                 __syncthreads();
             } else if (tid == 0) {

@@ -787,11 +787,28 @@ __device__ __forceinline__ int attempt_flag(long long q, const uint32_t* __restr
     return ((len - 4) << 1) | (check_subset(s4, t4) ? 1 : 0);
 }
 
+// The redraw length of the attempt at q as a flag with the pass bit unknown (what the attempt kernel
+// records), for positions past the precomputed window
+__device__ __forceinline__ int length_flag(long long q, const uint32_t* __restrict__ stream, long long slen,
+                                           unsigned N, unsigned long long M);
+
 // The chain only visits ~1/4 of the window's positions (attempts start 4 draws apart), so the
 // attempt kernel records the draws an attempt would consume (its repeated-index redraws) for every
 // position, and checkSubset runs later for the chain's attempts only (ransac_check_kernel).
 // kPassUnknown marks such a flag: bits 1..6 valid, bit 0 not evaluated.
 constexpr int kPassUnknown = 0x80;
+
+__device__ __forceinline__ int length_flag(long long q, const uint32_t* __restrict__ stream, long long slen,
+                                           unsigned N, unsigned long long M) {
+    if (q + 4 > slen) return kAttemptSerial;
+    int idx[4] = {(int)fastmod(stream[q], M, N), (int)fastmod(stream[q + 1], M, N),
+                  (int)fastmod(stream[q + 2], M, N), (int)fastmod(stream[q + 3], M, N)};
+    if (!(idx[1] == idx[0] || idx[2] == idx[0] || idx[2] == idx[1] || idx[3] == idx[0] || idx[3] == idx[1] ||
+          idx[3] == idx[2]))
+        return kPassUnknown;
+    const int len = resolve_at(q, stream, slen, N, M, idx);
+    return (len == 0 || len > 67) ? kAttemptSerial : (((len - 4) << 1) | kPassUnknown);
+}
 
 // RNG::uniform(0, n) = next() % n by Barrett reduction: m = floor((2^32 - 1) / n) >= 2^32/n - 1, so
 // q = mulhi(a, m) is the quotient or one less and a - q*n lies in [0, 2n); one unsigned min folds it
@@ -938,6 +955,7 @@ __device__ __forceinline__ int wave_max(int v) {
 
 constexpr int kFlagWin = 16384;       // LDS window of attempt flags (bytes)
 constexpr int kFlagUnknown = 0xFE;    // past the precomputed window: evaluate inline
+constexpr int kWalkBatchN = 128;      // below this many points the sampler walks lengths, 64 attempts a batch
 
 __device__ __forceinline__ int ctz64(unsigned long long m) { return __builtin_ctzll(m); }
 // wave-uniform values: keep them in SGPRs so the walk's control flow stays scalar
@@ -1500,34 +1518,118 @@ __global__ __launch_bounds__(64) void ransac_sample_kernel(RansacState* __restri
     long long lb = -(1LL << 40);
     int produced = S.produced, fail_run = S.fail_run;
     bool stop_all = false;
+    // (re)load the LDS window of flags at relative position `at` (16-byte aligned), every lane
+    auto refill = [&](long long at) {
+        lb = at;
+        __syncthreads();
+#pragma unroll 4
+        for (int j = 0; j < kFlagWin / 1024; ++j) {
+            const long long r0 = lb + 16LL * (lane + 64 * j);
+            uint4 v;
+            if (r0 + 16 <= wlen) {
+                v = *reinterpret_cast<const uint4*>(F + r0);
+            } else {
+                // past the precomputed window: the redraw lengths computed here (pass bits unknown)
+                uint32_t w4[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    uint32_t w = 0;
+                    for (int b = 0; b < 4; ++b) {
+                        const long long r = r0 + 4 * k + b;
+                        w |= (uint32_t)(r < wlen ? F[r] : length_flag(wbase + r, stream, slen, N, M)) << (8 * b);
+                    }
+                    w4[k] = w;
+                }
+                v = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+            }
+            *reinterpret_cast<uint4*>(win + 16 * (lane + 64 * j)) = v;
+        }
+        __syncthreads();
+    };
+    if (N < kWalkBatchN) {
+        // ---- small n: dense redraws (repeated indices) end the sub-rounds below after a few
+        // attempts, so walk the chain on the attempt lengths alone (known from the flags), 64
+        // attempts at a time, then evaluate their checkSubset one per lane and settle passes,
+        // the wanted iteration and the 10000-rejection failure on the ballot of the 64 ----
+        while (!stop_all && produced < target) {
+            long long q = rel, pos_mine = 0;
+            int f_mine = 0, cnt = 0;
+            for (int j = 0; j < 64; ++j) {
+                if (q < lb || q >= lb + kFlagWin) refill(q & ~15LL);
+                int fi = win[q - lb];
+                if (fi == kFlagUnknown) {  // past the precomputed window: evaluate here (uniform)
+                    if (j > 0) break;
+                    fi = uni(attempt_flag(wbase + q, stream, slen, N, M, P));
+                }
+                if (fi == kAttemptSerial) {  // a very long redraw run or the stream end: alone
+                    if (j > 0) break;
+                    int idx[4] = {0, 0, 0, 0};
+                    const int len = uni(resolve_at(wbase + q, stream, slen, N, M, idx));
+                    if (len == 0) {  // RNG stream exhausted: report, never guess
+                        if (lane == 0) atomicOr(err, 1);
+                        S.fail_iter = -2;
+                        stop_all = true;
+                        break;
+                    }
+                    const float4 a = P[idx[0]], b = P[idx[1]], c = P[idx[2]], d = P[idx[3]];
+                    const float s4[8] = {a.x, a.y, b.x, b.y, c.x, c.y, d.x, d.y};
+                    const float t4[8] = {a.z, a.w, b.z, b.w, c.z, c.w, d.z, d.w};
+                    // as a flag: the length beyond 4 saturates the field; `len` is carried apart
+                    fi = (len == 4 ? 0 : 0x7E) | uni(check_subset(s4, t4) ? 1 : 0);
+                    if (lane == 0) { pos_mine = q; f_mine = fi; }
+                    q += len;
+                    cnt = 1;
+                    break;
+                }
+                if (lane == j) { pos_mine = q; f_mine = fi; }
+                q += 4 + ((fi & 0x7E) >> 1);
+                cnt = j + 1;
+            }
+            if (stop_all) break;
+            // checkSubset of the attempts whose pass bit is not known yet, one per lane
+            int pass = 0;
+            if (lane < cnt) {
+                if (f_mine & kPassUnknown) pass = attempt_flag(wbase + pos_mine, stream, slen, N, M, P) & 1;
+                else pass = f_mine & 1;
+            }
+            const unsigned long long Pm = __ballot(lane < cnt && pass);
+            const int need = target - produced;
+            const int a_p = Pm ? ctz64(Pm) : cnt;  // first pass
+            const int af = fail_run + a_p >= 10000 ? 10000 - fail_run - 1 : BIG;  // the 10000th rejection
+            int at = BIG;  // attempt completing the chunk's last wanted iteration
+            if (__popcll(Pm) >= need) {
+                unsigned long long m = Pm;
+                for (int k = 1; k < need; ++k) m &= m - 1;
+                at = ctz64(m);
+            }
+            int stop = cnt - 1, got = __popcll(Pm);
+            bool hit_t = false, hit_f = false;
+            if (af < BIG) { stop = af; hit_f = true; got = 0; }
+            else if (at < BIG) { stop = at; hit_t = true; got = need; }
+            if (pass && lane <= stop && !hit_f) {
+                const int rank = mbcnt64(Pm);
+                out[produced + rank] = make_int4((int)(wbase + pos_mine), (f_mine & 0x7E) ? -2 : -1, 0, 0);
+            }
+            produced += got;
+            fail_run = hit_t ? 0 : (hit_f ? 10000 : (Pm ? cnt - 1 - (63 - clz64(Pm)) : fail_run + cnt));
+            // next attempt: after `stop` (the walk's end when stop is the last one)
+            if (stop == cnt - 1) {
+                rel = uni64(q);
+            } else {
+                const long long ps = uni64(__shfl(pos_mine, stop));
+                const int fs = uni(__shfl(f_mine, stop));
+                rel = ps + 4 + ((fs & 0x7E) >> 1);
+            }
+            if (hit_f) {
+                S.fail_iter = produced;  // getSubset returned false in this iteration
+                stop_all = true;
+            }
+            if (hit_t) stop_all = true;
+        }
+    }
     while (!stop_all && produced < target) {
         const long long wb = rel & ~15LL;
-        if (wb < lb || wb + 1024 > lb + kFlagWin) {  // refill the LDS window at wb
-            lb = wb;
-            __syncthreads();
-#pragma unroll 4
-            for (int j = 0; j < kFlagWin / 1024; ++j) {
-                const long long r0 = lb + 16LL * (lane + 64 * j);
-                uint4 v;
-                if (r0 + 16 <= wlen) {
-                    v = *reinterpret_cast<const uint4*>(F + r0);
-                } else {
-                    uint32_t w4[4];
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) {
-                        uint32_t w = 0;
-                        for (int b = 0; b < 4; ++b) {
-                            const long long r = r0 + 4 * k + b;
-                            w |= (uint32_t)(r < wlen ? F[r] : kFlagUnknown) << (8 * b);
-                        }
-                        w4[k] = w;
-                    }
-                    v = make_uint4(w4[0], w4[1], w4[2], w4[3]);
-                }
-                *reinterpret_cast<uint4*>(win + 16 * (lane + 64 * j)) = v;
-            }
-            __syncthreads();
-        }
+        if (wb < lb || wb + 1024 > lb + kFlagWin) refill(wb);  // refill the LDS window at wb
         const uint4 w = *reinterpret_cast<const uint4*>(win + (wb - lb) + 16 * lane);
         const uint32_t wd[4] = {w.x, w.y, w.z, w.w};
         long long s = rel;  // chain position inside [wb, wb + 1024)

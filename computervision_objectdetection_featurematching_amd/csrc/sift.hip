@@ -39,7 +39,6 @@ constexpr int kBorder = 5;
 constexpr int kOriBins = 36;
 constexpr int kDW = 4, kDB = 8;
 constexpr int kHistLen = (kDW + 2) * (kDW + 2) * (kDB + 2);  // 360
-constexpr int kDescrThreads = 32;                             // threads (keypoints) per descriptor block
 
 __device__ __forceinline__ int reflect101(int p, int len) {
     if (len == 1) return 0;
@@ -223,10 +222,15 @@ __device__ __forceinline__ bool solve3(const float* H, const float* b, float* x)
     return true;
 }
 
-// adjustLocalExtrema + calcOrientationHist + the peak loop of findScaleSpaceExtrema, one thread per
-// candidate; keypoints in the doubled image's coordinates (octave field packed as OpenCV's)
+struct Surv {  // an extremum that passed adjustLocalExtrema: its keypoint (angle 0) and DoG position
+    mim_keypoint k;
+    int r, c, layer;
+};
+
+// adjustLocalExtrema (<= 5 Newton steps, contrast and edge tests), one thread per candidate; the
+// survivors go to orient_kernel (octave field packed as OpenCV's)
 __global__ void refine_kernel(const Pyr* __restrict__ pyr, const Cand* __restrict__ cand, const int* __restrict__ n_cand,
-                              int cap, mim_keypoint* __restrict__ kp, int* __restrict__ n_kp, int kp_cap) {
+                              int cap, Surv* __restrict__ surv, int* __restrict__ n_surv, int surv_cap) {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= min(*n_cand, cap)) return;
     const float kSigma = 1.6f, kContrast = 0.04f, kEdge = 10.f;
@@ -286,31 +290,62 @@ __global__ void refine_kernel(const Pyr* __restrict__ pyr, const Cand* __restric
     k.response = fabsf(contr);
     k.angle = 0;
 
-    // calcOrientationHist on the Gaussian layer, pixel order
-    const Layer g = pyr->gauss[octv][layer];
+    const int slot = atomicAdd(n_surv, 1);
+    if (slot < surv_cap) surv[slot] = Surv{k, r, c, layer};
+}
+
+// calcOrientationHist + the peak loop of findScaleSpaceExtrema, one wave per surviving extremum.  The
+// 36 bins accumulate in the reference's pixel order: per batch of 64 patch pixels each lane computes
+// one pixel's (bin, weight * magnitude), then the lanes walk the batch in order and lane b adds the
+// values of bin b (one bin per pixel: no reordering).  Keypoints in the doubled image's coordinates.
+__global__ __launch_bounds__(64) void orient_kernel(const Pyr* __restrict__ pyr, const Surv* __restrict__ surv,
+                                                    const int* __restrict__ n_surv, int surv_cap,
+                                                    mim_keypoint* __restrict__ kp, int* __restrict__ n_kp, int kp_cap) {
+    __shared__ int rb[64];
+    __shared__ float rv[64];
+    __shared__ float th[kOriBins + 4];
+    const int t = blockIdx.x, lane = threadIdx.x;
+    if (t >= min(*n_surv, surv_cap)) return;
+    const Surv sv = surv[t];
+    mim_keypoint k = sv.k;
+    const int octv = k.octave & 255;
+    const Layer g = pyr->gauss[octv][sv.layer];
     const float scl_octv = k.size * 0.5f / (1 << octv);
     const int radius = cv_round(4.5f * scl_octv);
     const float sigma = 1.5f * scl_octv;
     const float expf_scale = -1.f / (2.f * sigma * sigma);
-    float th[kOriBins + 4];
-    for (int b = 0; b < kOriBins + 4; ++b) th[b] = 0.f;
-    for (int ii = -radius; ii <= radius; ii++) {
-        const int y = r + ii;
-        if (y <= 0 || y >= g.rows - 1) continue;
-        for (int j = -radius; j <= radius; j++) {
-            const int x = c + j;
-            if (x <= 0 || x >= g.cols - 1) continue;
-            const float dx = AT(g, y, x + 1) - AT(g, y, x - 1);
-            const float dy = AT(g, y - 1, x) - AT(g, y + 1, x);
-            const float w = (float)exp((double)((float)(ii * ii + j * j) * expf_scale));
-            const float ori = fast_atan2(dy, dx);
-            const float mag = sqrtf(dx * dx + dy * dy);
-            int bin = cv_round((kOriBins / 360.f) * ori);
-            if (bin >= kOriBins) bin -= kOriBins;
-            if (bin < 0) bin += kOriBins;
-            th[bin + 2] += w * mag;
+    const int W = 2 * radius + 1, P = W * W;
+    float acc = 0.f;  // th[lane + 2] for lane < 36
+    for (int base = 0; base < P; base += 64) {
+        const int q = base + lane;
+        int bin = -1;
+        float val = 0.f;
+        if (q < P) {
+            const int ii = q / W - radius, j = q % W - radius;
+            const int y = sv.r + ii, x = sv.c + j;
+            if (y > 0 && y < g.rows - 1 && x > 0 && x < g.cols - 1) {
+                const float dx = AT(g, y, x + 1) - AT(g, y, x - 1);
+                const float dy = AT(g, y - 1, x) - AT(g, y + 1, x);
+                const float w = (float)exp((double)((float)(ii * ii + j * j) * expf_scale));
+                const float ori = fast_atan2(dy, dx);
+                const float mag = sqrtf(dx * dx + dy * dy);
+                bin = cv_round((kOriBins / 360.f) * ori);
+                if (bin >= kOriBins) bin -= kOriBins;
+                if (bin < 0) bin += kOriBins;
+                val = w * mag;
+            }
         }
+        rb[lane] = bin;
+        rv[lane] = val;
+        __syncthreads();
+        const int m = min(64, P - base);
+        for (int i = 0; i < m; ++i)
+            if (rb[i] == lane) acc += rv[i];
+        __syncthreads();
     }
+    if (lane < kOriBins) th[lane + 2] = acc;
+    __syncthreads();
+    if (lane != 0) return;
     th[1] = th[kOriBins + 1];
     th[0] = th[kOriBins];
     th[kOriBins + 2] = th[2];
@@ -335,14 +370,23 @@ __global__ void refine_kernel(const Pyr* __restrict__ pyr, const Cand* __restric
     }
 }
 
-// calcSIFTDescriptor, one thread per keypoint, its 360-bin histogram in LDS; keypoints in input
-// coordinates (after the 1/2 rescale), octave field as OpenCV packs it
-__global__ __launch_bounds__(kDescrThreads) void descr_kernel(const Pyr* __restrict__ pyr, const mim_keypoint* __restrict__ kp,
-                                                              int n, float* __restrict__ desc) {
-    __shared__ float hbuf[kDescrThreads * kHistLen];
-    const int t = blockIdx.x * kDescrThreads + threadIdx.x;
+__device__ __forceinline__ int ctz64(unsigned long long m) { return __builtin_ctzll(m); }
+
+// calcSIFTDescriptor, one wave per keypoint (keypoints in input coordinates, octave field packed as
+// OpenCV's).  Every bin must receive its contributions in the reference's pixel order (row-major over
+// the patch), so the work splits in two per batch of 64 consecutive patch pixels:
+//   A  each lane computes one pixel's contribution (gradient, fastAtan2, the double-rounded exp
+//      weight, the trilinear split into 8 values) in its registers;
+//   B  the lanes walk the 64 pixels in order (v_readlane of each); lane L owns the bins b = L (mod 64) in registers (at
+//      most 6 of the 360), and a pixel's 8 target bins idx + {0, 1, 10, 11, 60, 61, 70, 71} are 8
+//      distinct lanes (the offsets are distinct mod 64), so each lane adds at most one value per pixel
+//      and every bin's sum runs in pixel order: the oracle's float sums, bit for bit.
+// The wrap, the 0.2 clamp and the x 512 normalisation then run on lane 0 in the reference's order.
+__global__ __launch_bounds__(64) void descr_kernel(const Pyr* __restrict__ pyr, const mim_keypoint* __restrict__ kp,
+                                                   int n, float* __restrict__ desc) {
+    __shared__ float hist[kHistLen];
+    const int t = blockIdx.x, lane = threadIdx.x;
     if (t >= n) return;
-    float* hist = hbuf + threadIdx.x * kHistLen;
     const mim_keypoint p = kp[t];
     int octave = p.octave & 255;
     const int layer = (p.octave >> 8) & 255;
@@ -362,48 +406,92 @@ __global__ __launch_bounds__(kDescrThreads) void descr_kernel(const Pyr* __restr
     if (radius > rmax) radius = rmax;
     cos_t /= hist_width;
     sin_t /= hist_width;
-    for (int b = 0; b < kHistLen; ++b) hist[b] = 0.f;
-    for (int i = -radius; i <= radius; i++)
-        for (int j = -radius; j <= radius; j++) {
-            const float c_rot = j * cos_t - i * sin_t, r_rot = j * sin_t + i * cos_t;
-            float rbin = r_rot + kDW / 2 - 0.5f, cbin = c_rot + kDW / 2 - 0.5f;
-            const int r = py + i, c = px + j;
-            if (!(rbin > -1 && rbin < kDW && cbin > -1 && cbin < kDW && r > 0 && r < im.rows - 1 && c > 0 && c < im.cols - 1))
-                continue;
-            const float dx = AT(im, r, c + 1) - AT(im, r, c - 1), dy = AT(im, r - 1, c) - AT(im, r + 1, c);
-            const float w = (float)exp((double)((c_rot * c_rot + r_rot * r_rot) * exp_scale));
-            const float o = fast_atan2(dy, dx), m = sqrtf(dx * dx + dy * dy);
-            float obin = (o - ori) * bins_per_rad;
-            const float mag = m * w;
-            const int r0 = (int)floorf(rbin), c0 = (int)floorf(cbin);
-            int o0 = (int)floorf(obin);
-            rbin -= r0;
-            cbin -= c0;
-            obin -= o0;
-            if (o0 < 0) o0 += kDB;
-            if (o0 >= kDB) o0 -= kDB;
-            const float v_r1 = mag * rbin, v_r0 = mag - v_r1;
-            const float v_rc11 = v_r1 * cbin, v_rc10 = v_r1 - v_rc11, v_rc01 = v_r0 * cbin, v_rc00 = v_r0 - v_rc01;
-            const float v_rco111 = v_rc11 * obin, v_rco110 = v_rc11 - v_rco111, v_rco101 = v_rc10 * obin, v_rco100 = v_rc10 - v_rco101;
-            const float v_rco011 = v_rc01 * obin, v_rco010 = v_rc01 - v_rco011, v_rco001 = v_rc00 * obin, v_rco000 = v_rc00 - v_rco001;
-            const int idx = ((r0 + 1) * (kDW + 2) + c0 + 1) * (kDB + 2) + o0;
-            hist[idx] += v_rco000;
-            hist[idx + 1] += v_rco001;
-            hist[idx + (kDB + 2)] += v_rco010;
-            hist[idx + (kDB + 3)] += v_rco011;
-            hist[idx + (kDW + 2) * (kDB + 2)] += v_rco100;
-            hist[idx + (kDW + 2) * (kDB + 2) + 1] += v_rco101;
-            hist[idx + (kDW + 3) * (kDB + 2)] += v_rco110;
-            hist[idx + (kDW + 3) * (kDB + 2) + 1] += v_rco111;
+    const int W = 2 * radius + 1;
+    const int P = W * W;
+    float h[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // bins lane + 64 s
+#ifdef MIM_SIFT_PROF
+    long long ta = 0, tb = 0, t0 = clock64();
+#endif
+    for (int base = 0; base < P; base += 64) {
+        // ---- A: pixel base + lane: its bin index and the 4 factors of its trilinear split ----
+        int idx = -1;
+        float mag = 0.f, rb = 0.f, cb = 0.f, ob = 0.f;
+        {
+            const int q = base + lane;
+            if (q < P) {
+                const int i = q / W - radius, j = q % W - radius;
+                const float c_rot = j * cos_t - i * sin_t, r_rot = j * sin_t + i * cos_t;
+                float rbin = r_rot + kDW / 2 - 0.5f, cbin = c_rot + kDW / 2 - 0.5f;
+                const int r = py + i, c = px + j;
+                if (rbin > -1 && rbin < kDW && cbin > -1 && cbin < kDW && r > 0 && r < im.rows - 1 && c > 0 &&
+                    c < im.cols - 1) {
+                    const float dx = AT(im, r, c + 1) - AT(im, r, c - 1), dy = AT(im, r - 1, c) - AT(im, r + 1, c);
+                    const float w = (float)exp((double)((c_rot * c_rot + r_rot * r_rot) * exp_scale));
+                    const float o = fast_atan2(dy, dx), m = sqrtf(dx * dx + dy * dy);
+                    float obin = (o - ori) * bins_per_rad;
+                    mag = m * w;
+                    const int r0 = (int)floorf(rbin), c0 = (int)floorf(cbin);
+                    int o0 = (int)floorf(obin);
+                    rb = rbin - r0;
+                    cb = cbin - c0;
+                    ob = obin - o0;
+                    if (o0 < 0) o0 += kDB;
+                    if (o0 >= kDB) o0 -= kDB;
+                    idx = ((r0 + 1) * (kDW + 2) + c0 + 1) * (kDB + 2) + o0;
+                }
+            }
         }
+#ifdef MIM_SIFT_PROF
+        const long long t1 = clock64(); ta += t1 - t0; t0 = t1;
+#endif
+        // ---- B: the batch's contributing pixels in order (v_readlane of each, no memory round trip);
+        // lane L owns the bins = L (mod 64): among idx + {0, 1, 10, 11, 60, 61, 70, 71} that is
+        // d = (L - idx) mod 64 in {0, 1, 10, 11, 60, 61, 6, 7} (mask 0x3000000000000CC3), offset d or
+        // d + 64, value k = (r, c, o) bits of the offset; the lane recomputes its value from the 4
+        // factors with the reference's own operations (v_r1 = mag rbin, v_r0 = mag - v_r1, ...) ----
+        for (unsigned long long vm = __ballot(idx >= 0); vm; vm &= vm - 1) {
+            const int q = ctz64(vm);
+            const int iq = __builtin_amdgcn_readlane(idx, q);
+            const int d = (lane - iq) & 63;
+            const float smag = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mag), q));
+            const float srb = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(rb), q));
+            const float scb = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cb), q));
+            const float sob = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ob), q));
+            if ((0x3000000000000CC3ull >> d) & 1ull) {
+                const int off = (d == 6 || d == 7) ? d + 64 : d;
+                const bool kr = off >= 60, kc = (kr ? off - 60 : off) >= 10, ko = off & 1;
+                const float v_r1 = smag * srb, v_r0 = smag - v_r1;
+                const float rr = kr ? v_r1 : v_r0;
+                const float rc1 = rr * scb, rc0 = rr - rc1;
+                const float cc = kc ? rc1 : rc0;
+                const float co1 = cc * sob, co0 = cc - co1;
+                const float val = ko ? co1 : co0;
+                const int slot = (iq + off) >> 6;
+#pragma unroll
+                for (int s2 = 0; s2 < 6; ++s2)
+                    if (s2 == slot) h[s2] += val;
+            }
+        }
+#ifdef MIM_SIFT_PROF
+        const long long t2 = clock64(); tb += t2 - t0; t0 = t2;
+#endif
+    }
+#pragma unroll
+    for (int s2 = 0; s2 < 6; ++s2)
+        if (lane + 64 * s2 < kHistLen) hist[lane + 64 * s2] = h[s2];
+    __syncthreads();
+    if (lane != 0) return;
+#ifdef MIM_SIFT_PROF
+    const long long tt0 = clock64();
+#endif
     float* out = desc + (size_t)t * 128;
-    float nrm2 = 0;
     for (int i = 0; i < kDW; i++)
         for (int j = 0; j < kDW; j++) {
             const int idx = ((i + 1) * (kDW + 2) + (j + 1)) * (kDB + 2);
             hist[idx] += hist[idx + kDB];
             hist[idx + 1] += hist[idx + kDB + 1];
         }
+    float nrm2 = 0;
     for (int i = 0; i < kDW; i++)
         for (int j = 0; j < kDW; j++)
             for (int k = 0; k < kDB; k++) {
@@ -426,6 +514,9 @@ __global__ __launch_bounds__(kDescrThreads) void descr_kernel(const Pyr* __restr
                 const int v = cv_round(hist[((i + 1) * (kDW + 2) + (j + 1)) * (kDB + 2) + k] * nrm2);
                 out[(i * kDW + j) * kDB + k] = (float)(v < 0 ? 0 : (v > 255 ? 255 : v));
             }
+#ifdef MIM_SIFT_PROF
+    if (t % 512 == 0) printf("[descr] t=%d P=%d A=%lld B=%lld tail=%lld\n", t, P, ta, tb, (long long)clock64() - tt0);
+#endif
 }
 
 // ---- host ---------------------------------------------------------------------------------------
@@ -583,15 +674,17 @@ int sift_detect_compute(SiftWs* w, hipStream_t st, const uint8_t* img, int rows,
         for (int i = 0; i < kNOL + 2; ++i) h_pyr.dog[o][i] = Layer{P + doff[o] + i * plane, orows[o], ocols[o]};
     }
     const int cand_cap = 1 << 20, kp_cap = 1 << 19;
-    const size_t aux_bytes = sizeof(Pyr) + 256 + sizeof(Cand) * cand_cap + sizeof(mim_keypoint) * kp_cap;
+    const size_t aux_bytes = sizeof(Pyr) + 256 + sizeof(Cand) * cand_cap + sizeof(mim_keypoint) * kp_cap +
+                             sizeof(Surv) * cand_cap;
     SCHK(grow(w->aux, w->aux_cap, aux_bytes));
     char* A = (char*)w->aux;
     Pyr* d_pyr = (Pyr*)A;
-    int* d_cnt = (int*)(A + sizeof(Pyr));  // [0] candidates, [1] keypoints
+    int* d_cnt = (int*)(A + sizeof(Pyr));  // [0] candidates, [1] keypoints, [2] survivors of adjustLocalExtrema
     Cand* d_cand = (Cand*)(A + sizeof(Pyr) + 256);
     mim_keypoint* d_kp = (mim_keypoint*)(d_cand + cand_cap);
+    Surv* d_surv = (Surv*)(d_kp + kp_cap);
     SCHK(hipMemcpyAsync(d_pyr, &h_pyr, sizeof(Pyr), hipMemcpyHostToDevice, st));
-    SCHK(hipMemsetAsync(d_cnt, 0, 2 * sizeof(int), st));
+    SCHK(hipMemsetAsync(d_cnt, 0, 3 * sizeof(int), st));
     const int threshold = (int)floor(0.5 * 0.04 / kNOL * 255);
     for (int o = 0; o < n_oct; ++o) {
         if (orows[o] <= 2 * kBorder || ocols[o] <= 2 * kBorder) continue;
@@ -602,7 +695,11 @@ int sift_detect_compute(SiftWs* w, hipStream_t st, const uint8_t* img, int rows,
     SCHK(hipMemcpyAsync(h_cnt, d_cnt, sizeof(int), hipMemcpyDeviceToHost, st));
     SCHK(hipStreamSynchronize(st));
     if (h_cnt[0] > cand_cap) { err = "more than 2^20 SIFT candidates"; return -2; }
-    if (h_cnt[0] > 0) refine_kernel<<<(h_cnt[0] + 127) / 128, 128, 0, st>>>(d_pyr, d_cand, d_cnt, cand_cap, d_kp, d_cnt + 1, kp_cap);
+    if (h_cnt[0] > 0) {
+        refine_kernel<<<(h_cnt[0] + 127) / 128, 128, 0, st>>>(d_pyr, d_cand, d_cnt, cand_cap, d_surv, d_cnt + 2, cand_cap);
+        // survivors <= candidates: blocks past the survivor count return at once
+        orient_kernel<<<h_cnt[0], 64, 0, st>>>(d_pyr, d_surv, d_cnt + 2, cand_cap, d_kp, d_cnt + 1, kp_cap);
+    }
     SCHK(hipGetLastError());
     SCHK(hipMemcpyAsync(h_cnt + 1, d_cnt + 1, sizeof(int), hipMemcpyDeviceToHost, st));
     SCHK(hipStreamSynchronize(st));
@@ -638,7 +735,7 @@ int sift_detect_compute(SiftWs* w, hipStream_t st, const uint8_t* img, int rows,
     if (n <= 0) return 0;
     SCHK(hipMemcpyAsync(d_kp, k.data(), sizeof(mim_keypoint) * n, hipMemcpyHostToDevice, st));
     SCHK(grow(w->desc, w->desc_cap, sizeof(float) * 128 * (size_t)n));
-    descr_kernel<<<(n + kDescrThreads - 1) / kDescrThreads, kDescrThreads, 0, st>>>(d_pyr, d_kp, n, (float*)w->desc);
+    descr_kernel<<<n, 64, 0, st>>>(d_pyr, d_kp, n, (float*)w->desc);
     SCHK(hipGetLastError());
     SCHK(hipMemcpyAsync(desc, w->desc, sizeof(float) * 128 * (size_t)n, hipMemcpyDeviceToHost, st));
     SCHK(hipStreamSynchronize(st));

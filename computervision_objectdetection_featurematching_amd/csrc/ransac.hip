@@ -2899,9 +2899,6 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
         const int stop = max(S.niters, S.best_iter + 1);
         res.iters = (S.fail_iter >= 0 && S.fail_iter < stop) ? S.fail_iter : stop;
         if (ok) {
-#ifdef MIM_REFINE_PROF
-            const long long tp0 = clock64();
-#endif
             // bestModel = runKernel(sample[best_iter]) (bit-identical to the hypo kernel's)
             if (tid == 0 && !exact_all && best_h[(long long)p * 9 + 8] != 0.0) {
                 for (int i = 0; i < 9; ++i) sh.Hb[i] = best_h[(long long)p * 9 + i];  // from the exact pass
@@ -2947,9 +2944,6 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
             __syncthreads();
             const int k = sh.n_inl;
             if (k > 0) {
-#ifdef MIM_REFINE_PROF
-                const long long tp1 = clock64();
-#endif
                 // ---- refit: runKernel over all inliers, OpenCV's sequential sums (fundam.cpp) ----
                 if (tid < 4) {  // centroids cm (scene), cM (object): one sequential sum each
                     double c = 0;
@@ -2973,9 +2967,6 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                 }
                 __syncthreads();
                 const double cmx = sh.norm[0], cmy = sh.norm[1], cMx = sh.norm[2], cMy = sh.norm[3];
-#ifdef MIM_REFINE_PROF
-                const long long tq1 = clock64();
-#endif
                 const bool degenerate = fabs(sh.norm[4]) < DBL_EPSILON || fabs(sh.norm[5]) < DBL_EPSILON ||
                                         fabs(sh.norm[6]) < DBL_EPSILON || fabs(sh.norm[7]) < DBL_EPSILON;
                 if (!degenerate) {
@@ -3003,10 +2994,6 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                         sh.lt[tid] = acc;
                     }
                     __syncthreads();
-#ifdef MIM_REFINE_PROF
-                    const long long tq2 = clock64();
-                    if (tid == 0 && p < 2) printf("[refit] p=%d centroid=%lld ltl=%lld\n", p, tq1 - tp1, tq2 - tq1);
-#endif
                     const double invHnorm[9] = {1. / smx, 0, cmx, 0, 1. / smy, cmy, 0, 0, 1};
                     const double Hnorm2[9] = {sMx, 0, -cMx * sMx, 0, sMy, -cMy * sMy, 0, 0, 1};
                     if (tid < 16) {  // the Jacobi of runKernel, one 16-lane group (bit-identical)
@@ -3019,9 +3006,6 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                     for (int i = 0; i < 9; ++i) sh.H[i] = sh.Hb[i];  // runKernel returned 0: H kept
                 }
                 __syncthreads();
-#ifdef MIM_REFINE_PROF
-                const long long tp2 = clock64();
-#endif
                 // ---- LMSolverImpl (levmarq.cpp) on H8 = H[0..7], maxIters 10, eps FLT_EPSILON ----
                 if (tid < 8) sh.x[tid] = sh.H[tid];
                 __syncthreads();
@@ -3038,9 +3022,6 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                 }
                 __syncthreads();
                 int iter = 0;
-#ifdef MIM_REFINE_PROF
-                long long tsolve = 0, tcost = 0, tupd = 0, tnorm = 0, tl0 = clock64();
-#endif
                 for (;;) {
                     if (tid < 16) {  // the step solve on one 16-lane group (group Jacobi)
                         for (int i = tid; i < 64; i += 16) sh.Ap[i] = (i % 9) == 0 ? sh.A[i] + sh.lambda * sh.D[i / 9] : sh.A[i];
@@ -3060,15 +3041,9 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                         }
                     }
                     __syncthreads();
-#ifdef MIM_REFINE_PROF
-                    const long long tl1 = clock64(); tsolve += tl1 - tl0;
-#endif
                     double xd[8];
                     for (int i = 0; i < 8; ++i) xd[i] = sh.xd[i];
                     const double Sd = lm_cost(X, k, xd, sh.lm, sh.red);
-#ifdef MIM_REFINE_PROF
-                    const long long tl2 = clock64(); tcost += tl2 - tl1;
-#endif
                     if (tid < 16) {  // every slot evaluates the same update; slot 0 stores it
                         const double Rlo = 0.25, Rhi = 0.75;
                         double lambda = sh.lambda, lc = sh.lc;
@@ -3108,9 +3083,6 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                         }
                     }
                     __syncthreads();
-#ifdef MIM_REFINE_PROF
-                    const long long tl3 = clock64(); tupd += tl3 - tl2;
-#endif
                     if (sh.accept) {
                         for (int i = 0; i < 8; ++i) x[i] = sh.x[i];
                         lm_normal(X, k, x, sh.lm, sh.red, sh.nrm, rinf);
@@ -3122,9 +3094,6 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                             sh.rinf = rinf;
                         }
                     }
-#ifdef MIM_REFINE_PROF
-                    tl0 = clock64(); tnorm += tl0 - tl3;
-#endif
                     ++iter;
                     if (tid == 0) sh.proceed = iter < 10 && sh.dinf >= FLT_EPSILON && sh.rinf >= FLT_EPSILON;
                     __syncthreads();
@@ -3132,11 +3101,6 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                     __syncthreads();
                     if (!proceed) break;
                 }
-#ifdef MIM_REFINE_PROF
-                if (tid == 0 && p < 4)
-                    printf("[refine] p=%d ng=%d k=%d lm_iters=%d compact=%lld refit=%lld lm=%lld solve=%lld cost=%lld upd=%lld norm=%lld\n",
-                           p, ng, k, iter, tp1 - tp0, tp2 - tp1, (long long)clock64() - tp2, tsolve, tcost, tupd, tnorm);
-#endif
                 if (tid < 8) sh.H[tid] = sh.x[tid];
                 __syncthreads();
             } else if (tid == 0) {

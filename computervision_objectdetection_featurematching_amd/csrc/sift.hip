@@ -409,9 +409,6 @@ __global__ __launch_bounds__(64) void descr_kernel(const Pyr* __restrict__ pyr, 
     const int W = 2 * radius + 1;
     const int P = W * W;
     float h[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // bins lane + 64 s
-#ifdef MIM_SIFT_PROF
-    long long ta = 0, tb = 0, t0 = clock64();
-#endif
     for (int base = 0; base < P; base += 64) {
         // ---- A: pixel base + lane: its bin index and the 4 factors of its trilinear split ----
         int idx = -1;
@@ -441,9 +438,6 @@ __global__ __launch_bounds__(64) void descr_kernel(const Pyr* __restrict__ pyr, 
                 }
             }
         }
-#ifdef MIM_SIFT_PROF
-        const long long t1 = clock64(); ta += t1 - t0; t0 = t1;
-#endif
         // ---- B: the batch's contributing pixels in order (v_readlane of each, no memory round trip);
         // lane L owns the bins = L (mod 64): among idx + {0, 1, 10, 11, 60, 61, 70, 71} that is
         // d = (L - idx) mod 64 in {0, 1, 10, 11, 60, 61, 6, 7} (mask 0x3000000000000CC3), offset d or
@@ -472,18 +466,12 @@ __global__ __launch_bounds__(64) void descr_kernel(const Pyr* __restrict__ pyr, 
                     if (s2 == slot) h[s2] += val;
             }
         }
-#ifdef MIM_SIFT_PROF
-        const long long t2 = clock64(); tb += t2 - t0; t0 = t2;
-#endif
     }
 #pragma unroll
     for (int s2 = 0; s2 < 6; ++s2)
         if (lane + 64 * s2 < kHistLen) hist[lane + 64 * s2] = h[s2];
     __syncthreads();
     if (lane != 0) return;
-#ifdef MIM_SIFT_PROF
-    const long long tt0 = clock64();
-#endif
     float* out = desc + (size_t)t * 128;
     for (int i = 0; i < kDW; i++)
         for (int j = 0; j < kDW; j++) {
@@ -514,9 +502,6 @@ __global__ __launch_bounds__(64) void descr_kernel(const Pyr* __restrict__ pyr, 
                 const int v = cv_round(hist[((i + 1) * (kDW + 2) + (j + 1)) * (kDB + 2) + k] * nrm2);
                 out[(i * kDW + j) * kDB + k] = (float)(v < 0 ? 0 : (v > 255 ? 255 : v));
             }
-#ifdef MIM_SIFT_PROF
-    if (t % 512 == 0) printf("[descr] t=%d P=%d A=%lld B=%lld tail=%lld\n", t, P, ta, tb, (long long)clock64() - tt0);
-#endif
 }
 
 // ---- host ---------------------------------------------------------------------------------------

@@ -2607,56 +2607,20 @@ __global__ __launch_bounds__(64) void ransac_select_kernel(RansacState* __restri
 // ------------------------------------------------------------------------------------------------
 // refine: best mask, refit DLT + LM on the inliers, gates (TestsDetector.cpp:74-84)
 // ------------------------------------------------------------------------------------------------
-constexpr int kRT = 256;  // refine block
+constexpr int kRW = 4;        // refine: problems (waves) per block
+constexpr int kRT = 64 * kRW;  // refine block
 
-// deterministic block sum of K doubles (wave shuffles, then the 4 wave partials in order)
-template <int K>
-__device__ void block_sum(double (&v)[K], double* red) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-        double x = v[k];
-#pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) x += __shfl_xor(x, off);
-        v[k] = x;
-    }
-    __syncthreads();
-    if (lane == 0)
-#pragma unroll
-        for (int k = 0; k < K; ++k) red[wave * K + k] = v[k];
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < K; ++k) v[k] = ((red[k] + red[K + k]) + red[2 * K + k]) + red[3 * K + k];
-    __syncthreads();
+// LDS visibility between the lanes of one wave (the refine runs one problem per wave)
+__device__ __forceinline__ void wsync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-__device__ double block_max(double x, double* red) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+__device__ __forceinline__ double wave_max_d(double x) {
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) x = fmax(x, __shfl_xor(x, off));
-    __syncthreads();
-    if (lane == 0) red[wave] = x;
-    __syncthreads();
-    x = fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
-    __syncthreads();
     return x;
-}
-
-// HomographyRefineCallback::compute for one point: residuals and (optionally) the Jacobian rows
-__device__ __forceinline__ void refine_point(const double* h, double Mx, double My, double mx, double my,
-                                             double& ex, double& ey, double* Jx, double* Jy) {
-    double ww = h[6] * Mx + h[7] * My + 1.;
-    ww = fabs(ww) > DBL_EPSILON ? 1. / ww : 0;
-    const double xi = (h[0] * Mx + h[1] * My + h[2]) * ww;
-    const double yi = (h[3] * Mx + h[4] * My + h[5]) * ww;
-    ex = xi - mx;
-    ey = yi - my;
-    if (Jx) {
-        Jx[0] = Mx * ww; Jx[1] = My * ww; Jx[2] = ww; Jx[3] = Jx[4] = Jx[5] = 0.;
-        Jx[6] = -Mx * ww * xi; Jx[7] = -My * ww * xi;
-        Jy[0] = Jy[1] = Jy[2] = 0.; Jy[3] = Mx * ww; Jy[4] = My * ww; Jy[5] = ww;
-        Jy[6] = -Mx * ww * yi; Jy[7] = -My * ww * yi;
-    }
 }
 
 // ---- LM sums in OpenCV's order ------------------------------------------------------------------
@@ -2678,7 +2642,7 @@ struct LmStage {
 // thread's max |residual|
 __device__ double lm_stage(const float4* __restrict__ X, int c0, int n, const double* h, LmStage& L, bool jac) {
     double mx = 0;
-    for (int i = threadIdx.x; i < n; i += kRT) {
+    for (int i = threadIdx.x & 63; i < n; i += 64) {
         const float4 q = X[c0 + i];
         const double Mx = q.x, My = q.y;
         double ww = h[6] * Mx + h[7] * My + 1.;
@@ -2704,9 +2668,9 @@ __device__ double lm_stage(const float4* __restrict__ X, int c0, int n, const do
 // A = J^T J, v = J^T r, S = |r|^2 as the 45 entries (a, b), a <= b <= 8, of [J r]^T [J r] (column 8
 // = r): out[e] in the packing order A upper (36), v (8), S; each entry one lane's sequential sum over
 // the rows (x row, then y row, point by point).  rinf = |r|_inf.
-__device__ void lm_normal(const float4* __restrict__ X, int n, const double* h, LmStage& L, double* red,
+__device__ void lm_normal(const float4* __restrict__ X, int n, const double* h, LmStage& L,
                           double* out, double& rinf) {
-    const int e = threadIdx.x;
+    const int e = threadIdx.x & 63;
     int a = 8, b = 8;  // e == 44: S
     if (e < 36) {      // (a, b), b >= a, row-major upper triangle of A
         a = 0;
@@ -2719,9 +2683,9 @@ __device__ void lm_normal(const float4* __restrict__ X, int n, const double* h, 
     double acc = 0, mx = 0;
     for (int c0 = 0; c0 < n; c0 += kLmChunk) {
         const int m = min(kLmChunk, n - c0);
-        __syncthreads();
+        wsync();
         mx = fmax(mx, lm_stage(X, c0, m, h, L, true));
-        __syncthreads();
+        wsync();
         if (e < 45) {
 #pragma unroll 4
             for (int i = 0; i < m; ++i) {
@@ -2733,7 +2697,8 @@ __device__ void lm_normal(const float4* __restrict__ X, int n, const double* h, 
         }
     }
     if (e < 45) out[e] = acc;
-    rinf = block_max(mx, red);  // max is order-free; block_max synchronises
+    rinf = wave_max_d(mx);  // max is order-free
+    wsync();
 }
 
 // S(h) = |r(h)|^2, sequential over the rows
@@ -2741,10 +2706,10 @@ __device__ double lm_cost(const float4* __restrict__ X, int n, const double* h, 
     double acc = 0;
     for (int c0 = 0; c0 < n; c0 += kLmChunk) {
         const int m = min(kLmChunk, n - c0);
-        __syncthreads();
+        wsync();
         lm_stage(X, c0, m, h, L, false);
-        __syncthreads();
-        if (threadIdx.x == 0)
+        wsync();
+        if ((threadIdx.x & 63) == 0)
 #pragma unroll 8
             for (int i = 0; i < m; ++i) {
                 const double ex = L.rx[i * kLmRow + 8], ey = L.ry[i * kLmRow + 8];
@@ -2752,10 +2717,10 @@ __device__ double lm_cost(const float4* __restrict__ X, int n, const double* h, 
                 acc += ey * ey;
             }
     }
-    if (threadIdx.x == 0) red[0] = acc;
-    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[0] = acc;
+    wsync();
     const double r = red[0];
-    __syncthreads();
+    wsync();
     return r;
 }
 
@@ -2833,8 +2798,8 @@ __device__ double inv_diag_max8(const double* A, double* J) {
     return maxval;
 }
 
-struct RefineShared {
-    double red[4 * 45];
+struct RefineShared {  // one per wave (problem)
+    double red[2];
     double lt[45];
     double nrm[45];       // LM sums: A upper (36), v (8), S
     LmStage lm;
@@ -2844,7 +2809,6 @@ struct RefineShared {
     double S, Sd, rinf, dinf, lambda, lc;
     double J9[kJ9D];
     int flag, n_inl, proceed, accept;
-    int wcnt[4];
 };
 
 __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* __restrict__ st,
@@ -2855,9 +2819,15 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                                                             const uint32_t* __restrict__ stream,
                                                             float4* __restrict__ inl, uint8_t* __restrict__ masks,
                                                             mim_result* __restrict__ results, RansacParams prm,
-                                                            int raw, const double* __restrict__ best_h, int exact_all) {
-    __shared__ RefineShared sh;
-    const int p = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+                                                            int raw, const double* __restrict__ best_h, int exact_all,
+                                                            int n_probs) {
+    // one problem per wave: kRW problems per block, so the latency-bound refine holds few CUs'
+    // registers and LDS while the next batches' distance and bound kernels fill the GPU
+    __shared__ RefineShared shs[kRW];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = lane;
+    const int p = blockIdx.x * kRW + wave;
+    if (p >= n_probs) return;
+    RefineShared& sh = shs[wave];
     const RansacState S = st[p];
     const int ng = n_good_arr[p];
     const long long go = probs[p].good_off;
@@ -2887,7 +2857,7 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                 for (int i = 0; i < 9; ++i) sh.H[i] = Hl[i];
             }
         }
-        __syncthreads();
+        wsync();
         ok = sh.flag;
         if (tid < 4) mask[tid] = ok ? 1 : 0;
         sh.n_inl = ok ? 4 : 0;
@@ -2913,13 +2883,13 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                 if (tid == 0)
                     for (int i = 0; i < 9; ++i) sh.Hb[i] = Hl[i];
             }
-            __syncthreads();
+            wsync();
             float Hf[8];
             for (int i = 0; i < 8; ++i) Hf[i] = (float)sh.Hb[i];
             const float thr2 = (float)(prm.thresh * prm.thresh);
             // best mask + ordered compaction of the inliers (compressElems)
             int base = 0;
-            for (int b0 = 0; b0 < ng; b0 += kRT) {
+            for (int b0 = 0; b0 < ng; b0 += 64) {
                 const int i = b0 + tid;
                 bool in = false;
                 float4 q = make_float4(0, 0, 0, 0);
@@ -2931,17 +2901,11 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                 const unsigned long long bal = __ballot(in);
                 const int within = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
                                                              __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0));
-                if (lane == 0) sh.wcnt[wave] = __popcll(bal);
-                __syncthreads();
-                int wb = 0;
-                for (int w = 0; w < wave; ++w) wb += sh.wcnt[w];
-                const int tot = sh.wcnt[0] + sh.wcnt[1] + sh.wcnt[2] + sh.wcnt[3];
-                if (in) X[base + wb + within] = q;
-                base += tot;
-                __syncthreads();
+                if (in) X[base + within] = q;
+                base += __popcll(bal);
             }
             if (tid == 0) sh.n_inl = base;
-            __syncthreads();
+            wsync();
             const int k = sh.n_inl;
             if (k > 0) {
                 // ---- refit: runKernel over all inliers, OpenCV's sequential sums (fundam.cpp) ----
@@ -2954,7 +2918,7 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                     }
                     sh.norm[tid] = c / k;
                 }
-                __syncthreads();
+                wsync();
                 if (tid < 4) {  // mean absolute deviations
                     const double c = sh.norm[tid];
                     double sd = 0;
@@ -2965,7 +2929,7 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                     }
                     sh.norm[4 + tid] = sd;
                 }
-                __syncthreads();
+                wsync();
                 const double cmx = sh.norm[0], cmy = sh.norm[1], cMx = sh.norm[2], cMy = sh.norm[3];
                 const bool degenerate = fabs(sh.norm[4]) < DBL_EPSILON || fabs(sh.norm[5]) < DBL_EPSILON ||
                                         fabs(sh.norm[6]) < DBL_EPSILON || fabs(sh.norm[7]) < DBL_EPSILON;
@@ -2993,7 +2957,7 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                         }
                         sh.lt[tid] = acc;
                     }
-                    __syncthreads();
+                    wsync();
                     const double invHnorm[9] = {1. / smx, 0, cmx, 0, 1. / smy, cmy, 0, 0, 1};
                     const double Hnorm2[9] = {sMx, 0, -cMx * sMx, 0, sMy, -cMy * sMy, 0, 0, 1};
                     if (tid < 16) {  // the Jacobi of runKernel, one 16-lane group (bit-identical)
@@ -3005,14 +2969,14 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                 } else if (tid == 0) {
                     for (int i = 0; i < 9; ++i) sh.H[i] = sh.Hb[i];  // runKernel returned 0: H kept
                 }
-                __syncthreads();
+                wsync();
                 // ---- LMSolverImpl (levmarq.cpp) on H8 = H[0..7], maxIters 10, eps FLT_EPSILON ----
                 if (tid < 8) sh.x[tid] = sh.H[tid];
-                __syncthreads();
+                wsync();
                 double x[8];
                 for (int i = 0; i < 8; ++i) x[i] = sh.x[i];
                 double rinf;
-                lm_normal(X, k, x, sh.lm, sh.red, sh.nrm, rinf);
+                lm_normal(X, k, x, sh.lm, sh.nrm, rinf);
                 if (tid == 0) {
                     int e = 0;
                     for (int a = 0; a < 8; ++a)
@@ -3020,7 +2984,7 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                     for (int i = 0; i < 8; ++i) { sh.v[i] = sh.nrm[36 + i]; sh.D[i] = sh.A[9 * i]; }
                     sh.S = sh.nrm[44]; sh.rinf = rinf; sh.lambda = 1; sh.lc = 0.75;
                 }
-                __syncthreads();
+                wsync();
                 int iter = 0;
                 for (;;) {
                     if (tid < 16) {  // the step solve on one 16-lane group (group Jacobi)
@@ -3040,7 +3004,7 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                             sh.dinf = dinf;
                         }
                     }
-                    __syncthreads();
+                    wsync();
                     double xd[8];
                     for (int i = 0; i < 8; ++i) xd[i] = sh.xd[i];
                     const double Sd = lm_cost(X, k, xd, sh.lm, sh.red);
@@ -3082,10 +3046,10 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                             }
                         }
                     }
-                    __syncthreads();
+                    wsync();
                     if (sh.accept) {
                         for (int i = 0; i < 8; ++i) x[i] = sh.x[i];
-                        lm_normal(X, k, x, sh.lm, sh.red, sh.nrm, rinf);
+                        lm_normal(X, k, x, sh.lm, sh.nrm, rinf);
                         if (tid == 0) {
                             int e = 0;
                             for (int a = 0; a < 8; ++a)
@@ -3096,23 +3060,23 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                     }
                     ++iter;
                     if (tid == 0) sh.proceed = iter < 10 && sh.dinf >= FLT_EPSILON && sh.rinf >= FLT_EPSILON;
-                    __syncthreads();
+                    wsync();
                     const bool proceed = sh.proceed;
-                    __syncthreads();
+                    wsync();
                     if (!proceed) break;
                 }
                 if (tid < 8) sh.H[tid] = sh.x[tid];
-                __syncthreads();
+                wsync();
             } else if (tid == 0) {
                 for (int i = 0; i < 9; ++i) sh.H[i] = sh.Hb[i];
             }
-            __syncthreads();
+            wsync();
         } else {
-            for (int i = tid; i < ng; i += kRT) mask[i] = 0;
+            for (int i = tid; i < ng; i += 64) mask[i] = 0;
             if (tid == 0) sh.n_inl = 0;
         }
     }
-    __syncthreads();
+    wsync();
     if (tid != 0) return;
     res.n_inl = ok ? sh.n_inl : 0;
     if (!ok) {
@@ -3290,8 +3254,8 @@ void ransac_enqueue(const RansacParams& prm, int n_probs, const ProbDev* probs, 
         c0 = c1;
         chunk = 1 << 30;  // one chunk after the first: every chunk costs a latency-bound exact pass
     }
-    ransac_refine_kernel<<<n_probs, kRT, 0, s>>>(b.state, probs, pts, n_good, b.samples, b.stream, b.inl, masks, results, prm,
-                                                 raw, b.best_h, exact_all);
+    ransac_refine_kernel<<<(n_probs + kRW - 1) / kRW, kRT, 0, s>>>(b.state, probs, pts, n_good, b.samples, b.stream, b.inl,
+                                                                  masks, results, prm, raw, b.best_h, exact_all, n_probs);
     mark(mark_ctx, "refine", s);
 }
 

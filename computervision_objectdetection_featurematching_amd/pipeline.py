@@ -5,6 +5,7 @@ Mirrors (names, argument meaning, outputs):
   process_model_views               ModelsDetector.cpp:46-80  one object: detectAndCompute(view, mask) per view
   detect_objects                    TestsDetector.cpp:32-251  scene -> [(Rect, model name)]
   save_detections                   utils.cpp:12-20
+  process_all_test_images           Output.cpp:15-57          every scene -> results files
 Every compute stage runs in libmim: resize and SIFT on the GPU (mim_resize_linear_u8,
 mim_sift_detect_compute), the (model, scale, view) problems as ONE device batch (knnMatch k=2 + ratio
 + findHomography RANSAC + gates, mim_batch_run), the boxes in the library's host stage
@@ -130,5 +131,20 @@ def save_detections(path: str, detections) -> None:
             f.write(f"{name} {x} {y} {x + w} {y + h}\n")
 
 
+def process_all_test_images(matcher: Matcher, scenes, models: list[ObjectModel], output_dir: str, params=None,
+                            box_params: BoxParams | None = None) -> dict:
+    """Output.cpp:15-57 without the file decoding and drawing: scenes = [(object folder, scene name,
+    gray image)]; writes <output_dir>/<folder>/<scene name>_results.txt (scene name = the image stem,
+    e.g. "4_0001_000121-color") and returns {(folder, scene name): detections}."""
+    import os
+    out = {}
+    for folder, name, gray in scenes:
+        os.makedirs(os.path.join(output_dir, folder), exist_ok=True)
+        dets = detect_objects(matcher, gray, models, params=params, box_params=box_params)
+        save_detections(os.path.join(output_dir, folder, f"{name}_results.txt"), dets)
+        out[(folder, name)] = dets
+    return out
+
+
 __all__ = ["ObjectModel", "SCALES", "SceneRun", "default_box_params", "detect_boxes", "detect_objects",
-           "process_model_views", "save_detections", "DIM"]
+           "process_all_test_images", "process_model_views", "save_detections", "DIM"]

@@ -1392,6 +1392,10 @@ __global__ __launch_bounds__(kChainThreads) void ransac_count_kernel(RansacState
     if (T < 0) return;
     RansacState S = st[p];
     const int target = min(c1, S.niters);
+    // with the sampler stream the previous chunk's replay may lower niters after the walk kernel
+    // read it: nothing is left to produce then (never write past the target: the samples of a
+    // problem hold at most maxIters rows, the next problem's follow)
+    if (S.produced >= target) return;
     const long long wbase = G->wbase;
     const uint32_t* PB = pass_bits + (long long)p * (wcap / 32);
     // contiguous ranges of attempts, whole 32-bit words per thread
@@ -2905,6 +2909,12 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                 base += __popcll(bal);
             }
             if (tid == 0) sh.n_inl = base;
+#ifdef MIM_REFINE_DEBUG  // debug build: the best model's mask must hold maxGoodCount inliers
+            if (tid == 0 && base != S.max_good)
+                printf("[refine] p=%d n=%d max_good=%d mask=%d best_iter=%d niters=%d produced=%d fail=%d from_best_h=%d\n",
+                       p, S.n, S.max_good, base, S.best_iter, S.niters, S.produced, S.fail_iter,
+                       (int)(!exact_all && best_h[(long long)p * 9 + 8] != 0.0));
+#endif
             wsync();
             const int k = sh.n_inl;
             if (k > 0) {
@@ -3136,7 +3146,12 @@ void ransac_enqueue(const RansacParams& prm, int n_probs, const ProbDev* probs, 
     // MIM_SAMPLER_WALK=1: attempt-by-attempt walker only (reference mode for cross-checks)
     const char* sw = getenv("MIM_SAMPLER_WALK");
     const int use_chain = !(sw && sw[0] == '1');
-    int c0 = 0, chunk = 4096;
+    // first chunk: 4,096 iterations, 512 when maxIters <= 4,096 (findHomography's default 2,000): a
+    // problem that terminates early (niters falls after a good model) then never samples the rest —
+    // with few, duplicated points getSubset can need ~100 draws per iteration (MIM_FIRST_CHUNK: knob)
+    int first = max_iters <= 4096 ? 512 : 4096;
+    if (const char* fc = getenv("MIM_FIRST_CHUNK")) first = std::max(1, atoi(fc));
+    int c0 = 0, chunk = first;
     const float thr2 = (float)(prm.thresh * prm.thresh);
     if (!exact_all) ransac_tiles_kernel<<<n_probs, 256, 0, s>>>(b.state, probs, pts, b.tiles);
     // the getSubset replay on the sampler stream when there is one (not in the reference mode)

@@ -594,8 +594,9 @@ int sift_detect_compute(SiftWs* w, hipStream_t st, const uint8_t* img, int rows,
     *n_out = 0;
     const int R = rows * 2, C = cols * 2;
     const int n_oct = (int)lrint(log((double)std::min(R, C)) / log(2.) - 2) + 1;
-    if (n_oct < 1 || n_oct > 16) {
-        err = "image too small or too large for SIFT";
+    if (n_oct < 1) return 0;  // no octave (sides < 2 px after doubling): no keypoints, as OpenCV
+    if (n_oct > 16) {
+        err = "image too large for SIFT (more than 16 octaves)";
         return -2;
     }
     // pyramid layout: per octave 6 Gaussian + 5 DoG planes

@@ -107,6 +107,21 @@ def test_c1_surrogate_scene_matches_oracle(matcher, oracle):
     matcher.clear_sets()
 
 
+@pytest.mark.parametrize("first_chunk", [16, 64])
+def test_c1_surrogate_small_first_chunks(matcher, oracle, first_chunk, monkeypatch):
+    """Several chunks with the sampler stream on: the next chunk's getSubset replay runs beside this
+    chunk's selection, which lowers niters for the problems that terminate early; the sampler must
+    then stop, never write past a problem's maxIters sample rows (regression: it wrote into the next
+    problem's rows and the refine rebuilt a wrong bestModel)."""
+    monkeypatch.setenv("MIM_FIRST_CHUNK", str(first_chunk))  # read at every batch (the sampler stream is on by default)
+    ds = make_config_dataset("c1")
+    res, det = _run_batch(matcher, ds, 2000)
+    outs = _oracle_all(oracle, ds, 2000, workers=8, threads=1)
+    _compare(res, det, outs)
+    assert (res["iters"] > first_chunk).any() and ((res["iters"] < 2000) & (res["n_good"] > 4)).any()
+    matcher.clear_sets()
+
+
 def test_c5_dense_50k_sampled_rows(matcher, oracle):
     import torch
     ds = make_dataset(1, 1, 50000, 50000, 0, seed=SEED_BASE + 5)

@@ -175,6 +175,10 @@ def test_sift_edge_cases(matcher, oracle):
     assert len(k) == 0
     tiny = blobs(9, 12, 14, n=4)  # octaves too small for the 5-pixel border: no extrema
     run_both(matcher, oracle, tiny, label="tiny")
+    for shape in ((1, 1), (1, 7), (3, 2)):  # no octave at all: no keypoints, no error
+        k, d = matcher.sift_detect_compute(np.full(shape, 50, np.uint8))
+        ko, _ = oracle.sift_detect_compute(np.full(shape, 50, np.uint8))
+        assert len(k) == len(ko) == 0 and d.shape == (0, 128)
     # strided input equals the dense copy
     big = blobs(10, 150, 220)
     a = matcher.sift_detect_compute(big[:, 20:200])

@@ -2750,10 +2750,9 @@ __device__ __forceinline__ void eig8_group(const double* Ain, double* J, double 
 }
 
 // solve(Ap, v, d, DECOMP_EIG) = Jacobi + SVBkSb(eps = 2 DBL_EPSILON) (Ap, b in LDS); called by a
-// 16-lane group, every slot gets x
-__device__ void solve_eig8(const double* Ap, const double* b, double (&x)[8], double* J) {
-    double w[8];
-    int perm[8];
+// 16-lane group, every slot gets x and the decomposition (w sorted, perm; V stays in J + 36)
+__device__ void solve_eig8(const double* Ap, const double* b, double (&x)[8], double* J, double (&w)[8],
+                           int (&perm)[8]) {
     eig8_group(Ap, J, w, perm);
     const double* V = J + 36;
     double threshold = 0;
@@ -2777,12 +2776,11 @@ __device__ void solve_eig8(const double* Ap, const double* b, double (&x)[8], do
     }
 }
 
-// invert(A, Ai, DECOMP_EIG), max |Ai(i,i)| (LMSolverImpl's lambda restart); 16-lane group
-__device__ double inv_diag_max8(const double* A, double* J) {
-    double w[8];
-    int perm[8];
-    eig8_group(A, J, w, perm);
-    const double* V = J + 36;
+// invert(A, Ai, DECOMP_EIG), max |Ai(i,i)| (LMSolverImpl's lambda restart) from an eigendecomposition
+// of A.  LMSolverImpl restarts lambda only when it is 0, and then this iteration's step matrix
+// Ap = A + 0 * diag(A) is A bit for bit (the diagonal of JᵀJ is never −0): the step solve's
+// decomposition is invert's, so no second Jacobi
+__device__ double inv_diag_max8(const double (&w)[8], const int (&perm)[8], const double* V) {
     double threshold = 0;
 #pragma unroll
     for (int i = 0; i < 8; i++) threshold += w[i];
@@ -2996,6 +2994,8 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                 }
                 wsync();
                 int iter = 0;
+                double ew[8];  // the step solve's eigendecomposition (group lanes), for the lambda restart
+                int eperm[8];
                 for (;;) {
                     if (tid < 16) {  // the step solve on one 16-lane group (group Jacobi)
                         for (int i = tid; i < 64; i += 16) sh.Ap[i] = (i % 9) == 0 ? sh.A[i] + sh.lambda * sh.D[i / 9] : sh.A[i];
@@ -3003,7 +3003,7 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                         __builtin_amdgcn_wave_barrier();
                         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
                         double dl[8];
-                        solve_eig8(sh.Ap, sh.v, dl, sh.J9);
+                        solve_eig8(sh.Ap, sh.v, dl, sh.J9, ew, eperm);
                         if (tid == 0) {
                             double dinf = 0;
                             for (int i = 0; i < 8; ++i) {
@@ -3040,7 +3040,7 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                             double nu = (Sd - Scur) / (fabs(t) > DBL_EPSILON ? t : 1) + 2;
                             nu = fmin(fmax(nu, 2.), 10.);
                             if (lambda == 0) {
-                                const double maxval = inv_diag_max8(sh.A, sh.J9);
+                                const double maxval = inv_diag_max8(ew, eperm, sh.J9 + 36);
                                 lambda = lc = 1. / maxval;
                                 nu *= 0.5;
                             }

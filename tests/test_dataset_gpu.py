@@ -58,5 +58,16 @@ def test_dataset_end_to_end(matcher, data, tmp_path):
     r = subprocess.run([drv, "metrics", os.path.join(HERE, "golden", "dataset"), str(out)], capture_output=True,
                        text=True, check=True)
     vals = {" ".join(line.split()[:-1]): float.fromhex(line.split()[-1]) for line in r.stdout.splitlines()}
-    assert vals == exp["metrics"]
+    # class IoU and accuracy bit for bit; the mean is a float sum over the class folders in directory
+    # order (metrics.cpp:12-26, filesystem-dependent, as in the reference): any order of the same sum
+    assert {k: v for k, v in vals.items() if k != "mean_iou"} == {k: v for k, v in exp["metrics"].items() if k != "mean_iou"}
+    import itertools
+    ious = [np.float32(v) for k, v in vals.items() if k.startswith("class_iou")]
+    means = set()
+    for perm in itertools.permutations(ious):
+        acc = np.float32(0)
+        for v in perm:
+            acc = np.float32(acc + v)
+        means.add(float(np.float32(acc / np.float32(len(ious)))))
+    assert vals["mean_iou"] in means and exp["metrics"]["mean_iou"] in means
     print("mean IoU", vals["mean_iou"], {k: v for k, v in vals.items() if k.startswith("accuracy")})

@@ -53,7 +53,10 @@ def main():
         "models": {"objects": len(models), "views": n_views, "seconds": round(t1 - t0, 4)},
         "scenes": {"n": len(scenes), "problems_per_scene": 5 * n_views,
                    "seconds": round(t2 - t1, 4), "ms_per_scene": round(1e3 * (t2 - t1) / len(scenes), 2)},
-        "metrics": vals, "metrics_equal_to_oracle_run": vals == exp["metrics"],
+        "metrics": vals,
+        # the mean is summed in the class folders' directory order (filesystem-dependent): compare the rest
+        "class_metrics_equal_to_oracle_run": {k: v for k, v in vals.items() if k != "mean_iou"} ==
+                                             {k: v for k, v in exp["metrics"].items() if k != "mean_iou"},
         "scenes_with_detections_differing_from_oracle_run": int(mism)}))
     m.close()
 

@@ -758,9 +758,17 @@ __global__ void ransac_init_kernel(RansacState* __restrict__ st, const int* __re
 // 1 passes, 2 an index repeats (resolved serially by the walker), 3 beyond the RNG stream.
 // attempts precomputed ahead of the walker: the expected draws of the remaining iterations of the
 // chunk (draws per iteration measured so far, 28 before any) + 6 % (25 % unmeasured) + 4096, capped by the buffer
+constexpr int kWalkBatchN = 128;  // below this many points the sampler walks lengths, 64 attempts a batch
+
+// draws per iteration assumed before any is measured: ~28 (redraws rare, checkSubset passing ~1/5);
+// below kWalkBatchN points repeated indices and duplicated keypoints (real SIFT views) push it to
+// ~100-180, so small problems get a window sized for that (the attempt kernel fills it GPU-wide;
+// positions past the window cost the sampler a serial redraw resolution each)
+constexpr double kRateLargeN = 28.0, kRateSmallN = 160.0;
 __device__ __forceinline__ int window_len(const RansacState& S, int c1, int wcap) {
     const int need = min(c1, S.niters) - S.produced;
-    const double rate = S.produced > 0 ? (double)S.stream_pos / S.produced : 28.0;
+    const double rate = S.produced > 0 ? (double)S.stream_pos / S.produced
+                                       : (S.n < kWalkBatchN ? kRateSmallN : kRateLargeN);
     // measured rate: the draws of ~46k iterations vary by < 0.5 % (1 sigma), 6 % + 4096 covers them
     const long long w = (long long)((double)need * rate * (S.produced > 0 ? 1.06 : 1.25)) + 4096;
     return (int)min((long long)wcap, w) & ~63;  // whole 16-byte flag vectors and 32-bit pass words
@@ -955,7 +963,6 @@ __device__ __forceinline__ int wave_max(int v) {
 
 constexpr int kFlagWin = 16384;       // LDS window of attempt flags (bytes)
 constexpr int kFlagUnknown = 0xFE;    // past the precomputed window: evaluate inline
-constexpr int kWalkBatchN = 128;      // below this many points the sampler walks lengths, 64 attempts a batch
 
 __device__ __forceinline__ int ctz64(unsigned long long m) { return __builtin_ctzll(m); }
 // wave-uniform values: keep them in SGPRs so the walk's control flow stays scalar
@@ -1486,6 +1493,208 @@ __global__ __launch_bounds__(kChainThreads) void ransac_count_kernel(RansacState
 
 
 // ------------------------------------------------------------------------------------------------
+// small: the getSubset replay of problems with fewer than kWalkBatchN points, one block each.
+// Repeated indices make most attempts' lengths irregular there (n = 8: 59 % redraw), and
+// degenerate real-data problems (duplicated keypoints) pass checkSubset ~1/30 attempts, so the
+// first chunk's 512 iterations can take ~20k attempts: walked one by one that is ~580 cycles per
+// attempt.  Here a round covers 16 KiB of the attempt-length window:
+//   1. every thread walks its own 64-position segment from the segment's first position
+//      (speculative: the visited positions as a 64-bit mask, and the exit position);
+//   2. wave 0 joins the segments in order: the true chain enters segment i at e; a speculative walk
+//      through e is the chain from there on, otherwise the chain is walked from e until it meets
+//      the speculative one (chains of random lengths merge within a few attempts) or leaves;
+//   3. checkSubset of every chain attempt, each thread its segment's;
+//   4. ranks of the passes, the wanted iteration and the 10000-rejection failure by block scans.
+// Attempts past the window, an attempt that must be resolved serially (RNG stream end, > 67
+// draws) and what a round cannot settle are left to ransac_sample_kernel, which resumes from the
+// state stored here (stream_pos; win_base / win_len: the window the flags are relative to).
+// ------------------------------------------------------------------------------------------------
+constexpr int kSmallThreads = 256;
+constexpr int kSmallRound = kSmallThreads * 64;  // positions per round (one 64-bit mask per thread)
+
+struct SmallShared {
+    uint8_t win[kSmallRound];
+    unsigned long long V[kSmallThreads];  // speculative visited masks, then the chain's masks
+    int X[kSmallThreads];                 // speculative exits
+    int wred[kSmallThreads / 64];
+    int wred2[kSmallThreads / 64];
+    int bad, e_end, q_sel;
+};
+
+__global__ __launch_bounds__(kSmallThreads) void ransac_small_kernel(RansacState* __restrict__ st,
+                                                                     const ProbDev* __restrict__ probs,
+                                                                     const float4* __restrict__ pts,
+                                                                     const uint32_t* __restrict__ stream, long long slen,
+                                                                     int4* __restrict__ samples, int c1,
+                                                                     const uint8_t* __restrict__ flags, int wcap,
+                                                                     int after_chain) {
+    __shared__ __attribute__((aligned(16))) SmallShared sh;
+    constexpr int BIG = 1 << 30;
+    const int p = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+    RansacState S = st[p];
+    if (!S.active || S.done || S.fail_iter != -1 || S.n >= kWalkBatchN) return;
+    const int target = min(c1, S.niters);
+    if (S.produced >= target) return;
+    const long long wbase = after_chain ? S.win_base : S.stream_pos;
+    const int wlen = after_chain ? S.win_len : window_len(S, c1, wcap);
+    const uint8_t* F = flags + (long long)p * wcap;
+    const unsigned N = (unsigned)S.n;
+    const unsigned long long M = S.modM;
+    const float4* P = pts + probs[p].good_off;
+    int4* out = samples + probs[p].it_off;
+    int rel = (int)(S.stream_pos - wbase);  // next attempt, relative to wbase
+    int produced = S.produced, fail_run = S.fail_run;
+    bool stop_all = false;
+    while (!stop_all && produced < target) {
+        const int b = rel & ~15;
+        // flags of the round; an attempt the walker must resolve serially ends it before its segment
+        const int R0 = min(kSmallRound, max(wlen - b, 0)) & ~63;
+        if (tid == 0) sh.bad = R0;
+        __syncthreads();
+        int bad_mine = BIG;
+        if (64 * tid < R0) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint4 v = *reinterpret_cast<const uint4*>(F + b + 64 * tid + 16 * k);
+                *reinterpret_cast<uint4*>(sh.win + 64 * tid + 16 * k) = v;
+                const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                for (int c = 0; c < 4; ++c)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        if (((w4[c] >> (8 * j)) & 0xFF) == kAttemptSerial && 64 * tid + 16 * k + 4 * c + j >= rel - b)
+                            bad_mine = min(bad_mine, 64 * tid + 16 * k + 4 * c + j);
+            }
+        }
+        if (bad_mine < BIG) atomicMin(&sh.bad, bad_mine);
+        __syncthreads();
+        const int R = sh.bad & ~63, nseg = R >> 6;
+        if (rel - b >= R) break;  // window end or a serial attempt in the first segment: the sampler's
+        // 1. speculative walk of segment tid
+        if (tid < nseg) {
+            unsigned long long v = 0;
+            int q = 64 * tid;
+            while (q < 64 * tid + 64) {
+                v |= 1ull << (q - 64 * tid);
+                q += 4 + ((sh.win[q] & 0x7E) >> 1);
+            }
+            sh.V[tid] = v;
+            sh.X[tid] = q;
+        }
+        __syncthreads();
+        // 2. join the segments (wave 0, scalar): the chain's mask per segment replaces V
+        if (tid < 64) {
+            unsigned long long Vk[kSmallThreads / 64], Ck[kSmallThreads / 64];
+            int Xk[kSmallThreads / 64];
+#pragma unroll
+            for (int k = 0; k < kSmallThreads / 64; ++k) {
+                Vk[k] = sh.V[64 * k + lane];
+                Xk[k] = sh.X[64 * k + lane];
+                Ck[k] = 0;
+            }
+            int e = rel - b;  // chain position relative to the round, uniform
+#pragma unroll
+            for (int k = 0; k < kSmallThreads / 64; ++k) {
+                for (int l = 0; l < 64 && 64 * k + l < nseg; ++l) {
+                    const int s0 = 64 * (64 * k + l);
+                    if (e >= s0 + 64) continue;  // the chain jumps over the segment
+                    const unsigned long long V =
+                        ((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(Vk[k] >> 32), l) << 32) |
+                        (unsigned)__builtin_amdgcn_readlane((int)(unsigned)Vk[k], l);
+                    const int X = __builtin_amdgcn_readlane(Xk[k], l);
+                    unsigned long long C = 0;
+                    int q = e;
+                    while (q < s0 + 64 && !((V >> (q - s0)) & 1)) {  // until it meets the speculative walk
+                        C |= 1ull << (q - s0);
+                        q += 4 + ((uni((int)sh.win[q]) & 0x7E) >> 1);
+                    }
+                    if (q < s0 + 64) {
+                        C |= V & (~0ull << (q - s0));
+                        e = X;
+                    } else {
+                        e = q;
+                    }
+                    if (lane == l) Ck[k] = C;
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < kSmallThreads / 64; ++k) sh.V[64 * k + lane] = Ck[k];
+            if (lane == 0) sh.e_end = e;
+        }
+        __syncthreads();
+        const unsigned long long C = tid < nseg ? sh.V[tid] : 0ull;
+        const int e_end = sh.e_end;
+        // 3. checkSubset of the segment's chain attempts
+        unsigned long long PM = 0;
+        for (unsigned long long m = C; m; m &= m - 1) {
+            const int bit = ctz64(m);
+            PM |= (unsigned long long)(attempt_flag(wbase + b + 64 * tid + bit, stream, slen, N, M, P) & 1) << bit;
+        }
+        // 4. ranks: attempts A (chain order) and passes B before this segment
+        int Tr, Pt;
+        const int A = block_excl_sum(__popcll(C), sh.wred, Tr);
+        const int B = block_excl_sum(__popcll(PM), sh.wred, Pt);
+        const int first_ord = PM ? A + __popcll(C & ((PM & -PM) - 1)) : BIG;
+        const int last_ord = PM ? A + __popcll(C & (~0ull >> (63 - (63 - clz64(PM))))) - 1 : -1;
+        const int a_p = min(block_min(first_ord, sh.wred2), Tr);
+        int last_all;
+        block_excl_max(last_ord, -1, sh.wred2, last_all);
+        const int need = target - produced;
+        const int af = fail_run + a_p >= 10000 ? 10000 - fail_run - 1 : BIG;  // the 10000th rejection
+        int keep, stop_ord = -1;  // stop_ord: the round's last attempt taken (-1: all of them)
+        bool hit_t = false, hit_f = false;
+        if (af < BIG) {
+            keep = 0;
+            hit_f = true;
+            stop_ord = af;
+        } else if (Pt >= need) {
+            keep = need;
+            hit_t = true;
+        } else {
+            keep = Pt;
+        }
+        // samples of the kept passes, and the position of the attempt the round stops at
+        if (tid == 0) sh.q_sel = -1;
+        __syncthreads();
+        {
+            int r = B;
+            for (unsigned long long m = PM; m && r < keep; m &= m - 1, ++r) {
+                const int q = b + 64 * tid + ctz64(m);
+                out[produced + r] = make_int4((int)(wbase + q), (sh.win[q - b] & 0x7E) ? -2 : -1, 0, 0);
+                if (hit_t && r == need - 1) sh.q_sel = q;
+            }
+            if (hit_f && A <= stop_ord && stop_ord < A + __popcll(C)) {
+                unsigned long long m = C;
+                for (int k = stop_ord - A; k > 0; --k) m &= m - 1;
+                sh.q_sel = b + 64 * tid + ctz64(m);
+            }
+        }
+        __syncthreads();
+        if (hit_t || hit_f) {
+            const int q = sh.q_sel;
+            rel = q + 4 + ((sh.win[q - b] & 0x7E) >> 1);
+            produced += keep;
+            fail_run = hit_t ? 0 : 10000;
+            if (hit_f) S.fail_iter = produced;  // getSubset returned false in this iteration
+            stop_all = true;
+        } else {
+            produced += Pt;
+            fail_run = Pt > 0 ? Tr - 1 - last_all : fail_run + Tr;
+            rel = b + e_end;
+        }
+        __syncthreads();  // sh.win / sh.V are reloaded by the next round
+    }
+    if (tid == 0) {
+        S.stream_pos = wbase + rel;
+        S.produced = produced;
+        S.fail_run = fail_run;
+        S.win_base = wbase;
+        S.win_len = wlen;
+        store_sampler_state(st + p, S);
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
 // sample: walk the chain of getSubset attempts with the outcomes precomputed by
 // ransac_attempt_kernel; reproduces getSubset's redraw-on-repeat, the checkSubset rejections and
 // the 10000-attempt failure exactly (ptsetreg.cpp).
@@ -1511,8 +1720,10 @@ __global__ __launch_bounds__(64) void ransac_sample_kernel(RansacState* __restri
     const int target = min(c1, S.niters);
     if (S.produced >= target) return;
     // resume where ransac_chain_kernel stopped; flags[rel] is the attempt starting at wbase + rel
-    const long long wbase = after_chain ? S.win_base : S.stream_pos;
-    const int wlen = after_chain ? S.win_len : window_len(S, c1, wcap);
+    // (ransac_small_kernel ran first for n < kWalkBatchN and left its window in the state)
+    const bool from_state = after_chain || S.n < kWalkBatchN;
+    const long long wbase = from_state ? S.win_base : S.stream_pos;
+    const int wlen = from_state ? S.win_len : window_len(S, c1, wcap);
     const uint8_t* F = flags + (long long)p * wcap;
     const unsigned N = (unsigned)S.n;
     const unsigned long long M = S.modM;
@@ -1551,16 +1762,37 @@ __global__ __launch_bounds__(64) void ransac_sample_kernel(RansacState* __restri
         __syncthreads();
     };
     if (N < kWalkBatchN) {
+#ifdef MIM_WALK_PROF
+        long long tw = 0, tc = 0, tr0 = 0, t00 = clock64();
+        int rounds = 0, atts = 0, refills = 0;
+#endif
         // ---- small n: dense redraws (repeated indices) end the sub-rounds below after a few
         // attempts, so walk the chain on the attempt lengths alone (known from the flags), 64
         // attempts at a time, then evaluate their checkSubset one per lane and settle passes,
         // the wanted iteration and the 10000-rejection failure on the ballot of the 64 ----
         while (!stop_all && produced < target) {
-            long long q = rel, pos_mine = 0;
+            long long q = rel, pos_mine = 0, lineq = -1;
             int f_mine = 0, cnt = 0;
+            uint4 line = make_uint4(0, 0, 0, 0);  // the 16 flag bytes around q (attempts are >= 4 apart)
             for (int j = 0; j < 64; ++j) {
-                if (q < lb || q >= lb + kFlagWin) refill(q & ~15LL);
-                int fi = win[q - lb];
+                if (q < lb || q >= lb + kFlagWin) {
+#ifdef MIM_WALK_PROF
+                    const long long ta = clock64();
+#endif
+                    refill(q & ~15LL);
+                    lineq = -1;
+#ifdef MIM_WALK_PROF
+                    tr0 += clock64() - ta;
+                    ++refills;
+#endif
+                }
+                if ((q & ~15LL) != lineq) {
+                    lineq = q & ~15LL;
+                    line = *reinterpret_cast<const uint4*>(win + (lineq - lb));
+                }
+                const int wsel = (int)(q >> 2) & 3;
+                const uint32_t wd = wsel == 0 ? line.x : wsel == 1 ? line.y : wsel == 2 ? line.z : line.w;
+                int fi = uni((int)((wd >> (8 * (int)(q & 3))) & 0xFF));  // uniform: scalar control flow
                 if (fi == kFlagUnknown) {  // past the precomputed window: evaluate here (uniform)
                     if (j > 0) break;
                     fi = uni(attempt_flag(wbase + q, stream, slen, N, M, P));
@@ -1590,6 +1822,12 @@ __global__ __launch_bounds__(64) void ransac_sample_kernel(RansacState* __restri
                 cnt = j + 1;
             }
             if (stop_all) break;
+#ifdef MIM_WALK_PROF
+            const long long tb = clock64();
+            tw += tb - t00;
+            ++rounds;
+            atts += cnt;
+#endif
             // checkSubset of the attempts whose pass bit is not known yet, one per lane
             int pass = 0;
             if (lane < cnt) {
@@ -1629,7 +1867,16 @@ __global__ __launch_bounds__(64) void ransac_sample_kernel(RansacState* __restri
                 stop_all = true;
             }
             if (hit_t) stop_all = true;
+#ifdef MIM_WALK_PROF
+            t00 = clock64();
+            tc += t00 - tb;
+#endif
         }
+#ifdef MIM_WALK_PROF
+        if (lane == 0)
+            printf("[walk] p=%d N=%u produced=%d rounds=%d attempts=%d refills=%d walk=%lld (refill %lld) check=%lld wlen=%d\n",
+                   p, N, produced, rounds, atts, refills, tw, tr0, tc, wlen);
+#endif
     }
     while (!stop_all && produced < target) {
         const long long wb = rel & ~15LL;
@@ -3171,7 +3418,9 @@ void ransac_enqueue(const RansacParams& prm, int n_probs, const ProbDev* probs, 
         // attempt outcomes for a window of ~28 draws per wanted iteration (pass rate ~1/5), the walk
         // falls back to inline evaluation past the window
         // (a multiple of 64: flags are read as 16-byte vectors, pass bits as 32-bit words)
-        const int wcap = (int)(std::min<long long>((long long)(c1 - c0) * 28 + 4096, b.flag_cap / std::max(n_probs, 1)) & ~63LL);
+        // the first chunk of a maxIters <= 4,096 batch sizes the window for the small problems' rate
+        const long long rate = (c0 == 0 && max_iters <= 4096) ? (long long)kRateSmallN : (long long)kRateLargeN;
+        const int wcap = (int)(std::min<long long>((long long)(c1 - c0) * rate + 4096, b.flag_cap / std::max(n_probs, 1)) & ~63LL);
         const int bppw = (wcap + kAttemptSpan - 1) / kAttemptSpan;
         ransac_attempt_kernel<<<n_probs * bppw, 256, 0, ss>>>(b.state, b.stream, b.stream_len, b.flags, wcap, bppw, c1);
         mark(mark_ctx, "attempt", ss);
@@ -3191,6 +3440,8 @@ void ransac_enqueue(const RansacParams& prm, int n_probs, const ProbDev* probs, 
                                                                   b.samples, c1);
             mark(mark_ctx, "chain", ss);
         }
+        ransac_small_kernel<<<n_probs, kSmallThreads, 0, ss>>>(b.state, probs, pts, b.stream, b.stream_len, b.samples,
+                                                              c1, b.flags, wcap, use_chain);
         ransac_sample_kernel<<<n_probs, 64, 0, ss>>>(b.state, probs, pts, b.stream, b.stream_len, b.samples, c1, b.err,
                                                     b.flags, wcap, use_chain);
         mark(mark_ctx, "sample", ss);

@@ -842,10 +842,8 @@ static mim_status ransac_prepare(mim_ctx* c, int n, const mim_params* prm, Ransa
     HIPCHK(c, c->rws.counts.ensure(sizeof(int) * it_total));
     HIPCHK(c, c->rws.bounds.ensure(sizeof(int2) * it_total));
     // attempt-outcome windows: largest chunk x 28 draws per problem, 64-byte granular per problem
-    // (a maxIters <= 4,096 batch's first 512-iteration chunk at 160 draws per iteration, ransac.hip)
     const long long chunk_max = std::min<long long>(max_iters, 1 << 18);
-    const long long first_need = max_iters <= 4096 ? 512LL * 160 : 0;
-    flag_per = (std::max(chunk_max * 28, first_need) + 4096 + 63) & ~63LL;
+    flag_per = (chunk_max * 28 + 4096 + 63) & ~63LL;
     const long long flag_cap = (long long)std::max(n, 1) * flag_per;
     HIPCHK(c, c->rws.flags.ensure((size_t)flag_cap));
     const int irr_blocks = (int)((flag_per + kIrrBlock - 1) / kIrrBlock);

@@ -758,17 +758,12 @@ __global__ void ransac_init_kernel(RansacState* __restrict__ st, const int* __re
 // 1 passes, 2 an index repeats (resolved serially by the walker), 3 beyond the RNG stream.
 // attempts precomputed ahead of the walker: the expected draws of the remaining iterations of the
 // chunk (draws per iteration measured so far, 28 before any) + 6 % (25 % unmeasured) + 4096, capped by the buffer
-constexpr int kWalkBatchN = 128;  // below this many points the sampler walks lengths, 64 attempts a batch
+// problems with fewer points are replayed by ransac_small_kernel from the stream alone (no window)
+constexpr int kSmallMaxN = 128;
 
-// draws per iteration assumed before any is measured: ~28 (redraws rare, checkSubset passing ~1/5);
-// below kWalkBatchN points repeated indices and duplicated keypoints (real SIFT views) push it to
-// ~100-180, so small problems get a window sized for that (the attempt kernel fills it GPU-wide;
-// positions past the window cost the sampler a serial redraw resolution each)
-constexpr double kRateLargeN = 28.0, kRateSmallN = 160.0;
 __device__ __forceinline__ int window_len(const RansacState& S, int c1, int wcap) {
     const int need = min(c1, S.niters) - S.produced;
-    const double rate = S.produced > 0 ? (double)S.stream_pos / S.produced
-                                       : (S.n < kWalkBatchN ? kRateSmallN : kRateLargeN);
+    const double rate = S.produced > 0 ? (double)S.stream_pos / S.produced : 28.0;
     // measured rate: the draws of ~46k iterations vary by < 0.5 % (1 sigma), 6 % + 4096 covers them
     const long long w = (long long)((double)need * rate * (S.produced > 0 ? 1.06 : 1.25)) + 4096;
     return (int)min((long long)wcap, w) & ~63;  // whole 16-byte flag vectors and 32-bit pass words
@@ -866,7 +861,7 @@ __global__ __launch_bounds__(256) void ransac_attempt_kernel(const RansacState* 
     __shared__ __attribute__((aligned(16))) unsigned sdraw[kStageWords];
     const int p = blockIdx.x / bpp;
     const RansacState S = st[p];
-    if (!S.active || S.done || S.fail_iter != -1 || S.produced >= min(c1, S.niters)) return;
+    if (!S.active || S.done || S.fail_iter != -1 || S.n < kSmallMaxN || S.produced >= min(c1, S.niters)) return;
     const int wlen = window_len(S, c1, wcap);  // a multiple of 64
     const int boff = (blockIdx.x % bpp) * kAttemptSpan;
     if (boff >= wlen) return;  // uniform over the block
@@ -993,7 +988,7 @@ __global__ __launch_bounds__(256) void ransac_irr_kernel(const RansacState* __re
     __shared__ int wsum[4];
     const int p = blockIdx.x / bpp, b = blockIdx.x % bpp, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const RansacState S = st[p];
-    if (!S.active || S.done || S.fail_iter != -1 || S.produced >= min(c1, S.niters)) return;
+    if (!S.active || S.done || S.fail_iter != -1 || S.n < kSmallMaxN || S.produced >= min(c1, S.niters)) return;
     const int wlen = window_len(S, c1, wcap);
     const int b0 = b * kIrrBlock;
     if (b0 >= wlen) return;
@@ -1138,8 +1133,8 @@ __global__ __launch_bounds__(kChainThreads) void ransac_walk_kernel(const Ransac
     const int p = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
     const RansacState S = st[p];
     ChainSegs* G = chains + p;
-    if (!S.active || S.done || S.fail_iter != -1 || S.produced >= min(c1, S.niters)) {
-        if (tid == 0) G->T = -1;  // nothing to do this chunk
+    if (!S.active || S.done || S.fail_iter != -1 || S.n < kSmallMaxN || S.produced >= min(c1, S.niters)) {
+        if (tid == 0) G->T = -1;  // nothing to do this chunk (small problems: ransac_small_kernel)
         return;
     }
     const int wlen = window_len(S, c1, wcap);
@@ -1493,160 +1488,320 @@ __global__ __launch_bounds__(kChainThreads) void ransac_count_kernel(RansacState
 
 
 // ------------------------------------------------------------------------------------------------
-// small: the getSubset replay of problems with fewer than kWalkBatchN points, one block each.
-// Repeated indices make most attempts' lengths irregular there (n = 8: 59 % redraw), and
-// degenerate real-data problems (duplicated keypoints) pass checkSubset ~1/30 attempts, so the
-// first chunk's 512 iterations can take ~20k attempts: walked one by one that is ~580 cycles per
-// attempt.  Here a round covers 16 KiB of the attempt-length window:
+// small: the getSubset replay of problems with fewer than kSmallMaxN points, one block each.
+// Repeated indices make most attempts' lengths irregular there (n = 8: 59 % redraw) and degenerate
+// real-data problems (duplicated keypoints) pass checkSubset ~1/30 attempts, so the first chunk's
+// 512 iterations can take ~20k attempts; walked one by one that is ~580 cycles per attempt.  A
+// round of this kernel covers 16k stream positions from the chain's current position:
+//   0. the round's draws, reduced mod n, are staged in LDS as bytes (n < 256), with the draws
+//      consumed by the attempt starting at each position (getSubset's redraw-on-repeat);
 //   1. every thread walks its own 64-position segment from the segment's first position
 //      (speculative: the visited positions as a 64-bit mask, and the exit position);
 //   2. wave 0 joins the segments in order: the true chain enters segment i at e; a speculative walk
 //      through e is the chain from there on, otherwise the chain is walked from e until it meets
 //      the speculative one (chains of random lengths merge within a few attempts) or leaves;
-//   3. checkSubset of every chain attempt, each thread its segment's;
+//   3. checkSubset of every chain attempt (indices from LDS, points staged in LDS);
 //   4. ranks of the passes, the wanted iteration and the 10000-rejection failure by block scans.
-// Attempts past the window, an attempt that must be resolved serially (RNG stream end, > 67
-// draws) and what a round cannot settle are left to ransac_sample_kernel, which resumes from the
-// state stored here (stream_pos; win_base / win_len: the window the flags are relative to).
+// An attempt that needs more draws than staged (> 67, or the RNG stream end) closes the round
+// before it and is then resolved alone.  These problems never use the attempt window.
 // ------------------------------------------------------------------------------------------------
 constexpr int kSmallThreads = 256;
 constexpr int kSmallRound = kSmallThreads * 64;  // positions per round (one 64-bit mask per thread)
+constexpr int kSmallExtra = 128;                 // draws staged past the round's last position
+constexpr uint8_t kSmallAlone = 0xFF;            // attempt resolved alone
 
 struct SmallShared {
-    uint8_t win[kSmallRound];
-    unsigned long long V[kSmallThreads];  // speculative visited masks, then the chain's masks
-    int X[kSmallThreads];                 // speculative exits
+    uint8_t idx[kSmallRound + kSmallExtra];  // draw k of the round, mod n
+    uint8_t len[kSmallRound];                // draws - 4 of the attempt starting at each position
+    float4 P[kSmallMaxN];
+    unsigned long long V[kSmallThreads];     // per segment: exits of the walks from its first 16 positions
+    int X[kSmallThreads];                    // per segment: the chain's entry (-1: jumped over)
+    unsigned long long Wt[kSmallThreads / 64];  // exit tables composed over each wave's segments
     int wred[kSmallThreads / 64];
     int wred2[kSmallThreads / 64];
     int bad, e_end, q_sel;
 };
+
+// exit tables: nibble r = where the walk entering a segment at offset r leaves it (offset into the
+// next segment; 15: 15 or more, the table cannot continue).  compose_exits(A, B) = B after A.
+__device__ __forceinline__ unsigned long long compose_exits(unsigned long long A, unsigned long long B) {
+    unsigned long long R = 0;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int x = (int)(A >> (4 * r)) & 15;
+        const int y = x == 15 ? 15 : (int)(B >> (4 * x)) & 15;
+        R |= (unsigned long long)y << (4 * r);
+    }
+    return R;
+}
+
+__device__ __forceinline__ unsigned long long shfl_up64(unsigned long long v, int off) {
+    const int lo = __shfl_up((int)(unsigned)v, off), hi = __shfl_up((int)(v >> 32), off);
+    return ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo;
+}
+
+// getSubset's sample from 16 consecutive draws: the first 4 distinct; c < 4 if they do not suffice
+__device__ __forceinline__ int first4_distinct(const unsigned (&u)[16], int (&a)[4]) {
+    a[0] = (int)u[0];
+    a[1] = a[2] = a[3] = 0;
+    int c = 1, len = 0;
+#pragma unroll
+    for (int k = 1; k < 16; ++k) {
+        const int v = (int)u[k];
+        const bool take = c < 4 && v != a[0] && (c < 2 || v != a[1]) && (c < 3 || v != a[2]);
+        a[1] = take && c == 1 ? v : a[1];
+        a[2] = take && c == 2 ? v : a[2];
+        a[3] = take && c == 3 ? v : a[3];
+        len = take && c == 3 ? k + 1 : len;
+        c += take ? 1 : 0;
+    }
+    return len;  // 0: more than 16 draws
+}
 
 __global__ __launch_bounds__(kSmallThreads) void ransac_small_kernel(RansacState* __restrict__ st,
                                                                      const ProbDev* __restrict__ probs,
                                                                      const float4* __restrict__ pts,
                                                                      const uint32_t* __restrict__ stream, long long slen,
                                                                      int4* __restrict__ samples, int c1,
-                                                                     const uint8_t* __restrict__ flags, int wcap,
-                                                                     int after_chain) {
+                                                                     int* __restrict__ err) {
     __shared__ __attribute__((aligned(16))) SmallShared sh;
     constexpr int BIG = 1 << 30;
     const int p = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
     RansacState S = st[p];
-    if (!S.active || S.done || S.fail_iter != -1 || S.n >= kWalkBatchN) return;
+    if (!S.active || S.done || S.fail_iter != -1 || S.n >= kSmallMaxN) return;
     const int target = min(c1, S.niters);
     if (S.produced >= target) return;
-    const long long wbase = after_chain ? S.win_base : S.stream_pos;
-    const int wlen = after_chain ? S.win_len : window_len(S, c1, wcap);
-    const uint8_t* F = flags + (long long)p * wcap;
     const unsigned N = (unsigned)S.n;
     const unsigned long long M = S.modM;
-    const float4* P = pts + probs[p].good_off;
+    const float4* Pg = pts + probs[p].good_off;
+    if (tid < (int)N) sh.P[tid] = Pg[tid];
     int4* out = samples + probs[p].it_off;
-    int rel = (int)(S.stream_pos - wbase);  // next attempt, relative to wbase
+    long long pos = S.stream_pos;  // the chain's next attempt (absolute stream position)
     int produced = S.produced, fail_run = S.fail_run;
     bool stop_all = false;
+#ifdef MIM_SMALL_PROF
+    long long tp[6] = {0, 0, 0, 0, 0, 0}, t0 = clock64();
+    int rounds = 0;
+#endif
     while (!stop_all && produced < target) {
-        const int b = rel & ~15;
-        // flags of the round; an attempt the walker must resolve serially ends it before its segment
-        const int R0 = min(kSmallRound, max(wlen - b, 0)) & ~63;
-        if (tid == 0) sh.bad = R0;
+        // 0. stage the draws of [pos, pos + kSmallRound + kSmallExtra), then the attempt lengths
+        const long long avail = slen - pos;  // draws left in the RNG stream (past it: 64 zero draws)
+        {
+            // 16-byte loads from the aligned vector holding pos, all in flight at once
+            constexpr int kVec = (kSmallRound + kSmallExtra + 3) / 4 + 1, kVecPer = (kVec + kSmallThreads - 1) / kSmallThreads;
+            const long long v0 = pos >> 2, nvec = (slen + 64) >> 2;
+            const int shift = (int)(pos & 3);
+            const uint4* __restrict__ sv = reinterpret_cast<const uint4*>(stream);
+            uint4 v[kVecPer];
+#pragma unroll
+            for (int j = 0; j < kVecPer; ++j) v[j] = sv[min(v0 + tid + kSmallThreads * j, nvec - 1)];
+#pragma unroll
+            for (int j = 0; j < kVecPer; ++j) {
+                const unsigned vv[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const int e = 4 * (tid + kSmallThreads * j) + c - shift;
+                    if (e >= 0 && e < kSmallRound + kSmallExtra) sh.idx[e] = (uint8_t)fastmod(vv[c], M, N);
+                }
+            }
+        }
+        if (tid == 0) sh.bad = kSmallRound;
         __syncthreads();
+#ifdef MIM_SMALL_PROF
+        if (tid == 0) tp[5] += clock64() - t0, t0 = clock64();
+#endif
+        // the draws consumed by the attempt at each of the thread's 64 positions, by two pointers:
+        // the attempt at j ends at k4(j), the first r with 4 distinct draws in [j, r), and k4 never
+        // decreases with j.  The window's distinct draws are 4 (value, last occurrence) slots.
         int bad_mine = BIG;
-        if (64 * tid < R0) {
+        {
+            const int jend = 64 * tid + 64;
+            int j = 64 * tid, r = j, cnt = 0;
+            int val[4] = {0, 0, 0, 0}, last[4] = {-1, -1, -1, -1};  // last < 0: free slot
+            while (j < jend) {
+                const int v = sh.idx[min(r, kSmallRound + kSmallExtra - 1)], u = sh.idx[j];
+                if (cnt < 4 && r < kSmallRound + kSmallExtra) {  // extend the window by draw r
+                    int hit = -1, fr = -1;
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const uint4 v = *reinterpret_cast<const uint4*>(F + b + 64 * tid + 16 * k);
-                *reinterpret_cast<uint4*>(sh.win + 64 * tid + 16 * k) = v;
-                const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+                    for (int k = 3; k >= 0; --k) {
+                        hit = last[k] >= 0 && val[k] == v ? k : hit;
+                        fr = last[k] < 0 ? k : fr;
+                    }
+                    const int sl = hit >= 0 ? hit : fr;
 #pragma unroll
-                for (int c = 0; c < 4; ++c)
+                    for (int k = 0; k < 4; ++k) {
+                        val[k] = k == sl ? v : val[k];
+                        last[k] = k == sl ? r : last[k];
+                    }
+                    cnt += hit < 0 ? 1 : 0;
+                    ++r;
+                } else {  // the attempt at j: r - j draws (more than staged: resolved alone)
+                    const int len = cnt == 4 ? r - j : 0;
+                    const bool alone = len == 0 || len > 67 || j + len > avail;
+                    sh.len[j] = alone ? kSmallAlone : (uint8_t)(len - 4);
+                    if (alone) bad_mine = min(bad_mine, j);
 #pragma unroll
-                    for (int j = 0; j < 4; ++j)
-                        if (((w4[c] >> (8 * j)) & 0xFF) == kAttemptSerial && 64 * tid + 16 * k + 4 * c + j >= rel - b)
-                            bad_mine = min(bad_mine, 64 * tid + 16 * k + 4 * c + j);
+                    for (int k = 0; k < 4; ++k)  // draw j leaves the window: its slot if it was the last
+                        if (last[k] == j && val[k] == u) {
+                            last[k] = -1;
+                            --cnt;
+                        }
+                    ++j;
+                }
             }
         }
         if (bad_mine < BIG) atomicMin(&sh.bad, bad_mine);
         __syncthreads();
-        const int R = sh.bad & ~63, nseg = R >> 6;
-        if (rel - b >= R) break;  // window end or a serial attempt in the first segment: the sampler's
-        // 1. speculative walk of segment tid
+        const int Rz = sh.bad;  // the round: positions [0, Rz), the chain's attempts starting there
+#ifdef MIM_SMALL_PROF
+        if (tid == 0) tp[0] += clock64() - t0, t0 = clock64();
+#endif
+        if (Rz == 0) {
+            // the chain's next attempt is resolved alone (uniform)
+            int idx[4] = {0, 0, 0, 0};
+            const int len = resolve_at(pos, stream, slen, N, M, idx);
+            if (len == 0) {  // RNG stream exhausted: report, never guess
+                if (tid == 0) atomicOr(err, 1);
+                S.fail_iter = -2;
+                break;
+            }
+            const float4 a = sh.P[idx[0]], b = sh.P[idx[1]], c = sh.P[idx[2]], d = sh.P[idx[3]];
+            const float s4[8] = {a.x, a.y, b.x, b.y, c.x, c.y, d.x, d.y};
+            const float t4[8] = {a.z, a.w, b.z, b.w, c.z, c.w, d.z, d.w};
+            if (uni(check_subset(s4, t4) ? 1 : 0)) {
+                if (tid == 0) out[produced] = make_int4((int)pos, len != 4 ? -2 : -1, 0, 0);
+                ++produced;
+                fail_run = 0;
+            } else if (++fail_run >= 10000) {
+                S.fail_iter = produced;  // getSubset returned false in this iteration
+                stop_all = true;
+            }
+            pos += len;
+            __syncthreads();  // sh.idx / sh.len are restaged
+            continue;
+        }
+        const int nseg = (Rz + 63) >> 6;
+        // 1. the segment's walks from its first 16 positions: where each leaves the segment, as a
+        //    nibble (exit - segment end; 15: 15 or more, then walked again in step 2)
         if (tid < nseg) {
-            unsigned long long v = 0;
-            int q = 64 * tid;
-            while (q < 64 * tid + 64) {
-                v |= 1ull << (q - 64 * tid);
-                q += 4 + ((sh.win[q] & 0x7E) >> 1);
-            }
-            sh.V[tid] = v;
-            sh.X[tid] = q;
+            const int s0 = 64 * tid, se = min(s0 + 64, Rz);
+            int q[16];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) q[r] = s0 + r;
+#pragma unroll
+            for (int step = 0; step < 16; ++step)  // >= 4 draws an attempt: <= 16 attempts a walk
+#pragma unroll
+                for (int r = 0; r < 16; ++r)
+                    if (q[r] < se) q[r] += 4 + sh.len[q[r]];
+            unsigned long long nib = 0;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) nib |= (unsigned long long)min(max(q[r] - se, 0), 15) << (4 * r);
+            sh.V[tid] = nib;
         }
         __syncthreads();
-        // 2. join the segments (wave 0, scalar): the chain's mask per segment replaces V
-        if (tid < 64) {
-            unsigned long long Vk[kSmallThreads / 64], Ck[kSmallThreads / 64];
-            int Xk[kSmallThreads / 64];
+#ifdef MIM_SMALL_PROF
+        if (tid == 0) tp[1] += clock64() - t0, t0 = clock64();
+#endif
+        // 2. the chain's entry into every segment: a block scan of the exit tables under
+        //    composition (segment 0 is entered at 0; segment i at T_{i-1}(...T_0(0))).  An exit of
+        //    15 or more breaks the tables: from that segment on wave 0 joins in order, walking on LDS.
+        {
+            constexpr unsigned long long kId = 0xFEDCBA9876543210ull;  // identity table
+            const unsigned long long T = tid < nseg ? sh.V[tid] : kId;
+            unsigned long long incl = T;
 #pragma unroll
-            for (int k = 0; k < kSmallThreads / 64; ++k) {
-                Vk[k] = sh.V[64 * k + lane];
-                Xk[k] = sh.X[64 * k + lane];
-                Ck[k] = 0;
+            for (int off = 1; off < 64; off <<= 1) {
+                const unsigned long long o = shfl_up64(incl, off);
+                if (lane >= off) incl = compose_exits(o, incl);
             }
-            int e = rel - b;  // chain position relative to the round, uniform
-#pragma unroll
-            for (int k = 0; k < kSmallThreads / 64; ++k) {
-                for (int l = 0; l < 64 && 64 * k + l < nseg; ++l) {
-                    const int s0 = 64 * (64 * k + l);
-                    if (e >= s0 + 64) continue;  // the chain jumps over the segment
-                    const unsigned long long V =
-                        ((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(Vk[k] >> 32), l) << 32) |
-                        (unsigned)__builtin_amdgcn_readlane((int)(unsigned)Vk[k], l);
-                    const int X = __builtin_amdgcn_readlane(Xk[k], l);
-                    unsigned long long C = 0;
-                    int q = e;
-                    while (q < s0 + 64 && !((V >> (q - s0)) & 1)) {  // until it meets the speculative walk
-                        C |= 1ull << (q - s0);
-                        q += 4 + ((uni((int)sh.win[q]) & 0x7E) >> 1);
+            if (lane == 63) sh.Wt[tid >> 6] = incl;
+            __syncthreads();
+            unsigned long long pw = kId;  // the waves before this one
+            for (int w = 0; w < (tid >> 6); ++w) pw = compose_exits(pw, sh.Wt[w]);
+            unsigned long long excl = shfl_up64(incl, 1);
+            if (lane == 0) excl = kId;
+            excl = compose_exits(pw, excl);
+            incl = compose_exits(pw, incl);
+            const int ent = (int)(excl & 15);
+            if (tid < nseg) sh.X[tid] = ent;
+            if (tid == nseg - 1) sh.e_end = (int)(incl & 15) == 15 ? -1 : Rz + (int)(incl & 15);
+            const int esc = block_min(tid < nseg && ent == 15 ? tid : BIG, sh.wred2);
+            const bool esc_end = sh.e_end < 0;  // (written before block_min's barriers)
+            if ((esc < BIG || esc_end) && tid < 64) {  // wave 0, uniform: join in order from the break
+                int i = esc < BIG ? esc - 1 : nseg - 1;
+                int e = 64 * i + sh.X[i];
+                for (; i < nseg; ++i) {
+                    const int s0 = 64 * i, se = min(s0 + 64, Rz);
+                    int ent_i = -1;
+                    if (e < se) {  // else the chain jumps over the segment
+                        const int off = e - s0;
+                        ent_i = off;
+                        const int x = off < 16 ? (int)(uni64((long long)sh.V[i]) >> (4 * off)) & 15 : 15;
+                        if (x < 15) {
+                            e = se + x;
+                        } else {
+                            int qq = e;
+                            while (qq < se) qq += 4 + uni((int)sh.len[qq]);
+                            e = qq;
+                        }
                     }
-                    if (q < s0 + 64) {
-                        C |= V & (~0ull << (q - s0));
-                        e = X;
-                    } else {
-                        e = q;
-                    }
-                    if (lane == l) Ck[k] = C;
+                    if (lane == 0) sh.X[i] = ent_i;
                 }
+                if (lane == 0) sh.e_end = e;
             }
-#pragma unroll
-            for (int k = 0; k < kSmallThreads / 64; ++k) sh.V[64 * k + lane] = Ck[k];
-            if (lane == 0) sh.e_end = e;
+            __syncthreads();
         }
-        __syncthreads();
-        const unsigned long long C = tid < nseg ? sh.V[tid] : 0ull;
+#ifdef MIM_SMALL_PROF
+        if (tid == 0) tp[2] += clock64() - t0, t0 = clock64();
+#endif
+        // the chain's attempts in the segment, from its entry
+        unsigned long long C = 0;
+        if (tid < nseg && sh.X[tid] >= 0) {
+            const int s0 = 64 * tid, se = min(s0 + 64, Rz);
+            for (int q = s0 + sh.X[tid]; q < se; q += 4 + sh.len[q]) C |= 1ull << (q - s0);
+        }
         const int e_end = sh.e_end;
         // 3. checkSubset of the segment's chain attempts
         unsigned long long PM = 0;
         for (unsigned long long m = C; m; m &= m - 1) {
-            const int bit = ctz64(m);
-            PM |= (unsigned long long)(attempt_flag(wbase + b + 64 * tid + bit, stream, slen, N, M, P) & 1) << bit;
+            const int bit = ctz64(m), q = 64 * tid + bit;
+            unsigned u[16];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) u[k] = sh.idx[q + k];
+            int a[4];
+            if (first4_distinct(u, a) == 0) {  // more than 16 draws (staged: the length was <= 67)
+                int c = 1, k = q + 16;
+                while (c < 4) {
+                    const int v = sh.idx[k++];
+                    if (v == a[0] || (c > 1 && v == a[1]) || (c > 2 && v == a[2])) continue;
+                    a[c++] = v;
+                }
+            }
+            const float4 A0 = sh.P[a[0]], A1 = sh.P[a[1]], A2 = sh.P[a[2]], A3 = sh.P[a[3]];
+            const float s4[8] = {A0.x, A0.y, A1.x, A1.y, A2.x, A2.y, A3.x, A3.y};
+            const float t4[8] = {A0.z, A0.w, A1.z, A1.w, A2.z, A2.w, A3.z, A3.w};
+            PM |= (unsigned long long)(check_subset(s4, t4) ? 1 : 0) << bit;
         }
+        __syncthreads();
+#ifdef MIM_SMALL_PROF
+        if (tid == 0) tp[3] += clock64() - t0, t0 = clock64();
+#endif
         // 4. ranks: attempts A (chain order) and passes B before this segment
         int Tr, Pt;
         const int A = block_excl_sum(__popcll(C), sh.wred, Tr);
         const int B = block_excl_sum(__popcll(PM), sh.wred, Pt);
         const int first_ord = PM ? A + __popcll(C & ((PM & -PM) - 1)) : BIG;
-        const int last_ord = PM ? A + __popcll(C & (~0ull >> (63 - (63 - clz64(PM))))) - 1 : -1;
+        const int last_ord = PM ? A + __popcll(C & (~0ull >> clz64(PM))) - 1 : -1;
         const int a_p = min(block_min(first_ord, sh.wred2), Tr);
         int last_all;
         block_excl_max(last_ord, -1, sh.wred2, last_all);
         const int need = target - produced;
         const int af = fail_run + a_p >= 10000 ? 10000 - fail_run - 1 : BIG;  // the 10000th rejection
-        int keep, stop_ord = -1;  // stop_ord: the round's last attempt taken (-1: all of them)
+        int keep;
         bool hit_t = false, hit_f = false;
         if (af < BIG) {
             keep = 0;
             hit_f = true;
-            stop_ord = af;
         } else if (Pt >= need) {
             keep = need;
             hit_t = true;
@@ -1659,20 +1814,20 @@ __global__ __launch_bounds__(kSmallThreads) void ransac_small_kernel(RansacState
         {
             int r = B;
             for (unsigned long long m = PM; m && r < keep; m &= m - 1, ++r) {
-                const int q = b + 64 * tid + ctz64(m);
-                out[produced + r] = make_int4((int)(wbase + q), (sh.win[q - b] & 0x7E) ? -2 : -1, 0, 0);
+                const int q = 64 * tid + ctz64(m);
+                out[produced + r] = make_int4((int)(pos + q), sh.len[q] ? -2 : -1, 0, 0);
                 if (hit_t && r == need - 1) sh.q_sel = q;
             }
-            if (hit_f && A <= stop_ord && stop_ord < A + __popcll(C)) {
+            if (hit_f && A <= af && af < A + __popcll(C)) {
                 unsigned long long m = C;
-                for (int k = stop_ord - A; k > 0; --k) m &= m - 1;
-                sh.q_sel = b + 64 * tid + ctz64(m);
+                for (int k = af - A; k > 0; --k) m &= m - 1;
+                sh.q_sel = 64 * tid + ctz64(m);
             }
         }
         __syncthreads();
         if (hit_t || hit_f) {
             const int q = sh.q_sel;
-            rel = q + 4 + ((sh.win[q - b] & 0x7E) >> 1);
+            pos += q + 4 + sh.len[q];
             produced += keep;
             fail_run = hit_t ? 0 : 10000;
             if (hit_f) S.fail_iter = produced;  // getSubset returned false in this iteration
@@ -1680,17 +1835,26 @@ __global__ __launch_bounds__(kSmallThreads) void ransac_small_kernel(RansacState
         } else {
             produced += Pt;
             fail_run = Pt > 0 ? Tr - 1 - last_all : fail_run + Tr;
-            rel = b + e_end;
+            pos += e_end;
         }
-        __syncthreads();  // sh.win / sh.V are reloaded by the next round
+        __syncthreads();  // sh.idx / sh.len / sh.V are restaged by the next round
+#ifdef MIM_SMALL_PROF
+        if (tid == 0) tp[4] += clock64() - t0, t0 = clock64();
+#endif
+#ifdef MIM_SMALL_PROF
+        ++rounds;
+#endif
     }
     if (tid == 0) {
-        S.stream_pos = wbase + rel;
+        S.stream_pos = pos;
         S.produced = produced;
         S.fail_run = fail_run;
-        S.win_base = wbase;
-        S.win_len = wlen;
         store_sampler_state(st + p, S);
+#ifdef MIM_SMALL_PROF
+        if (rounds > 1)
+            printf("[small] p=%d N=%u produced=%d rounds=%d stage %lld lengths %lld join-tables %lld join %lld checks %lld ranks %lld\n",
+                   p, N, produced, rounds, tp[5], tp[0], tp[1], tp[2], tp[3], tp[4]);
+#endif
     }
 }
 
@@ -1716,14 +1880,12 @@ __global__ __launch_bounds__(64) void ransac_sample_kernel(RansacState* __restri
     constexpr int BIG = 1 << 30;
     const int p = blockIdx.x, lane = threadIdx.x;
     RansacState S = st[p];
-    if (!S.active || S.done || S.fail_iter != -1) return;
+    if (!S.active || S.done || S.fail_iter != -1 || S.n < kSmallMaxN) return;  // small: ransac_small_kernel
     const int target = min(c1, S.niters);
     if (S.produced >= target) return;
     // resume where ransac_chain_kernel stopped; flags[rel] is the attempt starting at wbase + rel
-    // (ransac_small_kernel ran first for n < kWalkBatchN and left its window in the state)
-    const bool from_state = after_chain || S.n < kWalkBatchN;
-    const long long wbase = from_state ? S.win_base : S.stream_pos;
-    const int wlen = from_state ? S.win_len : window_len(S, c1, wcap);
+    const long long wbase = after_chain ? S.win_base : S.stream_pos;
+    const int wlen = after_chain ? S.win_len : window_len(S, c1, wcap);
     const uint8_t* F = flags + (long long)p * wcap;
     const unsigned N = (unsigned)S.n;
     const unsigned long long M = S.modM;
@@ -1761,123 +1923,6 @@ __global__ __launch_bounds__(64) void ransac_sample_kernel(RansacState* __restri
         }
         __syncthreads();
     };
-    if (N < kWalkBatchN) {
-#ifdef MIM_WALK_PROF
-        long long tw = 0, tc = 0, tr0 = 0, t00 = clock64();
-        int rounds = 0, atts = 0, refills = 0;
-#endif
-        // ---- small n: dense redraws (repeated indices) end the sub-rounds below after a few
-        // attempts, so walk the chain on the attempt lengths alone (known from the flags), 64
-        // attempts at a time, then evaluate their checkSubset one per lane and settle passes,
-        // the wanted iteration and the 10000-rejection failure on the ballot of the 64 ----
-        while (!stop_all && produced < target) {
-            long long q = rel, pos_mine = 0, lineq = -1;
-            int f_mine = 0, cnt = 0;
-            uint4 line = make_uint4(0, 0, 0, 0);  // the 16 flag bytes around q (attempts are >= 4 apart)
-            for (int j = 0; j < 64; ++j) {
-                if (q < lb || q >= lb + kFlagWin) {
-#ifdef MIM_WALK_PROF
-                    const long long ta = clock64();
-#endif
-                    refill(q & ~15LL);
-                    lineq = -1;
-#ifdef MIM_WALK_PROF
-                    tr0 += clock64() - ta;
-                    ++refills;
-#endif
-                }
-                if ((q & ~15LL) != lineq) {
-                    lineq = q & ~15LL;
-                    line = *reinterpret_cast<const uint4*>(win + (lineq - lb));
-                }
-                const int wsel = (int)(q >> 2) & 3;
-                const uint32_t wd = wsel == 0 ? line.x : wsel == 1 ? line.y : wsel == 2 ? line.z : line.w;
-                int fi = uni((int)((wd >> (8 * (int)(q & 3))) & 0xFF));  // uniform: scalar control flow
-                if (fi == kFlagUnknown) {  // past the precomputed window: evaluate here (uniform)
-                    if (j > 0) break;
-                    fi = uni(attempt_flag(wbase + q, stream, slen, N, M, P));
-                }
-                if (fi == kAttemptSerial) {  // a very long redraw run or the stream end: alone
-                    if (j > 0) break;
-                    int idx[4] = {0, 0, 0, 0};
-                    const int len = uni(resolve_at(wbase + q, stream, slen, N, M, idx));
-                    if (len == 0) {  // RNG stream exhausted: report, never guess
-                        if (lane == 0) atomicOr(err, 1);
-                        S.fail_iter = -2;
-                        stop_all = true;
-                        break;
-                    }
-                    const float4 a = P[idx[0]], b = P[idx[1]], c = P[idx[2]], d = P[idx[3]];
-                    const float s4[8] = {a.x, a.y, b.x, b.y, c.x, c.y, d.x, d.y};
-                    const float t4[8] = {a.z, a.w, b.z, b.w, c.z, c.w, d.z, d.w};
-                    // as a flag: the length beyond 4 saturates the field; `len` is carried apart
-                    fi = (len == 4 ? 0 : 0x7E) | uni(check_subset(s4, t4) ? 1 : 0);
-                    if (lane == 0) { pos_mine = q; f_mine = fi; }
-                    q += len;
-                    cnt = 1;
-                    break;
-                }
-                if (lane == j) { pos_mine = q; f_mine = fi; }
-                q += 4 + ((fi & 0x7E) >> 1);
-                cnt = j + 1;
-            }
-            if (stop_all) break;
-#ifdef MIM_WALK_PROF
-            const long long tb = clock64();
-            tw += tb - t00;
-            ++rounds;
-            atts += cnt;
-#endif
-            // checkSubset of the attempts whose pass bit is not known yet, one per lane
-            int pass = 0;
-            if (lane < cnt) {
-                if (f_mine & kPassUnknown) pass = attempt_flag(wbase + pos_mine, stream, slen, N, M, P) & 1;
-                else pass = f_mine & 1;
-            }
-            const unsigned long long Pm = __ballot(lane < cnt && pass);
-            const int need = target - produced;
-            const int a_p = Pm ? ctz64(Pm) : cnt;  // first pass
-            const int af = fail_run + a_p >= 10000 ? 10000 - fail_run - 1 : BIG;  // the 10000th rejection
-            int at = BIG;  // attempt completing the chunk's last wanted iteration
-            if (__popcll(Pm) >= need) {
-                unsigned long long m = Pm;
-                for (int k = 1; k < need; ++k) m &= m - 1;
-                at = ctz64(m);
-            }
-            int stop = cnt - 1, got = __popcll(Pm);
-            bool hit_t = false, hit_f = false;
-            if (af < BIG) { stop = af; hit_f = true; got = 0; }
-            else if (at < BIG) { stop = at; hit_t = true; got = need; }
-            if (pass && lane <= stop && !hit_f) {
-                const int rank = mbcnt64(Pm);
-                out[produced + rank] = make_int4((int)(wbase + pos_mine), (f_mine & 0x7E) ? -2 : -1, 0, 0);
-            }
-            produced += got;
-            fail_run = hit_t ? 0 : (hit_f ? 10000 : (Pm ? cnt - 1 - (63 - clz64(Pm)) : fail_run + cnt));
-            // next attempt: after `stop` (the walk's end when stop is the last one)
-            if (stop == cnt - 1) {
-                rel = uni64(q);
-            } else {
-                const long long ps = uni64(__shfl(pos_mine, stop));
-                const int fs = uni(__shfl(f_mine, stop));
-                rel = ps + 4 + ((fs & 0x7E) >> 1);
-            }
-            if (hit_f) {
-                S.fail_iter = produced;  // getSubset returned false in this iteration
-                stop_all = true;
-            }
-            if (hit_t) stop_all = true;
-#ifdef MIM_WALK_PROF
-            t00 = clock64();
-            tc += t00 - tb;
-#endif
-        }
-#ifdef MIM_WALK_PROF
-        if (lane == 0)
-            printf("[walk] p=%d N=%u produced=%d rounds=%d attempts=%d refills=%d walk=%lld (refill %lld) check=%lld wlen=%d\n",
-                   p, N, produced, rounds, atts, refills, tw, tr0, tc, wlen);
-#endif
-    }
     while (!stop_all && produced < target) {
         const long long wb = rel & ~15LL;
         if (wb < lb || wb + 1024 > lb + kFlagWin) refill(wb);  // refill the LDS window at wb
@@ -3418,9 +3463,7 @@ void ransac_enqueue(const RansacParams& prm, int n_probs, const ProbDev* probs, 
         // attempt outcomes for a window of ~28 draws per wanted iteration (pass rate ~1/5), the walk
         // falls back to inline evaluation past the window
         // (a multiple of 64: flags are read as 16-byte vectors, pass bits as 32-bit words)
-        // the first chunk of a maxIters <= 4,096 batch sizes the window for the small problems' rate
-        const long long rate = (c0 == 0 && max_iters <= 4096) ? (long long)kRateSmallN : (long long)kRateLargeN;
-        const int wcap = (int)(std::min<long long>((long long)(c1 - c0) * rate + 4096, b.flag_cap / std::max(n_probs, 1)) & ~63LL);
+        const int wcap = (int)(std::min<long long>((long long)(c1 - c0) * 28 + 4096, b.flag_cap / std::max(n_probs, 1)) & ~63LL);
         const int bppw = (wcap + kAttemptSpan - 1) / kAttemptSpan;
         ransac_attempt_kernel<<<n_probs * bppw, 256, 0, ss>>>(b.state, b.stream, b.stream_len, b.flags, wcap, bppw, c1);
         mark(mark_ctx, "attempt", ss);
@@ -3441,7 +3484,7 @@ void ransac_enqueue(const RansacParams& prm, int n_probs, const ProbDev* probs, 
             mark(mark_ctx, "chain", ss);
         }
         ransac_small_kernel<<<n_probs, kSmallThreads, 0, ss>>>(b.state, probs, pts, b.stream, b.stream_len, b.samples,
-                                                              c1, b.flags, wcap, use_chain);
+                                                              c1, b.err);
         ransac_sample_kernel<<<n_probs, 64, 0, ss>>>(b.state, probs, pts, b.stream, b.stream_len, b.samples, c1, b.err,
                                                     b.flags, wcap, use_chain);
         mark(mark_ctx, "sample", ss);

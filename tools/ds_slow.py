@@ -1,4 +1,5 @@
-"""Diagnostic: per-problem sampler time on one scene of the full dataset (all models)."""
+"""Diagnostic: per-problem sampler time on one scene of the full dataset (all models); saves the three
+slowest match sets to gpurun_out/ds_slow.npz (copied to tests/golden/ds_small_problems.npz)."""
 import json
 import os
 import sys

@@ -86,6 +86,12 @@ struct Arena {
         return hipSuccess;
     }
     void rewind() { chunk_i = 0; off = 0; }
+    struct Mark {
+        size_t chunk_i, off;
+        bool operator<(const Mark& o) const { return chunk_i < o.chunk_i || (chunk_i == o.chunk_i && off < o.off); }
+    };
+    Mark pos() const { return Mark{chunk_i, off}; }
+    void seek(Mark m) { chunk_i = m.chunk_i; off = m.off; }
     void release() {
         for (auto& c : chunks) (void)hipFree(c.first);
         chunks.clear();
@@ -95,6 +101,7 @@ struct Arena {
 
 struct SetRec {
     SetDev d;
+    Arena::Mark mark;  // the arena before the set's storage (mim_sets_truncate)
 };
 
 // Pinned staging for the per-batch tables, two generations: a batch's host->device table copies
@@ -171,6 +178,8 @@ struct mim_ctx {
     // sets created since the last batch: their prep runs as one launch at the next build_tables
     std::vector<PrepJob> pend;
     std::vector<int> pend_set;
+    // per prep flush: the lowest set id it covered and the arena after its flags block
+    std::vector<std::pair<int, Arena::Mark>> flushes;
     PinnedStage prep_stage;
     DevBuf prep_jobs;
     int last_n = 0;
@@ -340,6 +349,7 @@ static mim_status set_create_locked(mim_ctx* c, const float* desc, const float* 
     if (dim != kDim) return fail(c, MIM_EINVAL, "set_create: dim must be %d (got %d)", kDim, dim);
     HIPCHK(c, hipSetDevice(c->device));
     SetRec r{};
+    r.mark = c->arena.pos();
     r.d.n = n;
     r.d.n_tiles = (n + 63) / 64;
     const size_t tiles = (size_t)std::max(r.d.n_tiles, 1);
@@ -394,6 +404,7 @@ static mim_status flush_preps(mim_ctx* c) {
     HIPCHK(c, c->prep_stage.release_after(c->stream));
     launch_prep_batch(c->prep_jobs.as<PrepJob>(), nj, tiles, c->stream);
     HIPCHK(c, hipGetLastError());
+    c->flushes.push_back({*std::min_element(c->pend_set.begin(), c->pend_set.end()), c->arena.pos()});
     c->pend.clear();
     c->pend_set.clear();
     return MIM_OK;
@@ -415,7 +426,38 @@ mim_status mim_sets_clear(mim_ctx* c) {
     c->sets.clear();
     c->pend.clear();
     c->pend_set.clear();
+    c->flushes.clear();
     c->arena.rewind();
+    ++c->sets_gen;
+    return MIM_OK;
+}
+
+mim_status mim_sets_truncate(mim_ctx* c, int32_t n_keep) {
+    if (!c) return MIM_EINVAL;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (n_keep < 0 || n_keep > (int)c->sets.size())
+        return fail(c, MIM_EINVAL, "sets_truncate: %d sets registered, %d to keep", (int)c->sets.size(), n_keep);
+    if (n_keep == (int)c->sets.size()) return MIM_OK;
+    HIPCHK(c, hipSetDevice(c->device));
+    // the dropped sets' pending preps go; their storage (and prep flags blocks that cover only dropped
+    // sets) is reused by later sets, ordered on the ctx stream after the work already enqueued, as
+    // for mim_sets_clear
+    size_t m = 0;
+    for (size_t j = 0; j < c->pend.size(); ++j)
+        if (c->pend_set[j] < n_keep) {
+            c->pend[m] = c->pend[j];
+            c->pend_set[m++] = c->pend_set[j];
+        }
+    c->pend.resize(m);
+    c->pend_set.resize(m);
+    Arena::Mark target = c->sets[n_keep].mark;
+    for (const auto& f : c->flushes)
+        if (f.first < n_keep && target < f.second) target = f.second;  // a kept set's flags lie beyond
+    c->flushes.erase(std::remove_if(c->flushes.begin(), c->flushes.end(),
+                                    [n_keep](const std::pair<int, Arena::Mark>& f) { return f.first >= n_keep; }),
+                     c->flushes.end());
+    c->arena.seek(target);
+    c->sets.resize(n_keep);
     ++c->sets_gen;
     return MIM_OK;
 }

@@ -114,24 +114,41 @@ struct Taps {
     int n;
 };
 
-__global__ void blur_row_kernel(const float* __restrict__ src, float* __restrict__ dst, int rows, int cols, Taps t) {
-    const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
-    if (x >= cols) return;
-    const float* S = src + (size_t)y * cols;
-    const int a = t.n / 2;
-    float acc = t.k[0] * S[reflect101(x - a, cols)];
-    for (int i = 1; i < t.n; ++i) acc += t.k[i] * S[reflect101(x - a + i, cols)];
-    dst[(size_t)y * cols + x] = acc;
-}
+// GaussianBlur (sepFilter2D, BORDER_REFLECT_101) of one 64 x 16 output tile: the source rows the
+// column pass needs (reflected) are staged in LDS with their reflected column margins, the row pass
+// writes its 16 + 2a rows x 64 columns to LDS, the column pass reads them.  Each output is computed
+// with the same float operations in the same order as the separate row / column passes of OpenCV's
+// filter engine (row: k0 s0 + k1 s1 + ...; column, symmetric kernel: k_a m + sum of k_{a+i} (m_+i + m_-i)).
+constexpr int kBlurTW = 64, kBlurTH = 16;
 
-__global__ void blur_col_kernel(const float* __restrict__ src, float* __restrict__ dst, int rows, int cols, Taps t) {
-    const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
-    if (x >= cols) return;
-    const int a = t.n / 2;
-    float acc = t.k[a] * src[(size_t)y * cols + x] + 0.f;
-    for (int i = 1; i <= a; ++i)
-        acc += t.k[a + i] * (src[(size_t)reflect101(y + i, rows) * cols + x] + src[(size_t)reflect101(y - i, rows) * cols + x]);
-    dst[(size_t)y * cols + x] = acc;
+__global__ __launch_bounds__(256) void blur_kernel(const float* __restrict__ src, float* __restrict__ dst, int rows,
+                                                   int cols, Taps t) {
+    extern __shared__ float lds[];
+    const int a = t.n / 2, W = kBlurTW + 2 * a, H = kBlurTH + 2 * a;
+    float* in = lds;             // H x W
+    float* mid = lds + H * W;    // H x kBlurTW
+    const int x0 = blockIdx.x * kBlurTW, y0 = blockIdx.y * kBlurTH, tid = threadIdx.x;
+    for (int e = tid; e < H * W; e += 256) {
+        const int r = e / W, c = e - r * W;
+        in[e] = src[(size_t)reflect101(y0 - a + r, rows) * cols + reflect101(x0 - a + c, cols)];
+    }
+    __syncthreads();
+    for (int e = tid; e < H * kBlurTW; e += 256) {
+        const int r = e / kBlurTW, c = e - r * kBlurTW;
+        const float* S = in + r * W + c;
+        float acc = t.k[0] * S[0];
+        for (int i = 1; i < t.n; ++i) acc += t.k[i] * S[i];
+        mid[e] = acc;
+    }
+    __syncthreads();
+    for (int e = tid; e < kBlurTH * kBlurTW; e += 256) {
+        const int r = e / kBlurTW, c = e - r * kBlurTW, y = y0 + r, x = x0 + c;
+        if (y >= rows || x >= cols) continue;
+        const float* M = mid + (r + a) * kBlurTW + c;
+        float acc = t.k[a] * M[0] + 0.f;
+        for (int i = 1; i <= a; ++i) acc += t.k[a + i] * (M[i * kBlurTW] + M[-i * kBlurTW]);
+        dst[(size_t)y * cols + x] = acc;
+    }
 }
 
 __global__ void down2_kernel(const float* __restrict__ src, int scols, float* __restrict__ dst, int rows, int cols) {
@@ -471,37 +488,40 @@ __global__ __launch_bounds__(64) void descr_kernel(const Pyr* __restrict__ pyr, 
     for (int s2 = 0; s2 < 6; ++s2)
         if (lane + 64 * s2 < kHistLen) hist[lane + 64 * s2] = h[s2];
     __syncthreads();
-    if (lane != 0) return;
-    float* out = desc + (size_t)t * 128;
-    for (int i = 0; i < kDW; i++)
-        for (int j = 0; j < kDW; j++) {
-            const int idx = ((i + 1) * (kDW + 2) + (j + 1)) * (kDB + 2);
-            hist[idx] += hist[idx + kDB];
-            hist[idx + 1] += hist[idx + kDB + 1];
-        }
-    float nrm2 = 0;
-    for (int i = 0; i < kDW; i++)
-        for (int j = 0; j < kDW; j++)
-            for (int k = 0; k < kDB; k++) {
-                const float v = hist[((i + 1) * (kDW + 2) + (j + 1)) * (kDB + 2) + k];
-                nrm2 += v * v;
-            }
+    // the orientation wrap (cells independent: one lane each), then the two norms summed in the
+    // reference's order (descriptor index order) over values held two per lane, the clamp and the
+    // x 512 rounding per lane
+    if (lane < kDW * kDW) {
+        const int idx = ((lane / kDW + 1) * (kDW + 2) + (lane % kDW + 1)) * (kDB + 2);
+        hist[idx] += hist[idx + kDB];
+        hist[idx + 1] += hist[idx + kDB + 1];
+    }
+    __syncthreads();
+    float v[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        const int k = lane + 64 * u, cell = k / kDB;  // k = (i kDW + j) kDB + o
+        v[u] = hist[((cell / kDW + 1) * (kDW + 2) + (cell % kDW + 1)) * (kDB + 2) + k % kDB];
+    }
+    auto ordered_sumsq = [&]() {
+        const float q0 = v[0] * v[0], q1 = v[1] * v[1];
+        float acc = 0;
+        for (int k = 0; k < 64; ++k) acc += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(q0), k));
+        for (int k = 0; k < 64; ++k) acc += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(q1), k));
+        return acc;
+    };
+    float nrm2 = ordered_sumsq();
     const float thr = sqrtf(nrm2) * 0.2f;
-    nrm2 = 0;
-    for (int i = 0; i < kDW; i++)
-        for (int j = 0; j < kDW; j++)
-            for (int k = 0; k < kDB; k++) {
-                float& v = hist[((i + 1) * (kDW + 2) + (j + 1)) * (kDB + 2) + k];
-                v = fminf(v, thr);
-                nrm2 += v * v;
-            }
+    v[0] = fminf(v[0], thr);
+    v[1] = fminf(v[1], thr);
+    nrm2 = ordered_sumsq();
     nrm2 = 512.f / fmaxf(sqrtf(nrm2), FLT_EPSILON);
-    for (int i = 0; i < kDW; i++)
-        for (int j = 0; j < kDW; j++)
-            for (int k = 0; k < kDB; k++) {
-                const int v = cv_round(hist[((i + 1) * (kDW + 2) + (j + 1)) * (kDB + 2) + k] * nrm2);
-                out[(i * kDW + j) * kDB + k] = (float)(v < 0 ? 0 : (v > 255 ? 255 : v));
-            }
+    float* out = desc + (size_t)t * 128;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        const int r = cv_round(v[u] * nrm2);
+        out[lane + 64 * u] = (float)(r < 0 ? 0 : (r > 255 ? 255 : r));
+    }
 }
 
 // ---- host ---------------------------------------------------------------------------------------
@@ -615,18 +635,18 @@ int sift_detect_compute(SiftWs* w, hipStream_t st, const uint8_t* img, int rows,
     const size_t img_bytes = (size_t)rows * cols;
     SCHK(grow(w->img, w->img_cap, img_bytes));
     SCHK(grow(w->pyr, w->pyr_cap, total * sizeof(float)));
-    SCHK(grow(w->tmp, w->tmp_cap, (size_t)R * C * sizeof(float) * 2));
+    SCHK(grow(w->tmp, w->tmp_cap, (size_t)R * C * sizeof(float)));
     float* P = (float*)w->pyr;
     float* T0 = (float*)w->tmp;
-    float* T1 = T0 + (size_t)R * C;
     SCHK(hipMemcpy2DAsync(w->img, cols, img, step, cols, rows, hipMemcpyHostToDevice, st));
 
     auto blur = [&](const float* s, float* d, int rr, int cc, double sigma) -> bool {
         Taps t;
         if (gauss_taps(sigma, t) < 0) return false;
-        const dim3 g((cc + 255) / 256, rr);
-        blur_row_kernel<<<g, 256, 0, st>>>(s, T1, rr, cc, t);
-        blur_col_kernel<<<g, 256, 0, st>>>(T1, d, rr, cc, t);
+        const int a = t.n / 2;
+        const size_t lds = sizeof(float) * (size_t)(kBlurTH + 2 * a) * (kBlurTW + 2 * a + kBlurTW);
+        if (lds > 64 * 1024) return false;
+        blur_kernel<<<dim3((cc + kBlurTW - 1) / kBlurTW, (rr + kBlurTH - 1) / kBlurTH), 256, lds, st>>>(s, d, rr, cc, t);
         return true;
     };
     // createInitialImage

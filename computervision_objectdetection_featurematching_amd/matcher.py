@@ -53,7 +53,9 @@ class Matcher:
         if st != _lib.MIM_OK:
             raise MimError(st, f"mim_ctx_create(device={device}) failed (no HIP device?)")
         self.device = device
-        self._borrowed = []  # device tensors the registered sets read until clear_sets (mim.h)
+        self._borrowed = []  # (set id, tensors) the registered sets read until they are dropped (mim.h)
+        self._n_sets = 0
+        self.sets_generation = 0  # bumped whenever registered sets are dropped
         self._retired = []   # (event on the matcher stream, tensors) kept alive until the event completes
 
     def close(self):
@@ -116,25 +118,42 @@ class Matcher:
             cur = torch.cuda.current_stream(desc.device)
             if cur.cuda_stream != mine.cuda_stream:
                 mine.wait_stream(cur)
-            self._borrowed += [desc, kp]
         n = int(desc.shape[0])
         sid = C.c_int32()
         self._check(self.L.mim_set_create(self._ctx, C.c_void_p(_lib.ptr(desc)), C.c_void_p(_lib.ptr(kp)), n,
                                           int(desc.shape[1]), on_dev, C.byref(sid)))
+        if on_dev:
+            self._borrowed.append((sid.value, [desc, kp]))
+        self._n_sets = sid.value + 1
         return sid.value
+
+    @property
+    def n_sets(self) -> int:
+        return self._n_sets
+
+    def _retire(self, keep: int):
+        # the dropped sets' tensors stay referenced until the work already enqueued on the matcher's
+        # stream (their last readers) has completed: an event per drop, polled at the next drops
+        # (not record_stream: the allocator would later record events on this stream after close())
+        self._retired = [(ev, ts) for ev, ts in self._retired if not ev.query()]
+        gone = [ts for sid, ts in self._borrowed if sid >= keep]
+        if gone:
+            import torch
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.ExternalStream(self.stream_handle(), device=gone[0][0].device))
+            self._retired.append((ev, gone))
+        self._borrowed = [(sid, ts) for sid, ts in self._borrowed if sid < keep]
+        self._n_sets = min(self._n_sets, keep)
+        self.sets_generation += 1
 
     def clear_sets(self):
         self._check(self.L.mim_sets_clear(self._ctx))
-        # the cleared sets' tensors stay referenced until the work already enqueued on the matcher's
-        # stream (their last readers) has completed: an event per clear, polled at the next clears
-        # (not record_stream: the allocator would later record events on this stream after close())
-        self._retired = [(ev, ts) for ev, ts in self._retired if not ev.query()]
-        if self._borrowed:
-            import torch
-            ev = torch.cuda.Event()
-            ev.record(torch.cuda.ExternalStream(self.stream_handle(), device=self._borrowed[0].device))
-            self._retired.append((ev, self._borrowed))
-        self._borrowed = []
+        self._retire(0)
+
+    def truncate_sets(self, n_keep: int):
+        """Drop the sets registered after the first n_keep (mim_sets_truncate); ids < n_keep stay."""
+        self._check(self.L.mim_sets_truncate(self._ctx, int(n_keep)))
+        self._retire(int(n_keep))
 
     # ---- primitives -----------------------------------------------------------------------
     def knn_match_arrays(self, query, train):

@@ -75,6 +75,24 @@ def detect_boxes(points: np.ndarray, bp: BoxParams | None = None) -> list[tuple[
     return [(out[i].x, out[i].y, out[i].width, out[i].height) for i in range(n.value)]
 
 
+def _model_sets(matcher: Matcher, models: list[ObjectModel]) -> list[list[int]]:
+    """The models' views as the matcher's first sets, registered once and kept across scenes: the
+    matcher's sets are detect_objects' own; a later call with the same view arrays (by identity) drops
+    only the previous scene's sets (mim_sets_truncate), anything else re-registers from scratch."""
+    arrays = [d for m in models for d in m.descriptors]
+    c = getattr(matcher, "_pipeline_models", None)
+    if (c is not None and c["gen"] == matcher.sets_generation and len(c["arrays"]) == len(arrays)
+            and all(a is b for a, b in zip(c["arrays"], arrays)) and matcher.n_sets >= c["n"]):
+        matcher.truncate_sets(c["n"])
+        c["gen"] = matcher.sets_generation
+        return c["ids"]
+    matcher.clear_sets()
+    ids = [[matcher.add_set(d, np.stack([k["x"], k["y"]], 1)) for k, d in zip(m.keypoints, m.descriptors)]
+           for m in models]
+    matcher._pipeline_models = {"arrays": arrays, "ids": ids, "n": matcher.n_sets, "gen": matcher.sets_generation}
+    return ids
+
+
 @dataclass
 class SceneRun:
     """detect_objects' intermediate products (for tests and benches)."""
@@ -97,9 +115,7 @@ def detect_objects(matcher: Matcher, scene_gray, models: list[ObjectModel], scal
         k, d = matcher.sift_detect_compute(scaled)
         scene_kp.append(k)
         scene_desc.append(d)
-    matcher.clear_sets()
-    view_ids = [[matcher.add_set(d, np.stack([k["x"], k["y"]], 1)) for k, d in zip(m.keypoints, m.descriptors)]
-                for m in models]
+    view_ids = _model_sets(matcher, models)
     scene_ids = [matcher.add_set(d, np.stack([k["x"], k["y"]], 1)) for k, d in zip(scene_kp, scene_desc)]
     tags = [(mi, si, vi) for mi in range(len(models)) for si in range(len(scales)) for vi in range(len(view_ids[mi]))]
     res = matcher.match_batch([(view_ids[mi][vi], scene_ids[si]) for mi, si, vi in tags], params)

@@ -102,6 +102,11 @@ mim_status mim_synchronize(struct mim_ctx* ctx);
 mim_status mim_set_create(struct mim_ctx* ctx, const float* desc, const float* kp_xy, int32_t n,
                           int32_t dim, int32_t on_device, int32_t* set_id);
 mim_status mim_sets_clear(struct mim_ctx* ctx);
+/* Drops the sets registered after the first n_keep (ids >= n_keep) and reuses their device storage;
+ * the first n_keep keep their ids and layout.  The same rules as mim_sets_clear for work already
+ * enqueued and borrowed pointers.  For a caller that keeps its model views registered across
+ * scenes and replaces only the scene scales (TestsDetector.cpp:38-107 recomputes neither). */
+mim_status mim_sets_truncate(struct mim_ctx* ctx, int32_t n_keep);
 
 /* ---- primitive ops, host buffers, synchronous ------------------------------------------------
  * Each primitive call replaces the ctx's "last batch": after mim_knn2_l2 / mim_ratio_filter /

@@ -223,7 +223,8 @@ struct mim_ctx {
     std::vector<Ev> evs;
     std::vector<hipEvent_t> ev_pool;  // recycled events (creating one per mark costs host time)
     std::map<std::string, double> last_ms;
-    mim::SiftWs* sift = nullptr;  // SIFT pyramid / candidate / descriptor workspace (first use)
+    mim::SiftWs* sift = nullptr;
+    std::vector<mim::SiftWs*> sift_scales;  // mim_sift_detect_compute_scales: one per scale + the scene  // SIFT pyramid / candidate / descriptor workspace (first use)
 };
 
 static mim_status fail(mim_ctx* c, mim_status code, const char* fmt, ...) {
@@ -302,6 +303,7 @@ void mim_ctx_destroy(mim_ctx* c) {
         if (e) (void)hipEventDestroy(e);
     if (c->samp) (void)hipStreamDestroy(c->samp);
     mim::sift_ws_destroy(c->sift);
+    for (mim::SiftWs* w : c->sift_scales) mim::sift_ws_destroy(w);
     c->stage.destroy();
     c->prep_stage.destroy();
     c->arena.release();
@@ -779,6 +781,27 @@ mim_status mim_sift_detect_compute(mim_ctx* c, const uint8_t* gray, int32_t rows
     *n_kp = n;
     if (r == -1) return MIM_EDEVICE;
     if (r == -2) return MIM_ERANGE;
+    return MIM_OK;
+}
+
+mim_status mim_sift_detect_compute_scales(mim_ctx* c, const uint8_t* gray, int32_t rows, int32_t cols, int64_t step,
+                                          int32_t n_scales, const float* scales, int32_t max_kp, mim_keypoint* kps,
+                                          float* desc, int32_t* n_kp) {
+    if (!c) return MIM_EINVAL;
+    if (!gray || !n_kp || !scales || n_scales <= 0 || n_scales > 64 || rows <= 0 || cols <= 0 || step < cols ||
+        max_kp < 0 || (max_kp > 0 && (!kps || !desc)))
+        return fail(c, MIM_EINVAL, "sift_detect_compute_scales: bad arguments");
+    for (int i = 0; i < n_scales; ++i)
+        if (!(scales[i] > 0)) return fail(c, MIM_EINVAL, "sift_detect_compute_scales: scale %d is not > 0", i);
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIPCHK(c, hipSetDevice(c->device));
+    std::vector<int> n(n_scales, 0);
+    const int r = mim::sift_detect_compute_scales(c->sift_scales, c->stream, gray, rows, cols, step, n_scales, scales,
+                                                  max_kp, kps, desc, n.data(), c->err);
+    for (int i = 0; i < n_scales; ++i) n_kp[i] = n[i];
+    if (r == -1) return MIM_EDEVICE;
+    if (r == -2) return MIM_ERANGE;
+    if (r == -3) return MIM_EINVAL;
     return MIM_OK;
 }
 

@@ -145,6 +145,7 @@ struct RansacBufs {
 // mim_resize_linear_u8 (api.cpp).  Return 0, -1 on a HIP error, -2 on a bad argument / capacity;
 // `err` gets the text.
 #include <string>
+#include <vector>
 #include "../../include/mim.h"
 namespace mim {
 struct SiftWs;
@@ -153,6 +154,9 @@ void sift_ws_destroy(SiftWs* w);
 int sift_detect_compute(SiftWs* w, hipStream_t st, const uint8_t* img, int rows, int cols, long long step,
                         const uint8_t* mask, long long mstep, int max_kp, mim_keypoint* kps, float* desc, int* n_out,
                         std::string& err);
+int sift_detect_compute_scales(std::vector<SiftWs*>& ws, hipStream_t st, const uint8_t* img, int rows, int cols,
+                               long long step, int n_scales, const float* scales, int max_kp, mim_keypoint* kps,
+                               float* desc, int* n_out, std::string& err);
 int sift_resize_u8(SiftWs* w, hipStream_t st, const uint8_t* src, int rows, int cols, long long step, uint8_t* dst,
                    int drows, int dcols, double fx, double fy, std::string& err);
 }  // namespace mim

@@ -608,17 +608,43 @@ int sift_resize_u8(SiftWs* w, hipStream_t st, const uint8_t* src, int rows, int 
     return 0;
 }
 
-int sift_detect_compute(SiftWs* w, hipStream_t st, const uint8_t* img, int rows, int cols, long long step,
-                        const uint8_t* mask, long long mstep, int max_kp, mim_keypoint* kps, float* desc, int* n_out,
-                        std::string& err) {
-    *n_out = 0;
-    const int R = rows * 2, C = cols * 2;
-    const int n_oct = (int)lrint(log((double)std::min(R, C)) / log(2.) - 2) + 1;
-    if (n_oct < 1) return 0;  // no octave (sides < 2 px after doubling): no keypoints, as OpenCV
-    if (n_oct > 16) {
+// One image of a SIFT call: its workspace (the 8-bit image already in w->img, rows x cols packed),
+// its mask (host, optional), where its keypoints / descriptors go and their capacity.
+struct SiftJob {
+    SiftWs* w;
+    int rows, cols;
+    const uint8_t* mask;
+    long long mstep;
+    int cap;
+    mim_keypoint* kps;
+    float* desc;
+    int n = 0;  // keypoints found (may exceed cap: then only cap are written)
+    // internal
+    int n_oct = 0;
+    Pyr h_pyr{};
+    int* d_cnt = nullptr;
+    Cand* d_cand = nullptr;
+    mim_keypoint* d_kp = nullptr;
+    Surv* d_surv = nullptr;
+    Pyr* d_pyr = nullptr;
+    int h_cnt[3] = {0, 0, 0};
+    std::vector<mim_keypoint> k;
+};
+
+constexpr int kCandCap = 1 << 20, kKpCap = 1 << 19;
+
+// Gaussian pyramid, DoG and the scale-space extrema of one image (enqueued; the candidate count is
+// copied to J.h_cnt[0])
+static int sift_build(SiftJob& J, hipStream_t st, std::string& err) {
+    SiftWs* w = J.w;
+    const int R = J.rows * 2, C = J.cols * 2;
+    J.n_oct = (int)lrint(log((double)std::min(R, C)) / log(2.) - 2) + 1;
+    if (J.n_oct < 1) return 0;  // no octave (sides < 2 px after doubling): no keypoints, as OpenCV
+    if (J.n_oct > 16) {
         err = "image too large for SIFT (more than 16 octaves)";
         return -2;
     }
+    const int n_oct = J.n_oct;
     // pyramid layout: per octave 6 Gaussian + 5 DoG planes
     std::vector<int> orows(n_oct), ocols(n_oct);
     std::vector<size_t> goff(n_oct), doff(n_oct);
@@ -632,13 +658,10 @@ int sift_detect_compute(SiftWs* w, hipStream_t st, const uint8_t* img, int rows,
         doff[o] = total;
         total += plane * (kNOL + 2);
     }
-    const size_t img_bytes = (size_t)rows * cols;
-    SCHK(grow(w->img, w->img_cap, img_bytes));
     SCHK(grow(w->pyr, w->pyr_cap, total * sizeof(float)));
     SCHK(grow(w->tmp, w->tmp_cap, (size_t)R * C * sizeof(float)));
     float* P = (float*)w->pyr;
     float* T0 = (float*)w->tmp;
-    SCHK(hipMemcpy2DAsync(w->img, cols, img, step, cols, rows, hipMemcpyHostToDevice, st));
 
     auto blur = [&](const float* s, float* d, int rr, int cc, double sigma) -> bool {
         Taps t;
@@ -650,7 +673,7 @@ int sift_detect_compute(SiftWs* w, hipStream_t st, const uint8_t* img, int rows,
         return true;
     };
     // createInitialImage
-    up2_kernel<<<dim3((C + 255) / 256, R), 256, 0, st>>>((const uint8_t*)w->img, rows, cols, T0);
+    up2_kernel<<<dim3((C + 255) / 256, R), 256, 0, st>>>((const uint8_t*)w->img, J.rows, J.cols, T0);
     const float sig_diff = sqrtf(std::max(1.6f * 1.6f - 0.5f * 0.5f * 4, 0.01f));
     if (!blur(T0, P + goff[0], R, C, sig_diff)) { err = "kernel size"; return -2; }
     // buildGaussianPyramid + DoG
@@ -673,13 +696,13 @@ int sift_detect_compute(SiftWs* w, hipStream_t st, const uint8_t* img, int rows,
     }
     SCHK(hipGetLastError());
     // layer table
-    Pyr h_pyr{};
+    Pyr& h_pyr = J.h_pyr;
     for (int o = 0; o < n_oct; ++o) {
         const size_t plane = (size_t)orows[o] * ocols[o];
         for (int i = 0; i < kNOL + 3; ++i) h_pyr.gauss[o][i] = Layer{P + goff[o] + i * plane, orows[o], ocols[o]};
         for (int i = 0; i < kNOL + 2; ++i) h_pyr.dog[o][i] = Layer{P + doff[o] + i * plane, orows[o], ocols[o]};
     }
-    const int cand_cap = 1 << 20, kp_cap = 1 << 19;
+    const int cand_cap = kCandCap, kp_cap = kKpCap;
     const size_t aux_bytes = sizeof(Pyr) + 256 + sizeof(Cand) * cand_cap + sizeof(mim_keypoint) * kp_cap +
                              sizeof(Surv) * cand_cap;
     SCHK(grow(w->aux, w->aux_cap, aux_bytes));
@@ -689,6 +712,11 @@ int sift_detect_compute(SiftWs* w, hipStream_t st, const uint8_t* img, int rows,
     Cand* d_cand = (Cand*)(A + sizeof(Pyr) + 256);
     mim_keypoint* d_kp = (mim_keypoint*)(d_cand + cand_cap);
     Surv* d_surv = (Surv*)(d_kp + kp_cap);
+    J.d_pyr = d_pyr;
+    J.d_cnt = d_cnt;
+    J.d_cand = d_cand;
+    J.d_kp = d_kp;
+    J.d_surv = d_surv;
     SCHK(hipMemcpyAsync(d_pyr, &h_pyr, sizeof(Pyr), hipMemcpyHostToDevice, st));
     SCHK(hipMemsetAsync(d_cnt, 0, 3 * sizeof(int), st));
     const int threshold = (int)floor(0.5 * 0.04 / kNOL * 255);
@@ -697,23 +725,38 @@ int sift_detect_compute(SiftWs* w, hipStream_t st, const uint8_t* img, int rows,
         extrema_kernel<<<dim3((ocols[o] - 2 * kBorder + 127) / 128, orows[o] - 2 * kBorder, kNOL), 128, 0, st>>>(
             P + doff[o], orows[o], ocols[o], o, threshold, d_cand, d_cnt, cand_cap);
     }
-    int h_cnt[2] = {0, 0};
-    SCHK(hipMemcpyAsync(h_cnt, d_cnt, sizeof(int), hipMemcpyDeviceToHost, st));
-    SCHK(hipStreamSynchronize(st));
-    if (h_cnt[0] > cand_cap) { err = "more than 2^20 SIFT candidates"; return -2; }
-    if (h_cnt[0] > 0) {
-        refine_kernel<<<(h_cnt[0] + 127) / 128, 128, 0, st>>>(d_pyr, d_cand, d_cnt, cand_cap, d_surv, d_cnt + 2, cand_cap);
+    SCHK(hipMemcpyAsync(J.h_cnt, d_cnt, sizeof(int), hipMemcpyDeviceToHost, st));
+    return 0;
+}
+
+// adjustLocalExtrema + orientations of the candidates (enqueued; keypoint count to J.h_cnt[1])
+static int sift_orient(SiftJob& J, hipStream_t st, std::string& err) {
+    if (J.n_oct < 1) return 0;
+    if (J.h_cnt[0] > kCandCap) { err = "more than 2^20 SIFT candidates"; return -2; }
+    if (J.h_cnt[0] > 0) {
+        refine_kernel<<<(J.h_cnt[0] + 127) / 128, 128, 0, st>>>(J.d_pyr, J.d_cand, J.d_cnt, kCandCap, J.d_surv, J.d_cnt + 2,
+                                                              kCandCap);
         // survivors <= candidates: blocks past the survivor count return at once
-        orient_kernel<<<h_cnt[0], 64, 0, st>>>(d_pyr, d_surv, d_cnt + 2, cand_cap, d_kp, d_cnt + 1, kp_cap);
+        orient_kernel<<<J.h_cnt[0], 64, 0, st>>>(J.d_pyr, J.d_surv, J.d_cnt + 2, kCandCap, J.d_kp, J.d_cnt + 1, kKpCap);
     }
     SCHK(hipGetLastError());
-    SCHK(hipMemcpyAsync(h_cnt + 1, d_cnt + 1, sizeof(int), hipMemcpyDeviceToHost, st));
-    SCHK(hipStreamSynchronize(st));
-    if (h_cnt[1] > kp_cap) { err = "more than 2^19 SIFT keypoints"; return -2; }
-    std::vector<mim_keypoint> k(h_cnt[1]);
-    if (!k.empty()) SCHK(hipMemcpyAsync(k.data(), d_kp, sizeof(mim_keypoint) * k.size(), hipMemcpyDeviceToHost, st));
-    SCHK(hipStreamSynchronize(st));
-    // removeDuplicatedSorted, the octave -1 rescale, runByPixelsMask (features2d keypoint.cpp, sift)
+    SCHK(hipMemcpyAsync(J.h_cnt + 1, J.d_cnt + 1, sizeof(int), hipMemcpyDeviceToHost, st));
+    return 0;
+}
+
+static int sift_fetch_kp(SiftJob& J, hipStream_t st, std::string& err) {
+    if (J.n_oct < 1) return 0;
+    if (J.h_cnt[1] > kKpCap) { err = "more than 2^19 SIFT keypoints"; return -2; }
+    J.k.resize(J.h_cnt[1]);
+    if (!J.k.empty()) SCHK(hipMemcpyAsync(J.k.data(), J.d_kp, sizeof(mim_keypoint) * J.k.size(), hipMemcpyDeviceToHost, st));
+    return 0;
+}
+
+// removeDuplicatedSorted, the octave -1 rescale, runByPixelsMask (features2d keypoint.cpp, sift) on
+// the host, then the descriptors of the first cap keypoints (enqueued, into J.desc)
+static int sift_describe(SiftJob& J, hipStream_t st, std::string& err) {
+    if (J.n_oct < 1) return 0;
+    std::vector<mim_keypoint>& k = J.k;
     std::sort(k.begin(), k.end(), kp_greater);
     size_t m = 0;
     for (size_t j = 0; j < k.size(); ++j) {
@@ -728,24 +771,120 @@ int sift_detect_compute(SiftWs* w, hipStream_t st, const uint8_t* img, int rows,
         p.y *= 0.5f;
         p.size *= 0.5f;
     }
-    if (mask) {
+    if (J.mask) {
         m = 0;
         for (size_t j = 0; j < k.size(); ++j) {
             const int yy = (int)(k[j].y + 0.5f), xx = (int)(k[j].x + 0.5f);
-            if (mask[(size_t)yy * mstep + xx] != 0) k[m++] = k[j];
+            if (J.mask[(size_t)yy * J.mstep + xx] != 0) k[m++] = k[j];
         }
         k.resize(m);
     }
-    *n_out = (int)k.size();
-    const int n = std::min((int)k.size(), max_kp);
+    J.n = (int)k.size();
+    const int n = std::min(J.n, J.cap);
     if (n <= 0) return 0;
-    SCHK(hipMemcpyAsync(d_kp, k.data(), sizeof(mim_keypoint) * n, hipMemcpyHostToDevice, st));
-    SCHK(grow(w->desc, w->desc_cap, sizeof(float) * 128 * (size_t)n));
-    descr_kernel<<<n, 64, 0, st>>>(d_pyr, d_kp, n, (float*)w->desc);
+    SCHK(hipMemcpyAsync(J.d_kp, k.data(), sizeof(mim_keypoint) * n, hipMemcpyHostToDevice, st));
+    SCHK(grow(J.w->desc, J.w->desc_cap, sizeof(float) * 128 * (size_t)n));
+    descr_kernel<<<n, 64, 0, st>>>(J.d_pyr, J.d_kp, n, (float*)J.w->desc);
     SCHK(hipGetLastError());
-    SCHK(hipMemcpyAsync(desc, w->desc, sizeof(float) * 128 * (size_t)n, hipMemcpyDeviceToHost, st));
+    SCHK(hipMemcpyAsync(J.desc, J.w->desc, sizeof(float) * 128 * (size_t)n, hipMemcpyDeviceToHost, st));
+    std::copy(k.begin(), k.begin() + n, J.kps);
+    return 0;
+}
+
+// every stage for all images, then one synchronisation per stage (4 per call)
+static int sift_run(std::vector<SiftJob>& jobs, hipStream_t st, std::string& err) {
+    for (auto& J : jobs)
+        if (int r = sift_build(J, st, err)) return r;
     SCHK(hipStreamSynchronize(st));
-    std::copy(k.begin(), k.begin() + n, kps);
+    for (auto& J : jobs)
+        if (int r = sift_orient(J, st, err)) return r;
+    SCHK(hipStreamSynchronize(st));
+    for (auto& J : jobs)
+        if (int r = sift_fetch_kp(J, st, err)) return r;
+    SCHK(hipStreamSynchronize(st));
+    for (auto& J : jobs)
+        if (int r = sift_describe(J, st, err)) return r;
+    SCHK(hipStreamSynchronize(st));  // the descriptors (and the kps copies' sources) before returning
+    return 0;
+}
+
+int sift_detect_compute(SiftWs* w, hipStream_t st, const uint8_t* img, int rows, int cols, long long step,
+                        const uint8_t* mask, long long mstep, int max_kp, mim_keypoint* kps, float* desc, int* n_out,
+                        std::string& err) {
+    *n_out = 0;
+    SCHK(grow(w->img, w->img_cap, (size_t)rows * cols));
+    SCHK(hipMemcpy2DAsync(w->img, cols, img, step, cols, rows, hipMemcpyHostToDevice, st));
+    std::vector<SiftJob> jobs(1);
+    SiftJob& J = jobs[0];
+    J.w = w;
+    J.rows = rows;
+    J.cols = cols;
+    J.mask = mask;
+    J.mstep = mstep;
+    J.cap = max_kp;
+    J.kps = kps;
+    J.desc = desc;
+    const int r = sift_run(jobs, st, err);
+    *n_out = J.n;
+    return r;
+}
+
+// TestsDetector.cpp:99-107 for one scene: resize(scene, scaled, Size(), s, s, INTER_LINEAR) and
+// detectAndCompute(scaled) at every scale, all in one call (the scene uploaded once, the resizes on
+// the device, 4 synchronisations in all).  Keypoints / descriptors of the scales are concatenated in
+// scale order into kps / desc (capacity max_kp in all); n_out[s] = the keypoints of scale s.
+int sift_detect_compute_scales(std::vector<SiftWs*>& ws, hipStream_t st, const uint8_t* img, int rows, int cols,
+                               long long step, int n_scales, const float* scales, int max_kp, mim_keypoint* kps,
+                               float* desc, int* n_out, std::string& err) {
+    while ((int)ws.size() < n_scales + 1) ws.push_back(sift_ws_create());
+    SiftWs* src = ws[n_scales];  // the scene itself
+    SCHK(grow(src->img, src->img_cap, (size_t)rows * cols));
+    SCHK(hipMemcpy2DAsync(src->img, cols, img, step, cols, rows, hipMemcpyHostToDevice, st));
+    std::vector<SiftJob> jobs(n_scales);
+    for (int i = 0; i < n_scales; ++i) {
+        const double f = (double)scales[i];
+        const int dc = (int)lrint(cols * f), dr = (int)lrint(rows * f);  // Size() + fx: saturate_cast<int>
+        if (dc <= 0 || dr <= 0) { err = "sift scales: a scale leaves no pixels"; return -3; }
+        SiftJob& J = jobs[i];
+        J.w = ws[i];
+        J.rows = dr;
+        J.cols = dc;
+        J.mask = nullptr;
+        J.mstep = 0;
+        J.cap = 0;
+        SCHK(grow(J.w->img, J.w->img_cap, (size_t)dr * dc));
+        resize_u8_kernel<<<dim3((dc + 255) / 256, dr), 256, 0, st>>>((const uint8_t*)src->img, rows, cols,
+                                                                   (uint8_t*)J.w->img, dr, dc, 1. / f, 1. / f);
+        SCHK(hipGetLastError());
+    }
+    // capacities: in scale order, what is left of max_kp (known after the keypoint counts; set in
+    // sift_describe's order, so the stages run as sift_run but with the caps assigned before describe)
+    for (auto& J : jobs)
+        if (int r = sift_build(J, st, err)) return r;
+    SCHK(hipStreamSynchronize(st));
+    for (auto& J : jobs)
+        if (int r = sift_orient(J, st, err)) return r;
+    SCHK(hipStreamSynchronize(st));
+    for (auto& J : jobs)
+        if (int r = sift_fetch_kp(J, st, err)) return r;
+    SCHK(hipStreamSynchronize(st));
+    int used = 0;
+    for (int i = 0; i < n_scales; ++i) {
+        SiftJob& J = jobs[i];
+        J.cap = std::max(0, max_kp - used);
+        J.kps = kps + used;
+        J.desc = desc + (size_t)128 * used;
+        if (int r = sift_describe(J, st, err)) return r;
+        n_out[i] = J.n;
+        used += std::min(J.n, J.cap);
+    }
+    SCHK(hipStreamSynchronize(st));
+    int total = 0;
+    for (int i = 0; i < n_scales; ++i) total += n_out[i];
+    if (total > max_kp) {
+        err = "sift scales: more keypoints than max_kp";
+        return -2;
+    }
     return 0;
 }
 

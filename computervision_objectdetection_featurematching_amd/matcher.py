@@ -200,6 +200,27 @@ class Matcher:
             raise ValueError(f"sift_detect_compute: {n.value} keypoints > max_kp={max_kp}")
         return kps[:n.value].copy(), desc[:n.value].copy()
 
+    def sift_detect_compute_scales(self, gray, scales, max_kp: int = 1 << 20):
+        """resize(gray, Size(), s, s, INTER_LINEAR) + detectAndCompute at every scale in one call
+        (TestsDetector.cpp:99-107).  Returns [(keypoints, descriptors)] per scale, identical to
+        resize_linear + sift_detect_compute scale by scale."""
+        g = np.ascontiguousarray(gray, np.uint8)
+        if g.ndim != 2:
+            raise ValueError("sift_detect_compute_scales: a single-channel image is required")
+        sc = np.ascontiguousarray(scales, np.float32).reshape(-1)
+        kps = np.zeros(max(max_kp, 1), KEYPOINT_DTYPE)
+        desc = np.zeros((max(max_kp, 1), DIM), np.float32)
+        n = np.zeros(len(sc), np.int32)
+        self._check(self.L.mim_sift_detect_compute_scales(
+            self._ctx, C.c_void_p(g.ctypes.data), g.shape[0], g.shape[1], g.strides[0], len(sc),
+            C.c_void_p(sc.ctypes.data), max_kp, C.c_void_p(kps.ctypes.data), C.c_void_p(desc.ctypes.data),
+            C.c_void_p(n.ctypes.data)))
+        out, o = [], 0
+        for c in n:
+            out.append((kps[o:o + c].copy(), desc[o:o + c].copy()))
+            o += int(c)
+        return out
+
     def resize_linear(self, src, dsize=None, fx: float = 0.0, fy: float = 0.0):
         """cv::resize(src, dst, dsize, fx, fy, INTER_LINEAR) of a CV_8UC1 image.
 

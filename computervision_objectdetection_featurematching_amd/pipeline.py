@@ -109,12 +109,9 @@ def detect_objects(matcher: Matcher, scene_gray, models: list[ObjectModel], scal
 
     Returns [((x, y, w, h), name)], or the SceneRun when keep=True."""
     params = params or default_params()
-    scene_kp, scene_desc = [], []
-    for s in scales:  # :99-107
-        scaled = matcher.resize_linear(scene_gray, fx=s)
-        k, d = matcher.sift_detect_compute(scaled)
-        scene_kp.append(k)
-        scene_desc.append(d)
+    per_scale = matcher.sift_detect_compute_scales(scene_gray, scales)  # :99-107, all scales in one call
+    scene_kp = [k for k, _ in per_scale]
+    scene_desc = [d for _, d in per_scale]
     view_ids = _model_sets(matcher, models)
     scene_ids = [matcher.add_set(d, np.stack([k["x"], k["y"]], 1)) for k, d in zip(scene_kp, scene_desc)]
     tags = [(mi, si, vi) for mi in range(len(models)) for si in range(len(scales)) for vi in range(len(view_ids[mi]))]

@@ -169,6 +169,17 @@ typedef struct {
 mim_status mim_sift_detect_compute(struct mim_ctx* ctx, const uint8_t* gray, int32_t rows, int32_t cols,
                                    int64_t step, const uint8_t* mask, int64_t mask_step, int32_t max_kp,
                                    mim_keypoint* kps, float* desc, int32_t* n_kp);
+/* TestsDetector.cpp:99-107 for one scene in one call: for each of the n_scales scales s,
+ * resize(scene, scaled, Size(), s, s, INTER_LINEAR) then SIFT detectAndCompute(scaled) — the scene
+ * uploaded once, the resizes on the device, the stages of all scales enqueued together (4 host
+ * synchronisations in all instead of 3 per image plus one per resize).  Results are those of
+ * mim_resize_linear_u8 + mim_sift_detect_compute per scale: keypoints / descriptors concatenated in
+ * scale order into kps / desc (max_kp rows in all), n_kp[s] = keypoints of scale s.  More than max_kp
+ * in all: MIM_ERANGE with the counts set (only the first max_kp written). */
+mim_status mim_sift_detect_compute_scales(struct mim_ctx* ctx, const uint8_t* gray, int32_t rows, int32_t cols,
+                                          int64_t step, int32_t n_scales, const float* scales, int32_t max_kp,
+                                          mim_keypoint* kps, float* desc, int32_t* n_kp);
+
 
 /* cv::resize(src, dst, dsize, fx, fy, INTER_LINEAR) of a CV_8UC1 image (TestsDetector.cpp:102, the
  * scene scales).  fx, fy > 0: resize(src, dst, Size(), fx, fy) — the caller passes

@@ -20,7 +20,7 @@ Inputs (descriptors + keypoints) are resident in HBM before the timed region; ea
 the sets (the i8 layout prep is inside the step) and runs the batch.  Multi-GPU: one process per GPU
 (`--gpus N` launches N ranks through torch.distributed.run when WORLD_SIZE is unset), each rank
 owns its own scenes (weak scaling, no data-path collective); the per-problem result records are
-all-gathered over RCCL at the end of every step.  Three scene batches are in flight on one GPU
+all-gathered over RCCL at the end of every step.  Twelve scene batches are in flight on one GPU
 (--inflight).
 
 Prints ONE JSON line on rank 0 with, besides the contract fields: "roofline" (dominant kernel, HIP
@@ -78,7 +78,8 @@ def parse():
     ap.add_argument("--inflight", type=int, default=0,
                     help="scene batches in flight: one library context + HIP stream each, steps assigned "
                          "round-robin, so a batch's latency-bound RANSAC tail overlaps the next batch's kNN "
-                         "(0: 3 on one GPU, 2 with RCCL, whose stream takes one of the 4 hardware queues)")
+                         "(0: 12, c1 3; with GPU_MAX_HW_QUEUES=16 their streams, torch's and RCCL's each get a "
+                         "hardware queue)")
     ap.add_argument("--dry-run", action="store_true",
                     help="no GPU: launch the ranks, gather fake records over gloo, print the JSON line")
     return ap.parse_args()
@@ -365,6 +366,10 @@ def cpu_baseline_c1img(scene, model, run, names):
 
 def main():
     args = parse()
+    # HIP hardware queues per process (read at HIP init, inherited by launched ranks): the batches in
+    # flight each keep their own stream, and with HIP's default 4 queues streams past the 4th share a
+    # queue, serialising unrelated batches (4 queues / 3 batches 25.1k, 16 / 12 27.8k)
+    os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args))  # children only: this process never touches the GPU
     if args.dry_run:
@@ -404,7 +409,8 @@ def main():
     skp = [torch.from_numpy(k).to(dev) for k in ds.scene_kp]
     torch.cuda.synchronize()
 
-    nf = args.inflight if args.inflight > 0 else (1 if knn_only else (3 if world == 1 else 2))
+    # C3: 12 batches in flight (+11 % over 3, same box); the C1 surrogate's small batches: 3 (12: -40 %)
+    nf = args.inflight if args.inflight > 0 else (1 if knn_only else (3 if args.config == "c1" else 12))
     if nf > 1:  # the sampler stream helps one batch alone (+5 %), not batches already overlapping
         os.environ.setdefault("MIM_SAMPLER_STREAM", "0")
     matchers = [Matcher(local) for _ in range(nf)]

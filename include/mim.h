@@ -140,7 +140,10 @@ mim_status mim_batch_results(struct mim_ctx* ctx, mim_result* out);
 /* Device pointer to the n mim_result records of the last batch (valid until the next batch). */
 const mim_result* mim_batch_results_dev(struct mim_ctx* ctx);
 /* Copies the n records of the last batch into dst (device memory when dst_on_device != 0: async on
- * the ctx stream, for an RCCL gather; host memory otherwise: synchronous). */
+ * the ctx stream, for an RCCL gather; host memory otherwise: synchronous, as mim_batch_results).
+ * The device copy does not wait, so it cannot grow the stream and re-run: a record whose status is
+ * MIM_STREAM_SHORT is a problem cut short, and the caller re-runs the batch through
+ * mim_batch_results (bench.py counts such records as stream_short). */
 mim_status mim_batch_results_copy(struct mim_ctx* ctx, void* dst, int32_t dst_on_device);
 /* Waits, then copies problem i's good matches (n_good query/train indices, ascending query order)
  * and its RANSAC inlier mask (n_good bytes).  Any output may be NULL. */

@@ -80,6 +80,8 @@ def parse():
                          "round-robin, so a batch's latency-bound RANSAC tail overlaps the next batch's kNN "
                          "(0: 12, c1 3; with GPU_MAX_HW_QUEUES=16 their streams, torch's and RCCL's each get a "
                          "hardware queue)")
+    ap.add_argument("--hw-queues", type=int, default=16,
+                    help="GPU_MAX_HW_QUEUES for this process and the ranks it launches (set before HIP initialises)")
     ap.add_argument("--dry-run", action="store_true",
                     help="no GPU: launch the ranks, gather fake records over gloo, print the JSON line")
     return ap.parse_args()
@@ -369,7 +371,8 @@ def main():
     # HIP hardware queues per process (read at HIP init, inherited by launched ranks): the batches in
     # flight each keep their own stream, and with HIP's default 4 queues streams past the 4th share a
     # queue, serialising unrelated batches (4 queues / 3 batches 25.1k, 16 / 12 27.8k)
-    os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
+    # (the GPU box exports GPU_MAX_HW_QUEUES=4, HIP's default: overridden here, not defaulted)
+    os.environ["GPU_MAX_HW_QUEUES"] = str(args.hw_queues)
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args))  # children only: this process never touches the GPU
     if args.dry_run:
@@ -554,7 +557,8 @@ def main():
             "data": "synthetic SIFT-like integer descriptors (seeded)" + ("" if knn_only else
                                                                         ", planted geometric inliers"),
             "config": {"workload": workload, "problems_per_gpu": n_probs, "global_batch": world * n_probs,
-                       "parallelism": f"dp{world}", "batches_in_flight": nf},
+                       "parallelism": f"dp{world}", "batches_in_flight": nf,
+                       "hw_queues": int(os.environ["GPU_MAX_HW_QUEUES"])},
         }
         if res is not None:
             out["accepted_problems_rank0"] = int((res["status"] == 0).sum())

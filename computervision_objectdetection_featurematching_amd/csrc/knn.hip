@@ -755,11 +755,15 @@ __device__ __forceinline__ float l2sqr_sse_order(const float* q, const float* t)
 
 __global__ __launch_bounds__(256) void knn2_f32_kernel(const ProbDev* __restrict__ probs,
                                                        const KnnWork* __restrict__ works,
-                                                       Top2* __restrict__ parts) {
+                                                       Top2* __restrict__ parts, int n_works) {
     __shared__ __attribute__((aligned(16))) float tl[kTileRows * kDim];
-    const KnnWork w = works[blockIdx.x];
+    // grid-stride over the work items: the grid is capped (knn_launch), since nearly every item is
+    // integer-valued and exits at the flag test; one early-exit block per item (32 KiB of LDS, 128
+    // query VGPRs) cost ~0.12 ms of dispatch per C3 batch
+  for (int wi = blockIdx.x; wi < n_works; wi += gridDim.x) {
+    const KnnWork w = works[wi];
     const ProbDev* P = probs + w.problem;
-    if (!(*P->q.flags | *P->t.flags)) return;  // integer-valued: exact MFMA kernel handles it
+    if (!(*P->q.flags | *P->t.flags)) continue;  // integer-valued: exact MFMA kernel handles it (block-uniform)
     const int tid = threadIdx.x;
     const int nq = P->q.n, nt = P->t.n;
   for (int qo = 0; qo < kKnnBlockQ; qo += 256) {  // the work item's queries, 256 per pass
@@ -796,6 +800,8 @@ __global__ __launch_bounds__(256) void knn2_f32_kernel(const ProbDev* __restrict
         }
     }
     if (qvalid) parts[P->part_off + (long long)w.split * P->q_pad + q] = Top2{k1, i1, k2, i2};
+  }
+    __syncthreads();  // the next work item's first tile load overwrites tl
   }
 }
 
@@ -901,7 +907,7 @@ void launch_knn(const ProbDev* probs, const KnnWork* works, int n_works, Top2* p
     knn2_i8_kernel<<<n_works, kThreads, 0, st>>>(probs, works, parts);
 #endif
     knn2_rescan_kernel<<<n_works, 256, 0, st>>>(probs, works, parts);
-    knn2_f32_kernel<<<n_works, 256, 0, st>>>(probs, works, parts);
+    knn2_f32_kernel<<<std::min(n_works, 2048), 256, 0, st>>>(probs, works, parts, n_works);
 }
 
 void launch_knn_emit(const ProbDev* probs, int nq, const Top2* parts, int32_t* knn_idx, float* knn_dist,

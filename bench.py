@@ -286,21 +286,39 @@ def run_c1img(args, rank, world, local):
         d = {k: z[k] for k in z.files if not k.startswith("exp/")}
     names = sorted(k[5:] for k in d if k.startswith("view/"))
     scenes = sorted(k[6:] for k in d if k.startswith("scene/"))
-    m = Matcher(local)
-    model = process_model_views(m, "004_sugar_box", [(d[f"view/{n}"], d[f"mask/{n}"]) for n in names])
+    # scenes in flight: one library context (own streams, own copy of the model views) per host
+    # thread; a scene's host stages and synchronisations overlap the other scenes' GPU work (the
+    # C ABI calls release the GIL)
+    nf = args.inflight if args.inflight > 0 else 3
+    ms = [Matcher(local) for _ in range(nf)]
+    views = [(d[f"view/{n}"], d[f"mask/{n}"]) for n in names]
+    models = [process_model_views(mm, "004_sugar_box", views) for mm in ms]
+    m, model = ms[0], models[0]
     sid = scenes[rank % len(scenes)]
     scene = d[f"scene/{sid}"]
     n_probs = len(SCALES) * len(names)
+    for mm, md in zip(ms[1:], models[1:]):
+        detect_objects(mm, scene, [md])
     for _ in range(max(args.warmup, 1)):
         run = detect_objects(m, scene, [model], keep=True)
-    m.set_timing(not args.no_timing)
+    for mm in ms:
+        mm.set_timing(not args.no_timing)
+    out_dets = [None] * nf
+
+    def worker(k):
+        for _ in range(k, args.steps, nf):
+            out_dets[k] = detect_objects(ms[k], scene, [models[k]])
+
+    from concurrent.futures import ThreadPoolExecutor
+    pool = ThreadPoolExecutor(nf)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        dets = detect_objects(m, scene, [model])
+    list(pool.map(worker, range(nf)))
     torch.cuda.synchronize()
+    pool.shutdown()
+    dets = out_dets[0]
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
@@ -324,7 +342,8 @@ def run_c1img(args, rank, world, local):
                "data": "reference images: 29 sugar_box model views + masks, test view " + sid,
                "config": {"workload": f"c1img: detectObjects of one 640x480 scene against {len(names)} views x "
                                       f"{len(SCALES)} scales = {n_probs} problems per step per GPU",
-                          "problems_per_gpu": n_probs, "global_batch": world * n_probs, "parallelism": f"dp{world}"},
+                          "problems_per_gpu": n_probs, "global_batch": world * n_probs, "parallelism": f"dp{world}",
+                          "scenes_in_flight": nf},
                "scenes_per_s": round(world * args.steps / el, 3),
                "sift_640x480_ms": round(1e3 * statistics.median(ts), 3),
                "detections_rank0": [list(b) for b, _ in dets],
@@ -333,7 +352,8 @@ def run_c1img(args, rank, world, local):
             out["cpu_baseline"] = cpu_baseline_c1img(scene, model, run, names)
             out["parity"] = out["cpu_baseline"]["parity"]
         print(json.dumps(out), flush=True)
-    m.close()
+    for mm in ms:
+        mm.close()
     if world > 1:
         dist.destroy_process_group()
 

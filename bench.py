@@ -286,14 +286,14 @@ def run_c1img(args, rank, world, local):
         d = {k: z[k] for k in z.files if not k.startswith("exp/")}
     names = sorted(k[5:] for k in d if k.startswith("view/"))
     scenes = sorted(k[6:] for k in d if k.startswith("scene/"))
-    # scenes in flight: one library context (own streams, own copy of the model views) per host
-    # thread; a scene's host stages and synchronisations overlap the other scenes' GPU work (the
-    # C ABI calls release the GIL)
+    # scenes in flight: one library context (own streams and device copy of the model's sets) per
+    # host thread; a scene's host stages and synchronisations overlap the other scenes' GPU work (the
+    # C ABI calls release the GIL).  The model (host arrays) is computed once and shared.
     nf = args.inflight if args.inflight > 0 else 3
     ms = [Matcher(local) for _ in range(nf)]
-    views = [(d[f"view/{n}"], d[f"mask/{n}"]) for n in names]
-    models = [process_model_views(mm, "004_sugar_box", views) for mm in ms]
-    m, model = ms[0], models[0]
+    m = ms[0]
+    model = process_model_views(m, "004_sugar_box", [(d[f"view/{n}"], d[f"mask/{n}"]) for n in names])
+    models = [model] * nf
     sid = scenes[rank % len(scenes)]
     scene = d[f"scene/{sid}"]
     n_probs = len(SCALES) * len(names)

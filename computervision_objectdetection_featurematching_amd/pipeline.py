@@ -144,18 +144,38 @@ def save_detections(path: str, detections) -> None:
             f.write(f"{name} {x} {y} {x + w} {y + h}\n")
 
 
-def process_all_test_images(matcher: Matcher, scenes, models: list[ObjectModel], output_dir: str, params=None,
+def process_all_test_images(matcher, scenes, models, output_dir: str, params=None,
                             box_params: BoxParams | None = None) -> dict:
     """Output.cpp:15-57 without the file decoding and drawing: scenes = [(object folder, scene name,
     gray image)]; writes <output_dir>/<folder>/<scene name>_results.txt (scene name = the image stem,
-    e.g. "4_0001_000121-color") and returns {(folder, scene name): detections}."""
+    e.g. "4_0001_000121-color") and returns {(folder, scene name): detections}.
+
+    Scenes in flight: `matcher` may be a list of Matchers (library contexts); scene i then runs on
+    context i mod len, one host thread per context, so a scene's host stages overlap the other
+    contexts' GPU work.  The models are host arrays, registered in each context on its first scene.
+    Per-scene results are those of the one-context run (the contexts share no device state), and the
+    files and returned dict are the same."""
     import os
-    out = {}
-    for folder, name, gray in scenes:
+    from concurrent.futures import ThreadPoolExecutor
+    if isinstance(matcher, Matcher):
+        matcher = [matcher]
+    for folder, _, _ in scenes:
         os.makedirs(os.path.join(output_dir, folder), exist_ok=True)
-        dets = detect_objects(matcher, gray, models, params=params, box_params=box_params)
-        save_detections(os.path.join(output_dir, folder, f"{name}_results.txt"), dets)
-        out[(folder, name)] = dets
+    dets = [None] * len(scenes)
+
+    def worker(k):
+        for i in range(k, len(scenes), len(matcher)):
+            dets[i] = detect_objects(matcher[k], scenes[i][2], models, params=params, box_params=box_params)
+
+    if len(matcher) == 1:
+        worker(0)
+    else:
+        with ThreadPoolExecutor(len(matcher)) as pool:
+            list(pool.map(worker, range(len(matcher))))
+    out = {}
+    for (folder, name, _), d in zip(scenes, dets):
+        save_detections(os.path.join(output_dir, folder, f"{name}_results.txt"), d)
+        out[(folder, name)] = d
     return out
 
 

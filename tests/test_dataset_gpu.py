@@ -71,3 +71,30 @@ def test_dataset_end_to_end(matcher, data, tmp_path):
         means.add(float(np.float32(acc / np.float32(len(ious)))))
     assert vals["mean_iou"] in means and exp["metrics"]["mean_iou"] in means
     print("mean IoU", vals["mean_iou"], {k: v for k, v in vals.items() if k.startswith("accuracy")})
+
+
+def test_dataset_scenes_in_flight(data, tmp_path):
+    """The same run with 3 scenes in flight (3 contexts, one host thread each, scene i on context
+    i mod 3): every scene's detections equal the oracle run's."""
+    from computervision_objectdetection_featurematching_amd import Matcher
+    from computervision_objectdetection_featurematching_amd.pipeline import (process_all_test_images,
+                                                                              process_model_views)
+    imgs, exp = data
+    objs = sorted({k.split("/")[0] for k in imgs})
+    ms = [Matcher(0) for _ in range(3)]
+    try:
+        models = [process_model_views(ms[0], obj, [(imgs[k], imgs.get(k.replace("/view/", "/mask/")))
+                                                   for k in sorted(k for k in imgs if k.startswith(f"{obj}/view/"))])
+                  for obj in objs]
+        scenes = [(obj, k.split("/")[-1] + "-color", imgs[k]) for obj in objs
+                  for k in sorted(k for k in imgs if k.startswith(f"{obj}/scene/"))]
+        got = process_all_test_images(ms, scenes, models, str(tmp_path / "output"))
+        assert list(got) == [(f, n) for f, n, _ in scenes]
+        bad = [(f, n) for (f, n), dets in got.items()
+               if [[*b, nm] for b, nm in dets] != exp["scenes"][f"{f}/{n[:-6]}"]["detections"]]
+        assert not bad, bad[:3]
+        for f, n, _ in scenes:
+            assert (tmp_path / "output" / f / f"{n}_results.txt").exists()
+    finally:
+        for mm in ms:
+            mm.close()

@@ -554,6 +554,10 @@ def main():
                         r["isolated_frac"] = round(r["isolated_achieved"] / r["peak"], 4)
                 roof.update({k: v for k, v in rooflines[key].items() if k.startswith("isolated")})
             roof["others"] = {k: v for k, v in rooflines.items() if k != key}
+            if nf > 1:
+                roof["note"] = (f"achieved/frac: the kernel's HIP-event span in the timed region, where {nf} batches in "
+                                "flight share the GPU (its launches overlap the other batches' kernels); "
+                                "isolated_*: the same kernel with one batch alone")
         metric = {"c3": "matches+homographies/sec (10k x 10k SIFT, 50k RANSAC iters)",
                   "c2": "matches+homographies/sec (2k x 2k SIFT, 2k RANSAC iters)",
                   "c1": "matches+homographies/sec (C1 surrogate: 29 views x 5 scales, ragged 100-500 x 1k-4k, "

@@ -16,7 +16,7 @@ MIM_STREAM_SHORT = 5
 # every symbol include/mim.h declares (checked by tests/test_abi.py)
 EXPORTS = [
     "mim_version", "mim_default_params", "mim_ctx_create", "mim_ctx_destroy", "mim_last_error",
-    "mim_ctx_set_stream", "mim_ctx_get_stream", "mim_synchronize", "mim_set_create", "mim_sets_clear", "mim_sets_truncate",
+    "mim_ctx_set_stream", "mim_ctx_set_sampler_stream", "mim_ctx_get_stream", "mim_synchronize", "mim_set_create", "mim_sets_clear", "mim_sets_truncate",
     "mim_knn2_l2", "mim_ratio_filter", "mim_find_homography", "mim_batch_run", "mim_batch_results",
     "mim_batch_results_dev", "mim_batch_results_copy", "mim_batch_problem_detail", "mim_knn2_sets_dev", "mim_last_kernel_ms",
     "mim_set_timing", "mim_sift_detect_compute", "mim_sift_detect_compute_scales", "mim_resize_linear_u8",
@@ -101,6 +101,7 @@ def load():
     L.mim_last_kernel_ms.argtypes = [vp, C.c_char_p]
     L.mim_last_kernel_ms.restype = C.c_double
     L.mim_set_timing.argtypes = [vp, i32]
+    L.mim_ctx_set_sampler_stream.argtypes = [vp, i32]
     L.mim_sift_detect_compute.argtypes = [vp, u8p, i32, i32, C.c_int64, u8p, C.c_int64, i32, vp, f32p,
                                           C.POINTER(C.c_int32)]
     L.mim_sift_detect_compute_scales.argtypes = [vp, u8p, i32, i32, C.c_int64, i32, vp, i32, vp, f32p, vp]
@@ -109,7 +110,7 @@ def load():
     L.mim_detect_boxes.argtypes = [f32p, i32, C.POINTER(BoxParams), C.POINTER(Rect), i32, C.POINTER(C.c_int32)]
     for name in ("mim_ctx_create", "mim_ctx_set_stream", "mim_synchronize", "mim_set_create", "mim_sets_clear",
                  "mim_sets_truncate", "mim_knn2_l2", "mim_ratio_filter", "mim_find_homography", "mim_batch_run", "mim_batch_results",
-                 "mim_batch_problem_detail", "mim_knn2_sets_dev", "mim_set_timing",
+                 "mim_batch_problem_detail", "mim_knn2_sets_dev", "mim_set_timing", "mim_ctx_set_sampler_stream",
                  "mim_sift_detect_compute", "mim_sift_detect_compute_scales", "mim_resize_linear_u8",
                  "mim_detect_boxes"):
         getattr(L, name).restype = C.c_int32

@@ -324,6 +324,13 @@ mim_status mim_ctx_set_stream(mim_ctx* c, void* stream) {
     return MIM_OK;
 }
 
+mim_status mim_ctx_set_sampler_stream(mim_ctx* c, int32_t on) {
+    if (!c) return MIM_EINVAL;
+    std::lock_guard<std::mutex> lk(c->mu);
+    c->samp_on = on != 0;  // the stream itself is created on the first batch that uses it
+    return MIM_OK;
+}
+
 void* mim_ctx_get_stream(const mim_ctx* c) { return c ? (void*)c->stream : nullptr; }
 
 mim_status mim_synchronize(mim_ctx* c) {

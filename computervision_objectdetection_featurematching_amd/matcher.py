@@ -307,6 +307,11 @@ class Matcher:
         self._check(self.L.mim_knn2_sets_dev(self._ctx, qset, tset, C.c_void_p(_lib.ptr(idx_dev)),
                                              C.c_void_p(_lib.ptr(dist_dev))))
 
+    def set_sampler_stream(self, on: bool):
+        """Second-stream getSubset replay (mim_ctx_set_sampler_stream): on for a batch alone, off when
+        several contexts already overlap their batches."""
+        self._check(self.L.mim_ctx_set_sampler_stream(self._ctx, int(on)))
+
     def set_timing(self, on: bool):
         self._check(self.L.mim_set_timing(self._ctx, int(on)))
 

@@ -159,6 +159,9 @@ def process_all_test_images(matcher, scenes, models, output_dir: str, params=Non
     from concurrent.futures import ThreadPoolExecutor
     if isinstance(matcher, Matcher):
         matcher = [matcher]
+    if len(matcher) > 1:  # the contexts overlap each other: one stream each (no sampler stream)
+        for mm in matcher:
+            mm.set_sampler_stream(False)
     for folder, _, _ in scenes:
         os.makedirs(os.path.join(output_dir, folder), exist_ok=True)
     dets = [None] * len(scenes)

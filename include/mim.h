@@ -85,6 +85,11 @@ void mim_ctx_destroy(struct mim_ctx* ctx);
 const char* mim_last_error(const struct mim_ctx* ctx);
 /* Use an external HIP stream (hipStream_t cast to void*); NULL restores the ctx's own stream. */
 mim_status mim_ctx_set_stream(struct mim_ctx* ctx, void* stream);
+/* Sampler stream on (1) or off (0): with it a batch's second-chunk getSubset replay runs on a second
+ * stream of the ctx beside the first chunk's selection kernels (faster for a batch alone); off, one
+ * stream (better when several ctxs already overlap their batches).  Default: on, unless the
+ * environment has MIM_SAMPLER_STREAM=0.  Takes effect from the next batch. */
+mim_status mim_ctx_set_sampler_stream(struct mim_ctx* ctx, int32_t on);
 /* The HIP stream the ctx currently enqueues on (its own non-blocking stream unless set above). */
 void* mim_ctx_get_stream(const struct mim_ctx* ctx);
 mim_status mim_synchronize(struct mim_ctx* ctx);

@@ -392,7 +392,7 @@ def main():
     args = parse()
     # HIP hardware queues per process (read at HIP init, inherited by launched ranks): the batches in
     # flight each keep their own stream, and with HIP's default 4 queues streams past the 4th share a
-    # queue, serialising unrelated batches (4 queues / 3 batches 25.1k, 16 / 12 27.8k)
+    # queue, serialising unrelated batches (same box: 4 queues / 3 batches 23.0k, 16 / 12 25.9k problems/s)
     # (the GPU box exports GPU_MAX_HW_QUEUES=4, HIP's default: overridden here, not defaulted)
     os.environ["GPU_MAX_HW_QUEUES"] = str(args.hw_queues)
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:

@@ -435,7 +435,8 @@ def main():
     torch.cuda.synchronize()
 
     # C3: 12 batches in flight (+11 % over 3, same box); the C1 surrogate's small batches: 3 (12: -40 %)
-    nf = args.inflight if args.inflight > 0 else (1 if knn_only else (3 if args.config == "c1" else 12))
+    # C5: 2 (one contraction's set prep overlaps the other's distance kernel: 2,020 -> 2,696/s)
+    nf = args.inflight if args.inflight > 0 else (2 if knn_only else (3 if args.config == "c1" else 12))
     if nf > 1:  # the sampler stream helps one batch alone (+5 %), not batches already overlapping
         os.environ.setdefault("MIM_SAMPLER_STREAM", "0")
     matchers = [Matcher(local) for _ in range(nf)]
@@ -445,8 +446,8 @@ def main():
     prm = default_params(max_iters=max(cfg["max_iters"], 1))
     mine = [torch.empty(n_probs * RESULT_DTYPE.itemsize, dtype=torch.uint8, device=dev) for _ in range(nf)]
     nq0 = int(ds.model_desc[0].shape[0])
-    knn_idx = torch.empty((nq0, 2), dtype=torch.int32, device=dev)
-    knn_dist = torch.empty((nq0, 2), dtype=torch.float32, device=dev)
+    knn_idx = [torch.empty((nq0, 2), dtype=torch.int32, device=dev) for _ in range(nf)]  # per context
+    knn_dist = [torch.empty((nq0, 2), dtype=torch.float32, device=dev) for _ in range(nf)]
     counter = [0]
 
     def step():
@@ -458,7 +459,7 @@ def main():
             q_ids = [m.add_set(d, kp) for d, kp in zip(mdesc, mkp)]
             t_ids = [m.add_set(d, kp) for d, kp in zip(sdesc, skp)]
             if knn_only:  # C5: the distance contraction + top-2 alone
-                m.knn_sets_dev(q_ids[0], t_ids[0], knn_idx, knn_dist)
+                m.knn_sets_dev(q_ids[0], t_ids[0], knn_idx[k], knn_dist[k])
                 return
             m.match_batch_async([(q_ids[a], t_ids[b]) for a, b in ds.problems], prm)
             m.batch_results_copy_to(mine[k])
@@ -596,8 +597,8 @@ def main():
         if args.cpu_sample > 0:
             if knn_only:
                 m0.synchronize()
-                out["cpu_baseline"] = cpu_baseline_knn(ds.model_desc[0], ds.scene_desc[0], knn_idx.cpu().numpy(),
-                                                       knn_dist.cpu().numpy(), 96 * args.cpu_sample)
+                out["cpu_baseline"] = cpu_baseline_knn(ds.model_desc[0], ds.scene_desc[0], knn_idx[0].cpu().numpy(),
+                                                       knn_dist[0].cpu().numpy(), 96 * args.cpu_sample)
             else:
                 def detail(i):
                     return m0.problem_detail(i, int(res["n_good"][i]))

@@ -8,6 +8,11 @@
 //   * the scene is converted (preprocessImage), resized and SIFT-described ONCE per scale (:99-107),
 //     not once per scale per model: SIFT is deterministic, so every model sees
 //     the keypoints/descriptors the reference computes for it;
+//   * with MIM_GPU_SIFT (CMake -DMIM_GPU_SIFT=ON) the five resizes and SIFT runs of :102,106 happen on
+//     the device in one call (mim_sift_detect_compute_scales: the scene uploaded once), and
+//     adapter/opencv/ModelsDetector.cpp describes the model views on the device too
+//     (ModelsDetector.cpp:75).  libmim's SIFT is SIFT::create() with its defaults (main.cpp:17), which is
+//     the detector the reference always passes; `detector` is then not called;
 //   * every (model, view, scale) problem of the scene — knnMatch k=2 (:60), ratio test (:66-72),
 //     gates (:74, :79, :81, :84), findHomography RANSAC (:78), inlier gather and 1/scale (:87-94) —
 //     runs as ONE device batch through libmim (mim::Detector::detect_scene, include/mim.hpp);
@@ -26,8 +31,8 @@
 #include <iostream>
 #include <unordered_map>
 
-#include "mim.hpp"
 #include "mim_detect.hpp"
+#include "mim_device.hpp"
 #include "preprocessing.hpp"
 
 namespace {
@@ -51,18 +56,21 @@ mim::ModelViews to_views(const ObjectModel& m) {
     return mv;
 }
 
-// the converted models, kept per ObjectModel object across scenes (the models are loaded once, main.cpp:22)
+// the converted models, kept across scenes (the models are loaded once, main.cpp:22).  Keyed by the
+// ObjectModel's address AND its descriptor matrices' data pointers and sizes, so a different model
+// that happens to reuse a freed address is converted anew.
 const mim::ModelViews& views_of(const ObjectModel& m) {
-    static std::unordered_map<const ObjectModel*, std::pair<size_t, mim::ModelViews>> cache;
+    struct Entry {
+        std::vector<std::pair<const void*, size_t>> key;
+        mim::ModelViews views;
+    };
+    static std::unordered_map<const ObjectModel*, Entry> cache;
+    std::vector<std::pair<const void*, size_t>> key;
+    key.reserve(m.descriptors.size());
+    for (const cv::Mat& d : m.descriptors) key.emplace_back(static_cast<const void*>(d.data), d.total());
     auto it = cache.find(&m);
-    if (it == cache.end() || it->second.first != m.descriptors.size())
-        it = cache.insert_or_assign(&m, std::make_pair(m.descriptors.size(), to_views(m))).first;
-    return it->second.second;
-}
-
-mim::Detector& device() {
-    static mim::Detector det(0);  // one context: device 0, its own HIP stream
-    return det;
+    if (it == cache.end() || it->second.key != key) it = cache.insert_or_assign(&m, Entry{key, to_views(m)}).first;
+    return it->second.views;
 }
 
 }  // namespace
@@ -76,6 +84,17 @@ std::vector<std::pair<cv::Rect, std::string>> detectObjects(const cv::Mat& scene
     const std::vector<float> scales = {0.7f, 0.85f, 1.0f, 1.15f, 1.3f};
     std::vector<std::vector<mim::Point2f>> scene_kp(scales.size());
     std::vector<std::vector<float>> scene_desc(scales.size());
+#ifdef MIM_GPU_SIFT
+    (void)detector;  // SIFT::create() defaults, on the device
+    CV_Assert(preprocessed.type() == CV_8UC1);
+    {
+        std::vector<std::vector<mim_keypoint>> kps;
+        mim_device().sift_scales(preprocessed.data, preprocessed.rows, preprocessed.cols, (int64_t)preprocessed.step[0],
+                                 scales, kps, scene_desc);
+        for (size_t s = 0; s < scales.size(); ++s)
+            for (const mim_keypoint& k : kps[s]) scene_kp[s].push_back({k.x, k.y});
+    }
+#else
     for (size_t s = 0; s < scales.size(); ++s) {
         cv::Mat scaled;
         cv::resize(preprocessed, scaled, cv::Size(), scales[s], scales[s]);
@@ -89,6 +108,7 @@ std::vector<std::pair<cv::Rect, std::string>> detectObjects(const cv::Mat& scene
             scene_desc[s].assign(dc.ptr<float>(), dc.ptr<float>() + dc.total());
         }
     }
+#endif
 
     // :38-109 for every model at once: one device batch of all (model, scale, view) problems
     std::vector<const mim::ModelViews*> mv;
@@ -96,7 +116,7 @@ std::vector<std::pair<cv::Rect, std::string>> detectObjects(const cv::Mat& scene
     std::vector<mim::Detector::ScaledScene> ss;
     for (size_t s = 0; s < scales.size(); ++s) ss.push_back({&scene_kp[s], &scene_desc[s], scales[s]});
     std::vector<std::vector<mim::Point2f>> all_pts;  // allUnfilteredScenePts per model (:39)
-    device().detect_scene(mv, ss, all_pts);
+    mim_device().detect_scene(mv, ss, all_pts);
 
     // :111-248 per model, in model order
     mim::Detections dets;

@@ -1,16 +1,18 @@
 #!/usr/bin/env python3
-"""Benchmark: matches+homographies/sec (10k x 10k SIFT, 50k RANSAC iters) — BASELINE.json metric.
+"""Benchmark: matches+homographies/sec (10k x 10k SIFT, 50k RANSAC iters) at 1/2/4/8 GPUs — BASELINE.json metric.
 
 One step = one pass of the hot path (knnMatch k=2 + ratio test + findHomography RANSAC + refine +
 gates, /root/reference/src/TestsDetector.cpp:58-95) over one batch of problems.  Configs
-(BASELINE.json `configs`; `--config`, default c3):
-  c3  configs[2]: 3 model descriptor sets x 32 scene sets per GPU, 10,000 x 10,000 128-D SIFT-like
-      descriptors per problem, RANSAC maxIters 50,000, conf 0.995, 8 % geometric inliers among 2,000
-      planted matches (no early termination: SURVEY.md App. B).  C4 (configs[3]) is this workload
-      with --gpus 8: every rank owns its own 32 scenes.
+(BASELINE.json `configs`; `--config`, default c4):
+  c4  configs[3]: ONE global batch of 256 scenes x 1 model descriptor set, 10,000 x 10,000 128-D
+      SIFT-like descriptors per problem, RANSAC maxIters 50,000, conf 0.995, 8 % geometric inliers
+      among 2,000 planted matches (no early termination: SURVEY.md App. B).  Scene s is seeded by the
+      global seed and s alone; rank r owns shard_range(256, N, r) (strong scaling: 256 problems per step
+      at N = 1, 32 per GPU at N = 8), the per-problem records are all-gathered over RCCL every step.
+  c3  configs[2]: 3 model sets x 32 scene sets per GPU (96 problems), same shapes (weak scaling).
   c2  configs[1]: 1 x 1, 2k x 2k, maxIters 2000.
   c1  configs[0] surrogate: the reference's own shape, one scene = 29 model views x 5 scales = 145
-      ragged problems (Nq 100-500, Nt 1k-4k, maxIters 2000); the real data needs SIFT.
+      ragged problems (Nq 100-500, Nt 1k-4k, maxIters 2000).
   c5  configs[4]: the 50k x 50k dense distance contraction alone (mim_knn2_sets_dev), no RANSAC.
   c1img  configs[0] on the reference's own images (tests/golden/c1_sugar_box.npz): the sugar_box model
       (29 views, SIFT computed once before the timed region as processAllModelsImages does) against one
@@ -18,15 +20,19 @@ gates, /root/reference/src/TestsDetector.cpp:58-95) over one batch of problems. 
       device batch, clustering and boxes on the host (pipeline.detect_objects).
 Inputs (descriptors + keypoints) are resident in HBM before the timed region; each step registers
 the sets (the i8 layout prep is inside the step) and runs the batch.  Multi-GPU: one process per GPU
-(`--gpus N` launches N ranks through torch.distributed.run when WORLD_SIZE is unset), each rank
-owns its own scenes (weak scaling, no data-path collective); the per-problem result records are
-all-gathered over RCCL at the end of every step.  Twelve scene batches are in flight on one GPU
-(--inflight).
+(`--gpus N` launches N ranks through torch.distributed.run when WORLD_SIZE is unset).  Twelve scene
+batches are in flight on one GPU (--inflight).  The timed region runs with kernel
+timing off.
 
-Prints ONE JSON line on rank 0 with, besides the contract fields: "roofline" (dominant kernel, HIP
-events on the library's stream), "cpu_baseline" (oracle/ restatement on this host's cores, bounded
-sample, with a "parity" check of those problems against the GPU records) and "ranks_seen".
-`--dry-run` exercises the launcher and the gloo/RCCL record gather without a GPU (CPU test).
+Prints ONE JSON line on rank 0 with, besides the contract fields:
+  "roofline": the distance kernel's launch duration from HIP events in an isolated pass after the
+      timed region (one batch at a time on one context, so an event pair brackets exactly that
+      kernel; `rocprofv3 --kernel-trace --stats` of `--inflight 1` reproduces it), and
+      the RANSAC bound kernel as an instruction roofline ("others");
+  "cpu_baseline": oracle/ restatement on this host's cores, bounded sample (rank 0, N = 1);
+  "parity": oracle records vs GPU records of sampled problems, summed over all ranks;
+  "ranks_seen".
+`--dry-run` exercises the launcher, the C4 sharding and the gloo/RCCL record gather without a GPU.
 """
 from __future__ import annotations
 
@@ -45,20 +51,24 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 PEAK_I8_TOPS = 5000.0       # MI355X dense i8 MFMA = 2x dense bf16 2.5 PF (MI355X_MICROARCH.md, no sparsity)
-PEAK_F32_VALU_TFLOPS = 157.3  # MI355X fp32 vector (VALU) peak
-FLOP_PER_POINT_EVAL = 17      # one fp32 reprojection test of a hypothesis on a point
-H_TOL = 1e-4                  # SURVEY.md 8(c) contract item 4 (the GPU tests hold 1e-7)
+PEAK_F16_MFMA_TFLOPS = 2500.0  # dense f16 MFMA
+# VALU issue peak: 1024 SIMDs x one wave64 instruction per 2 cycles (SIMD-32) x 2.4 GHz
+PEAK_VALU_WAVE_INSTR_PER_S = 1024 * 0.5 * 2.4e9
+BOUND_VALU_PER_PAIR = 4       # ransac_bound_mfma_kernel tile loop: med3, fma, sub, sign bit per (point, hypothesis)
+BOUND_MFMA_FLOP_PER_PAIR = 96  # 3 v_mfma_f32_32x32x16_f16 per 32 x 32 (point, hypothesis) pairs
+H_TOL = 1e-4                  # SURVEY.md 8(c) contract item 4 (the GPU tests hold bit identity)
 
 
 def pmc_traffic(kernel, config):
-    """HBM bytes per step of `kernel` from the newest committed rocprofv3 PMC pass (or None)."""
-    for rnd in ("r02", "r01"):
+    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC pass (or None)."""
+    for rnd in ("r03", "r02", "r01"):
         try:
             with open(os.path.join(ROOT, "profiles", f"{rnd}_pmc_traffic.json")) as f:
                 d = json.load(f)
             if d.get("config", "c3") != config:
                 continue
-            return d["kernels"][kernel]["hbm_bytes_per_step"]
+            k = d["kernels"][kernel]
+            return k.get("hbm_bytes_per_launch", k.get("hbm_bytes_per_step"))
         except (OSError, KeyError, ValueError):
             continue
     return None
@@ -69,11 +79,15 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--config", default="c3", choices=["c1", "c1img", "c2", "c3", "c5"])
+    ap.add_argument("--config", default="c4", choices=["c1", "c1img", "c2", "c3", "c4", "c5"])
     ap.add_argument("--cpu-sample", type=int, default=6,
                     help="problems of the sequential CPU-baseline sample (1 warm-up + the median of the rest; "
                          "0: skip the CPU baseline)")
     ap.add_argument("--cpu-rounds", type=int, default=5, help="timed rounds of the parallel CPU row")
+    ap.add_argument("--parity-sample", type=int, default=2,
+                    help="problems per rank checked against the oracle when N > 1 (untimed)")
+    ap.add_argument("--iso-steps", type=int, default=10,
+                    help="steps of the isolated pass (one context, kernel timing on) after the timed region")
     ap.add_argument("--no-timing", action="store_true", help="disable per-kernel HIP events")
     ap.add_argument("--inflight", type=int, default=0,
                     help="scene batches in flight: one library context + HIP stream each, steps assigned "
@@ -115,13 +129,15 @@ def dist_env():
 
 
 def dry_run(args):
-    """Launcher + process group + record gather on gloo (CPU): what the N-rank bench does around its
-    GPU work.  Prints the JSON line with n_gpus / ranks_seen so a CPU test can check the launch."""
+    """Launcher + process group + C4 sharding + record gather on gloo (CPU): what the N-rank bench does
+    around its GPU work.  Prints the JSON line with n_gpus / ranks_seen and, for a sharded config, the
+    scene ids covered by the union of the ranks' shards, so a CPU test can check the launch."""
     import torch
     import torch.distributed as dist
 
     from computervision_objectdetection_featurematching_amd import shard
     from computervision_objectdetection_featurematching_amd._lib import RESULT_DTYPE
+    from computervision_objectdetection_featurematching_amd.synthetic import CONFIGS
 
     rank, world, _ = dist_env()
     if world > 1:
@@ -129,21 +145,35 @@ def dry_run(args):
     seen = dist.get_world_size() if world > 1 else 1
     if seen != args.gpus:
         raise SystemExit(f"rank {rank}: process group has {seen} ranks, --gpus {args.gpus}")
-    rec = np.zeros(4, RESULT_DTYPE)
-    rec["n_good"] = 1000 * rank + np.arange(4)
+    cfg = CONFIGS.get(args.config, {})
+    n_scenes = cfg.get("n_scenes", 4) if cfg.get("sharded") else 4 * world
+    ids = shard.shard_range(n_scenes, world, rank) if cfg.get("sharded") else range(4 * rank, 4 * rank + 4)
+    # per-rank records of its problems (the scene id in n_good), padded to the largest shard
+    per = -(-n_scenes // world)
+    rec = np.zeros(per, RESULT_DTYPE)
+    rec["n_good"] = -1
+    rec["n_good"][:len(ids)] = np.array(list(ids), np.int32)
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
     g = shard.decode(shard.gather_results(torch.from_numpy(rec.view(np.uint8).copy()), world))
+    cnt = torch.tensor([len(ids), 0], dtype=torch.int64)  # the parity sums use the same all-reduce
+    if world > 1:
+        dist.all_reduce(cnt)
     el = time.perf_counter() - t0
     t = torch.tensor([el], dtype=torch.float64)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     if rank == 0:
-        assert g.shape == (world, 4) and list(g["n_good"][:, 0]) == [1000 * r for r in range(world)]
+        got = g["n_good"].ravel()
+        got = np.sort(got[got >= 0])
+        assert g.shape == (world, per) and np.array_equal(got, np.arange(n_scenes)), got
+        assert int(cnt[0]) == n_scenes
         print(json.dumps({"metric": "dry-run", "value": 0.0, "unit": "problems/s", "n_gpus": world,
                           "ranks_seen": seen, "steps": 0, "warmup": 0, "ms_per_step": float(t.item()) * 1e3,
-                          "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dry_run": True}),
+                          "higher_is_better": True, "scaling": "strong" if cfg.get("sharded") else "weak",
+                          "vs_baseline": None, "dry_run": True, "config": {"workload": args.config},
+                          "scene_ids_covered": int(len(np.unique(got))), "global_batch": n_scenes}),
               flush=True)
     if world > 1:
         dist.destroy_process_group()
@@ -160,6 +190,10 @@ def cpu_model() -> str:
     except OSError:
         pass
     return "unknown"
+
+
+CORES_NOTE = ("threads = this job's CPU share (OMP_NUM_THREADS: 16 per GPU on the GPU box, whose nproc counts the "
+              "whole machine; the box's rules size worker pools to that share, so no all-machine row is run)")
 
 
 def host_cores() -> int:
@@ -235,7 +269,7 @@ def cpu_baseline_problems(ds, cfg, gpu_res, gpu_detail, n_sample, rounds):
             log(f"cpu baseline: parallel round {rnd} {time.perf_counter() - t0:.2f} s")
     par = cores / statistics.median(par_times)
     return {"value": round(seq, 4), "unit": "problems/s", "cores": cores, "kind": "port",
-            "cpu_model": cpu_model(),
+            "cpu_model": cpu_model(), "machine_cores": os.cpu_count(), "cores_note": CORES_NOTE,
             "sample": f"{len(ids)} problems of the same workload one after another (1 warm-up, median of "
                       f"{len(ids) - 1}): kNN on {cores} threads like OpenCV parallel_for_, RANSAC single-threaded "
                       f"as cv::findHomography; oracle/mim_oracle.c -O3 -ffp-contract=off",
@@ -265,7 +299,7 @@ def cpu_baseline_knn(q, t, idx_gpu, dist_gpu, n_rows):
     per_row = statistics.median(times[1:])
     ops = 2.0 * t.shape[0] * 128
     return {"value": round(ops / per_row / 1e9, 3), "unit": "GOP/s (distance)", "cores": cores, "kind": "port",
-            "cpu_model": cpu_model(),
+            "cpu_model": cpu_model(), "machine_cores": os.cpu_count(), "cores_note": CORES_NOTE,
             "sample": f"{n_rows} query rows x {t.shape[0]} train rows in 6 slices (1 warm-up, median of 5) on "
                       f"{cores} threads, oracle batchDistance restatement",
             "problems_per_s_equiv": round(1.0 / (per_row * q.shape[0]), 6),
@@ -388,6 +422,70 @@ def cpu_baseline_c1img(scene, model, run, names):
             "parity": {"checked": n, "mismatch": mism}}
 
 
+def kernel_rooflines(args, ds, res, iso, iso_step_ms, knn_only):
+    """Roofline objects from the isolated pass's per-step kernel times (ms)."""
+    nq_all = np.array([d.shape[0] for d in ds.model_desc])
+    nt_all = np.array([d.shape[0] for d in ds.scene_desc])
+    pq = np.array([nq_all[m] for m, _ in ds.problems], np.float64)
+    pt = np.array([nt_all[s] for _, s in ds.problems], np.float64)
+    knn_ops = float(np.sum(2.0 * pq * pt * 128))
+    knn_bytes = float(np.sum(512 * (pq + pt) + 16 * pq))
+    t = iso["knn"]
+    ach = knn_ops / (t * 1e-3) / 1e12
+    roof = {"kernel": "knn2_i8_kernel (exact-integer distance contraction on v_mfma_i32_16x16x64_i8 + top-2 "
+                      "selection), 1 launch per step",
+            "bound": "mfma", "achieved": round(ach, 2), "peak": PEAK_I8_TOPS, "unit": "TFLOP/s",
+            "frac": round(ach / PEAK_I8_TOPS, 4),
+            "traffic": pmc_traffic("knn2_i8_kernel", args.config),
+            "launch_ms": round(t, 4), "ops_per_launch": knn_ops,
+            "ops": "2 * Nq * Nt * 128 integer multiply-adds (i8 operands, i32 accumulate), summed over the batch",
+            "algorithmic_bytes_per_launch": knn_bytes,
+            "achieved_hbm_GBs": round(knn_bytes / (t * 1e-3) / 1e9, 1),
+            "timing": "HIP events on the library stream around the launch, isolated pass: one batch at a time on "
+                      "one context after the timed region (rocprofv3 --kernel-trace --stats of --inflight 1 "
+                      "reproduces it: profiles/)",
+            "isolated_step_ms": round(iso_step_ms, 3),
+            "kernel_ms_per_step_isolated": {k: round(v, 4) for k, v in iso.items()}}
+    if not knn_only and iso.get("score", 0) > 0:
+        pairs = float(np.sum(res["iters"].astype(np.float64) * res["n_good"]))
+        tb = iso["score"] * 1e-3
+        wi = pairs * BOUND_VALU_PER_PAIR / 64.0
+        roof["others"] = {"bound": {
+            "kernel": "ransac_bound_mfma_kernel (closed-form hypotheses, bounded inlier counts), 2 launches per step",
+            "bound": "valu", "unit": "VALU wave-instructions/s",
+            "achieved": round(wi / tb, 1), "peak": PEAK_VALU_WAVE_INSTR_PER_S,
+            "frac": round(wi / tb / PEAK_VALU_WAVE_INSTR_PER_S, 4),
+            "pairs_per_step": pairs, "valu_per_pair": BOUND_VALU_PER_PAIR,
+            "floor_ms": round(wi / PEAK_VALU_WAVE_INSTR_PER_S * 1e3, 4), "ms_per_step": round(iso["score"], 4),
+            "mfma": {"achieved_TFLOPs": round(pairs * BOUND_MFMA_FLOP_PER_PAIR / tb / 1e12, 1),
+                     "peak_TFLOPs": PEAK_F16_MFMA_TFLOPS,
+                     "frac": round(pairs * BOUND_MFMA_FLOP_PER_PAIR / tb / 1e12 / PEAK_F16_MFMA_TFLOPS, 4)},
+            "note": "pairs = iterations x good matches of every problem (OpenCV scores every hypothesis on every "
+                    "point); VALU peak = 1024 SIMDs x 1 wave64 instruction per 2 cycles x 2.4 GHz"}}
+    # consistency: one stream, one batch at a time -> the kernels' durations cannot exceed the step
+    worst = max(iso.values()) if iso else 0.0
+    total = sum(iso.values())
+    if worst > iso_step_ms * 1.02 + 0.02 or total > iso_step_ms * 1.05 + 0.05:
+        raise SystemExit(f"bench: isolated kernel times {iso} exceed the isolated step {iso_step_ms:.3f} ms")
+    roof["kernel_sum_ms_per_step_isolated"] = round(total, 4)
+    return roof
+
+
+def parity_sample(ds, cfg, res, detail, ids):
+    """Oracle records of problems `ids` (untimed) compared with the GPU's: (checked, mismatches)."""
+    from oracle import oracle as O
+    O.build()
+    prm = O.default_params(max_iters=cfg["max_iters"])
+    bad = []
+    for i in ids:
+        m, s = ds.problems[i]
+        o = O.match_problem(ds.model_desc[m], ds.model_kp[m], ds.scene_desc[s], ds.scene_kp[s], prm, host_cores())
+        d = _cmp_problem(o, res[i], detail(i))
+        if d:
+            bad.append((int(i), d))
+    return len(ids), bad
+
+
 def main():
     args = parse()
     # HIP hardware queues per process (read at HIP init, inherited by launched ranks): the batches in
@@ -400,19 +498,13 @@ def main():
     if args.dry_run:
         return dry_run(args)
     rank, world, local = dist_env()
-    if args.config == "c1img":
-        import torch
-        import torch.distributed as dist
-        if world > 1:
-            torch.cuda.set_device(local)
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        return run_c1img(args, rank, world, local)
     import torch
     import torch.distributed as dist
-
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    if args.config == "c1img":
+        return run_c1img(args, rank, world, local)
     ranks_seen = dist.get_world_size() if world > 1 else 1
     if ranks_seen != args.gpus:
         raise SystemExit(f"rank {rank}: {ranks_seen} ranks in the process group, --gpus {args.gpus}")
@@ -425,17 +517,25 @@ def main():
     build.build()
     cfg = CONFIGS[args.config]
     knn_only = bool(cfg.get("knn_only"))
-    # every rank: the same models, its own scenes (seeded by rank)
-    ds = make_config_dataset(args.config, seed=SEED_BASE + 1000 * rank)
+    sharded = bool(cfg.get("sharded"))
+    if sharded:  # one global batch: this rank's contiguous block of its scenes (same data at any N)
+        ids = shard.shard_range(cfg["n_scenes"], world, rank)
+        ds = make_config_dataset(args.config, seed=SEED_BASE, scene_ids=ids)
+        global_batch = cfg["n_scenes"] * cfg["n_models"]
+    else:  # every rank: the same models, its own scenes (seeded by rank)
+        ds = make_config_dataset(args.config, seed=SEED_BASE + 1000 * rank)
+        global_batch = world * len(ds.problems)
     n_probs = len(ds.problems)
+    # ranks hold shards differing by at most one scene: records are gathered at the largest size
+    n_rec = -(-global_batch // world) if sharded else n_probs
     mdesc = [torch.from_numpy(d).to(dev) for d in ds.model_desc]
     mkp = [torch.from_numpy(k).to(dev) for k in ds.model_kp]
     sdesc = [torch.from_numpy(d).to(dev) for d in ds.scene_desc]
     skp = [torch.from_numpy(k).to(dev) for k in ds.scene_kp]
     torch.cuda.synchronize()
 
-    # C3: 12 batches in flight (+11 % over 3, same box); the C1 surrogate's small batches: 3 (12: -40 %)
-    # C5: 2 (one contraction's set prep overlaps the other's distance kernel: 2,020 -> 2,696/s)
+    # C3/C4: 12 batches in flight (+11 % over 3, same box); the C1 surrogate's small batches: 3 (12: -40 %)
+    # C5: 2 (one contraction's set prep overlaps the other's distance kernel)
     nf = args.inflight if args.inflight > 0 else (2 if knn_only else (3 if args.config == "c1" else 12))
     if nf > 1:  # the sampler stream helps one batch alone (+5 %), not batches already overlapping
         os.environ.setdefault("MIM_SAMPLER_STREAM", "0")
@@ -444,7 +544,8 @@ def main():
     # is ordered on the same stream
     streams = [torch.cuda.ExternalStream(mm.stream_handle(), device=dev) for mm in matchers]
     prm = default_params(max_iters=max(cfg["max_iters"], 1))
-    mine = [torch.empty(n_probs * RESULT_DTYPE.itemsize, dtype=torch.uint8, device=dev) for _ in range(nf)]
+    mine = [torch.zeros(n_rec * RESULT_DTYPE.itemsize, dtype=torch.uint8, device=dev) for _ in range(nf)]
+    gath = [None] * nf
     nq0 = int(ds.model_desc[0].shape[0])
     knn_idx = [torch.empty((nq0, 2), dtype=torch.int32, device=dev) for _ in range(nf)]  # per context
     knn_dist = [torch.empty((nq0, 2), dtype=torch.float32, device=dev) for _ in range(nf)]
@@ -463,20 +564,15 @@ def main():
                 return
             m.match_batch_async([(q_ids[a], t_ids[b]) for a, b in ds.problems], prm)
             m.batch_results_copy_to(mine[k])
-            shard.gather_results(mine[k], world)  # RCCL all-gather of the result records
+            gath[k] = shard.gather_results(mine[k], world)  # RCCL all-gather of the result records
 
     for mm in matchers:
         mm.set_timing(False)
-    for _ in range(max(args.warmup, nf if args.warmup > 0 else 0)):
+    n_warm = max(args.warmup, nf if args.warmup > 0 else 0)  # every context once: its first-use allocations
+    for _ in range(n_warm):
         step()
     torch.cuda.synchronize()
-    # the warm-up output: records (and, for the CPU parity sample, good lists + masks) of context 0
-    m0 = matchers[0]
-    res = None if knn_only else m0.batch_results(n_probs)
 
-    for mm in matchers:
-        mm.set_timing(not args.no_timing)
-    kern = {}
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -488,122 +584,116 @@ def main():
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
-    names = ("knn", "ratio") if knn_only else ("knn", "ratio", "attempt", "chain", "check", "sample", "hypo", "score",
-                                               "cand", "exact", "select", "refine")
-    if not args.no_timing:
-        for mm in matchers:
-            if knn_only:
-                mm.synchronize()
-            mm.batch_results(0)  # collects the HIP events of every timed step (outside the timed region)
-        for k in names:
-            kern[k] = sum(max(mm.kernel_ms(k), 0.0) for mm in matchers)
-    # the same kernels without a concurrent batch (one context, steps back to back; not part of `value`)
-    iso = {}
-    if not args.no_timing and nf > 1:
-        for _ in range(args.steps):
-            counter[0] = 0  # always context 0
-            step()
-        torch.cuda.synchronize()
-        m0.batch_results(0)
-        iso = {k: max(m0.kernel_ms(k), 0.0) / max(args.steps, 1) for k in kern}
     if world > 1:
         t = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
-    total = world * n_probs * args.steps
+    total = global_batch * args.steps
     value = total / el
+    # the timed region's records as gathered (all ranks): a cut-short RANSAC (RNG stream exhausted,
+    # status 5) would have been counted as throughput; batch_results() re-runs such a batch, a device
+    # copy cannot, so they are counted here and fail the parity check
+    short_timed = 0
+    if not knn_only:
+        for gk in gath:
+            if gk is not None:
+                recs = shard.decode(gk)
+                short_timed += int((recs["status"] == 5).sum())
+
+    # ---- isolated pass: one context, one batch at a time, kernel timing on (not part of `value`)
+    m0 = matchers[0]
+    m0.set_timing(True)
+    n_iso = max(args.iso_steps, 1)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    for _ in range(n_iso):
+        counter[0] = 0  # always context 0
+        step()
+    m0.synchronize()
+    torch.cuda.synchronize()
+    iso_step_ms = 1e3 * (time.perf_counter() - t1) / n_iso
+    res = None
+    if knn_only:
+        m0.batch_results(0)  # collects the HIP events
+    else:
+        res = m0.batch_results(n_probs)
+    names = ("knn", "ratio") if knn_only else ("knn", "ratio", "attempt", "chain", "check", "sample", "hypo", "score",
+                                               "cand", "exact", "select", "refine")
+    iso = {k: max(m0.kernel_ms(k), 0.0) / n_iso for k in names if m0.kernel_ms(k) > 0}
+    roof = kernel_rooflines(args, ds, res, iso, iso_step_ms, knn_only) if rank == 0 else None
+
+    # ---- parity: oracle vs GPU records of sampled problems; the CPU baseline timing on rank 0 at N = 1
+    cpu = None
+    checked, bad = 0, []
+    if knn_only:
+        if rank == 0 and args.cpu_sample > 0:
+            m0.synchronize()
+            cpu = cpu_baseline_knn(ds.model_desc[0], ds.scene_desc[0], knn_idx[0].cpu().numpy(),
+                                   knn_dist[0].cpu().numpy(), 96 * args.cpu_sample)
+            checked, bad = cpu["parity"]["checked"], [None] * cpu["parity"]["mismatch"]
+    else:
+        def detail(i):
+            return m0.problem_detail(i, int(res["n_good"][i]))
+        if rank == 0 and world == 1 and args.cpu_sample > 0:
+            cpu = cpu_baseline_problems(ds, cfg, res, detail, args.cpu_sample, args.cpu_rounds)
+            checked, bad = cpu["parity"]["checked"], [cpu["parity"]["first"]] * cpu["parity"]["mismatch"]
+        elif world > 1 and args.parity_sample > 0:
+            k = min(args.parity_sample, n_probs)
+            checked, bad = parity_sample(ds, cfg, res, detail, [(7 * j + rank) % n_probs for j in range(k)])
+    tot = torch.tensor([checked, len(bad), short_timed], dtype=torch.int64, device=dev)
+    if world > 1:
+        dist.all_reduce(tot)  # every rank's parity sample and cut-short count
 
     if rank == 0:
-        nq_all = np.array([d.shape[0] for d in ds.model_desc])
-        nt_all = np.array([d.shape[0] for d in ds.scene_desc])
-        pq = np.array([nq_all[m] for m, _ in ds.problems], np.float64)
-        pt = np.array([nt_all[s] for _, s in ds.problems], np.float64)
-        knn_flops = float(np.sum(2.0 * pq * pt * 128))
-        knn_bytes = float(np.sum(4 * 128 * (pq + pt) + 16 * pq))
-        point_evals = 0.0 if knn_only else float(np.sum(res["iters"].astype(np.float64) * res["n_good"]))
-        steps = max(args.steps, 1)
-        kavg = {k: v / steps for k, v in kern.items()}
-        dom = max(kavg, key=kavg.get) if kavg else None
-        rooflines = {}
-        if kavg.get("knn", 0) > 0:
-            ach = knn_flops / (kavg["knn"] * 1e-3) / 1e12
-            rooflines["knn"] = {"kernel": "knn2_i8 (distance GEMM on i8 MFMA, exact integer, + top-2 selection), "
-                                          "1 launch/step; ops = 2*Nq*Nt*128 integer ops, peak = dense i8",
-                                "bound": "mfma",
-                                "achieved": round(ach, 2), "peak": PEAK_I8_TOPS, "unit": "TFLOP/s",
-                                "frac": round(ach / PEAK_I8_TOPS, 4),
-                                "traffic": pmc_traffic("knn2_i8_kernel", args.config),
-                                "algorithmic_bytes": knn_bytes,
-                                "achieved_hbm_GBs": round(knn_bytes / (kavg["knn"] * 1e-3) / 1e9, 1)}
-        if kavg.get("score", 0) > 0:
-            ach = FLOP_PER_POINT_EVAL * point_evals / (kavg["score"] * 1e-3) / 1e12
-            rooflines["score"] = {"kernel": "ransac_bound (closed-form hypotheses, bounded inlier counts), 2 launches/step",
-                                  "bound": "valu", "achieved": round(ach, 2), "peak": PEAK_F32_VALU_TFLOPS,
-                                  "unit": "TFLOP/s", "frac": round(ach / PEAK_F32_VALU_TFLOPS, 4),
-                                  "traffic": pmc_traffic("ransac_bound", args.config),
-                                  "point_evals_per_step": point_evals,
-                                  "hypothesis_point_evals_per_s": round(point_evals / (kavg["score"] * 1e-3), 1)}
-        roof = None
-        if rooflines:
-            key = max(rooflines, key=lambda k: kavg.get(k, 0))  # the dominant of the two hot kernels
-            roof = dict(rooflines[key])
-            roof["dominant_kernel_by_time"] = dom
-            roof["kernel_ms_per_step"] = {k: round(v, 3) for k, v in kavg.items()}
-            if iso:  # per-kernel times of one batch alone (no overlap with the other in-flight batches)
-                roof["isolated_kernel_ms_per_step"] = {k: round(v, 3) for k, v in iso.items()}
-                for key2, r in rooflines.items():
-                    t_iso = iso.get(key2, 0)
-                    if t_iso > 0:
-                        r["isolated_achieved"] = round(r["achieved"] * kavg[key2] / t_iso, 2)
-                        r["isolated_frac"] = round(r["isolated_achieved"] / r["peak"], 4)
-                roof.update({k: v for k, v in rooflines[key].items() if k.startswith("isolated")})
-            roof["others"] = {k: v for k, v in rooflines.items() if k != key}
-            if nf > 1:
-                roof["note"] = (f"achieved/frac: the kernel's HIP-event span in the timed region, where {nf} batches in "
-                                "flight share the GPU (its launches overlap the other batches' kernels); "
-                                "isolated_*: the same kernel with one batch alone")
         metric = {"c3": "matches+homographies/sec (10k x 10k SIFT, 50k RANSAC iters)",
+                  "c4": "matches+homographies/sec (10k x 10k SIFT, 50k RANSAC iters) at 1/2/4/8 GPUs",
                   "c2": "matches+homographies/sec (2k x 2k SIFT, 2k RANSAC iters)",
                   "c1": "matches+homographies/sec (C1 surrogate: 29 views x 5 scales, ragged 100-500 x 1k-4k, "
                         "2k RANSAC iters)",
                   "c5": "knnMatch(k=2) problems/sec (50k x 50k SIFT dense distance contraction)"}[args.config]
+        nq_all = np.array([d.shape[0] for d in ds.model_desc])
+        nt_all = np.array([d.shape[0] for d in ds.scene_desc])
         if cfg.get("ragged"):
             workload = (f"c1: {len(ds.model_desc)} model views (Nq {nq_all.min()}-{nq_all.max()}) x {len(ds.scene_desc)} "
                         f"scene scales (Nt {nt_all.min()}-{nt_all.max()}) per GPU, maxIters {cfg['max_iters']}")
         elif knn_only:
             workload = f"c5: {cfg['nq']} x {cfg['nt']} descriptors, distance + top-2 only"
+        elif sharded:
+            workload = (f"c4: one global batch of {cfg['n_scenes']} scenes x {cfg['n_models']} model set, "
+                        f"{cfg['nq']}x{cfg['nt']} descriptors, maxIters {cfg['max_iters']}, scenes sharded over "
+                        f"{world} GPU(s) ({n_probs} on rank 0)")
         else:
             workload = (f"{args.config}: {cfg['n_models']} models x {cfg['n_scenes']} scenes per GPU, "
                         f"{cfg['nq']}x{cfg['nt']} descriptors, maxIters {cfg['max_iters']}")
         out = {
             "metric": metric, "value": round(value, 3), "unit": "problems/s", "n_gpus": world,
             "ranks_seen": ranks_seen, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(1e3 * el / args.steps, 3),
+            "warmup": n_warm, "ms_per_step": round(1e3 * el / args.steps, 3),
             "host_enqueue_ms_per_step": round(1e3 * t_host / args.steps, 3), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None,
+            "scaling": "strong" if sharded else "weak", "vs_baseline": None,
             "dtype": "i8-MFMA exact-int distances (i32 acc)" + ("" if knn_only else
                                                                ", fp64 DLT/Jacobi, fp32 reprojection"),
             "data": "synthetic SIFT-like integer descriptors (seeded)" + ("" if knn_only else
                                                                         ", planted geometric inliers"),
-            "config": {"workload": workload, "problems_per_gpu": n_probs, "global_batch": world * n_probs,
+            "config": {"workload": workload, "problems_per_gpu": n_probs, "global_batch": global_batch,
                        "parallelism": f"dp{world}", "batches_in_flight": nf,
                        "hw_queues": int(os.environ["GPU_MAX_HW_QUEUES"])},
         }
+        if warm_note := ("" if n_warm == args.warmup else f"--warmup {args.warmup} raised to {n_warm}: every one of "
+                                                            f"the {nf} contexts runs once before the timed region"):
+            out["warmup_note"] = warm_note
         if res is not None:
             out["accepted_problems_rank0"] = int((res["status"] == 0).sum())
-            out["stream_short_rank0"] = int((res["status"] == 5).sum())
         if roof:
             out["roofline"] = roof
-        if args.cpu_sample > 0:
-            if knn_only:
-                m0.synchronize()
-                out["cpu_baseline"] = cpu_baseline_knn(ds.model_desc[0], ds.scene_desc[0], knn_idx[0].cpu().numpy(),
-                                                       knn_dist[0].cpu().numpy(), 96 * args.cpu_sample)
-            else:
-                def detail(i):
-                    return m0.problem_detail(i, int(res["n_good"][i]))
-                out["cpu_baseline"] = cpu_baseline_problems(ds, cfg, res, detail, args.cpu_sample, args.cpu_rounds)
-            out["parity"] = out["cpu_baseline"]["parity"]
+        if cpu is not None:
+            out["cpu_baseline"] = cpu
+        out["parity"] = {"checked": int(tot[0]), "mismatch": int(tot[1]), "ranks": world,
+                         "first": (bad[0] if bad else None),
+                         "stream_short_records_timed": int(tot[2]),
+                         "reference": "oracle/ restatement of OpenCV 4.5.4 (parity unpinned vs OpenCV itself)"}
+        if int(tot[2]):
+            out["parity"]["mismatch"] = int(tot[1]) + int(tot[2])
         print(json.dumps(out), flush=True)
     for mm in matchers:
         mm.close()

@@ -18,7 +18,7 @@ EXPORTS = [
     "mim_version", "mim_default_params", "mim_ctx_create", "mim_ctx_destroy", "mim_last_error",
     "mim_ctx_set_stream", "mim_ctx_set_sampler_stream", "mim_ctx_get_stream", "mim_synchronize", "mim_set_create", "mim_sets_clear", "mim_sets_truncate",
     "mim_knn2_l2", "mim_ratio_filter", "mim_find_homography", "mim_batch_run", "mim_batch_results",
-    "mim_batch_results_dev", "mim_batch_results_copy", "mim_batch_problem_detail", "mim_knn2_sets_dev", "mim_last_kernel_ms",
+    "mim_batch_results_dev", "mim_batch_results_copy", "mim_batch_problem_detail", "mim_batch_inlier_points", "mim_knn2_sets_dev", "mim_last_kernel_ms",
     "mim_set_timing", "mim_sift_detect_compute", "mim_sift_detect_compute_scales", "mim_resize_linear_u8",
     "mim_default_box_params", "mim_detect_boxes",
 ]
@@ -97,6 +97,7 @@ def load():
     L.mim_batch_results_copy.argtypes = [vp, vp, i32]
     L.mim_batch_results_copy.restype = C.c_int32
     L.mim_batch_problem_detail.argtypes = [vp, i32, i32p, i32p, u8p]
+    L.mim_batch_inlier_points.argtypes = [vp, f32p, f32p, C.c_int64, C.POINTER(C.c_int64)]
     L.mim_knn2_sets_dev.argtypes = [vp, i32, i32, vp, vp]
     L.mim_last_kernel_ms.argtypes = [vp, C.c_char_p]
     L.mim_last_kernel_ms.restype = C.c_double
@@ -110,7 +111,7 @@ def load():
     L.mim_detect_boxes.argtypes = [f32p, i32, C.POINTER(BoxParams), C.POINTER(Rect), i32, C.POINTER(C.c_int32)]
     for name in ("mim_ctx_create", "mim_ctx_set_stream", "mim_synchronize", "mim_set_create", "mim_sets_clear",
                  "mim_sets_truncate", "mim_knn2_l2", "mim_ratio_filter", "mim_find_homography", "mim_batch_run", "mim_batch_results",
-                 "mim_batch_problem_detail", "mim_knn2_sets_dev", "mim_set_timing", "mim_ctx_set_sampler_stream",
+                 "mim_batch_problem_detail", "mim_batch_inlier_points", "mim_knn2_sets_dev", "mim_set_timing", "mim_ctx_set_sampler_stream",
                  "mim_sift_detect_compute", "mim_sift_detect_compute_scales", "mim_resize_linear_u8",
                  "mim_detect_boxes"):
         getattr(L, name).restype = C.c_int32

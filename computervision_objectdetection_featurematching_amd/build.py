@@ -40,14 +40,17 @@ def build(force: bool = False, verbose: bool = False) -> str:
     if not force and not needs_build():
         return SO
     os.makedirs(LIBDIR, exist_ok=True)
+    odir = os.environ.get("MIM_BUILD_DIR", LIBDIR)  # objects (variant builds run in parallel: own dirs)
+    os.makedirs(odir, exist_ok=True)
     objs = []
     for src in sources():
-        obj = os.path.join(LIBDIR, os.path.basename(src) + ".o")
+        obj = os.path.join(odir, os.path.basename(src) + ".o")
         cmd = [HIPCC, *FLAGS, *SRC_FLAGS.get(os.path.basename(src), []), "-c", src, "-o", obj]
         if verbose:
             print(" ".join(cmd))
         subprocess.check_call(cmd)
         objs.append(obj)
+    os.makedirs(os.path.dirname(os.path.abspath(SO)), exist_ok=True)
     cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", SO + ".tmp", *objs]
     subprocess.check_call(cmd)
     os.replace(SO + ".tmp", SO)

@@ -24,12 +24,16 @@
 
 namespace mim {
 void launch_prep_batch(const PrepJob* jobs, int njobs, int total_tiles, hipStream_t st);
-void launch_knn(const ProbDev* probs, const KnnWork* works, int n_works, Top2* parts, hipStream_t st);
+void launch_knn(const ProbDev* probs, const KnnWork* works, int n_works, const int* seg_start, int n_blocks, Top2* parts,
+                hipStream_t st);
+int knn_blocks_per_cu();
 void launch_ratio(const ProbDev* probs, int n_probs, const Top2* parts, float ratio, int32_t* good_q,
                   int32_t* good_t, float4* pts, int* n_good, int32_t* knn_idx, float* knn_dist,
                   hipStream_t st);
 void launch_knn_emit(const ProbDev* probs, int nq, const Top2* parts, int32_t* knn_idx, float* knn_dist,
                      hipStream_t st);
+void launch_inlier_gather(const ProbDev* probs, int n, const mim_result* res, const int32_t* good_t,
+                          const uint8_t* masks, const long long* offs, const float* scales, float2* out, hipStream_t st);
 size_t ransac_chain_bytes();
 void launch_rng_stream(const unsigned long long* seg_state, uint32_t* out, long long len, int seg, int n_seg,
                        hipStream_t s);
@@ -168,11 +172,10 @@ struct mim_ctx {
     Arena arena;
     std::vector<SetRec> sets;
     // batch workspace
-    DevBuf probs, works, parts, good_q, good_t, pts, n_good, results, masks, knn_idx, knn_dist;
+    DevBuf probs, works, parts, good_q, good_t, pts, n_good, results, masks, knn_idx, knn_dist, inl_tab, inl_out;
     RansacWs rws;
     std::vector<ProbDev> h_probs;
-    std::vector<KnnWork> h_works;
-    int n_works = 0;
+    int n_works = 0;  // distance segments of the current batch (works, then the per-block segment starts)
     std::vector<long long> h_good_off;
     PinnedStage stage;
     // sets created since the last batch: their prep runs as one launch at the next build_tables
@@ -194,17 +197,8 @@ struct mim_ctx {
     long long stream_draws = 0;
     // MIM_RANSAC_EXACT=1: evaluate every hypothesis exactly (reference mode for cross-checks)
     int exact_all = 0;
-    // Pipelined batches: mim_batch_run splits the problems into groups, each on its own stream,
-    // so the latency-bound RANSAC kernels of one group overlap the GPU-filling distance and bound
-    // kernels of the next (DESIGN.md "Batch pipeline").  Group 0 runs on `stream`, the others
-    // fork from and join back into it; the distance kernels run one group after another (ev_knn
-    // chain).  A process has 4 hardware queues (GPU_MAX_HW_QUEUES): the caller's stream, `own`
-    // and two group streams fit, more groups would share a queue and serialise.
-    static constexpr int kMaxGroups = 3;
-    hipStream_t sub[kMaxGroups] = {};
-    hipEvent_t ev_fork = nullptr, ev_knn[kMaxGroups] = {}, ev_join[kMaxGroups] = {};
-    int n_groups = 1;
-    int grp_p0[kMaxGroups + 1] = {}, grp_w0[kMaxGroups + 1] = {};
+    int knn_grid = 0;      // resident distance-kernel blocks on the device (first batch)
+    int n_knn_blocks = 0;  // distance-kernel blocks of the current batch (<= knn_grid)
     hipStream_t cur = nullptr;  // stream the enqueue helpers launch on
     // sampler stream (RansacBufs::s2): the next chunk's getSubset replay beside this chunk's
     // selection kernels (MIM_SAMPLER_STREAM=0: one stream)
@@ -291,12 +285,6 @@ void mim_ctx_destroy(mim_ctx* c) {
     (void)hipStreamSynchronize(c->stream);
     for (auto& e : c->evs) (void)hipEventDestroy(e.e);
     for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
-    for (int g = 0; g < mim_ctx::kMaxGroups; ++g) {
-        if (c->sub[g]) (void)hipStreamDestroy(c->sub[g]);
-        if (c->ev_knn[g]) (void)hipEventDestroy(c->ev_knn[g]);
-        if (c->ev_join[g]) (void)hipEventDestroy(c->ev_join[g]);
-    }
-    if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
     if (c->samp) (void)hipStreamSynchronize(c->samp);
     if (c->ev_samp_fork) (void)hipEventDestroy(c->ev_samp_fork);
     for (auto e : c->ev_samp)
@@ -308,7 +296,7 @@ void mim_ctx_destroy(mim_ctx* c) {
     c->prep_stage.destroy();
     c->arena.release();
     for (DevBuf* b : {&c->probs, &c->works, &c->parts, &c->good_q, &c->good_t, &c->pts, &c->n_good,
-                      &c->results, &c->masks, &c->knn_idx, &c->knn_dist, &c->rws.state, &c->rws.samples,
+                      &c->results, &c->masks, &c->knn_idx, &c->knn_dist, &c->inl_tab, &c->inl_out, &c->rws.state, &c->rws.samples,
                       &c->rws.hyp, &c->rws.counts, &c->rws.bounds, &c->rws.flags, &c->rws.irr, &c->rws.irr_cnt, &c->rws.pass_bits, &c->rws.chains, &c->rws.best_h, &c->rws.cand, &c->rws.ncand, &c->rws.cex, &c->rws.cH, &c->rws.stream, &c->rws.scratch, &c->rws.inl, &c->rws.tiles, &c->rws.err, &c->prep_jobs})
         b->release();
     if (c->own) (void)hipStreamDestroy(c->own);
@@ -477,19 +465,16 @@ mim_status mim_sets_truncate(mim_ctx* c, int32_t n_keep) {
 // Problem table + distance work list.  Work items of one problem are placed at block indices
 // with equal (index % 8) so they share one XCD's L2 under round-robin dispatch (speed only).
 // ---------------------------------------------------------------------------------------------
-static int pick_groups(int n) {
-    const char* e = getenv("MIM_GROUPS");
-    int g = e ? atoi(e) : 1;  // measured: no gain on C3 while the exact/refine chains dominate
-    g = std::max(1, std::min(g, mim_ctx::kMaxGroups));
-    return std::min(g, std::max(n, 1));
-}
-
-static mim_status build_tables(mim_ctx* c, const mim_problem* problems, int n, int max_iters, int groups = 1) {
+static mim_status build_tables(mim_ctx* c, const mim_problem* problems, int n, int max_iters) {
     mim_status fs = flush_preps(c);  // the sets' device tiles and flags, before ProbDev copies them
     if (fs != MIM_OK) return fs;
+    if (c->knn_grid == 0) {  // resident distance-kernel blocks: CUs x blocks per CU (occupancy query)
+        hipDeviceProp_t prop;
+        HIPCHK(c, hipGetDeviceProperties(&prop, c->device));
+        c->knn_grid = std::max(1, prop.multiProcessorCount * std::max(1, knn_blocks_per_cu()));
+    }
     c->h_probs.assign(n, ProbDev{});
-    long long part = 0, good = 0, it = 0;
-    int total_qblocks = 0;
+    long long part = 0, good = 0, it = 0, units = 0;
     for (int i = 0; i < n; ++i) {
         const int qs = problems[i].query_set, ts = problems[i].train_set;
         if (qs < 0 || qs >= (int)c->sets.size() || ts < 0 || ts >= (int)c->sets.size())
@@ -497,21 +482,28 @@ static mim_status build_tables(mim_ctx* c, const mim_problem* problems, int n, i
         if (c->sets[ts].d.n >= (1 << 18))  // BFMatcher::knnMatchImpl: train rows < 1 << 18 (IMGIDX_SHIFT)
             return fail(c, MIM_EINVAL, "problem %d: train set of %d rows exceeds OpenCV's 2^18 limit", i,
                         c->sets[ts].d.n);
-        total_qblocks += (c->sets[qs].d.n + kKnnBlockQ - 1) / kKnnBlockQ;
+        units += (long long)((c->sets[qs].d.n + kKnnBlockQ - 1) / kKnnBlockQ) * c->sets[ts].d.n_tiles;
     }
-    // split the train side until the grid has ~2 blocks per CU (MIM_KNN_TARGET: blocks wanted)
-    static const int target = [] {
-        const char* e = getenv("MIM_KNN_TARGET");
-        return e ? std::max(1, atoi(e)) : 512;
-    }();
-    std::vector<std::vector<KnnWork>> per_prob(n);
+    // Balanced distance schedule: the (problem, query block, train tile) units, in that order, cut
+    // into one contiguous chunk per resident block, so every block of the single wave of blocks does
+    // the same number of tiles (no tail wave).  A query block cut into k pieces gets k train splits
+    // (partial top-2 lists merged by the ratio kernel); a problem's split count is the largest over
+    // its query blocks, and the missing splits of the others are empty segments (sentinel lists).
+    const long long chunk = std::max<long long>(kKnnMinChunk, (units + c->knn_grid - 1) / c->knn_grid);
+    const int nblk = (int)std::max<long long>(1, (units + chunk - 1) / chunk);
+    std::vector<std::vector<KnnWork>> blk(nblk);
+    long long pos = 0;
     for (int i = 0; i < n; ++i) {
         ProbDev& P = c->h_probs[i];
         P.q = c->sets[problems[i].query_set].d;
         P.t = c->sets[problems[i].train_set].d;
-        const int qb = (P.q.n + kKnnBlockQ - 1) / kKnnBlockQ;
-        int nsplit = total_qblocks > 0 ? (target + total_qblocks - 1) / total_qblocks : 1;
-        nsplit = std::max(1, std::min(nsplit, std::max(P.t.n_tiles, 1)));
+        const int qb = (P.q.n + kKnnBlockQ - 1) / kKnnBlockQ, nt = P.t.n_tiles;
+        // pieces of each query block: first pass for the split count
+        int nsplit = 1;
+        for (int b = 0; b < qb; ++b) {
+            const long long u0 = pos + (long long)b * nt, u1 = u0 + nt;
+            if (nt > 0) nsplit = std::max(nsplit, (int)((u1 - 1) / chunk - u0 / chunk + 1));
+        }
         P.nsplit = nsplit;
         P.q_pad = qb * kKnnBlockQ;
         P.part_off = part;
@@ -520,34 +512,28 @@ static mim_status build_tables(mim_ctx* c, const mim_problem* problems, int n, i
         good += (std::max(P.q.n, 1) + 31) & ~31;  // 32-aligned: the MFMA bound's point tiles
         P.it_off = it;
         it += std::max(max_iters, 1);
-        for (int qb_i = 0; qb_i < qb; ++qb_i)
-            for (int s = 0; s < nsplit; ++s) {
-                const int t0 = (int)((long long)P.t.n_tiles * s / nsplit);
-                const int t1 = (int)((long long)P.t.n_tiles * (s + 1) / nsplit);
-                per_prob[i].push_back(KnnWork{i, qb_i * kKnnBlockQ, t0, t1, s});
+        for (int b = 0; b < qb; ++b) {
+            const long long u0 = pos + (long long)b * nt, u1 = u0 + nt;
+            int k = 0, last = (int)std::min<long long>(nblk - 1, u0 / chunk);
+            for (long long a = u0; a < u1; ++k) {
+                const long long e = std::min(u1, (a / chunk + 1) * chunk);
+                last = (int)(a / chunk);
+                blk[last].push_back(KnnWork{i, b * kKnnBlockQ, (int)(a - u0), (int)(e - u0), k});
+                a = e;
             }
+            for (; k < nsplit; ++k) blk[last].push_back(KnnWork{i, b * kKnnBlockQ, nt, nt, k});  // empty split
+        }
+        pos += (long long)qb * nt;
     }
-    // problem groups (contiguous ranges), each with its own contiguous slice of the work list;
-    // inside a group, XCD-aware order: bucket problems over 8 lanes of the grid
-    c->n_groups = groups;
     std::vector<KnnWork> works;
-    for (int g = 0; g < groups; ++g) {
-        const int p0 = (int)((long long)n * g / groups), p1 = (int)((long long)n * (g + 1) / groups);
-        c->grp_p0[g] = p0;
-        c->grp_w0[g] = (int)works.size();
-        std::vector<std::vector<KnnWork>> xcd(8);
-        for (int i = p0; i < p1; ++i)
-            for (auto& w : per_prob[i]) xcd[i % 8].push_back(w);
-        size_t longest = 0;
-        for (auto& v : xcd) longest = std::max(longest, v.size());
-        for (size_t k = 0; k < longest; ++k)
-            for (int x = 0; x < 8; ++x)
-                if (k < xcd[x].size()) works.push_back(xcd[x][k]);
+    std::vector<int> seg(nblk + 1, 0);
+    for (int b = 0; b < nblk; ++b) {
+        seg[b] = (int)works.size();
+        works.insert(works.end(), blk[b].begin(), blk[b].end());
     }
-    c->grp_p0[groups] = n;
-    c->grp_w0[groups] = (int)works.size();
+    seg[nblk] = (int)works.size();
     HIPCHK(c, c->probs.ensure(sizeof(ProbDev) * std::max(n, 1)));
-    HIPCHK(c, c->works.ensure(sizeof(KnnWork) * std::max<size_t>(works.size(), 1)));
+    HIPCHK(c, c->works.ensure(sizeof(KnnWork) * std::max<size_t>(works.size(), 1) + sizeof(int) * seg.size()));
     HIPCHK(c, c->parts.ensure(sizeof(Top2) * std::max<long long>(part, 1)));
     HIPCHK(c, c->good_q.ensure(sizeof(int32_t) * good));
     HIPCHK(c, c->good_t.ensure(sizeof(int32_t) * good));
@@ -555,19 +541,20 @@ static mim_status build_tables(mim_ctx* c, const mim_problem* problems, int n, i
     HIPCHK(c, c->n_good.ensure(sizeof(int) * std::max(n, 1)));
     HIPCHK(c, c->masks.ensure(good));
     // the device tables are rewritten in stream order (after the previous batch's kernels)
-    const size_t pb = sizeof(ProbDev) * n, wb = sizeof(KnnWork) * works.size();
+    const size_t pb = sizeof(ProbDev) * n, wb = sizeof(KnnWork) * works.size(), sb = sizeof(int) * seg.size();
     char* st = nullptr;
-    HIPCHK(c, c->stage.acquire(pb + wb, &st));
+    HIPCHK(c, c->stage.acquire(pb + wb + sb, &st));
     memcpy(st, c->h_probs.data(), pb);
     memcpy(st + pb, works.data(), wb);
+    memcpy(st + pb + wb, seg.data(), sb);
     HIPCHK(c, hipMemcpyAsync(c->probs.p, st, pb, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(c, hipMemcpyAsync(c->works.p, st + pb, wb, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->works.p, st + pb, wb + sb, hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, c->stage.release_after(c->stream));
     c->h_good_off.resize(n);
     for (int i = 0; i < n; ++i) c->h_good_off[i] = c->h_probs[i].good_off;
     c->last_n = n;
-    c->h_works.swap(works);  // source of the async copy stays alive in the ctx
-    c->n_works = (int)c->h_works.size();
+    c->n_works = (int)works.size();
+    c->n_knn_blocks = nblk;
     return MIM_OK;
 }
 
@@ -607,26 +594,25 @@ static void ev_collect(mim_ctx* c) {
     c->evs.clear();
 }
 
-// distance + ratio kernels for problems [p0, p0 + np) whose work items are works[w0, w0 + nw)
-static mim_status knn_ratio_enqueue(mim_ctx* c, int p0, int np, int w0, int nw, float ratio, bool emit_knn,
-                                    hipEvent_t after_knn = nullptr) {
-    Top2* parts = c->parts.as<Top2>();
+static void knn_launch(mim_ctx* c) {
+    const KnnWork* w = c->works.as<KnnWork>();
+    launch_knn(c->probs.as<ProbDev>(), w, c->n_works, reinterpret_cast<const int*>(w + c->n_works), c->n_knn_blocks,
+               c->parts.as<Top2>(), c->cur);
+}
+
+// distance + ratio kernels of the batch's problems
+static mim_status knn_ratio_locked(mim_ctx* c, int n, float ratio, bool emit_knn) {
+    c->cur = c->stream;
     ev_mark(c, "begin");
-    launch_knn(c->probs.as<ProbDev>(), c->works.as<KnnWork>() + w0, nw, parts, c->cur);
+    knn_launch(c);
     HIPCHK(c, hipGetLastError());
     ev_mark(c, "knn");
-    if (after_knn) HIPCHK(c, hipEventRecord(after_knn, c->cur));
-    launch_ratio(c->probs.as<ProbDev>() + p0, np, parts, ratio, c->good_q.as<int32_t>(), c->good_t.as<int32_t>(),
-                 c->pts.as<float4>(), c->n_good.as<int>() + p0, emit_knn ? c->knn_idx.as<int32_t>() : nullptr,
+    launch_ratio(c->probs.as<ProbDev>(), n, c->parts.as<Top2>(), ratio, c->good_q.as<int32_t>(), c->good_t.as<int32_t>(),
+                 c->pts.as<float4>(), c->n_good.as<int>(), emit_knn ? c->knn_idx.as<int32_t>() : nullptr,
                  emit_knn ? c->knn_dist.as<float>() : nullptr, c->cur);
     HIPCHK(c, hipGetLastError());
     ev_mark(c, "ratio");
     return MIM_OK;
-}
-
-static mim_status knn_ratio_locked(mim_ctx* c, int n, float ratio, bool emit_knn) {
-    c->cur = c->stream;
-    return knn_ratio_enqueue(c, 0, n, 0, c->n_works, ratio, emit_knn);
 }
 
 extern "C" {
@@ -727,7 +713,7 @@ mim_status mim_knn2_sets_dev(mim_ctx* c, int32_t query_set, int32_t train_set, i
     if (s != MIM_OK) return s;
     c->cur = c->stream;
     ev_mark(c, "begin");
-    launch_knn(c->probs.as<ProbDev>(), c->works.as<KnnWork>(), c->n_works, c->parts.as<Top2>(), c->stream);
+    knn_launch(c);
     HIPCHK(c, hipGetLastError());
     ev_mark(c, "knn");
     launch_knn_emit(c->probs.as<ProbDev>(), c->h_probs[0].q.n, c->parts.as<Top2>(), idx_dev, dist_dev, c->stream);
@@ -990,7 +976,6 @@ static mim_status ransac_prepare(mim_ctx* c, int n, const mim_params* prm, Ransa
 static mim_status ransac_enqueue_range(mim_ctx* c, int p0, int np, const RansacBufs& b, const RansacParams& rp,
                                        long long flag_per, int raw) {
     RansacBufs g = b;
-    if (c->n_groups > 1) g.s2 = nullptr;  // pipelined groups: one stream per group
     g.state += p0;
     g.flags += (long long)p0 * flag_per;
     g.flag_cap = (long long)np * flag_per;
@@ -1019,16 +1004,6 @@ static mim_status ransac_locked(mim_ctx* c, int n, const mim_params* prm, int ra
     return ransac_enqueue_range(c, 0, n, b, rp, flag_per, raw);
 }
 
-static mim_status ensure_groups(mim_ctx* c) {
-    if (!c->ev_fork) HIPCHK(c, hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
-    for (int g = 0; g < c->n_groups; ++g) {
-        if (g > 0 && !c->sub[g]) HIPCHK(c, hipStreamCreateWithFlags(&c->sub[g], hipStreamNonBlocking));
-        if (!c->ev_knn[g]) HIPCHK(c, hipEventCreateWithFlags(&c->ev_knn[g], hipEventDisableTiming));
-        if (!c->ev_join[g]) HIPCHK(c, hipEventCreateWithFlags(&c->ev_join[g], hipEventDisableTiming));
-    }
-    return MIM_OK;
-}
-
 static mim_status check_params(mim_ctx* c, const mim_params* p) {
     if (!p) return fail(c, MIM_EINVAL, "null params");
     if (!(p->confidence > 0 && p->confidence < 1)) return fail(c, MIM_EINVAL, "confidence must be in (0,1)");
@@ -1046,44 +1021,16 @@ static mim_status batch_run_locked(mim_ctx* c, const mim_problem* problems, int3
     c->last_params = *params;
     c->last_gen = c->sets_gen;
     if (n == 0) { c->last_n = 0; return MIM_OK; }
-    mim_status s = build_tables(c, problems, n, std::max(params->max_iters, 1), pick_groups(n));
+    mim_status s = build_tables(c, problems, n, std::max(params->max_iters, 1));
     if (s != MIM_OK) return s;
     RansacBufs b;
     RansacParams rp;
     long long flag_per = 0;
     s = ransac_prepare(c, n, params, b, rp, flag_per);
     if (s != MIM_OK) return s;
-    if (c->n_groups == 1) {
-        s = knn_ratio_locked(c, n, params->ratio, false);
-        if (s != MIM_OK) return s;
-        return ransac_enqueue_range(c, 0, n, b, rp, flag_per, 0);
-    }
-    // pipelined groups: fork from the caller's stream, distance kernels one group after another,
-    // each group's RANSAC right behind its own distance + ratio kernels, join back
-    s = ensure_groups(c);
+    s = knn_ratio_locked(c, n, params->ratio, false);
     if (s != MIM_OK) return s;
-    HIPCHK(c, hipEventRecord(c->ev_fork, c->stream));
-    for (int g = 0; g < c->n_groups; ++g) {
-        c->cur = g ? c->sub[g] : c->stream;
-        if (g > 0) HIPCHK(c, hipStreamWaitEvent(c->cur, c->ev_fork, 0));
-        if (g > 0) HIPCHK(c, hipStreamWaitEvent(c->cur, c->ev_knn[g - 1], 0));
-        const int p0 = c->grp_p0[g], w0 = c->grp_w0[g];
-        s = knn_ratio_enqueue(c, p0, c->grp_p0[g + 1] - p0, w0, c->grp_w0[g + 1] - w0, params->ratio, false,
-                              c->ev_knn[g]);
-        if (s != MIM_OK) return s;
-    }
-    for (int g = 0; g < c->n_groups; ++g) {
-        c->cur = g ? c->sub[g] : c->stream;
-        const int p0 = c->grp_p0[g];
-        s = ransac_enqueue_range(c, p0, c->grp_p0[g + 1] - p0, b, rp, flag_per, 0);
-        if (s != MIM_OK) return s;
-    }
-    for (int g = 1; g < c->n_groups; ++g) {
-        HIPCHK(c, hipEventRecord(c->ev_join[g], c->sub[g]));
-        HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_join[g], 0));
-    }
-    c->cur = c->stream;
-    return MIM_OK;
+    return ransac_enqueue_range(c, 0, n, b, rp, flag_per, 0);
 }
 
 // Waits for the last batch; if a problem ran out of RNG draws (status MIM_STREAM_SHORT: OpenCV's
@@ -1150,7 +1097,11 @@ mim_status mim_batch_problem_detail(mim_ctx* c, int32_t i, int32_t* q_idx, int32
     std::lock_guard<std::mutex> lk(c->mu);
     if (i < 0 || i >= c->last_n) return fail(c, MIM_EINVAL, "problem %d out of range", i);
     HIPCHK(c, hipSetDevice(c->device));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    // the final records first: a batch cut short by the RNG stream is re-run here, as in
+    // mim_batch_results, so the mask is never that of an unfinished RANSAC
+    std::vector<mim_result> res;
+    mim_status fs = finish_batch_locked(c, res);
+    if (fs != MIM_OK) return fs;
     int ng = 0;
     HIPCHK(c, hipMemcpy(&ng, c->n_good.as<int>() + i, sizeof(int), hipMemcpyDeviceToHost));
     const long long o = c->h_good_off[i];
@@ -1159,6 +1110,42 @@ mim_status mim_batch_problem_detail(mim_ctx* c, int32_t i, int32_t* q_idx, int32
         if (t_idx) HIPCHK(c, hipMemcpy(t_idx, c->good_t.as<int32_t>() + o, sizeof(int32_t) * ng, hipMemcpyDeviceToHost));
         if (mask) HIPCHK(c, hipMemcpy(mask, c->masks.as<uint8_t>() + o, ng, hipMemcpyDeviceToHost));
     }
+    return MIM_OK;
+}
+
+mim_status mim_batch_inlier_points(mim_ctx* c, const float* scales, float* out_xy, int64_t cap, int64_t* offsets) {
+    if (!c) return MIM_EINVAL;
+    if (!offsets || cap < 0) return fail(c, MIM_EINVAL, "batch_inlier_points: bad arguments");
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIPCHK(c, hipSetDevice(c->device));
+    std::vector<mim_result> res;
+    mim_status fs = finish_batch_locked(c, res);  // waits; re-runs a batch cut short by the RNG stream
+    if (fs != MIM_OK) return fs;
+    const int n = c->last_n;
+    offsets[0] = 0;
+    for (int i = 0; i < n; ++i)  // TestsDetector.cpp:79-84: only accepted problems contribute
+        offsets[i + 1] = offsets[i] + (res[i].status == MIM_ACCEPTED ? res[i].n_inl : 0);
+    const long long total = n ? offsets[n] : 0;
+    if (!out_xy || total == 0) return MIM_OK;
+    if (total > cap) return fail(c, MIM_ERANGE, "batch_inlier_points: %lld points, buffer holds %lld", total, (long long)cap);
+    // table: offsets (n + 1) then the scales (n), one copy; the gather; one copy of the points back
+    const size_t tb = sizeof(long long) * (n + 1) + (scales ? sizeof(float) * n : 0);
+    HIPCHK(c, c->inl_tab.ensure(tb));
+    HIPCHK(c, c->inl_out.ensure(sizeof(float2) * total));
+    char* st = nullptr;
+    HIPCHK(c, c->stage.acquire(tb, &st));
+    memcpy(st, offsets, sizeof(long long) * (n + 1));
+    if (scales) memcpy(st + sizeof(long long) * (n + 1), scales, sizeof(float) * n);
+    HIPCHK(c, hipMemcpyAsync(c->inl_tab.p, st, tb, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, c->stage.release_after(c->stream));
+    const long long* offs = c->inl_tab.as<long long>();
+    launch_inlier_gather(c->probs.as<ProbDev>(), n, c->results.as<mim_result>(), c->good_t.as<int32_t>(),
+                         c->masks.as<uint8_t>(), offs,
+                         scales ? reinterpret_cast<const float*>(offs + n + 1) : nullptr, c->inl_out.as<float2>(),
+                         c->stream);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipMemcpyAsync(out_xy, c->inl_out.p, sizeof(float2) * total, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
     return MIM_OK;
 }
 

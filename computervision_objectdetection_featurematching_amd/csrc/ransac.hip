@@ -1579,10 +1579,6 @@ __global__ __launch_bounds__(kSmallThreads) void ransac_small_kernel(RansacState
     long long pos = S.stream_pos;  // the chain's next attempt (absolute stream position)
     int produced = S.produced, fail_run = S.fail_run;
     bool stop_all = false;
-#ifdef MIM_SMALL_PROF
-    long long tp[6] = {0, 0, 0, 0, 0, 0}, t0 = clock64();
-    int rounds = 0;
-#endif
     while (!stop_all && produced < target) {
         // 0. stage the draws of [pos, pos + kSmallRound + kSmallExtra), then the attempt lengths
         const long long avail = slen - pos;  // draws left in the RNG stream (past it: 64 zero draws)
@@ -1607,9 +1603,6 @@ __global__ __launch_bounds__(kSmallThreads) void ransac_small_kernel(RansacState
         }
         if (tid == 0) sh.bad = kSmallRound;
         __syncthreads();
-#ifdef MIM_SMALL_PROF
-        if (tid == 0) tp[5] += clock64() - t0, t0 = clock64();
-#endif
         // the draws consumed by the attempt at each of the thread's 64 positions, by two pointers:
         // the attempt at j ends at k4(j), the first r with 4 distinct draws in [j, r), and k4 never
         // decreases with j.  The window's distinct draws are 4 (value, last occurrence) slots.
@@ -1653,9 +1646,6 @@ __global__ __launch_bounds__(kSmallThreads) void ransac_small_kernel(RansacState
         if (bad_mine < BIG) atomicMin(&sh.bad, bad_mine);
         __syncthreads();
         const int Rz = sh.bad;  // the round: positions [0, Rz), the chain's attempts starting there
-#ifdef MIM_SMALL_PROF
-        if (tid == 0) tp[0] += clock64() - t0, t0 = clock64();
-#endif
         if (Rz == 0) {
             // the chain's next attempt is resolved alone (uniform)
             int idx[4] = {0, 0, 0, 0};
@@ -1699,9 +1689,6 @@ __global__ __launch_bounds__(kSmallThreads) void ransac_small_kernel(RansacState
             sh.V[tid] = nib;
         }
         __syncthreads();
-#ifdef MIM_SMALL_PROF
-        if (tid == 0) tp[1] += clock64() - t0, t0 = clock64();
-#endif
         // 2. the chain's entry into every segment: a block scan of the exit tables under
         //    composition (segment 0 is entered at 0; segment i at T_{i-1}(...T_0(0))).  An exit of
         //    15 or more breaks the tables: from that segment on wave 0 joins in order, walking on LDS.
@@ -1751,9 +1738,6 @@ __global__ __launch_bounds__(kSmallThreads) void ransac_small_kernel(RansacState
             }
             __syncthreads();
         }
-#ifdef MIM_SMALL_PROF
-        if (tid == 0) tp[2] += clock64() - t0, t0 = clock64();
-#endif
         // the chain's attempts in the segment, from its entry
         unsigned long long C = 0;
         if (tid < nseg && sh.X[tid] >= 0) {
@@ -1783,9 +1767,6 @@ __global__ __launch_bounds__(kSmallThreads) void ransac_small_kernel(RansacState
             PM |= (unsigned long long)(check_subset(s4, t4) ? 1 : 0) << bit;
         }
         __syncthreads();
-#ifdef MIM_SMALL_PROF
-        if (tid == 0) tp[3] += clock64() - t0, t0 = clock64();
-#endif
         // 4. ranks: attempts A (chain order) and passes B before this segment
         int Tr, Pt;
         const int A = block_excl_sum(__popcll(C), sh.wred, Tr);
@@ -1838,23 +1819,12 @@ __global__ __launch_bounds__(kSmallThreads) void ransac_small_kernel(RansacState
             pos += e_end;
         }
         __syncthreads();  // sh.idx / sh.len / sh.V are restaged by the next round
-#ifdef MIM_SMALL_PROF
-        if (tid == 0) tp[4] += clock64() - t0, t0 = clock64();
-#endif
-#ifdef MIM_SMALL_PROF
-        ++rounds;
-#endif
     }
     if (tid == 0) {
         S.stream_pos = pos;
         S.produced = produced;
         S.fail_run = fail_run;
         store_sampler_state(st + p, S);
-#ifdef MIM_SMALL_PROF
-        if (rounds > 1)
-            printf("[small] p=%d N=%u produced=%d rounds=%d stage %lld lengths %lld join-tables %lld join %lld checks %lld ranks %lld\n",
-                   p, N, produced, rounds, tp[5], tp[0], tp[1], tp[2], tp[3], tp[4]);
-#endif
     }
 }
 

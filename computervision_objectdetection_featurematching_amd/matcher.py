@@ -299,6 +299,22 @@ class Matcher:
                                                     C.c_void_p(m.ctypes.data)))
         return q[:n_good], t[:n_good], m[:n_good]
 
+    def batch_inlier_points(self, n: int, scales=None):
+        """allUnfilteredScenePts of the last batch (mim_batch_inlier_points, TestsDetector.cpp:87-94):
+        (offsets (n + 1,) int64, points (offsets[n], 2) float32); problem i's inlier scene points, divided
+        by scales[i] when it is not 1, are points[offsets[i]:offsets[i + 1]]."""
+        offs = np.zeros(n + 1, np.int64)
+        sc = None if scales is None else np.ascontiguousarray(scales, np.float32)
+        if sc is not None and sc.shape != (n,):
+            raise ValueError(f"batch_inlier_points: {sc.shape} scales for {n} problems")
+        scp = None if sc is None else sc.ctypes.data_as(C.POINTER(C.c_float))
+        op = offs.ctypes.data_as(C.POINTER(C.c_int64))
+        self._check(self.L.mim_batch_inlier_points(self._ctx, scp, None, 0, op))
+        pts = np.zeros((max(int(offs[n]), 1), 2), np.float32)
+        self._check(self.L.mim_batch_inlier_points(self._ctx, scp, pts.ctypes.data_as(C.POINTER(C.c_float)),
+                                                   int(offs[n]), op))
+        return offs, pts[:int(offs[n])]
+
     def match_batch(self, problems, params: Params | None = None) -> np.ndarray:
         n = self.match_batch_async(problems, params)
         return self.batch_results(n)

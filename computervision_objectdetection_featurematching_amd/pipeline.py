@@ -66,12 +66,14 @@ def detect_boxes(points: np.ndarray, bp: BoxParams | None = None) -> list[tuple[
     L = _lib.load()
     pts = np.ascontiguousarray(points, np.float32).reshape(-1, 2)
     bp = bp or default_box_params()
-    cap = max(16, len(pts) // 8 + 1)
+    cap = max(1, len(pts))  # every box holds at least one point: never more boxes than points
     out = (Rect * cap)()
     n = C.c_int32()
     st = L.mim_detect_boxes(C.c_void_p(pts.ctypes.data), len(pts), C.byref(bp), out, cap, C.byref(n))
     if st != 0:
         raise _lib.MimError(st, "mim_detect_boxes failed")
+    if n.value > cap:
+        raise _lib.MimError(2, f"mim_detect_boxes: {n.value} boxes for {len(pts)} points")
     return [(out[i].x, out[i].y, out[i].width, out[i].height) for i in range(n.value)]
 
 
@@ -116,19 +118,14 @@ def detect_objects(matcher: Matcher, scene_gray, models: list[ObjectModel], scal
     scene_ids = [matcher.add_set(d, np.stack([k["x"], k["y"]], 1)) for k, d in zip(scene_kp, scene_desc)]
     tags = [(mi, si, vi) for mi in range(len(models)) for si in range(len(scales)) for vi in range(len(view_ids[mi]))]
     res = matcher.match_batch([(view_ids[mi][vi], scene_ids[si]) for mi, si, vi in tags], params)
-    pts = [[] for _ in models]
-    for i, (mi, si, vi) in enumerate(tags):
-        r = res[i]
-        if r["status"] != 0:  # :74, :79, :81, :84
-            continue
-        q, t, mask = matcher.problem_detail(i, int(r["n_good"]))
-        k = scene_kp[si][t[mask.astype(bool)]]
-        p = np.stack([k["x"], k["y"]], 1).astype(np.float32)
-        s = np.float32(scales[si])
-        if s != np.float32(1.0):  # scalePoints (:48-55): pt /= scale in float
-            p = p / s
-        pts[mi].append(p)
-    points = [np.concatenate(p).astype(np.float32) if p else np.zeros((0, 2), np.float32) for p in pts]
+    # :87-94 inlier scene points of the accepted problems (:74, :79, :81, :84), /scale when scale != 1,
+    # gathered on the device in batch order; a model's problems are contiguous (model-major tags)
+    offs, allpts = matcher.batch_inlier_points(len(tags), np.array([scales[si] for _, si, _ in tags], np.float32))
+    points, i0 = [], 0
+    for mi in range(len(models)):
+        i1 = i0 + len(scales) * len(view_ids[mi])
+        points.append(allpts[offs[i0]:offs[i1]].copy())
+        i0 = i1
     dets = []
     for mi, m in enumerate(models):  # :111-248, model order
         dets += [(b, m.name) for b in detect_boxes(points[mi], box_params)]

@@ -78,9 +78,13 @@ class Dataset:
 
 
 def make_dataset(n_models: int, n_scenes: int, nq: int, nt: int, n_plant: int,
-                 inlier_frac: float = 0.08, seed: int = SEED_BASE) -> Dataset:
+                 inlier_frac: float = 0.08, seed: int = SEED_BASE, scene_ids=None) -> Dataset:
+    """``scene_ids``: generate only these scenes of the ``n_scenes``-scene batch (scene s is seeded by
+    ``seed + 1 + s`` alone, so a rank's shard of a global batch is the same data whichever rank, and
+    however many ranks, generate it: C4's sharding, bench.py)."""
     if n_models * n_plant > nt or n_plant > nq:
         raise ValueError("planted rows do not fit")
+    ids = list(range(n_scenes)) if scene_ids is None else [int(x) for x in scene_ids]
     mrng = np.random.default_rng(seed)
     model_desc, model_kp = [], []
     for _ in range(n_models):
@@ -88,10 +92,10 @@ def make_dataset(n_models: int, n_scenes: int, nq: int, nt: int, n_plant: int,
         model_kp.append(np.c_[mrng.uniform(0, IMG_W, nq), mrng.uniform(0, IMG_H, nq)].astype(np.float32))
     n_inl = int(round(inlier_frac * n_plant))
     scene_desc, scene_kp = [], []
-    H_true = np.zeros((n_models, n_scenes, 3, 3))
-    plant_pos = np.zeros((n_models, n_scenes, n_plant), dtype=np.int64)
-    for s in range(n_scenes):
-        srng = np.random.default_rng(seed + 1 + s)
+    H_true = np.zeros((n_models, len(ids), 3, 3))
+    plant_pos = np.zeros((n_models, len(ids), n_plant), dtype=np.int64)
+    for s, gs in enumerate(ids):
+        srng = np.random.default_rng(seed + 1 + gs)
         d = sift_like(srng, nt)
         kp = np.c_[srng.uniform(0, IMG_W, nt), srng.uniform(0, IMG_H, nt)].astype(np.float32)
         pos = srng.permutation(nt)[: n_models * n_plant].reshape(n_models, n_plant)
@@ -161,19 +165,22 @@ def c1_shapes(seed: int = SEED_BASE):
     return nqs, nts
 
 
-def make_config_dataset(name: str, seed: int = SEED_BASE) -> Dataset:
+def make_config_dataset(name: str, seed: int = SEED_BASE, scene_ids=None) -> Dataset:
     cfg = CONFIGS[name]
     if cfg.get("ragged"):
         nqs, nts = c1_shapes(seed)
         return make_ragged_dataset(nqs, nts, seed=seed)
-    return make_dataset(cfg["n_models"], cfg["n_scenes"], cfg["nq"], cfg["nt"], cfg["n_plant"], seed=seed)
+    return make_dataset(cfg["n_models"], cfg["n_scenes"], cfg["nq"], cfg["nt"], cfg["n_plant"], seed=seed,
+                        scene_ids=scene_ids)
 
 
 # Configs of BASELINE.json: C1 is the reference's own real-data case (no SIFT here: its surrogate
-# shapes); C4 is C3's workload sharded over 8 GPUs; C5 is the distance kernel alone.
+# shapes); C4 is one global 256-scene batch (1 model set) whose scenes are sharded
+# over the GPUs; C5 is the distance kernel alone.
 CONFIGS = {
     "c1": dict(ragged=True, n_models=29, n_scenes=5, nq=500, nt=4000, max_iters=2000),
     "c2": dict(n_models=1, n_scenes=1, nq=2000, nt=2000, n_plant=400, max_iters=2000),
     "c3": dict(n_models=3, n_scenes=32, nq=10000, nt=10000, n_plant=2000, max_iters=50000),
+    "c4": dict(n_models=1, n_scenes=256, nq=10000, nt=10000, n_plant=2000, max_iters=50000, sharded=True),
     "c5": dict(n_models=1, n_scenes=1, nq=50000, nt=50000, n_plant=0, max_iters=0, knn_only=True),
 }

@@ -154,6 +154,17 @@ mim_status mim_batch_results_copy(struct mim_ctx* ctx, void* dst, int32_t dst_on
  * and its RANSAC inlier mask (n_good bytes).  Any output may be NULL. */
 mim_status mim_batch_problem_detail(struct mim_ctx* ctx, int32_t i, int32_t* q_idx, int32_t* t_idx,
                                     uint8_t* mask);
+/* allUnfilteredScenePts of the last batch, gathered on the device (TestsDetector.cpp:87-94): for every
+ * accepted problem (MIM_ACCEPTED) in batch order, the scene keypoints of its RANSAC inliers in mask
+ * order, each divided by scales[i] in float when scales[i] != 1.0f (scalePoints, :48-55; scales NULL:
+ * no division).  offsets (n + 1 entries): problem i's points are out_xy[2 offsets[i] .. 2 offsets[i+1]);
+ * rejected problems have none, so a model whose problems are contiguous in the batch gets its points
+ * as one slice.  Waits for the batch (re-running it if the RNG stream was short, as
+ * mim_batch_results), then one table copy in, one kernel, one copy out — instead of a
+ * mim_batch_problem_detail round trip per accepted problem.  out_xy NULL: offsets only;
+ * offsets[n] > cap: MIM_ERANGE (offsets valid, nothing copied). */
+mim_status mim_batch_inlier_points(struct mim_ctx* ctx, const float* scales, float* out_xy, int64_t cap,
+                                   int64_t* offsets);
 
 /* ---- distance kernel alone on registered sets (C5 dense-contraction config) ------------------
  * Asynchronous.  idx_dev / dist_dev: device buffers of 2*nq int32 / float32. */

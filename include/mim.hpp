@@ -82,6 +82,53 @@ class Detector {
         run(models, scales, out);
     }
 
+    // SIFT::create()->detectAndCompute(gray, mask, kps, desc) on the device (ModelsDetector.cpp:75 with
+    // the view's mask, TestsDetector.cpp:106 without): keypoints in OpenCV's order + n x 128 CV_32F rows.
+    void sift(const uint8_t* gray, int rows, int cols, int64_t step, const uint8_t* mask, int64_t mask_step,
+              std::vector<mim_keypoint>& kps, std::vector<float>& desc) {
+        int32_t cap = 1 << 14, n = 0;
+        for (;;) {
+            kps.resize(cap);
+            desc.resize((size_t)cap * 128);
+            const mim_status s = mim_sift_detect_compute(ctx_, gray, rows, cols, step, mask, mask_step, cap, kps.data(),
+                                                         desc.data(), &n);
+            if (s != MIM_OK && s != MIM_ERANGE) check(s, "mim_sift_detect_compute", ctx_);
+            if (n <= cap) break;
+            cap = n;  // more keypoints than the buffer: call again with room for all
+        }
+        kps.resize(n);
+        desc.resize((size_t)n * 128);
+    }
+
+    // TestsDetector.cpp:99-107 in one call: resize(scene, Size(), s, s) + SIFT for every scale s.
+    void sift_scales(const uint8_t* gray, int rows, int cols, int64_t step, const std::vector<float>& scales,
+                     std::vector<std::vector<mim_keypoint>>& kps, std::vector<std::vector<float>>& desc) {
+        const int ns = (int)scales.size();
+        std::vector<int32_t> n(ns, 0);
+        std::vector<mim_keypoint> k;
+        std::vector<float> d;
+        int32_t cap = 1 << 16;
+        for (;;) {
+            k.resize(cap);
+            d.resize((size_t)cap * 128);
+            const mim_status s = mim_sift_detect_compute_scales(ctx_, gray, rows, cols, step, ns, scales.data(), cap,
+                                                                k.data(), d.data(), n.data());
+            if (s == MIM_OK) break;
+            if (s != MIM_ERANGE) check(s, "mim_sift_detect_compute_scales", ctx_);
+            int64_t tot = 0;
+            for (int32_t x : n) tot += x;
+            cap = (int32_t)tot;
+        }
+        kps.assign(ns, {});
+        desc.assign(ns, {});
+        size_t o = 0;
+        for (int i = 0; i < ns; ++i) {
+            kps[i].assign(k.begin() + o, k.begin() + o + n[i]);
+            desc[i].assign(d.begin() + o * 128, d.begin() + (o + n[i]) * 128);
+            o += n[i];
+        }
+    }
+
    private:
     static void check(mim_status s, const char* what, mim_ctx* c = nullptr) {
         if (s != MIM_OK) throw Error(s, std::string(what) + ": " + (c ? mim_last_error(c) : "failed"));
@@ -120,26 +167,19 @@ class Detector {
         if (probs.empty()) return;
         check(mim_batch_run(ctx_, probs.data(), (int32_t)probs.size(), &params_), "mim_batch_run", ctx_);
         check(mim_batch_results(ctx_, results_.data()), "mim_batch_results", ctx_);
-        std::vector<int32_t> qi, ti;
-        std::vector<uint8_t> mask;
-        for (size_t i = 0; i < probs.size(); ++i) {
-            const mim_result& r = results_[i];
-            if (r.status != MIM_ACCEPTED) continue;  // :74, :79, :81, :84
-            qi.resize(r.n_good);
-            ti.resize(r.n_good);
-            mask.resize(r.n_good);
-            check(mim_batch_problem_detail(ctx_, (int32_t)i, qi.data(), ti.data(), mask.data()), "detail", ctx_);
-            const ScaledScene& sc = scales[tags[i].s];
-            for (int j = 0; j < r.n_good; ++j) {  // :87-94 inlier scene points, /scale when scale != 1
-                if (!mask[j]) continue;
-                Point2f p = (*sc.kp)[ti[j]];
-                if (sc.scale != 1.0f) {
-                    p.x /= sc.scale;
-                    p.y /= sc.scale;
-                }
-                out[tags[i].m].push_back(p);
-            }
-        }
+        // :87-94 inlier scene points of the accepted problems (:74, :79, :81, :84), divided by the scale
+        // when it is not 1, gathered on the device in batch order (one copy); model m's problems are
+        // contiguous in the batch, so its points are one slice
+        std::vector<float> sc(probs.size());
+        for (size_t i = 0; i < probs.size(); ++i) sc[i] = scales[tags[i].s].scale;
+        std::vector<int64_t> offs(probs.size() + 1);
+        check(mim_batch_inlier_points(ctx_, sc.data(), nullptr, 0, offs.data()), "mim_batch_inlier_points", ctx_);
+        std::vector<Point2f> pts((size_t)offs.back());
+        if (!pts.empty())
+            check(mim_batch_inlier_points(ctx_, sc.data(), &pts[0].x, offs.back(), offs.data()),
+                  "mim_batch_inlier_points", ctx_);
+        for (size_t i = 0; i < probs.size(); ++i)
+            out[tags[i].m].insert(out[tags[i].m].end(), pts.begin() + offs[i], pts.begin() + offs[i + 1]);
     }
 
     mim_ctx* ctx_ = nullptr;

@@ -260,3 +260,55 @@ def test_train_set_limit_is_einval(matcher):
         matcher.match_batch([(a, b)], default_params())
     matcher.match_batch([(b, a)], default_params())  # as the query side it is fine
     matcher.clear_sets()
+
+
+def test_problem_detail_after_short_stream_reruns(oracle):
+    """MIM_STREAM_DRAWS=8192, problem details read BEFORE mim_batch_results: mim_batch_problem_detail
+    finishes the batch first (grows the stream and re-runs it), so the masks are the final ones."""
+    from computervision_objectdetection_featurematching_amd import Matcher, default_params
+    os.environ["MIM_STREAM_DRAWS"] = "8192"
+    m = Matcher(0)
+    try:
+        ds = make_dataset(1, 3, 800, 1500, 300, inlier_frac=0.08, seed=1234)
+        q = [m.add_set(d, k) for d, k in zip(ds.model_desc, ds.model_kp)]
+        t = [m.add_set(d, k) for d, k in zip(ds.scene_desc, ds.scene_kp)]
+        n = m.match_batch_async([(q[a], t[b]) for a, b in ds.problems], default_params(max_iters=2000))
+        outs = _oracle_all(oracle, ds, 2000)
+        det = [m.problem_detail(i, outs[i]["n_good"]) for i in range(n)]  # before any batch_results
+        res = m.batch_results(n)
+        assert not (res["status"] == 5).any()
+        _compare(res, det, outs)
+    finally:
+        m.close()
+        os.environ.pop("MIM_STREAM_DRAWS", None)
+
+
+def test_batch_inlier_points_equals_per_problem_gather(matcher):
+    """mim_batch_inlier_points (TestsDetector.cpp:87-94 on the device) against the per-problem route
+    (problem_detail + host gather + scalePoints): same points, same order, same float bits, with
+    scales 1 (no division) and the reference's 0.7 .. 1.3."""
+    from computervision_objectdetection_featurematching_amd import default_params
+    ds = make_dataset(2, 5, 1200, 2000, 400, inlier_frac=0.3, seed=4242)
+    matcher.clear_sets()
+    q = [matcher.add_set(d, k) for d, k in zip(ds.model_desc, ds.model_kp)]
+    t = [matcher.add_set(d, k) for d, k in zip(ds.scene_desc, ds.scene_kp)]
+    probs = [(q[a], t[b]) for a, b in ds.problems]
+    res = matcher.match_batch(probs, default_params(max_iters=2000))
+    assert (res["status"] == 0).sum() >= 4 and (res["status"] != 0).sum() >= 1 or (res["status"] == 0).all()
+    scales = np.array([0.7, 0.85, 1.0, 1.15, 1.3], np.float32)[[b for _, b in ds.problems]]
+    for sc in (None, scales):
+        offs, pts = matcher.batch_inlier_points(len(probs), sc)
+        exp = []
+        for i, r in enumerate(res):
+            n = int(offs[i + 1] - offs[i])
+            if r["status"] != 0:
+                assert n == 0
+                continue
+            _, ti, mk = matcher.problem_detail(i, int(r["n_good"]))
+            p = ds.scene_kp[ds.problems[i][1]][ti[mk.astype(bool)]].astype(np.float32)
+            if sc is not None and sc[i] != np.float32(1.0):
+                p = p / sc[i]
+            assert n == len(p) == int(r["n_inl"])
+            exp.append(p)
+        exp = np.concatenate(exp) if exp else np.zeros((0, 2), np.float32)
+        np.testing.assert_array_equal(pts.view(np.int32), exp.astype(np.float32).view(np.int32))

@@ -8,7 +8,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from computervision_objectdetection_featurematching_amd import Matcher  # noqa: E402
 
-z = np.load(os.path.join(ROOT, "tools", "ds_slow.npz"))
+z = np.load(os.path.join(ROOT, "tests", "golden", "ds_small_problems.npz"))
 m = Matcher(0)
 m.set_timing(True)
 for k in sorted(z.files):

@@ -61,9 +61,9 @@ H_TOL = 1e-4                  # SURVEY.md 8(c) contract item 4 (the GPU tests ho
 
 def pmc_traffic(kernel, config):
     """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC pass (or None)."""
-    for rnd in ("r03", "r02", "r01"):
+    for name in (f"r03_pmc_traffic_{config}.json",):  # this round's kernels only (older passes measured other code)
         try:
-            with open(os.path.join(ROOT, "profiles", f"{rnd}_pmc_traffic.json")) as f:
+            with open(os.path.join(ROOT, "profiles", name)) as f:
                 d = json.load(f)
             if d.get("config", "c3") != config:
                 continue
@@ -96,6 +96,9 @@ def parse():
                          "hardware queue)")
     ap.add_argument("--hw-queues", type=int, default=16,
                     help="GPU_MAX_HW_QUEUES for this process and the ranks it launches (set before HIP initialises)")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl = RCCL over xGMI (one GPU per rank); gloo = rehearsal of the N-rank path with several "
+                         "ranks on one GPU (the record gather through host memory)")
     ap.add_argument("--dry-run", action="store_true",
                     help="no GPU: launch the ranks, gather fake records over gloo, print the JSON line")
     return ap.parse_args()
@@ -368,6 +371,21 @@ def run_c1img(args, rank, world, local):
         t1 = time.perf_counter()
         m.sift_detect_compute(scene)
         ts.append(time.perf_counter() - t1)
+    # isolated pass (not part of `value`): one scene at a time on one context, kernel timing on — the
+    # single-scene latency and the distance kernel's launch duration
+    m.set_sampler_stream(True)
+    m.set_timing(True)
+    n_iso = max(args.iso_steps, 1)
+    t1 = time.perf_counter()
+    for _ in range(n_iso):
+        run = detect_objects(m, scene, [model], keep=True)
+    scene_ms = 1e3 * (time.perf_counter() - t1) / n_iso
+    m.batch_results(0)
+    iso = {k: m.kernel_ms(k) / n_iso for k in ("knn", "ratio", "attempt", "chain", "check", "sample", "score", "cand",
+                                                 "exact", "select", "refine") if m.kernel_ms(k) > 0}
+    nq = np.array([d.shape[0] for d in model.descriptors], np.float64)
+    nt = np.array([len(k) for k in run.scene_kp], np.float64)
+    knn_ops = float(2.0 * 128 * nq.sum() * nt.sum())  # every (view, scale) pair
     if rank == 0:
         out = {"metric": "matches+homographies/sec (configs[0]: sugar_box model vs one test view, reference images, "
                          "SIFT + match + RANSAC + boxes)",
@@ -382,6 +400,16 @@ def run_c1img(args, rank, world, local):
                           "scenes_in_flight": nf},
                "scenes_per_s": round(world * args.steps / el, 3),
                "sift_640x480_ms": round(1e3 * statistics.median(ts), 3),
+               "single_scene_ms": round(scene_ms, 3),
+               "roofline": {"kernel": "knn2_i8_kernel (145 ragged problems of one scene, 1 launch per scene)",
+                            "bound": "mfma", "unit": "TFLOP/s", "peak": PEAK_I8_TOPS,
+                            "achieved": round(knn_ops / (iso["knn"] * 1e-3) / 1e12, 2),
+                            "frac": round(knn_ops / (iso["knn"] * 1e-3) / 1e12 / PEAK_I8_TOPS, 4),
+                            "traffic": None, "launch_ms": round(iso["knn"], 4), "ops_per_launch": knn_ops,
+                            "timing": "HIP events, isolated pass (one scene at a time, one context)",
+                            "kernel_ms_per_scene_isolated": {k: round(v, 4) for k, v in iso.items()},
+                            "note": "small problems (Nq ~100-500 x Nt ~1-4k): launch- and latency-bound, the "
+                                    "MFMA fraction is not the limiter at this size"},
                "detections_rank0": [list(b) for b, _ in dets],
                "accepted_problems_rank0": int((run.results["status"] == 0).sum())}
         if args.cpu_sample > 0:
@@ -500,15 +528,21 @@ def main():
     rank, world, local = dist_env()
     import torch
     import torch.distributed as dist
+    if args.dist_backend == "gloo":  # rehearsal: every rank on the visible GPU(s), round robin
+        local = local % max(torch.cuda.device_count(), 1)
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
     if args.config == "c1img":
         return run_c1img(args, rank, world, local)
     ranks_seen = dist.get_world_size() if world > 1 else 1
     if ranks_seen != args.gpus:
         raise SystemExit(f"rank {rank}: {ranks_seen} ranks in the process group, --gpus {args.gpus}")
     dev = torch.device("cuda", local)
+    cdev = dev if args.dist_backend == "nccl" else torch.device("cpu")  # where the collectives' tensors live
 
     from computervision_objectdetection_featurematching_amd import Matcher, build, default_params, shard
     from computervision_objectdetection_featurematching_amd._lib import RESULT_DTYPE
@@ -564,7 +598,8 @@ def main():
                 return
             m.match_batch_async([(q_ids[a], t_ids[b]) for a, b in ds.problems], prm)
             m.batch_results_copy_to(mine[k])
-            gath[k] = shard.gather_results(mine[k], world)  # RCCL all-gather of the result records
+            # RCCL all-gather of the result records (gloo rehearsal: through host memory)
+            gath[k] = shard.gather_results(mine[k] if cdev.type == "cuda" else mine[k].cpu(), world)
 
     for mm in matchers:
         mm.set_timing(False)
@@ -585,7 +620,7 @@ def main():
         dist.barrier()
     el = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        t = torch.tensor([el], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     total = global_batch * args.steps
@@ -640,7 +675,7 @@ def main():
         elif world > 1 and args.parity_sample > 0:
             k = min(args.parity_sample, n_probs)
             checked, bad = parity_sample(ds, cfg, res, detail, [(7 * j + rank) % n_probs for j in range(k)])
-    tot = torch.tensor([checked, len(bad), short_timed], dtype=torch.int64, device=dev)
+    tot = torch.tensor([checked, len(bad), short_timed], dtype=torch.int64, device=cdev)
     if world > 1:
         dist.all_reduce(tot)  # every rank's parity sample and cut-short count
 
@@ -676,7 +711,7 @@ def main():
             "data": "synthetic SIFT-like integer descriptors (seeded)" + ("" if knn_only else
                                                                         ", planted geometric inliers"),
             "config": {"workload": workload, "problems_per_gpu": n_probs, "global_batch": global_batch,
-                       "parallelism": f"dp{world}", "batches_in_flight": nf,
+                       "parallelism": f"dp{world}", "batches_in_flight": nf, "dist_backend": args.dist_backend,
                        "hw_queues": int(os.environ["GPU_MAX_HW_QUEUES"])},
         }
         if warm_note := ("" if n_warm == args.warmup else f"--warmup {args.warmup} raised to {n_warm}: every one of "

@@ -46,15 +46,9 @@ __device__ __forceinline__ void prep_tile(const float* __restrict__ src, int n, 
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
         const int ci = k * 256 + tid;  // output chunk (16 B) within the tile
-#ifndef MIM_KNN_LEGACY32  // [row block rb 0..3][kstep 0..1][lane]: row 16 rb + (lane & 15), col 64 ks + 16 (lane >> 4)
-        const int rb = ci >> 7, s = (ci >> 6) & 1, lane = ci & 63;
-        const int row = tile * 64 + 16 * rb + (lane & 15);
-        const int col = 64 * s + 16 * (lane >> 4);
-#else
         const int u = ci >> 8, s = (ci >> 6) & 3, lane = ci & 63;
         const int row = tile * 64 + 32 * u + (lane & 31);
         const int col = 32 * s + 16 * (lane >> 5);
-#endif
         uint32_t o[4] = {0, 0, 0, 0};
         if (row < n) {
             const float4* p = reinterpret_cast<const float4*>(src + (size_t)row * kDim + col);
@@ -176,12 +170,22 @@ constexpr int kRescan = -2;  // Top2::i2 marker: the split's top-2 needs the exa
 #define MIM_KNN_EARLY 4
 #endif
 constexpr int kEarlyTiles = MIM_KNN_EARLY;
+// timing probes only (results invalid): MIM_KNN_NODMA = stages past the first never re-staged (the loop
+// reads stale LDS: isolates the LDS-DMA issue cost), MIM_KNN_NOBAR = no per-stage barrier either
+#ifdef MIM_KNN_NODMA
+constexpr bool kProbeNoDma = true;
+#else
+constexpr bool kProbeNoDma = false;
+#endif
+#ifdef MIM_KNN_NOBAR
+constexpr bool kProbeNoBarrier = true;
+#else
+constexpr bool kProbeNoBarrier = false;
+#endif
 #ifndef MIM_KNN_LATE_UNROLL
 #define MIM_KNN_LATE_UNROLL 1
 #endif
-#ifndef MIM_KNN_PF
-#define MIM_KNN_PF 1
-#endif
+
 
 // Threshold on R of a lane in the late tiles.  Lanes l, l ^ 32 hold the same query over disjoint
 // row halves; the union of their two top-2 lists always contains the query's top-2 so far.  A new
@@ -215,7 +219,6 @@ static_assert(kStageChunks * 16 * kThreads == kStage * kTileBytes, "stage split"
 #ifndef MIM_KNN_OCC
 #define MIM_KNN_OCC 4
 #endif
-#ifdef MIM_KNN_LEGACY32  // round-2 kernel (v_mfma_i32_32x32x32_i8, no deferred epilogue), kept for A/B
 __global__ __launch_bounds__(kThreads, MIM_KNN_OCC) void knn2_i8_kernel(  // OCC = waves per SIMD
     const ProbDev* __restrict__ probs, const KnnWork* __restrict__ works, const int* __restrict__ seg_start,
     Top2* __restrict__ parts) {
@@ -410,18 +413,18 @@ __global__ __launch_bounds__(kThreads, MIM_KNN_OCC) void knn2_i8_kernel(  // OCC
     for (; stage < tile_e; stage += kStage) {
         const int buf = ((stage - w.tile0) / kStage) & 1;
         const bool more = stage + kStage < w.tile1;
-        if (more) stage_dma(stage + kStage, buf ^ 1);
+        if (more && !kProbeNoDma) stage_dma(stage + kStage, buf ^ 1);
         const unsigned char* sb = smem + buf * kStage * kLdsTile;
 #pragma unroll
         for (int ts = 0; ts < kStage; ++ts)
             if (kStage == 1 || stage + ts < w.tile1) tile_early(sb + ts * kLdsTile, stage + ts);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA into the next buffer landed
-        __syncthreads();
+        if (!kProbeNoBarrier) __syncthreads();
     }
     for (; stage < w.tile1; stage += kStage) {
         const int buf = ((stage - w.tile0) / kStage) & 1;
         const bool more = stage + kStage < w.tile1;
-        if (more) stage_dma(stage + kStage, buf ^ 1);
+        if (more && !kProbeNoDma) stage_dma(stage + kStage, buf ^ 1);
         const unsigned char* sb = smem + buf * kStage * kLdsTile;
 #pragma unroll
         for (int u = 0; u < QT; ++u) {
@@ -440,7 +443,7 @@ __global__ __launch_bounds__(kThreads, MIM_KNN_OCC) void knn2_i8_kernel(  // OCC
         for (int ts = 0; ts < kStage; ++ts)
             if (kStage == 1 || stage + ts < w.tile1) tile_late(sb + ts * kLdsTile, stage + ts);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA into the next buffer landed
-        __syncthreads();
+        if (!kProbeNoBarrier) __syncthreads();
     }
 
     // ---- merge the two lane halves (disjoint train rows of the same query), keys ----
@@ -471,263 +474,6 @@ __global__ __launch_bounds__(kThreads, MIM_KNN_OCC) void knn2_i8_kernel(  // OCC
   }
 }
 
-#endif  // MIM_KNN_LEGACY32
-
-#ifndef MIM_KNN_LEGACY32
-// ------------------------------------------------------------------------------------------------
-// Exact distance kernel on v_mfma_i32_16x16x64_i8 with a deferred selection epilogue.
-//
-// Block = kKnnWaves waves, wave = kKnnCT column tiles of 16 queries (q' fragments in VGPRs for the
-// whole sweep).  Train rows stream HBM -> LDS by LDS-DMA in stages of kKnnStage 64-row tiles (double
-// buffer, one barrier per stage).  A 64-row tile is four 16-row blocks; per block a wave reads two A
-// fragments (ds_read_b128), the 4 seeds floor(n2/2) of its lane's rows and the parity bits, and issues
-// 2 x kKnnCT MFMAs: lane l then holds query 16 ct + (l & 15) against train rows 16 rb + 4 (l >> 4) + i,
-// i = 0..3, as R = q'.t'' + floor(n2/2) (D = d^2 - c(q) = 2R + (n2 & 1), exact).
-//
-// Software pipeline: the selection of block b (min of the lane's 4 R per column tile, threshold
-// test, rare insertions) runs after block b + 1's MFMAs are issued, on accumulators carried in
-// registers, so its VALU work overlaps the matrix pipe instead of waiting for the MFMA results
-// (the round-2 kernel drained the pipe before every epilogue).  The 16x16 shape also holds a higher
-// clock under load than 32x32x32.
-//
-// Selection: per column tile the min over a lane's 4 R is tested against the threshold
-// T = floor(Dc / 2), Dc = the 2nd smallest D of the query's 4-lane group (exact at each stage start
-// and at every tile of the first kEarlyTiles, lowered by the lane's own 2nd best after an insertion:
-// always >= the group's 2nd best, so no row that can enter the query's top-2 is skipped; INT_MAX
-// until the group holds two rows, so the first rows all enter); a hit ballots the 4 rows and inserts
-// the ones some lane holds under T.
-// ------------------------------------------------------------------------------------------------
-constexpr int kCT = kKnnCT;
-
-// 2nd smallest D of the query's 4-lane group (lanes l & 15 + 16 g), each lane holding m1 <= m2,
-// as a threshold on R: R <= floor(Dc / 2)
-__device__ __forceinline__ int sel_filter4(const LaneSel& s) {
-    int a1 = s.m1, a2 = s.m2;
-    {
-        const auto x = __builtin_amdgcn_permlane16_swap(a1, a1, false, false);
-        const auto y = __builtin_amdgcn_permlane16_swap(a2, a2, false, false);
-        const bool odd = threadIdx.x & 16;
-        const int b1 = odd ? (int)x[0] : (int)x[1], b2 = odd ? (int)y[0] : (int)y[1];
-        const int n2 = min(max(a1, b1), min(a2, b2));
-        a1 = min(a1, b1);
-        a2 = n2;
-    }
-    {
-        const auto x = __builtin_amdgcn_permlane32_swap(a1, a1, false, false);
-        const auto y = __builtin_amdgcn_permlane32_swap(a2, a2, false, false);
-        const bool hi = threadIdx.x & 32;
-        const int b1 = hi ? (int)x[0] : (int)x[1], b2 = hi ? (int)y[0] : (int)y[1];
-        a2 = min(max(a1, b1), min(a2, b2));
-    }
-    return a2 >> 1;
-}
-
-__global__ __launch_bounds__(kThreads, MIM_KNN_OCC) void knn2_i8_kernel(  // OCC = waves per SIMD
-    const ProbDev* __restrict__ probs, const KnnWork* __restrict__ works, const int* __restrict__ seg_start,
-    Top2* __restrict__ parts) {
-    __shared__ __attribute__((aligned(16))) unsigned char smem[2 * kStage * kLdsTile];
-  for (int si = seg_start[blockIdx.x]; si < seg_start[blockIdx.x + 1]; ++si) {  // the block's segments
-    const KnnWork w = works[si];
-    const ProbDev* P = probs + w.problem;
-    if (*P->q.flags | *P->t.flags) continue;  // not integer-valued: generic kernel handles it
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, g = lane >> 4, c16 = lane & 15;
-    const int nq = P->q.n;
-    const uint4* __restrict__ tsrc = reinterpret_cast<const uint4*>(P->t.frag);
-    const int* __restrict__ tnorm = P->t.norm;
-
-    // ---- query fragments q': column tile ct = query rows qbase + 16 ct .. + 15 ----
-    const int qbase = w.q0 + wave * 16 * kCT;
-    i32x4 B[kCT][2];
-#pragma unroll
-    for (int ct = 0; ct < kCT; ++ct) {
-        const int qr = qbase + 16 * ct, qt = qr >> 6, cb = (qr >> 4) & 3;
-        const int qtc = qt < P->q.n_tiles ? qt : 0;  // rows past the set: tile 0, never written out
-        const gi32x4* qsrc = (const gi32x4*)(P->q.frag) + (size_t)qtc * 512;
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) B[ct][ks] = ~qsrc[(cb * 2 + ks) * 64 + lane];  // q' = ~t''
-    }
-    LaneSel st[kCT];
-    int T[kCT];
-#pragma unroll
-    for (int ct = 0; ct < kCT; ++ct) {
-        sel_init(st[ct]);
-        T[ct] = INT_MAX;
-    }
-
-    // ---- LDS-DMA staging (global_load_lds_dwordx4 / _dword), double buffered: one wave-instruction
-    // writes 64 lanes x size contiguous bytes at a wave-uniform LDS base, which the fragment-major
-    // tile already is; the tile's norm half (floor(n2/2), parity mask) is two 256-B pieces ----
-    const int wv = __builtin_amdgcn_readfirstlane(wave);
-    auto stage_dma = [&](int t0, int buf) {
-        unsigned char* base = smem + buf * kStage * kLdsTile;
-#pragma unroll
-        for (int c = 0; c < kStageChunks; ++c) {
-            const int cw = c * kThreads + wv * 64, tt = cw >> 9;  // the wave's first chunk: uniform
-            if (kStage == 1 || t0 + tt < w.tile1)
-                __builtin_amdgcn_global_load_lds((const void*)(tsrc + (size_t)t0 * 512 + cw + lane),
-                                                 (__attribute__((address_space(3))) void*)(base + tt * kLdsTile + (cw & 511) * 16),
-                                                 16, 0, 0);
-        }
-#pragma unroll
-        for (int p = wv; p < 2 * kStage; p += kKnnWaves) {  // piece p: tile p >> 1, norm words 64 (p & 1) ..
-            const int tt = p >> 1;
-            if (kStage == 1 || t0 + tt < w.tile1)
-                __builtin_amdgcn_global_load_lds((const void*)(tnorm + (size_t)(t0 + tt) * kNormWords + 64 * (p & 1) + lane),
-                                                 (__attribute__((address_space(3))) void*)(base + tt * kLdsTile + kTileBytes + 256 * (p & 1)),
-                                                 4, 0, 0);
-        }
-    };
-    if (w.tile0 < w.tile1) stage_dma(w.tile0, 0);
-    __builtin_amdgcn_s_waitcnt(0);  // the q' fragments and the first stage, before the loop
-    __syncthreads();
-
-    // ---- the deferred block: accumulators, parity bits and first row of the block whose selection
-    // is still to run.  Starts as a block of padded rows (R = 2^30 - 1, parity 1: D = INT_MAX, never
-    // inserted).  Row indices are kept without the lane's 4g (added at the end) so they stay uniform.
-    i32x4 accP[kCT];
-#pragma unroll
-    for (int ct = 0; ct < kCT; ++ct) accP[ct] = i32x4{(1 << 30) - 1, (1 << 30) - 1, (1 << 30) - 1, (1 << 30) - 1};
-    unsigned pwP = 0xF;
-    int rowP = 0;
-
-    auto epi_late = [&]() {  // min of the lane's 4 R per column tile against its threshold
-        int mn[kCT];
-        bool hit = false;
-#pragma unroll
-        for (int ct = 0; ct < kCT; ++ct) {
-            mn[ct] = min(min(min(accP[ct][0], accP[ct][1]), accP[ct][2]), accP[ct][3]);
-            hit |= mn[ct] <= T[ct];
-        }
-        if (__builtin_expect(__ballot(hit) != 0, 0)) {
-#pragma unroll
-            for (int ct = 0; ct < kCT; ++ct) {
-                if (__ballot(mn[ct] <= T[ct])) {
-                    // the 4 row ballots first (independent compares into SGPR pairs), then a scalar
-                    // test per row; a row some lane holds under its threshold is pushed in every lane
-                    // (the lane lists stay the exact top-2 of the rows pushed)
-                    unsigned long long hm[4];
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) hm[i] = __ballot(accP[ct][i] <= T[ct]);
-#pragma unroll
-                    for (int i = 0; i < 4; ++i)
-                        if (__builtin_expect(hm[i] != 0, 0))
-                            sel_push(st[ct], dval(accP[ct][i], (pwP >> i) & 1), rowP + i);
-                    T[ct] = min(T[ct], st[ct].m2 >> 1);
-                }
-            }
-        }
-    };
-    // one 16-row block: its MFMAs, then the deferred block's selection (independent of them)
-    // a block's operands in LDS: its two A fragments, the seeds floor(n2/2) and the parity bits of the
-    // lane's 4 rows
-    struct Frag {
-        i32x4 a0, a1, sd;
-        unsigned pw;
-    };
-    auto load = [&](const unsigned char* tb, int rb) {
-        const i32x4* A = reinterpret_cast<const i32x4*>(tb);
-        Frag f;
-        f.sd = *reinterpret_cast<const i32x4*>(reinterpret_cast<const int*>(tb + kTileBytes) + 16 * rb + 4 * g);
-        f.pw = reinterpret_cast<const unsigned*>(tb + kTileBytes)[64 + (rb >> 1)] >> (16 * (rb & 1) + 4 * g);
-        f.a0 = A[(rb * 2) * 64 + lane];
-        f.a1 = A[(rb * 2 + 1) * 64 + lane];
-        return f;
-    };
-    // one 16-row block: its MFMAs, then the deferred block's selection (independent of them)
-    auto block = [&](const Frag& f, int row) {
-        i32x4 accN[kCT];
-#pragma unroll
-        for (int ct = 0; ct < kCT; ++ct) accN[ct] = __builtin_amdgcn_mfma_i32_16x16x64_i8(f.a0, B[ct][0], f.sd, 0, 0, 0);
-#pragma unroll
-        for (int ct = 0; ct < kCT; ++ct) accN[ct] = __builtin_amdgcn_mfma_i32_16x16x64_i8(f.a1, B[ct][1], accN[ct], 0, 0, 0);
-#ifdef MIM_KNN_NOSEL  // timing probe only (results invalid): the MFMA loop and LDS traffic without the selection
-#pragma unroll
-        for (int ct = 0; ct < kCT; ++ct)
-            st[ct].m1 = min(st[ct].m1, min(min(accP[ct][0], accP[ct][1]), min(accP[ct][2], accP[ct][3])));
-#else
-        epi_late();
-#endif
-#pragma unroll
-        for (int ct = 0; ct < kCT; ++ct) accP[ct] = accN[ct];
-        pwP = f.pw;
-        rowP = row;
-    };
-
-    // thresholds: the group's exact 2nd best at every tile of the first kEarlyTiles (the top-2 still
-    // changes often), then once per stage (in between lowered by the lane's own 2nd best)
-    for (int stage = w.tile0; stage < w.tile1; stage += kStage) {
-        const int buf = ((stage - w.tile0) / kStage) & 1;
-        if (stage + kStage < w.tile1) stage_dma(stage + kStage, buf ^ 1);
-        const unsigned char* sb = smem + buf * kStage * kLdsTile;
-        const bool early = stage - w.tile0 < kEarlyTiles;
-        const int nts = min(kStage, w.tile1 - stage);
-#if MIM_KNN_PF  // the next block's operands are read from LDS while this block's MFMAs run
-        Frag cur = load(sb, 0);
-#pragma unroll MIM_KNN_LATE_UNROLL
-        for (int ts = 0; ts < nts; ++ts) {
-            const unsigned char* tb = sb + ts * kLdsTile;
-            if (ts == 0 || early) {
-#pragma unroll
-                for (int ct = 0; ct < kCT; ++ct) T[ct] = sel_filter4(st[ct]);
-            }
-#pragma unroll
-            for (int rb = 0; rb < 4; ++rb) {
-                const Frag nxt = rb < 3 ? load(tb, rb + 1) : (ts + 1 < nts ? load(tb + kLdsTile, 0) : cur);
-                block(cur, (stage + ts) * 64 + 16 * rb);
-                cur = nxt;
-            }
-        }
-#else
-#pragma unroll MIM_KNN_LATE_UNROLL
-        for (int ts = 0; ts < nts; ++ts) {
-            if (ts == 0 || early) {
-#pragma unroll
-                for (int ct = 0; ct < kCT; ++ct) T[ct] = sel_filter4(st[ct]);
-            }
-#pragma unroll
-            for (int rb = 0; rb < 4; ++rb) block(load(sb + ts * kLdsTile, rb), (stage + ts) * 64 + 16 * rb);
-        }
-#endif
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA into the next buffer landed
-        __syncthreads();
-    }
-    // the last block's selection (its thresholds: exact again)
-#pragma unroll
-    for (int ct = 0; ct < kCT; ++ct) T[ct] = sel_filter4(st[ct]);
-    epi_late();
-
-    // ---- merge the four lanes of each query (disjoint train rows), keys ----
-#pragma unroll
-    for (int ct = 0; ct < kCT; ++ct) {
-        LaneSel m = st[ct];
-        if (m.i1 != INT_MAX) m.i1 += 4 * g;
-        if (m.i2 != INT_MAX) m.i2 += 4 * g;
-#pragma unroll
-        for (int x = 16; x <= 32; x <<= 1) {
-            LaneSel o;
-            o.m1 = __shfl_xor(m.m1, x); o.m2 = __shfl_xor(m.m2, x);
-            o.i1 = __shfl_xor(m.i1, x); o.i2 = __shfl_xor(m.i2, x);
-            m = sel_merge(m, o);
-        }
-        const int q = qbase + 16 * ct + c16;
-        if (g == 0 && q < nq) {
-            const int qr = qbase + 16 * ct, qt = qr >> 6, cb = (qr >> 4) & 3;
-            const int qq = ((const gint*)P->q.norm)[(size_t)qt * kNormWords + 128 + 16 * cb + c16];  // c(q)
-            Top2 t;
-            const int d1 = m.m1 + qq, d2 = m.m2 + qq;  // exact d^2 = D + c(q) (< 2^23)
-            t.k1 = m.i1 == INT_MAX ? FLT_MAX : sqrtf((float)d1);
-            t.k2 = m.i2 == INT_MAX ? FLT_MAX : sqrtf((float)d2);
-            t.i1 = m.i1;
-            t.i2 = m.i2;
-            // d^2 >= 4e6: distinct integers may share a key (sqrt class), where the lower index
-            // wins: rescan exactly.  Below, equal keys mean equal d^2, already in index order.
-            if (t.i2 != INT_MAX && d2 >= 4000000) t.i2 = kRescan;
-            parts[P->part_off + (long long)w.split * P->q_pad + q] = t;
-        }
-    }
-  }
-}
-#endif  // !MIM_KNN_LEGACY32
 
 // ------------------------------------------------------------------------------------------------
 // Exact rescan of the queries the distance kernel marked (kRescan): one wave per query over the

@@ -14,25 +14,18 @@ constexpr int kWave = 64;
 #ifndef MIM_KNN_QT
 #define MIM_KNN_QT 2
 #endif
-#ifndef MIM_KNN_CT
-#define MIM_KNN_CT 4
-#endif
+
 #ifndef MIM_KNN_WAVES
 #define MIM_KNN_WAVES 8
 #endif
 #ifndef MIM_KNN_STAGE
 #define MIM_KNN_STAGE 4
 #endif
-constexpr int kKnnQT = MIM_KNN_QT;             // 32-query MFMA column tiles per wave (legacy 32x32 kernel)
-constexpr int kKnnCT = MIM_KNN_CT;             // 16-query MFMA column tiles per wave (distance kernel)
+constexpr int kKnnQT = MIM_KNN_QT;             // 32-query MFMA column tiles per wave (distance kernel)
 constexpr int kKnnWaves = MIM_KNN_WAVES;       // waves per distance-kernel block
 constexpr int kKnnStage = MIM_KNN_STAGE;       // 64-row train tiles per LDS stage (per barrier)
 constexpr int kKnnMinChunk = 8;                // fewest train tiles per distance-kernel block
-#ifdef MIM_KNN_LEGACY32
 constexpr int kKnnBlockQ = kKnnWaves * 32 * kKnnQT;  // queries per distance-kernel work item
-#else
-constexpr int kKnnBlockQ = kKnnWaves * 16 * kKnnCT;  // queries per distance-kernel work item
-#endif
 
 // One descriptor set = one ObjectModel view (objectModel.hpp:11-16) or one scaled scene
 // (TestsDetector.cpp:104-106), resident in HBM.

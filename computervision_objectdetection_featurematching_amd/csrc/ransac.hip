@@ -2206,7 +2206,7 @@ __device__ __forceinline__ void bound_hypothesis(const float4* __restrict__ P, i
 typedef _Float16 h8v __attribute__((ext_vector_type(8)));
 typedef float f16acc __attribute__((ext_vector_type(16)));
 constexpr float kMfmaErr = 0x1p-15f;
-constexpr int kTileChunk = 16;  // 32-point tiles per LDS stage of the MFMA bound kernel (32 KiB)
+constexpr int kTileChunk = 8;  // 32-point tiles per LDS stage of the MFMA bound kernel (2 x 16 KiB)
 
 // hi + lo = a to 2^-22 relative, with hi = (f16)a and lo = (f16)(a - hi) taken from the SAME value a.
 // `a` is pinned in a register first: given split_f16(u * x), the compiler otherwise forms
@@ -2315,14 +2315,19 @@ __global__ __launch_bounds__(256) void ransac_bound_mfma_kernel(const RansacStat
                                                                 const uint32_t* __restrict__ stream,
                                                                 const uint4* __restrict__ tiles,
                                                                 int2* __restrict__ bounds, int c0, int c1, int bpp,
-                                                                float thr2) {
-    __shared__ uint4 lt[kTileChunk * 128];
-    const int p = blockIdx.x / bpp;
+                                                                float thr2, int n_probs) {
+    __shared__ uint4 lt[2][kTileChunk * 128];
+    // XCD-aware order: blocks b and b + 8 share an XCD under round-robin dispatch (speed only), so
+    // problem p's blocks are the ones with b % 8 == p % 8 and its point tiles are fetched into one
+    // XCD's L2 instead of eight (grid: 8 x ceil(n_probs / 8) x bpp, blocks past n_probs idle)
+    const int xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
+    const int p = xcd + 8 * (j / bpp), kb = j % bpp;
+    if (p >= n_probs) return;
     const int tid = threadIdx.x, lane = tid & 63;
-    const int it = c0 + (blockIdx.x % bpp) * 256 + tid;
+    const int it = c0 + kb * 256 + tid;
     const RansacState S = st[p];
     if (!S.active || S.done) return;  // uniform over the block
-    if (c0 + (blockIdx.x % bpp) * 256 >= min(c1, S.produced)) return;  // whole block idle
+    if (c0 + kb * 256 >= min(c1, S.produced)) return;  // whole block idle
     const bool act = it < c1 && it < S.produced;
     const long long o = probs[p].it_off + it;
     const long long go = probs[p].good_off;
@@ -2432,27 +2437,27 @@ __global__ __launch_bounds__(256) void ransac_bound_mfma_kernel(const RansacStat
     const uint4* __restrict__ T = tiles + (go >> 5) * 128;
     const int nt = (n + 31) >> 5;
     unsigned out0 = 0, out1 = 0, in0 = 0, in1 = 0;
-    for (int t0 = 0; t0 < nt; t0 += kTileChunk) {
+    // point tiles through LDS by LDS-DMA in chunks of kTileChunk, double buffered: the next chunk's
+    // pieces are in flight while this chunk is scored; one barrier per chunk
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    auto stage = [&](int t0, int buf) {
         const int tc = min(kTileChunk, nt - t0);
-        __syncthreads();
-#ifdef MIM_BOUND_REGSTAGE
-        for (int i = tid; i < tc * 128; i += 256) lt[i] = T[(long long)t0 * 128 + i];
-#else
-        // LDS-DMA: every 1-KiB piece of the chunk in flight at once (a register round trip per 16-B
-        // chunk waited for each load before its ds_write: one full load latency per piece)
-        const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
         for (int i0 = wv * 64; i0 < tc * 128; i0 += 256)
             __builtin_amdgcn_global_load_lds((const void*)(T + (long long)t0 * 128 + i0 + lane),
-                                             (__attribute__((address_space(3))) void*)(lt + i0), 16, 0, 0);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
-        __syncthreads();
-        if (!wave_counts) continue;
-        for (int t = 0; t < tc; ++t) {
-            const h8v ax = __builtin_bit_cast(h8v, lt[t * 128 + lane]);
-            const h8v ay = __builtin_bit_cast(h8v, lt[t * 128 + 64 + lane]);
+                                             (__attribute__((address_space(3))) void*)(lt[buf] + i0), 16, 0, 0);
+    };
+    if (nt > 0) stage(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int t0 = 0, buf = 0; t0 < nt; t0 += kTileChunk, buf ^= 1) {
+        const int tc = min(kTileChunk, nt - t0);
+        if (t0 + kTileChunk < nt) stage(t0 + kTileChunk, buf ^ 1);
+        if (wave_counts) {
+          for (int t = 0; t < tc; ++t) {
+            const h8v ax = __builtin_bit_cast(h8v, lt[buf][t * 128 + lane]);
+            const h8v ay = __builtin_bit_cast(h8v, lt[buf][t * 128 + 64 + lane]);
 #ifdef MIM_BOUND_DEBUG_IT
-            if (((t0 + t) * 32 + (lane & 31)) == MIM_BOUND_DEBUG_PT && (blockIdx.x % bpp) == (MIM_BOUND_DEBUG_IT - c0) / 256 &&
+            if (((t0 + t) * 32 + (lane & 31)) == MIM_BOUND_DEBUG_PT && kb == (MIM_BOUND_DEBUG_IT - c0) / 256 &&
                 (tid >> 6) == ((MIM_BOUND_DEBUG_IT - c0) % 256) / 64)
                 printf("[mim] tile pt=%d lane=%d ax=%g %g %g %g %g %g %g %g ay=%g %g %g %g %g %g %g %g\n", MIM_BOUND_DEBUG_PT, lane,
                        (double)ax[0], (double)ax[1], (double)ax[2], (double)ax[3], (double)ax[4], (double)ax[5], (double)ax[6], (double)ax[7],
@@ -2480,7 +2485,7 @@ __global__ __launch_bounds__(256) void ransac_bound_mfma_kernel(const RansacStat
 #ifdef MIM_BOUND_DEBUG_IT  // debug build: the box test of one (iteration, point)
                 {
                     const int row = (t0 + t) * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-                    const int itb = c0 + (blockIdx.x % bpp) * 256 + (tid & ~63);  // the wave's first iteration
+                    const int itb = c0 + kb * 256 + (tid & ~63);  // the wave's first iteration
                     for (int cb = 0; cb < 2; ++cb) {
                         const int itc = itb + 32 * cb + (lane & 31);
                         if (itc == MIM_BOUND_DEBUG_IT && row == MIM_BOUND_DEBUG_PT)
@@ -2506,7 +2511,10 @@ __global__ __launch_bounds__(256) void ransac_bound_mfma_kernel(const RansacStat
                 in0 += __popc(lb0);
                 in1 += __popc(lb1);
             }
+          }
         }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces of the next chunk landed
+        __syncthreads();
     }
     // rows (points) of a column are split over lanes l and l ^ 32
     const unsigned o0 = out0 + __shfl_xor(out0, 32), o1 = out1 + __shfl_xor(out1, 32);
@@ -3486,11 +3494,11 @@ void ransac_enqueue(const RansacParams& prm, int n_probs, const ProbDev* probs, 
             }
         } else {
             if (c0 == 0)
-                ransac_bound_mfma_kernel<true><<<n_probs * bpp256, 256, 0, s>>>(b.state, probs, pts, b.samples, b.stream,
-                                                                                b.tiles, b.bounds, c0, c1, bpp256, thr2);
+                ransac_bound_mfma_kernel<true><<<8 * ((n_probs + 7) / 8) * bpp256, 256, 0, s>>>(
+                    b.state, probs, pts, b.samples, b.stream, b.tiles, b.bounds, c0, c1, bpp256, thr2, n_probs);
             else
-                ransac_bound_mfma_kernel<false><<<n_probs * bpp256, 256, 0, s>>>(b.state, probs, pts, b.samples, b.stream,
-                                                                                 b.tiles, b.bounds, c0, c1, bpp256, thr2);
+                ransac_bound_mfma_kernel<false><<<8 * ((n_probs + 7) / 8) * bpp256, 256, 0, s>>>(
+                    b.state, probs, pts, b.samples, b.stream, b.tiles, b.bounds, c0, c1, bpp256, thr2, n_probs);
             mark(mark_ctx, "score", s);
             if (getenv("MIM_CHECK_BOUNDS")) {  // debug: every bracket against the exact count
                 unsigned long long* dst = nullptr;

@@ -75,6 +75,9 @@ def main():
     res = m.batch_results(len(d["pr"]))
     el = time.perf_counter() - t0
     out["c3_knn_ms"] = round(m.kernel_ms("knn") / args.steps, 4)
+    out["c3_kernels"] = {k: round(m.kernel_ms(k) / args.steps, 4) for k in
+                         ("ratio", "attempt", "chain", "check", "sample", "score", "cand", "exact", "select", "refine")
+                         if m.kernel_ms(k) > 0}
     out["c3_step_ms"] = round(1e3 * el / args.steps, 3)
     out["c3_tops"] = round(2.0 * 1e4 * 1e4 * 128 * 96 / (out["c3_knn_ms"] * 1e-3) / 1e12, 1)
     out["c3_frac"] = round(out["c3_tops"] / 5000.0, 4)

@@ -376,13 +376,17 @@ def run_c1img(args, rank, world, local):
     m.set_sampler_stream(True)
     m.set_timing(True)
     n_iso = max(args.iso_steps, 1)
-    t1 = time.perf_counter()
+    names_k = ("knn", "ratio", "attempt", "chain", "check", "sample", "score", "cand", "exact", "select", "refine")
+    acc = dict.fromkeys(names_k, 0.0)
+    el_iso = 0.0
     for _ in range(n_iso):
+        t1 = time.perf_counter()
         run = detect_objects(m, scene, [model], keep=True)
-    scene_ms = 1e3 * (time.perf_counter() - t1) / n_iso
-    m.batch_results(0)
-    iso = {k: m.kernel_ms(k) / n_iso for k in ("knn", "ratio", "attempt", "chain", "check", "sample", "score", "cand",
-                                                 "exact", "select", "refine") if m.kernel_ms(k) > 0}
+        el_iso += time.perf_counter() - t1
+        for k in names_k:  # each scene's batch collects its own events (match_batch -> batch_results)
+            acc[k] += max(m.kernel_ms(k), 0.0)
+    scene_ms = 1e3 * el_iso / n_iso
+    iso = {k: v / n_iso for k, v in acc.items() if v > 0}
     nq = np.array([d.shape[0] for d in model.descriptors], np.float64)
     nt = np.array([len(k) for k in run.scene_kp], np.float64)
     knn_ops = float(2.0 * 128 * nq.sum() * nt.sum())  # every (view, scale) pair
@@ -571,8 +575,10 @@ def main():
     # C3/C4: 12 batches in flight (+11 % over 3, same box); the C1 surrogate's small batches: 3 (12: -40 %)
     # C5: 2 (one contraction's set prep overlaps the other's distance kernel)
     nf = args.inflight if args.inflight > 0 else (2 if knn_only else (3 if args.config == "c1" else 12))
-    if nf > 1:  # the sampler stream helps one batch alone (+5 %), not batches already overlapping
-        os.environ.setdefault("MIM_SAMPLER_STREAM", "0")
+    # one stream per context: the sampler stream helps one batch alone (+5 %), not batches already
+    # overlapping; with it off the isolated pass's kernels run one after another on one stream, so
+    # their HIP-event durations add up to at most the step (checked in kernel_rooflines)
+    os.environ.setdefault("MIM_SAMPLER_STREAM", "0")
     matchers = [Matcher(local) for _ in range(nf)]
     # each context keeps its own non-blocking HIP stream; torch work of a step (the result gather)
     # is ordered on the same stream

@@ -270,6 +270,9 @@ __global__ __launch_bounds__(kThreads, MIM_KNN_OCC) void knn2_i8_kernel(  // OCC
     // seeds read as a struct type the waitcnt pass could not tell them from the DMA's target and
     // waited for the next stage's DMA before each tile.)
     const int wv = __builtin_amdgcn_readfirstlane(wave);
+#ifdef MIM_KNN_PRIO  // A/B: the second-dispatched half of the block wins issue arbitration (MI355X_MICROARCH.md, 2 waves per SIMD item 4)
+    if (wv >= kKnnWaves / 2) __builtin_amdgcn_s_setprio(1);
+#endif
     auto stage_dma = [&](int t0, int buf) {
         unsigned char* base = smem + buf * kStage * kLdsTile;
 #pragma unroll

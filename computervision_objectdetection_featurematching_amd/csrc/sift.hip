@@ -5,7 +5,9 @@
 // detectAndCompute), SIFT::create() defaults (main.cpp:17): 3 octave layers, contrast 0.04, edge 10,
 // sigma 1.6, first octave -1 (the image doubled), CV_32F descriptors of 0..255 integers.
 //
-// One launch per stage, every pixel / candidate / keypoint its own thread:
+// One launch per stage, every pixel / candidate / keypoint its own thread; the stages after the
+// extrema run on fixed grids over device-side counts, so a call synchronises twice (the counts, then
+// the copies of keypoints and descriptors):
 //   up2       u8 -> float, x2 INTER_LINEAR (createInitialImage)
 //   blur_row  Gaussian row pass, taps in order          } GaussianBlur(CV_32F, BORDER_REFLECT_101):
 //   blur_col  Gaussian column pass, symmetric pairs     } OpenCV's RowFilter / SymmColumnFilter sums
@@ -14,7 +16,8 @@
 //   extrema   26-neighbour test + threshold over layers 1..3, candidates appended
 //   refine    adjustLocalExtrema (<= 5 Newton steps, Cramer 3x3 solve), contrast + edge tests,
 //             calcOrientationHist (36 bins, smoothed), one keypoint per peak >= 80 % of the maximum
-//   (host)    KeyPointsFilter::removeDuplicatedSorted, the 1/2 rescale of octave -1, the mask filter
+//   kp_post   KeyPointsFilter::removeDuplicatedSorted (bitonic sort by KeypointGreater in LDS, one
+//             1024-thread block), the 1/2 rescale of octave -1, the mask filter (runByPixelsMask)
 //   descr     calcSIFTDescriptor: 4x4x8 trilinear histogram in LDS (per thread, pixel order),
 //             wrap, clamp at 0.2 of the norm, x 512 / norm, saturate to 0..255
 // The histograms accumulate in the reference's pixel order (one thread per keypoint), so the results
@@ -248,8 +251,8 @@ struct Surv {  // an extremum that passed adjustLocalExtrema: its keypoint (angl
 // survivors go to orient_kernel (octave field packed as OpenCV's)
 __global__ void refine_kernel(const Pyr* __restrict__ pyr, const Cand* __restrict__ cand, const int* __restrict__ n_cand,
                               int cap, Surv* __restrict__ surv, int* __restrict__ n_surv, int surv_cap) {
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= min(*n_cand, cap)) return;
+  const int n_c = min(*n_cand, cap);
+  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < n_c; t += gridDim.x * blockDim.x) {  // fixed grid
     const float kSigma = 1.6f, kContrast = 0.04f, kEdge = 10.f;
     const float img_scale = 1.f / 255, deriv_scale = img_scale * 0.5f, second_deriv_scale = img_scale;
     const float cross_deriv_scale = img_scale * 0.25f;
@@ -277,13 +280,19 @@ __global__ void refine_kernel(const Pyr* __restrict__ pyr, const Cand* __restric
         xr = -X[1];
         xc = -X[0];
         if (fabsf(xi) < 0.5f && fabsf(xr) < 0.5f && fabsf(xc) < 0.5f) break;
-        if (fabsf(xi) > (float)(INT_MAX / 3) || fabsf(xr) > (float)(INT_MAX / 3) || fabsf(xc) > (float)(INT_MAX / 3)) return;
+        if (fabsf(xi) > (float)(INT_MAX / 3) || fabsf(xr) > (float)(INT_MAX / 3) || fabsf(xc) > (float)(INT_MAX / 3)) {
+            i = 6;  // diverged: rejected
+            break;
+        }
         c += cv_round(xc);
         r += cv_round(xr);
         layer += cv_round(xi);
-        if (layer < 1 || layer > kNOL || c < kBorder || c >= im.cols - kBorder || r < kBorder || r >= im.rows - kBorder) return;
+        if (layer < 1 || layer > kNOL || c < kBorder || c >= im.cols - kBorder || r < kBorder || r >= im.rows - kBorder) {
+            i = 6;  // left the scale space: rejected
+            break;
+        }
     }
-    if (i >= 5) return;
+    if (i >= 5) continue;  // no convergence in 5 steps (or rejected above)
     {
         const Layer im = pyr->dog[octv][layer], pv = pyr->dog[octv][layer - 1], nx = pyr->dog[octv][layer + 1];
         const float dD[3] = {(AT(im, r, c + 1) - AT(im, r, c - 1)) * deriv_scale,
@@ -291,13 +300,13 @@ __global__ void refine_kernel(const Pyr* __restrict__ pyr, const Cand* __restric
                              (AT(nx, r, c) - AT(pv, r, c)) * deriv_scale};
         const float tt = dD[0] * xc + dD[1] * xr + dD[2] * xi;
         contr = AT(im, r, c) * img_scale + tt * 0.5f;
-        if (fabsf(contr) * kNOL < kContrast) return;
+        if (fabsf(contr) * kNOL < kContrast) continue;
         const float v2 = AT(im, r, c) * 2.f;
         const float dxx = (AT(im, r, c + 1) + AT(im, r, c - 1) - v2) * second_deriv_scale;
         const float dyy = (AT(im, r + 1, c) + AT(im, r - 1, c) - v2) * second_deriv_scale;
         const float dxy = (AT(im, r + 1, c + 1) - AT(im, r + 1, c - 1) - AT(im, r - 1, c + 1) + AT(im, r - 1, c - 1)) * cross_deriv_scale;
         const float tr = dxx + dyy, det = dxx * dyy - dxy * dxy;
-        if (det <= 0 || tr * tr * kEdge >= (kEdge + 1) * (kEdge + 1) * det) return;
+        if (det <= 0 || tr * tr * kEdge >= (kEdge + 1) * (kEdge + 1) * det) continue;
     }
     mim_keypoint k;
     k.x = (c + xc) * (1 << octv);
@@ -309,6 +318,7 @@ __global__ void refine_kernel(const Pyr* __restrict__ pyr, const Cand* __restric
 
     const int slot = atomicAdd(n_surv, 1);
     if (slot < surv_cap) surv[slot] = Surv{k, r, c, layer};
+  }
 }
 
 // calcOrientationHist + the peak loop of findScaleSpaceExtrema, one wave per surviving extremum.  The
@@ -321,8 +331,9 @@ __global__ __launch_bounds__(64) void orient_kernel(const Pyr* __restrict__ pyr,
     __shared__ int rb[64];
     __shared__ float rv[64];
     __shared__ float th[kOriBins + 4];
-    const int t = blockIdx.x, lane = threadIdx.x;
-    if (t >= min(*n_surv, surv_cap)) return;
+    const int lane = threadIdx.x;
+  const int n_s = min(*n_surv, surv_cap);
+  for (int t = blockIdx.x; t < n_s; t += gridDim.x) {  // fixed grid, block-uniform loop
     const Surv sv = surv[t];
     mim_keypoint k = sv.k;
     const int octv = k.octave & 255;
@@ -362,7 +373,7 @@ __global__ __launch_bounds__(64) void orient_kernel(const Pyr* __restrict__ pyr,
     }
     if (lane < kOriBins) th[lane + 2] = acc;
     __syncthreads();
-    if (lane != 0) return;
+    if (lane == 0) {
     th[1] = th[kOriBins + 1];
     th[0] = th[kOriBins];
     th[kOriBins + 2] = th[2];
@@ -385,6 +396,9 @@ __global__ __launch_bounds__(64) void orient_kernel(const Pyr* __restrict__ pyr,
             if (slot < kp_cap) kp[slot] = k;
         }
     }
+    }
+    __syncthreads();  // th, rb, rv reused by the block's next survivor
+  }
 }
 
 __device__ __forceinline__ int ctz64(unsigned long long m) { return __builtin_ctzll(m); }
@@ -400,10 +414,11 @@ __device__ __forceinline__ int ctz64(unsigned long long m) { return __builtin_ct
 //      and every bin's sum runs in pixel order: the oracle's float sums, bit for bit.
 // The wrap, the 0.2 clamp and the x 512 normalisation then run on lane 0 in the reference's order.
 __global__ __launch_bounds__(64) void descr_kernel(const Pyr* __restrict__ pyr, const mim_keypoint* __restrict__ kp,
-                                                   int n, float* __restrict__ desc) {
+                                                   const int* __restrict__ n_dev, int n_cap, float* __restrict__ desc) {
     __shared__ float hist[kHistLen];
-    const int t = blockIdx.x, lane = threadIdx.x;
-    if (t >= n) return;
+    const int lane = threadIdx.x;
+  const int n = min(*n_dev, n_cap);
+  for (int t = blockIdx.x; t < n; t += gridDim.x) {  // fixed grid, block-uniform loop
     const mim_keypoint p = kp[t];
     int octave = p.octave & 255;
     const int layer = (p.octave >> 8) & 255;
@@ -522,6 +537,95 @@ __global__ __launch_bounds__(64) void descr_kernel(const Pyr* __restrict__ pyr, 
         const int r = cv_round(v[u] * nrm2);
         out[lane + 64 * u] = (float)(r < 0 ? 0 : (r > 255 ? 255 : r));
     }
+    __syncthreads();  // hist reused by the block's next keypoint
+  }
+}
+
+// KeyPointsFilter::removeDuplicatedSorted (sort by KeypointGreater, drop consecutive keypoints equal in
+// x, y, size and angle), the 1/2 rescale of the doubled image's octave -1 and runByPixelsMask, in that
+// order (sift.dispatch.cpp detectAndCompute), on one 1024-thread block: a bitonic sort of the keypoint
+// indices in LDS (the keys compared from the L2-resident list), then two ordered compactions.  More
+// than kSortCap keypoints: *n_out = -n and the host finishes (sift_describe_host).
+constexpr int kSortCap = 16384;
+
+__device__ __forceinline__ bool kp_greater_d(const mim_keypoint& a, const mim_keypoint& b) {  // KeypointGreater
+    if (a.x != b.x) return a.x > b.x;
+    if (a.y != b.y) return a.y > b.y;
+    if (a.size != b.size) return a.size > b.size;
+    if (a.angle != b.angle) return a.angle > b.angle;
+    if (a.response != b.response) return a.response > b.response;
+    return a.octave > b.octave;
+}
+
+__global__ __launch_bounds__(1024) void kp_post_kernel(const mim_keypoint* __restrict__ kp, const int* __restrict__ n_kp,
+                                                      int kp_cap, const uint8_t* __restrict__ mask, long long mstep,
+                                                      mim_keypoint* __restrict__ out, int* __restrict__ n_out) {
+    __shared__ int idx[kSortCap];
+    __shared__ int wsum[16];
+    __shared__ int carry;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int n = min(*n_kp, kp_cap);
+    if (n > kSortCap) {
+        if (tid == 0) *n_out = -n;
+        return;
+    }
+    int P = 1;
+    while (P < n) P <<= 1;
+    for (int i = tid; i < P; i += 1024) idx[i] = i < n ? i : -1;  // -1: padding, sorts last
+    __syncthreads();
+    // before(a, b): a precedes b in KeypointGreater order (padding never precedes)
+    auto before = [&](int a, int b) { return a >= 0 && (b < 0 || kp_greater_d(kp[a], kp[b])); };
+    for (int k = 2; k <= P; k <<= 1)
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = tid; i < P; i += 1024) {
+                const int l = i ^ j;
+                if (l > i) {
+                    const int a = idx[i], b = idx[l];
+                    if ((i & k) == 0 ? before(b, a) : before(a, b)) {
+                        idx[i] = b;
+                        idx[l] = a;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    // dedupe (keep the first of equal x, y, size, angle), rescale, mask; ordered compaction in chunks
+    if (tid == 0) carry = 0;
+    __syncthreads();
+    for (int base = 0; base < n; base += 1024) {
+        const int i = base + tid;
+        bool keep = false;
+        mim_keypoint k{};
+        if (i < n) {
+            k = kp[idx[i]];
+            keep = true;
+            if (i > 0) {
+                const mim_keypoint& q = kp[idx[i - 1]];
+                keep = !(q.x == k.x && q.y == k.y && q.size == k.size && q.angle == k.angle);
+            }
+            if (keep) {
+                k.octave = (k.octave & ~255) | ((k.octave - 1) & 255);
+                k.x *= 0.5f;
+                k.y *= 0.5f;
+                k.size *= 0.5f;
+                if (mask) keep = mask[(long long)(int)(k.y + 0.5f) * mstep + (int)(k.x + 0.5f)] != 0;
+            }
+        }
+        const unsigned long long bal = __ballot(keep);
+        const int within = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0));
+        if (lane == 0) wsum[wave] = __popcll(bal);
+        __syncthreads();
+        int before_w = 0, all = 0;
+        for (int w = 0; w < 16; ++w) {
+            before_w += w < wave ? wsum[w] : 0;
+            all += wsum[w];
+        }
+        if (keep) out[carry + before_w + within] = k;
+        __syncthreads();
+        if (tid == 0) carry += all;
+        __syncthreads();
+    }
+    if (tid == 0) *n_out = carry;
 }
 
 // ---- host ---------------------------------------------------------------------------------------
@@ -559,6 +663,8 @@ struct SiftWs {
     void* tmp = nullptr;   size_t tmp_cap = 0;
     void* aux = nullptr;   size_t aux_cap = 0;  // candidates, keypoints, counters, Pyr table
     void* desc = nullptr;  size_t desc_cap = 0;
+    hipStream_t s = nullptr;  // the multi-scale call runs each scale on its workspace's stream
+    hipEvent_t ev = nullptr;
 };
 
 static hipError_t grow(void*& p, size_t& cap, size_t need) {
@@ -579,8 +685,11 @@ SiftWs* sift_ws_create() { return new SiftWs(); }
 
 void sift_ws_destroy(SiftWs* w) {
     if (!w) return;
+    if (w->s) (void)hipStreamSynchronize(w->s);
     for (void* p : {w->img, w->pyr, w->tmp, w->aux, w->desc})
         if (p) (void)hipFree(p);
+    if (w->ev) (void)hipEventDestroy(w->ev);
+    if (w->s) (void)hipStreamDestroy(w->s);
     delete w;
 }
 
@@ -627,7 +736,9 @@ struct SiftJob {
     mim_keypoint* d_kp = nullptr;
     Surv* d_surv = nullptr;
     Pyr* d_pyr = nullptr;
-    int h_cnt[3] = {0, 0, 0};
+    mim_keypoint* d_kp2 = nullptr;  // the post-processed keypoints (kp_post_kernel)
+    uint8_t* d_mask = nullptr;
+    int h_cnt[4] = {0, 0, 0, 0};  // candidates, keypoints, survivors, final keypoints
     std::vector<mim_keypoint> k;
 };
 
@@ -703,8 +814,9 @@ static int sift_build(SiftJob& J, hipStream_t st, std::string& err) {
         for (int i = 0; i < kNOL + 2; ++i) h_pyr.dog[o][i] = Layer{P + doff[o] + i * plane, orows[o], ocols[o]};
     }
     const int cand_cap = kCandCap, kp_cap = kKpCap;
+    const size_t mask_bytes = J.mask ? ((size_t)J.rows * J.cols + 255) / 256 * 256 : 0;
     const size_t aux_bytes = sizeof(Pyr) + 256 + sizeof(Cand) * cand_cap + sizeof(mim_keypoint) * kp_cap +
-                             sizeof(Surv) * cand_cap;
+                             sizeof(Surv) * cand_cap + sizeof(mim_keypoint) * kSortCap + mask_bytes;
     SCHK(grow(w->aux, w->aux_cap, aux_bytes));
     char* A = (char*)w->aux;
     Pyr* d_pyr = (Pyr*)A;
@@ -717,46 +829,46 @@ static int sift_build(SiftJob& J, hipStream_t st, std::string& err) {
     J.d_cand = d_cand;
     J.d_kp = d_kp;
     J.d_surv = d_surv;
+    J.d_kp2 = (mim_keypoint*)(d_surv + cand_cap);
+    J.d_mask = nullptr;
+    if (J.mask) {  // runByPixelsMask on the device: the mask packed rows x cols
+        J.d_mask = (uint8_t*)(J.d_kp2 + kSortCap);
+        SCHK(hipMemcpy2DAsync(J.d_mask, J.cols, J.mask, J.mstep, J.cols, J.rows, hipMemcpyHostToDevice, st));
+    }
     SCHK(hipMemcpyAsync(d_pyr, &h_pyr, sizeof(Pyr), hipMemcpyHostToDevice, st));
-    SCHK(hipMemsetAsync(d_cnt, 0, 3 * sizeof(int), st));
+    SCHK(hipMemsetAsync(d_cnt, 0, 4 * sizeof(int), st));
     const int threshold = (int)floor(0.5 * 0.04 / kNOL * 255);
     for (int o = 0; o < n_oct; ++o) {
         if (orows[o] <= 2 * kBorder || ocols[o] <= 2 * kBorder) continue;
         extrema_kernel<<<dim3((ocols[o] - 2 * kBorder + 127) / 128, orows[o] - 2 * kBorder, kNOL), 128, 0, st>>>(
             P + doff[o], orows[o], ocols[o], o, threshold, d_cand, d_cnt, cand_cap);
     }
-    SCHK(hipMemcpyAsync(J.h_cnt, d_cnt, sizeof(int), hipMemcpyDeviceToHost, st));
     return 0;
 }
 
-// adjustLocalExtrema + orientations of the candidates (enqueued; keypoint count to J.h_cnt[1])
-static int sift_orient(SiftJob& J, hipStream_t st, std::string& err) {
+// adjustLocalExtrema + orientations of the candidates, the keypoint post-processing and the
+// descriptors, all enqueued with device-side counts (fixed grids, grid-stride kernels); the final
+// keypoint count goes to J.h_cnt[3] (negative: more than kSortCap, the host finishes)
+static int sift_enqueue_rest(SiftJob& J, hipStream_t st, std::string& err) {
     if (J.n_oct < 1) return 0;
-    if (J.h_cnt[0] > kCandCap) { err = "more than 2^20 SIFT candidates"; return -2; }
-    if (J.h_cnt[0] > 0) {
-        refine_kernel<<<(J.h_cnt[0] + 127) / 128, 128, 0, st>>>(J.d_pyr, J.d_cand, J.d_cnt, kCandCap, J.d_surv, J.d_cnt + 2,
-                                                              kCandCap);
-        // survivors <= candidates: blocks past the survivor count return at once
-        orient_kernel<<<J.h_cnt[0], 64, 0, st>>>(J.d_pyr, J.d_surv, J.d_cnt + 2, kCandCap, J.d_kp, J.d_cnt + 1, kKpCap);
-    }
+    refine_kernel<<<1024, 128, 0, st>>>(J.d_pyr, J.d_cand, J.d_cnt, kCandCap, J.d_surv, J.d_cnt + 2, kCandCap);
+    orient_kernel<<<4096, 64, 0, st>>>(J.d_pyr, J.d_surv, J.d_cnt + 2, kCandCap, J.d_kp, J.d_cnt + 1, kKpCap);
+    kp_post_kernel<<<1, 1024, 0, st>>>(J.d_kp, J.d_cnt + 1, kKpCap, J.d_mask, J.cols, J.d_kp2, J.d_cnt + 3);
+    SCHK(grow(J.w->desc, J.w->desc_cap, sizeof(float) * 128 * (size_t)kSortCap));
+    descr_kernel<<<4096, 64, 0, st>>>(J.d_pyr, J.d_kp2, J.d_cnt + 3, kSortCap, (float*)J.w->desc);
     SCHK(hipGetLastError());
-    SCHK(hipMemcpyAsync(J.h_cnt + 1, J.d_cnt + 1, sizeof(int), hipMemcpyDeviceToHost, st));
+    SCHK(hipMemcpyAsync(J.h_cnt, J.d_cnt, 4 * sizeof(int), hipMemcpyDeviceToHost, st));
     return 0;
 }
 
-static int sift_fetch_kp(SiftJob& J, hipStream_t st, std::string& err) {
-    if (J.n_oct < 1) return 0;
+// KeyPointsFilter::removeDuplicatedSorted, the octave -1 rescale, runByPixelsMask on the host, then the
+// descriptors: only for an image with more than kSortCap keypoints (kp_post_kernel's limit)
+static int sift_describe_host(SiftJob& J, hipStream_t st, std::string& err) {
     if (J.h_cnt[1] > kKpCap) { err = "more than 2^19 SIFT keypoints"; return -2; }
-    J.k.resize(J.h_cnt[1]);
-    if (!J.k.empty()) SCHK(hipMemcpyAsync(J.k.data(), J.d_kp, sizeof(mim_keypoint) * J.k.size(), hipMemcpyDeviceToHost, st));
-    return 0;
-}
-
-// removeDuplicatedSorted, the octave -1 rescale, runByPixelsMask (features2d keypoint.cpp, sift) on
-// the host, then the descriptors of the first cap keypoints (enqueued, into J.desc)
-static int sift_describe(SiftJob& J, hipStream_t st, std::string& err) {
-    if (J.n_oct < 1) return 0;
     std::vector<mim_keypoint>& k = J.k;
+    k.resize(J.h_cnt[1]);
+    if (!k.empty()) SCHK(hipMemcpyAsync(k.data(), J.d_kp, sizeof(mim_keypoint) * k.size(), hipMemcpyDeviceToHost, st));
+    SCHK(hipStreamSynchronize(st));
     std::sort(k.begin(), k.end(), kp_greater);
     size_t m = 0;
     for (size_t j = 0; j < k.size(); ++j) {
@@ -784,27 +896,37 @@ static int sift_describe(SiftJob& J, hipStream_t st, std::string& err) {
     if (n <= 0) return 0;
     SCHK(hipMemcpyAsync(J.d_kp, k.data(), sizeof(mim_keypoint) * n, hipMemcpyHostToDevice, st));
     SCHK(grow(J.w->desc, J.w->desc_cap, sizeof(float) * 128 * (size_t)n));
-    descr_kernel<<<n, 64, 0, st>>>(J.d_pyr, J.d_kp, n, (float*)J.w->desc);
+    SCHK(hipMemcpyAsync(J.d_cnt + 3, &n, sizeof(int), hipMemcpyHostToDevice, st));
+    descr_kernel<<<4096, 64, 0, st>>>(J.d_pyr, J.d_kp, J.d_cnt + 3, n, (float*)J.w->desc);
     SCHK(hipGetLastError());
     SCHK(hipMemcpyAsync(J.desc, J.w->desc, sizeof(float) * 128 * (size_t)n, hipMemcpyDeviceToHost, st));
     std::copy(k.begin(), k.begin() + n, J.kps);
+    SCHK(hipStreamSynchronize(st));  // `n` and `k` are host locals of this call
     return 0;
 }
 
-// every stage for all images, then one synchronisation per stage (4 per call)
+// copies of the first J.cap keypoints / descriptors (enqueued)
+static int sift_fetch(SiftJob& J, hipStream_t st, std::string& err) {
+    if (J.n_oct < 1) return 0;
+    if (J.h_cnt[3] < 0) return sift_describe_host(J, st, err);
+    J.n = J.h_cnt[3];
+    const int n = std::min(J.n, J.cap);
+    if (n <= 0) return 0;
+    SCHK(hipMemcpyAsync(J.kps, J.d_kp2, sizeof(mim_keypoint) * n, hipMemcpyDeviceToHost, st));
+    SCHK(hipMemcpyAsync(J.desc, J.w->desc, sizeof(float) * 128 * (size_t)n, hipMemcpyDeviceToHost, st));
+    return 0;
+}
+
+// every stage of all images enqueued, then two synchronisations per call: the counts, the copies
 static int sift_run(std::vector<SiftJob>& jobs, hipStream_t st, std::string& err) {
     for (auto& J : jobs)
         if (int r = sift_build(J, st, err)) return r;
+    for (auto& J : jobs)
+        if (int r = sift_enqueue_rest(J, st, err)) return r;
     SCHK(hipStreamSynchronize(st));
     for (auto& J : jobs)
-        if (int r = sift_orient(J, st, err)) return r;
+        if (int r = sift_fetch(J, st, err)) return r;
     SCHK(hipStreamSynchronize(st));
-    for (auto& J : jobs)
-        if (int r = sift_fetch_kp(J, st, err)) return r;
-    SCHK(hipStreamSynchronize(st));
-    for (auto& J : jobs)
-        if (int r = sift_describe(J, st, err)) return r;
-    SCHK(hipStreamSynchronize(st));  // the descriptors (and the kps copies' sources) before returning
     return 0;
 }
 
@@ -837,9 +959,16 @@ int sift_detect_compute_scales(std::vector<SiftWs*>& ws, hipStream_t st, const u
                                long long step, int n_scales, const float* scales, int max_kp, mim_keypoint* kps,
                                float* desc, int* n_out, std::string& err) {
     while ((int)ws.size() < n_scales + 1) ws.push_back(sift_ws_create());
+    for (SiftWs* w : ws) {
+        if (!w->s) SCHK(hipStreamCreateWithFlags(&w->s, hipStreamNonBlocking));
+        if (!w->ev) SCHK(hipEventCreateWithFlags(&w->ev, hipEventDisableTiming));
+    }
     SiftWs* src = ws[n_scales];  // the scene itself
     SCHK(grow(src->img, src->img_cap, (size_t)rows * cols));
     SCHK(hipMemcpy2DAsync(src->img, cols, img, step, cols, rows, hipMemcpyHostToDevice, st));
+    SCHK(hipEventRecord(src->ev, st));
+    // the scales are independent: each on its workspace's stream (forked after the upload, joined back
+    // into st), so the small octaves' launches of one scale overlap the other scales' work
     std::vector<SiftJob> jobs(n_scales);
     for (int i = 0; i < n_scales; ++i) {
         const double f = (double)scales[i];
@@ -852,21 +981,17 @@ int sift_detect_compute_scales(std::vector<SiftWs*>& ws, hipStream_t st, const u
         J.mask = nullptr;
         J.mstep = 0;
         J.cap = 0;
+        hipStream_t si = J.w->s;
+        SCHK(hipStreamWaitEvent(si, src->ev, 0));
         SCHK(grow(J.w->img, J.w->img_cap, (size_t)dr * dc));
-        resize_u8_kernel<<<dim3((dc + 255) / 256, dr), 256, 0, st>>>((const uint8_t*)src->img, rows, cols,
+        resize_u8_kernel<<<dim3((dc + 255) / 256, dr), 256, 0, si>>>((const uint8_t*)src->img, rows, cols,
                                                                    (uint8_t*)J.w->img, dr, dc, 1. / f, 1. / f);
         SCHK(hipGetLastError());
+        if (int r = sift_build(J, si, err)) return r;
+        if (int r = sift_enqueue_rest(J, si, err)) return r;
+        SCHK(hipEventRecord(J.w->ev, si));
+        SCHK(hipStreamWaitEvent(st, J.w->ev, 0));
     }
-    // capacities: in scale order, what is left of max_kp (known after the keypoint counts; set in
-    // sift_describe's order, so the stages run as sift_run but with the caps assigned before describe)
-    for (auto& J : jobs)
-        if (int r = sift_build(J, st, err)) return r;
-    SCHK(hipStreamSynchronize(st));
-    for (auto& J : jobs)
-        if (int r = sift_orient(J, st, err)) return r;
-    SCHK(hipStreamSynchronize(st));
-    for (auto& J : jobs)
-        if (int r = sift_fetch_kp(J, st, err)) return r;
     SCHK(hipStreamSynchronize(st));
     int used = 0;
     for (int i = 0; i < n_scales; ++i) {
@@ -874,7 +999,7 @@ int sift_detect_compute_scales(std::vector<SiftWs*>& ws, hipStream_t st, const u
         J.cap = std::max(0, max_kp - used);
         J.kps = kps + used;
         J.desc = desc + (size_t)128 * used;
-        if (int r = sift_describe(J, st, err)) return r;
+        if (int r = sift_fetch(J, st, err)) return r;
         n_out[i] = J.n;
         used += std::min(J.n, J.cap);
     }

@@ -52,8 +52,9 @@ sys.path.insert(0, ROOT)
 
 PEAK_I8_TOPS = 5000.0       # MI355X dense i8 MFMA = 2x dense bf16 2.5 PF (MI355X_MICROARCH.md, no sparsity)
 PEAK_F16_MFMA_TFLOPS = 2500.0  # dense f16 MFMA
-# VALU issue peak: 1024 SIMDs x one wave64 instruction per 2 cycles (SIMD-32) x 2.4 GHz
-PEAK_VALU_WAVE_INSTR_PER_S = 1024 * 0.5 * 2.4e9
+# VALU issue peak: 1024 SIMDs x one wave64 instruction per 4 cycles (v_add/v_fma/v_max3 issue cost of one
+# wave's stream on one SIMD, MI355X_MICROARCH.md cycle-constants table) x 2.4 GHz
+PEAK_VALU_WAVE_INSTR_PER_S = 1024 * 0.25 * 2.4e9
 BOUND_VALU_PER_PAIR = 4       # ransac_bound_mfma_kernel tile loop: med3, fma, sub, sign bit per (point, hypothesis)
 BOUND_MFMA_FLOP_PER_PAIR = 96  # 3 v_mfma_f32_32x32x16_f16 per 32 x 32 (point, hypothesis) pairs
 H_TOL = 1e-4                  # SURVEY.md 8(c) contract item 4 (the GPU tests hold bit identity)
@@ -464,7 +465,7 @@ def kernel_rooflines(args, ds, res, iso, iso_step_ms, knn_only):
     knn_bytes = float(np.sum(512 * (pq + pt) + 16 * pq))
     t = iso["knn"]
     ach = knn_ops / (t * 1e-3) / 1e12
-    roof = {"kernel": "knn2_i8_kernel (exact-integer distance contraction on v_mfma_i32_16x16x64_i8 + top-2 "
+    roof = {"kernel": "knn2_i8_kernel (exact-integer distance contraction on v_mfma_i32_32x32x32_i8 + top-2 "
                       "selection), 1 launch per step",
             "bound": "mfma", "achieved": round(ach, 2), "peak": PEAK_I8_TOPS, "unit": "TFLOP/s",
             "frac": round(ach / PEAK_I8_TOPS, 4),
@@ -493,7 +494,7 @@ def kernel_rooflines(args, ds, res, iso, iso_step_ms, knn_only):
                      "peak_TFLOPs": PEAK_F16_MFMA_TFLOPS,
                      "frac": round(pairs * BOUND_MFMA_FLOP_PER_PAIR / tb / 1e12 / PEAK_F16_MFMA_TFLOPS, 4)},
             "note": "pairs = iterations x good matches of every problem (OpenCV scores every hypothesis on every "
-                    "point); VALU peak = 1024 SIMDs x 1 wave64 instruction per 2 cycles x 2.4 GHz"}}
+                    "point); VALU peak = 1024 SIMDs x 1 wave64 instruction per 4 cycles x 2.4 GHz"}}
     # consistency: one stream, one batch at a time -> the kernels' durations cannot exceed the step
     worst = max(iso.values()) if iso else 0.0
     total = sum(iso.values())

@@ -484,26 +484,66 @@ static mim_status build_tables(mim_ctx* c, const mim_problem* problems, int n, i
                         c->sets[ts].d.n);
         units += (long long)((c->sets[qs].d.n + kKnnBlockQ - 1) / kKnnBlockQ) * c->sets[ts].d.n_tiles;
     }
-    // Balanced distance schedule: the (problem, query block, train tile) units, in that order, cut
-    // into one contiguous chunk per resident block, so every block of the single wave of blocks does
-    // the same number of tiles (no tail wave).  A query block cut into k pieces gets k train splits
-    // (partial top-2 lists merged by the ratio kernel); a problem's split count is the largest over
-    // its query blocks, and the missing splits of the others are empty segments (sentinel lists).
-    const long long chunk = std::max<long long>(kKnnMinChunk, (units + c->knn_grid - 1) / c->knn_grid);
-    const int nblk = (int)std::max<long long>(1, (units + chunk - 1) / chunk);
-    std::vector<std::vector<KnnWork>> blk(nblk);
+    // Balanced distance schedule.  The (problem, query block, train tile) units are cut into equal
+    // sub-chunks, every resident block of the single wave of blocks doing the same number of tiles
+    // (no tail wave).  A query block cut into k pieces gets k train splits (partial top-2 lists merged
+    // by the ratio kernel); a problem's split count is the largest over its query blocks, and the
+    // missing splits of the others are empty work items (sentinel lists).
+    // L2 locality (MIM_KNN_SUB = s > 0, tiles): with the chunk of a block longer than s, the block
+    // does R = ceil(chunk / s) sub-chunks of ~s tiles in rounds, and a problem's train tiles are
+    // ordered in segments of <= s tiles (units: problem, segment, query block, tile), so the blocks
+    // running at one time on an XCD sweep the same few segments of the same one or two problems.
+    // Placement: workgroups are dispatched round-robin over the 8 XCDs (block b on XCD b % 8), and
+    // XCD x gets the x-th eighth of the sub-chunks.  MIM_KNN_SUB = 0: segments of <= chunk tiles, one
+    // round; < 0: whole query-block sweeps, one round.
+    static const int sub_target = [] {
+        const char* e = getenv("MIM_KNN_SUB");
+        return e ? atoi(e) : kKnnSubTiles;
+    }();
+    const long long G = c->knn_grid;
+    const long long chunk = std::max<long long>(kKnnMinChunk, (units + G - 1) / G);
+    const long long R = (sub_target > 0 && chunk > sub_target) ? (chunk + sub_target - 1) / sub_target : 1;
+    const long long sub = std::max<long long>(kKnnMinChunk, (chunk + R - 1) / R);
+    const long long NS = std::max<long long>(1, (units + sub - 1) / sub);  // sub-chunks
+    const long long per_x = (NS + 7) / 8;
+    const int m = (int)std::max<long long>(1, (per_x + R - 1) / R);  // blocks per XCD
+    const int nphys = NS < 8 ? (int)NS : 8 * m;
+    auto owner = [&](long long j) -> int {
+        if (NS < 8) return (int)j;
+        const long long x = j / per_x, jj = j % per_x;
+        return (int)(8 * (jj % m) + x);
+    };
+    std::vector<std::vector<KnnWork>> blk(nphys);
     long long pos = 0;
+    struct Piece { int b, t0, t1, k, owner; };
+    std::vector<Piece> pieces;
+    std::vector<int> cnt, last_owner;
     for (int i = 0; i < n; ++i) {
         ProbDev& P = c->h_probs[i];
         P.q = c->sets[problems[i].query_set].d;
         P.t = c->sets[problems[i].train_set].d;
         const int qb = (P.q.n + kKnnBlockQ - 1) / kKnnBlockQ, nt = P.t.n_tiles;
-        // pieces of each query block: first pass for the split count
-        int nsplit = 1;
-        for (int b = 0; b < qb; ++b) {
-            const long long u0 = pos + (long long)b * nt, u1 = u0 + nt;
-            if (nt > 0) nsplit = std::max(nsplit, (int)((u1 - 1) / chunk - u0 / chunk + 1));
+        const int nseg = (sub_target >= 0 && nt > sub) ? (int)((nt + sub - 1) / sub) : 1;
+        const int lseg = nseg > 1 ? (nt + nseg - 1) / nseg : nt;
+        pieces.clear();
+        cnt.assign(qb, 0);
+        last_owner.assign(qb, owner(std::min(NS - 1, pos / sub)));
+        for (int sg = 0; sg < nseg; ++sg) {
+            const int s0 = sg * lseg, s1 = std::min(nt, s0 + lseg);
+            for (int b = 0; b < qb && s0 < s1; ++b) {
+                const long long u0 = pos, u1 = pos + (s1 - s0);
+                for (long long a = u0; a < u1;) {
+                    const long long e = std::min(u1, (a / sub + 1) * sub);
+                    const int o = owner(std::min(NS - 1, a / sub));
+                    pieces.push_back(Piece{b, s0 + (int)(a - u0), s0 + (int)(e - u0), cnt[b]++, o});
+                    last_owner[b] = o;
+                    a = e;
+                }
+                pos = u1;
+            }
         }
+        int nsplit = 1;
+        for (int b = 0; b < qb; ++b) nsplit = std::max(nsplit, cnt[b]);
         P.nsplit = nsplit;
         P.q_pad = qb * kKnnBlockQ;
         P.part_off = part;
@@ -512,26 +552,18 @@ static mim_status build_tables(mim_ctx* c, const mim_problem* problems, int n, i
         good += (std::max(P.q.n, 1) + 31) & ~31;  // 32-aligned: the MFMA bound's point tiles
         P.it_off = it;
         it += std::max(max_iters, 1);
-        for (int b = 0; b < qb; ++b) {
-            const long long u0 = pos + (long long)b * nt, u1 = u0 + nt;
-            int k = 0, last = (int)std::min<long long>(nblk - 1, u0 / chunk);
-            for (long long a = u0; a < u1; ++k) {
-                const long long e = std::min(u1, (a / chunk + 1) * chunk);
-                last = (int)(a / chunk);
-                blk[last].push_back(KnnWork{i, b * kKnnBlockQ, (int)(a - u0), (int)(e - u0), k});
-                a = e;
-            }
-            for (; k < nsplit; ++k) blk[last].push_back(KnnWork{i, b * kKnnBlockQ, nt, nt, k});  // empty split
-        }
-        pos += (long long)qb * nt;
+        for (const Piece& pc : pieces) blk[pc.owner].push_back(KnnWork{i, pc.b * kKnnBlockQ, pc.t0, pc.t1, pc.k});
+        for (int b = 0; b < qb; ++b)
+            for (int k = cnt[b]; k < nsplit; ++k)
+                blk[last_owner[b]].push_back(KnnWork{i, b * kKnnBlockQ, nt, nt, k});  // empty split
     }
     std::vector<KnnWork> works;
-    std::vector<int> seg(nblk + 1, 0);
-    for (int b = 0; b < nblk; ++b) {
+    std::vector<int> seg(nphys + 1, 0);
+    for (int b = 0; b < nphys; ++b) {
         seg[b] = (int)works.size();
         works.insert(works.end(), blk[b].begin(), blk[b].end());
     }
-    seg[nblk] = (int)works.size();
+    seg[nphys] = (int)works.size();
     HIPCHK(c, c->probs.ensure(sizeof(ProbDev) * std::max(n, 1)));
     HIPCHK(c, c->works.ensure(sizeof(KnnWork) * std::max<size_t>(works.size(), 1) + sizeof(int) * seg.size()));
     HIPCHK(c, c->parts.ensure(sizeof(Top2) * std::max<long long>(part, 1)));
@@ -554,7 +586,7 @@ static mim_status build_tables(mim_ctx* c, const mim_problem* problems, int n, i
     for (int i = 0; i < n; ++i) c->h_good_off[i] = c->h_probs[i].good_off;
     c->last_n = n;
     c->n_works = (int)works.size();
-    c->n_knn_blocks = nblk;
+    c->n_knn_blocks = nphys;
     return MIM_OK;
 }
 

@@ -25,6 +25,10 @@ constexpr int kKnnQT = MIM_KNN_QT;             // 32-query MFMA column tiles per
 constexpr int kKnnWaves = MIM_KNN_WAVES;       // waves per distance-kernel block
 constexpr int kKnnStage = MIM_KNN_STAGE;       // 64-row train tiles per LDS stage (per barrier)
 constexpr int kKnnMinChunk = 8;                // fewest train tiles per distance-kernel block
+#ifndef MIM_KNN_SUB_TILES
+#define MIM_KNN_SUB_TILES -1
+#endif
+constexpr int kKnnSubTiles = MIM_KNN_SUB_TILES;  // distance schedule's sub-chunk target (api.cpp build_tables)
 constexpr int kKnnBlockQ = kKnnWaves * 32 * kKnnQT;  // queries per distance-kernel work item
 
 // One descriptor set = one ObjectModel view (objectModel.hpp:11-16) or one scaled scene

@@ -30,6 +30,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <string>
 #include <vector>
 
@@ -408,15 +409,21 @@ __device__ __forceinline__ int ctz64(unsigned long long m) { return __builtin_ct
 // the patch), so the work splits in two per batch of 64 consecutive patch pixels:
 //   A  each lane computes one pixel's contribution (gradient, fastAtan2, the double-rounded exp
 //      weight, the trilinear split into 8 values) in its registers;
-//   B  the lanes walk the 64 pixels in order (v_readlane of each); lane L owns the bins b = L (mod 64) in registers (at
-//      most 6 of the 360), and a pixel's 8 target bins idx + {0, 1, 10, 11, 60, 61, 70, 71} are 8
-//      distinct lanes (the offsets are distinct mod 64), so each lane adds at most one value per pixel
-//      and every bin's sum runs in pixel order: the oracle's float sums, bit for bit.
+//   B  lane L owns the bins b = L (mod 64) in registers (at most 6 of the 360); each bin gets the
+//      64-bit mask of the batch's pixels whose 8 target bins idx + {0, 1, 10, 11, 60, 61, 70, 71}
+//      include it, and the owner adds their values in increasing pixel order, so every bin's sum runs
+//      in pixel order: the oracle's float sums, bit for bit.  (Round 3: the wave walked the batch's
+//      pixels one at a time with v_readlane, 8 of 64 lanes busy per pixel; 0.76 ms per call.)
 // The wrap, the 0.2 clamp and the x 512 normalisation then run on lane 0 in the reference's order.
 __global__ __launch_bounds__(64) void descr_kernel(const Pyr* __restrict__ pyr, const mim_keypoint* __restrict__ kp,
                                                    const int* __restrict__ n_dev, int n_cap, float* __restrict__ desc) {
     __shared__ float hist[kHistLen];
+    __shared__ unsigned long long bm[kHistLen];  // per bin: the batch's pixels that hit it
+    __shared__ int pidx[64];
+    __shared__ float pmag[64], prb[64], pcb[64], pob[64];
     const int lane = threadIdx.x;
+    for (int b = lane; b < kHistLen; b += 64) bm[b] = 0ull;
+    __syncthreads();
   const int n = min(*n_dev, n_cap);
   for (int t = blockIdx.x; t < n; t += gridDim.x) {  // fixed grid, block-uniform loop
     const mim_keypoint p = kp[t];
@@ -470,34 +477,52 @@ __global__ __launch_bounds__(64) void descr_kernel(const Pyr* __restrict__ pyr, 
                 }
             }
         }
-        // ---- B: the batch's contributing pixels in order (v_readlane of each, no memory round trip);
-        // lane L owns the bins = L (mod 64): among idx + {0, 1, 10, 11, 60, 61, 70, 71} that is
-        // d = (L - idx) mod 64 in {0, 1, 10, 11, 60, 61, 6, 7} (mask 0x3000000000000CC3), offset d or
-        // d + 64, value k = (r, c, o) bits of the offset; the lane recomputes its value from the 4
-        // factors with the reference's own operations (v_r1 = mag rbin, v_r0 = mag - v_r1, ...) ----
-        for (unsigned long long vm = __ballot(idx >= 0); vm; vm &= vm - 1) {
-            const int q = ctz64(vm);
-            const int iq = __builtin_amdgcn_readlane(idx, q);
-            const int d = (lane - iq) & 63;
-            const float smag = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mag), q));
-            const float srb = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(rb), q));
-            const float scb = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cb), q));
-            const float sob = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ob), q));
-            if ((0x3000000000000CC3ull >> d) & 1ull) {
-                const int off = (d == 6 || d == 7) ? d + 64 : d;
+        // ---- B: every target bin of the batch gets a 64-bit mask of the pixels that hit it (8 LDS
+        // ORs per pixel, order-free), then lane L walks the masks of its own bins b = L + 64 s in
+        // increasing pixel order and adds each pixel's value for offset b - idx in {0, 1, 10, 11, 60,
+        // 61, 70, 71} (k = (r, c, o) bits of the offset), recomputed from the 4 factors with the
+        // reference's own operations (v_r1 = mag rbin, v_r0 = mag - v_r1, ...).  Lanes work on their
+        // bins at once instead of the wave walking the pixels one by one ----
+        pidx[lane] = idx;
+        pmag[lane] = mag;
+        prb[lane] = rb;
+        pcb[lane] = cb;
+        pob[lane] = ob;
+        if (idx >= 0) {
+            const unsigned long long bit = 1ull << lane;
+            atomicOr(&bm[idx], bit);
+            atomicOr(&bm[idx + 1], bit);
+            atomicOr(&bm[idx + kDB + 2], bit);
+            atomicOr(&bm[idx + kDB + 3], bit);
+            atomicOr(&bm[idx + (kDW + 2) * (kDB + 2)], bit);
+            atomicOr(&bm[idx + (kDW + 2) * (kDB + 2) + 1], bit);
+            atomicOr(&bm[idx + (kDW + 3) * (kDB + 2)], bit);
+            atomicOr(&bm[idx + (kDW + 3) * (kDB + 2) + 1], bit);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int s2 = 0; s2 < 6; ++s2) {
+            const int bin = lane + 64 * s2;
+            if (bin >= kHistLen) break;
+            unsigned long long mk = bm[bin];
+            float acc = h[s2];
+            while (mk) {
+                const int q = ctz64(mk);
+                mk &= mk - 1;
+                const int off = bin - pidx[q];
+                const float smag = pmag[q], srb = prb[q], scb = pcb[q], sob = pob[q];
                 const bool kr = off >= 60, kc = (kr ? off - 60 : off) >= 10, ko = off & 1;
                 const float v_r1 = smag * srb, v_r0 = smag - v_r1;
                 const float rr = kr ? v_r1 : v_r0;
                 const float rc1 = rr * scb, rc0 = rr - rc1;
                 const float cc = kc ? rc1 : rc0;
                 const float co1 = cc * sob, co0 = cc - co1;
-                const float val = ko ? co1 : co0;
-                const int slot = (iq + off) >> 6;
-#pragma unroll
-                for (int s2 = 0; s2 < 6; ++s2)
-                    if (s2 == slot) h[s2] += val;
+                acc += ko ? co1 : co0;
             }
+            h[s2] = acc;
+            bm[bin] = 0ull;  // this lane's bins, cleared for the next batch
         }
+        __syncthreads();
     }
 #pragma unroll
     for (int s2 = 0; s2 < 6; ++s2)
@@ -663,7 +688,7 @@ struct SiftWs {
     void* tmp = nullptr;   size_t tmp_cap = 0;
     void* aux = nullptr;   size_t aux_cap = 0;  // candidates, keypoints, counters, Pyr table
     void* desc = nullptr;  size_t desc_cap = 0;
-    hipStream_t s = nullptr;  // the multi-scale call runs each scale on its workspace's stream
+    hipStream_t s = nullptr;  // MIM_SIFT_SCALE_STREAMS=1: the multi-scale call's stream of this scale
     hipEvent_t ev = nullptr;
 };
 
@@ -959,16 +984,23 @@ int sift_detect_compute_scales(std::vector<SiftWs*>& ws, hipStream_t st, const u
                                long long step, int n_scales, const float* scales, int max_kp, mim_keypoint* kps,
                                float* desc, int* n_out, std::string& err) {
     while ((int)ws.size() < n_scales + 1) ws.push_back(sift_ws_create());
-    for (SiftWs* w : ws) {
-        if (!w->s) SCHK(hipStreamCreateWithFlags(&w->s, hipStreamNonBlocking));
-        if (!w->ev) SCHK(hipEventCreateWithFlags(&w->ev, hipEventDisableTiming));
-    }
+    // MIM_SIFT_SCALE_STREAMS=1: each scale on its workspace's stream (forked after the upload, joined
+    // back into st).  Off by default: measured slower on the MI355X (c1img single scene 17.95 -> 25.3 ms,
+    // 12 scenes in flight 168 -> 107 scenes/s; profiles/r03e_bench_c1img_streams.log), the scales' short
+    // launches then queue behind each other's cross-stream waits instead of running back to back
+    static const bool fork = [] {
+        const char* e = getenv("MIM_SIFT_SCALE_STREAMS");
+        return e && atoi(e) != 0;
+    }();
+    if (fork)
+        for (SiftWs* w : ws) {
+            if (!w->s) SCHK(hipStreamCreateWithFlags(&w->s, hipStreamNonBlocking));
+            if (!w->ev) SCHK(hipEventCreateWithFlags(&w->ev, hipEventDisableTiming));
+        }
     SiftWs* src = ws[n_scales];  // the scene itself
     SCHK(grow(src->img, src->img_cap, (size_t)rows * cols));
     SCHK(hipMemcpy2DAsync(src->img, cols, img, step, cols, rows, hipMemcpyHostToDevice, st));
-    SCHK(hipEventRecord(src->ev, st));
-    // the scales are independent: each on its workspace's stream (forked after the upload, joined back
-    // into st), so the small octaves' launches of one scale overlap the other scales' work
+    if (fork) SCHK(hipEventRecord(src->ev, st));
     std::vector<SiftJob> jobs(n_scales);
     for (int i = 0; i < n_scales; ++i) {
         const double f = (double)scales[i];
@@ -981,16 +1013,18 @@ int sift_detect_compute_scales(std::vector<SiftWs*>& ws, hipStream_t st, const u
         J.mask = nullptr;
         J.mstep = 0;
         J.cap = 0;
-        hipStream_t si = J.w->s;
-        SCHK(hipStreamWaitEvent(si, src->ev, 0));
+        hipStream_t si = fork ? J.w->s : st;
+        if (fork) SCHK(hipStreamWaitEvent(si, src->ev, 0));
         SCHK(grow(J.w->img, J.w->img_cap, (size_t)dr * dc));
         resize_u8_kernel<<<dim3((dc + 255) / 256, dr), 256, 0, si>>>((const uint8_t*)src->img, rows, cols,
                                                                    (uint8_t*)J.w->img, dr, dc, 1. / f, 1. / f);
         SCHK(hipGetLastError());
         if (int r = sift_build(J, si, err)) return r;
         if (int r = sift_enqueue_rest(J, si, err)) return r;
-        SCHK(hipEventRecord(J.w->ev, si));
-        SCHK(hipStreamWaitEvent(st, J.w->ev, 0));
+        if (fork) {
+            SCHK(hipEventRecord(J.w->ev, si));
+            SCHK(hipStreamWaitEvent(st, J.w->ev, 0));
+        }
     }
     SCHK(hipStreamSynchronize(st));
     int used = 0;

@@ -2465,30 +2465,12 @@ __global__ __launch_bounds__(256) void ransac_bound_mfma_kernel(const RansacStat
 #endif
             const f16acc zc = {};
             const f16acc ex0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ax, b0x, zc, 0, 0, 0);
+            const f16acc ey0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ay, b0y, zc, 0, 0, 0);
             const f16acc w0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ax, b0w, zc, 0, 0, 0);
             const f16acc ex1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ax, b1x, zc, 0, 0, 0);
+            const f16acc ey1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ay, b1y, zc, 0, 0, 0);
             const f16acc w1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ax, b1w, zc, 0, 0, 0);
             unsigned bits0 = 0, bits1 = 0, lb0 = 0, lb1 = 0;
-#ifdef MIM_BOUND_XONLY
-            if (!kLo) {
-                // upper bound from the x test alone: a point with |ex| > C|W| + E is out of the box
-                // whatever ey is, so the count of the others still bounds the exact count from above
-                // (looser: ~1 % of random points pass one coordinate); 3 VALU per pair (fma, sub with
-                // |ex| as a source modifier, sign bit) and no ey MFMA
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const float d0 = fmaf(C0, fabsf(w0[r]), E0) - fabsf(ex0[r]);
-                    const float d1 = fmaf(C1, fabsf(w1[r]), E1) - fabsf(ex1[r]);
-                    bits0 = __builtin_amdgcn_alignbit(bits0, __float_as_uint(d0), 31);
-                    bits1 = __builtin_amdgcn_alignbit(bits1, __float_as_uint(d1), 31);
-                }
-                out0 += __popc(bits0);
-                out1 += __popc(bits1);
-                continue;
-            }
-#endif
-            const f16acc ey0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ay, b0y, zc, 0, 0, 0);
-            const f16acc ey1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ay, b1y, zc, 0, 0, 0);
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 // sign bit of R - max(|ex|, |ey|), R = C |W| + E: set when the point is out of the box

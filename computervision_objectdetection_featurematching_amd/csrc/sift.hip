@@ -44,10 +44,13 @@ constexpr int kOriBins = 36;
 constexpr int kDW = 4, kDB = 8;
 constexpr int kHistLen = (kDW + 2) * (kDW + 2) * (kDB + 2);  // 360
 
+// BORDER_REFLECT_101 (borderInterpolate): the reflection is periodic with period 2 len - 2 and even, so
+// a closed form instead of OpenCV's reflect loop (no loop between a kernel's independent loads)
 __device__ __forceinline__ int reflect101(int p, int len) {
+    if ((unsigned)p < (unsigned)len) return p;
     if (len == 1) return 0;
-    while (p < 0 || p >= len) p = p < 0 ? -p : 2 * len - 2 - p;
-    return p;
+    const int period = 2 * len - 2, q = abs(p) % period;
+    return q < len ? q : period - q;
 }
 
 __device__ __forceinline__ int cv_round(float v) { return __float2int_rn(v); }  // ties to even
@@ -132,9 +135,22 @@ __global__ __launch_bounds__(256) void blur_kernel(const float* __restrict__ src
     float* in = lds;             // H x W
     float* mid = lds + H * W;    // H x kBlurTW
     const int x0 = blockIdx.x * kBlurTW, y0 = blockIdx.y * kBlurTH, tid = threadIdx.x;
-    for (int e = tid; e < H * W; e += 256) {
-        const int r = e / W, c = e - r * W;
-        in[e] = src[(size_t)reflect101(y0 - a + r, rows) * cols + reflect101(x0 - a + c, cols)];
+    // 8 loads in flight per thread: a launch is one or two rounds of this loop on the small octaves,
+    // where one dependent global load per iteration made every blur ~11 us whatever its size
+    // (profiles/r03e_kernel_stats_c1img.csv: 1-block launches 13.9 us)
+    for (int e0 = tid; e0 < H * W; e0 += 256 * 8) {
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int e = e0 + 256 * u;
+            if (e < H * W) {
+                const int r = e / W, c = e - r * W;
+                v[u] = src[(size_t)reflect101(y0 - a + r, rows) * cols + reflect101(x0 - a + c, cols)];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (e0 + 256 * u < H * W) in[e0 + 256 * u] = v[u];
     }
     __syncthreads();
     for (int e = tid; e < H * kBlurTW; e += 256) {
@@ -182,17 +198,20 @@ __global__ void extrema_kernel(const float* __restrict__ dog, int rows, int cols
     const float* cur = dog + layer * plane;
     const float val = cur[(size_t)r * cols + c];
     if (!(fabsf(val) > (float)threshold)) return;
+    // all 26 neighbours loaded at once (independent, L1/L2 hits) and tested branch-free: the same
+    // predicate as OpenCV's early-exit comparisons, without a dependent load per comparison
+    const bool pos = val > 0;
     bool ext = true;
-    for (int dz = -1; dz <= 1 && ext; ++dz) {
+#pragma unroll
+    for (int dz = -1; dz <= 1; ++dz) {
         const float* L = cur + dz * (long long)plane;
-        for (int dy = -1; dy <= 1 && ext; ++dy)
+#pragma unroll
+        for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
             for (int dx = -1; dx <= 1; ++dx) {
                 if (dz == 0 && dy == 0 && dx == 0) continue;
                 const float nb = L[(size_t)(r + dy) * cols + c + dx];
-                if (val > 0 ? !(val >= nb) : !(val <= nb)) {
-                    ext = false;
-                    break;
-                }
+                ext &= pos ? (val >= nb) : (val <= nb);
             }
     }
     if (!ext) return;
@@ -368,8 +387,14 @@ __global__ __launch_bounds__(64) void orient_kernel(const Pyr* __restrict__ pyr,
         rv[lane] = val;
         __syncthreads();
         const int m = min(64, P - base);
-        for (int i = 0; i < m; ++i)
-            if (rb[i] == lane) acc += rv[i];
+        // unrolled: the batch's (bin, value) reads are broadcast LDS loads independent of the sums, so
+        // 16 issue back to back instead of one dependent round trip per pixel (the adds stay in order)
+#pragma unroll 16
+        for (int i = 0; i < m; ++i) {
+            const int bi = rb[i];
+            const float vi = rv[i], sum = acc + vi;
+            acc = bi == lane ? sum : acc;
+        }
         __syncthreads();
     }
     if (lane < kOriBins) th[lane + 2] = acc;
@@ -404,25 +429,34 @@ __global__ __launch_bounds__(64) void orient_kernel(const Pyr* __restrict__ pyr,
 
 __device__ __forceinline__ int ctz64(unsigned long long m) { return __builtin_ctzll(m); }
 
-// calcSIFTDescriptor, one wave per keypoint (keypoints in input coordinates, octave field packed as
-// OpenCV's).  Every bin must receive its contributions in the reference's pixel order (row-major over
-// the patch), so the work splits in two per batch of 64 consecutive patch pixels:
-//   A  each lane computes one pixel's contribution (gradient, fastAtan2, the double-rounded exp
-//      weight, the trilinear split into 8 values) in its registers;
-//   B  lane L owns the bins b = L (mod 64) in registers (at most 6 of the 360); each bin gets the
-//      64-bit mask of the batch's pixels whose 8 target bins idx + {0, 1, 10, 11, 60, 61, 70, 71}
-//      include it, and the owner adds their values in increasing pixel order, so every bin's sum runs
-//      in pixel order: the oracle's float sums, bit for bit.  (Round 3: the wave walked the batch's
-//      pixels one at a time with v_readlane, 8 of 64 lanes busy per pixel; 0.76 ms per call.)
-// The wrap, the 0.2 clamp and the x 512 normalisation then run on lane 0 in the reference's order.
-__global__ __launch_bounds__(64) void descr_kernel(const Pyr* __restrict__ pyr, const mim_keypoint* __restrict__ kp,
-                                                   const int* __restrict__ n_dev, int n_cap, float* __restrict__ desc) {
+// calcSIFTDescriptor, one 256-thread block per keypoint (keypoints in input coordinates, octave field
+// packed as OpenCV's).  Every bin must receive its contributions in the reference's pixel order
+// (row-major over the patch), so the work splits in two per batch of 256 consecutive patch pixels:
+//   A  each thread computes one pixel's contribution (gradient, fastAtan2, the double-rounded exp
+//      weight) and its 8 trilinear values with the reference's own operations (v_r1 = mag rbin,
+//      v_r0 = mag - v_r1, v_rc11 = v_r1 cbin, ...) in registers, and sets its bit in the 256-bit
+//      pixel masks of its 8 target bins idx + {0, 1, 10, 11, 60, 61, 70, 71} (LDS ORs, order-free);
+//   B  a stable counting sort of the batch's contributions by bin: per bin the masks give its total
+//      and each pixel's rank among the pixels hitting it (popcounts), a block scan the segments, and
+//      every value is written to its bin's segment at its rank; thread b then adds the segments of
+//      bins b and b + 256 in order, so every bin's sum runs in pixel order: the oracle's float sums,
+//      bit for bit, with independent LDS reads instead of a dependent round trip per contribution.
+// The wrap, the 0.2 clamp and the x 512 normalisation then run on wave 0 in the reference's order.
+// (Round 3 history: one wave walking the pixels one at a time, 0.76 ms per call; one wave with 64-bit
+// masks walked by the owners, 0.64 ms; 256 threads with the mask walk, 0.37 ms: each contribution a
+// dependent chain of two LDS reads.)
+constexpr int kDescrT = 256, kDescrWords = kDescrT / 64;
+static_assert(kHistLen <= 2 * kDescrT, "two bins per thread");
+__global__ __launch_bounds__(kDescrT) void descr_kernel(const Pyr* __restrict__ pyr, const mim_keypoint* __restrict__ kp,
+                                                        const int* __restrict__ n_dev, int n_cap, float* __restrict__ desc) {
     __shared__ float hist[kHistLen];
-    __shared__ unsigned long long bm[kHistLen];  // per bin: the batch's pixels that hit it
-    __shared__ int pidx[64];
-    __shared__ float pmag[64], prb[64], pcb[64], pob[64];
-    const int lane = threadIdx.x;
-    for (int b = lane; b < kHistLen; b += 64) bm[b] = 0ull;
+    __shared__ unsigned long long bm[kHistLen][kDescrWords];  // per bin: the batch's pixels that hit it
+    __shared__ unsigned short pre[kHistLen][kDescrWords];      // per bin and word: pixels in earlier words
+    __shared__ int seg[kHistLen];                              // per bin: its segment of `sorted`
+    __shared__ int wsum[kDescrWords];
+    __shared__ float sorted[kDescrT * 8];                      // the batch's values grouped by bin
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    for (int e = tid; e < kHistLen * kDescrWords; e += kDescrT) (&bm[0][0])[e] = 0ull;
     __syncthreads();
   const int n = min(*n_dev, n_cap);
   for (int t = blockIdx.x; t < n; t += gridDim.x) {  // fixed grid, block-uniform loop
@@ -447,13 +481,13 @@ __global__ __launch_bounds__(64) void descr_kernel(const Pyr* __restrict__ pyr, 
     sin_t /= hist_width;
     const int W = 2 * radius + 1;
     const int P = W * W;
-    float h[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // bins lane + 64 s
-    for (int base = 0; base < P; base += 64) {
-        // ---- A: pixel base + lane: its bin index and the 4 factors of its trilinear split ----
+    float h0 = 0.f, h1 = 0.f;  // bins tid, tid + 256
+    for (int base = 0; base < P; base += kDescrT) {
+        // ---- A: pixel base + tid ----
         int idx = -1;
-        float mag = 0.f, rb = 0.f, cb = 0.f, ob = 0.f;
+        float vals[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
         {
-            const int q = base + lane;
+            const int q = base + tid;
             if (q < P) {
                 const int i = q / W - radius, j = q % W - radius;
                 const float c_rot = j * cos_t - i * sin_t, r_rot = j * sin_t + i * cos_t;
@@ -465,78 +499,104 @@ __global__ __launch_bounds__(64) void descr_kernel(const Pyr* __restrict__ pyr, 
                     const float w = (float)exp((double)((c_rot * c_rot + r_rot * r_rot) * exp_scale));
                     const float o = fast_atan2(dy, dx), m = sqrtf(dx * dx + dy * dy);
                     float obin = (o - ori) * bins_per_rad;
-                    mag = m * w;
+                    const float mag = m * w;
                     const int r0 = (int)floorf(rbin), c0 = (int)floorf(cbin);
                     int o0 = (int)floorf(obin);
-                    rb = rbin - r0;
-                    cb = cbin - c0;
-                    ob = obin - o0;
+                    const float rb = rbin - r0, cb = cbin - c0, ob = obin - o0;
                     if (o0 < 0) o0 += kDB;
                     if (o0 >= kDB) o0 -= kDB;
                     idx = ((r0 + 1) * (kDW + 2) + c0 + 1) * (kDB + 2) + o0;
+                    // calcSIFTDescriptor's trilinear split, same operations
+                    const float v_r1 = mag * rb, v_r0 = mag - v_r1;
+                    const float v_rc11 = v_r1 * cb, v_rc10 = v_r1 - v_rc11;
+                    const float v_rc01 = v_r0 * cb, v_rc00 = v_r0 - v_rc01;
+                    vals[7] = v_rc11 * ob; vals[6] = v_rc11 - vals[7];
+                    vals[5] = v_rc10 * ob; vals[4] = v_rc10 - vals[5];
+                    vals[3] = v_rc01 * ob; vals[2] = v_rc01 - vals[3];
+                    vals[1] = v_rc00 * ob; vals[0] = v_rc00 - vals[1];
                 }
             }
         }
-        // ---- B: every target bin of the batch gets a 64-bit mask of the pixels that hit it (8 LDS
-        // ORs per pixel, order-free), then lane L walks the masks of its own bins b = L + 64 s in
-        // increasing pixel order and adds each pixel's value for offset b - idx in {0, 1, 10, 11, 60,
-        // 61, 70, 71} (k = (r, c, o) bits of the offset), recomputed from the 4 factors with the
-        // reference's own operations (v_r1 = mag rbin, v_r0 = mag - v_r1, ...).  Lanes work on their
-        // bins at once instead of the wave walking the pixels one by one ----
-        pidx[lane] = idx;
-        pmag[lane] = mag;
-        prb[lane] = rb;
-        pcb[lane] = cb;
-        pob[lane] = ob;
+        // ---- B: stable counting sort of the batch's contributions by bin, then sequential sums ----
+        constexpr int kOff[8] = {0, 1, kDB + 2, kDB + 3, (kDW + 2) * (kDB + 2), (kDW + 2) * (kDB + 2) + 1,
+                                 (kDW + 3) * (kDB + 2), (kDW + 3) * (kDB + 2) + 1};
         if (idx >= 0) {
             const unsigned long long bit = 1ull << lane;
-            atomicOr(&bm[idx], bit);
-            atomicOr(&bm[idx + 1], bit);
-            atomicOr(&bm[idx + kDB + 2], bit);
-            atomicOr(&bm[idx + kDB + 3], bit);
-            atomicOr(&bm[idx + (kDW + 2) * (kDB + 2)], bit);
-            atomicOr(&bm[idx + (kDW + 2) * (kDB + 2) + 1], bit);
-            atomicOr(&bm[idx + (kDW + 3) * (kDB + 2)], bit);
-            atomicOr(&bm[idx + (kDW + 3) * (kDB + 2) + 1], bit);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) atomicOr(&bm[idx + kOff[k]][wv], bit);
         }
         __syncthreads();
+        // owned bins: per mask word the count of earlier pixels, and the bin's total
+        int tot[2] = {0, 0};
 #pragma unroll
-        for (int s2 = 0; s2 < 6; ++s2) {
-            const int bin = lane + 64 * s2;
-            if (bin >= kHistLen) break;
-            unsigned long long mk = bm[bin];
-            float acc = h[s2];
-            while (mk) {
-                const int q = ctz64(mk);
-                mk &= mk - 1;
-                const int off = bin - pidx[q];
-                const float smag = pmag[q], srb = prb[q], scb = pcb[q], sob = pob[q];
-                const bool kr = off >= 60, kc = (kr ? off - 60 : off) >= 10, ko = off & 1;
-                const float v_r1 = smag * srb, v_r0 = smag - v_r1;
-                const float rr = kr ? v_r1 : v_r0;
-                const float rc1 = rr * scb, rc0 = rr - rc1;
-                const float cc = kc ? rc1 : rc0;
-                const float co1 = cc * sob, co0 = cc - co1;
-                acc += ko ? co1 : co0;
+        for (int s2 = 0; s2 < 2; ++s2) {
+            const int bin = tid + kDescrT * s2;
+            if (bin < kHistLen) {
+                int run = 0;
+#pragma unroll
+                for (int w = 0; w < kDescrWords; ++w) {
+                    pre[bin][w] = (unsigned short)run;
+                    run += __popcll(bm[bin][w]);
+                }
+                tot[s2] = run;
             }
-            h[s2] = acc;
-            bm[bin] = 0ull;  // this lane's bins, cleared for the next batch
+        }
+        // segment starts: exclusive scan of the owners' totals over the block
+        const int mine = tot[0] + tot[1];
+        int incl = mine;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int y = __shfl_up(incl, d);
+            if (lane >= d) incl += y;
+        }
+        if (lane == 63) wsum[wv] = incl;
+        __syncthreads();
+        int excl = incl - mine;
+#pragma unroll
+        for (int w = 0; w < kDescrWords; ++w) excl += w < wv ? wsum[w] : 0;
+        if (tid < kHistLen) seg[tid] = excl;
+        if (tid + kDescrT < kHistLen) seg[tid + kDescrT] = excl + tot[0];
+        __syncthreads();
+        // scatter: the pixel's value for bin b goes to b's segment at its rank among the batch's pixels
+        // hitting b (the earlier pixels of its own mask word and the words before)
+        if (idx >= 0) {
+            const unsigned long long below = (1ull << lane) - 1;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const int b = idx + kOff[k];
+                sorted[seg[b] + pre[b][wv] + __popcll(bm[b][wv] & below)] = vals[k];
+            }
+        }
+        __syncthreads();
+        // owners: the bin's values in pixel order (independent LDS reads, one add chain)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+            const int bin = tid + kDescrT * s2;
+            if (bin < kHistLen) {
+                const int st0 = s2 ? excl + tot[0] : excl;
+                float acc = s2 ? h1 : h0;
+#pragma unroll 4
+                for (int i = 0; i < tot[s2]; ++i) acc += sorted[st0 + i];
+                if (s2) h1 = acc; else h0 = acc;
+#pragma unroll
+                for (int w = 0; w < kDescrWords; ++w) bm[bin][w] = 0ull;  // cleared for the next batch
+            }
         }
         __syncthreads();
     }
-#pragma unroll
-    for (int s2 = 0; s2 < 6; ++s2)
-        if (lane + 64 * s2 < kHistLen) hist[lane + 64 * s2] = h[s2];
+    hist[tid] = h0;
+    if (tid + kDescrT < kHistLen) hist[tid + kDescrT] = h1;
     __syncthreads();
-    // the orientation wrap (cells independent: one lane each), then the two norms summed in the
-    // reference's order (descriptor index order) over values held two per lane, the clamp and the
-    // x 512 rounding per lane
-    if (lane < kDW * kDW) {
-        const int idx = ((lane / kDW + 1) * (kDW + 2) + (lane % kDW + 1)) * (kDB + 2);
+    // the orientation wrap (cells independent: one thread each)
+    if (tid < kDW * kDW) {
+        const int idx = ((tid / kDW + 1) * (kDW + 2) + (tid % kDW + 1)) * (kDB + 2);
         hist[idx] += hist[idx + kDB];
         hist[idx + 1] += hist[idx + kDB + 1];
     }
     __syncthreads();
+    // wave 0: the two norms summed in the reference's order (descriptor index order) over values held
+    // two per lane, the clamp and the x 512 rounding per lane
+    if (wv == 0) {
     float v[2];
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
@@ -562,6 +622,7 @@ __global__ __launch_bounds__(64) void descr_kernel(const Pyr* __restrict__ pyr, 
         const int r = cv_round(v[u] * nrm2);
         out[lane + 64 * u] = (float)(r < 0 ? 0 : (r > 255 ? 255 : r));
     }
+    }
     __syncthreads();  // hist reused by the block's next keypoint
   }
 }
@@ -572,6 +633,13 @@ __global__ __launch_bounds__(64) void descr_kernel(const Pyr* __restrict__ pyr, 
 // indices in LDS (the keys compared from the L2-resident list), then two ordered compactions.  More
 // than kSortCap keypoints: *n_out = -n and the host finishes (sift_describe_host).
 constexpr int kSortCap = 16384;
+constexpr int kKeySortCap = 8192;  // keypoints sorted by LDS keys (more: comparisons on the keypoints)
+
+// float -> uint32 with the same order (negative values reversed below the positive ones)
+__device__ __forceinline__ unsigned f32_order_key(float f) {
+    const unsigned u = __float_as_uint(f + 0.f);  // -0 -> +0: the comparison sees them equal
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
 
 __device__ __forceinline__ bool kp_greater_d(const mim_keypoint& a, const mim_keypoint& b) {  // KeypointGreater
     if (a.x != b.x) return a.x > b.x;
@@ -586,6 +654,7 @@ __global__ __launch_bounds__(1024) void kp_post_kernel(const mim_keypoint* __res
                                                       int kp_cap, const uint8_t* __restrict__ mask, long long mstep,
                                                       mim_keypoint* __restrict__ out, int* __restrict__ n_out) {
     __shared__ int idx[kSortCap];
+    __shared__ unsigned long long skey[kKeySortCap];
     __shared__ int wsum[16];
     __shared__ int carry;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -597,23 +666,61 @@ __global__ __launch_bounds__(1024) void kp_post_kernel(const mim_keypoint* __res
     int P = 1;
     while (P < n) P <<= 1;
     for (int i = tid; i < P; i += 1024) idx[i] = i < n ? i : -1;  // -1: padding, sorts last
+    if (P <= kKeySortCap)  // (x, y) as one order-preserving 64-bit key per keypoint, in LDS
+        for (int i = tid; i < P; i += 1024) {
+            unsigned long long key = 0;
+            if (i < n) {
+                const mim_keypoint q = kp[i];
+                key = ((unsigned long long)f32_order_key(q.x) << 32) | f32_order_key(q.y);
+            }
+            skey[i] = key;
+        }
     __syncthreads();
     // before(a, b): a precedes b in KeypointGreater order (padding never precedes)
     auto before = [&](int a, int b) { return a >= 0 && (b < 0 || kp_greater_d(kp[a], kp[b])); };
-    for (int k = 2; k <= P; k <<= 1)
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int i = tid; i < P; i += 1024) {
-                const int l = i ^ j;
-                if (l > i) {
-                    const int a = idx[i], b = idx[l];
-                    if ((i & k) == 0 ? before(b, a) : before(a, b)) {
-                        idx[i] = b;
-                        idx[l] = a;
+    if (P <= kKeySortCap) {
+        // bitonic sort of (key, index) pairs in LDS: KeypointGreater compares x, then y first, so the
+        // key decides every pair with different (x, y); equal keys (duplicate positions) fall back to
+        // the full comparison of the keypoints.  Was: every comparison read two keypoints from L2
+        // (~150 us per call for ~5k keypoints).
+        auto before_k = [&](int a, unsigned long long ka, int b, unsigned long long kb) {
+            if (a < 0) return false;
+            if (b < 0) return true;
+            return ka != kb ? ka > kb : kp_greater_d(kp[a], kp[b]);
+        };
+        for (int k = 2; k <= P; k <<= 1)
+            for (int j = k >> 1; j > 0; j >>= 1) {
+                for (int i = tid; i < P; i += 1024) {
+                    const int l = i ^ j;
+                    if (l > i) {
+                        const int a = idx[i], b = idx[l];
+                        const unsigned long long ka = skey[i], kb = skey[l];
+                        if ((i & k) == 0 ? before_k(b, kb, a, ka) : before_k(a, ka, b, kb)) {
+                            idx[i] = b;
+                            idx[l] = a;
+                            skey[i] = kb;
+                            skey[l] = ka;
+                        }
                     }
                 }
+                __syncthreads();
             }
-            __syncthreads();
-        }
+    } else {
+        for (int k = 2; k <= P; k <<= 1)
+            for (int j = k >> 1; j > 0; j >>= 1) {
+                for (int i = tid; i < P; i += 1024) {
+                    const int l = i ^ j;
+                    if (l > i) {
+                        const int a = idx[i], b = idx[l];
+                        if ((i & k) == 0 ? before(b, a) : before(a, b)) {
+                            idx[i] = b;
+                            idx[l] = a;
+                        }
+                    }
+                }
+                __syncthreads();
+            }
+    }
     // dedupe (keep the first of equal x, y, size, angle), rescale, mask; ordered compaction in chunks
     if (tid == 0) carry = 0;
     __syncthreads();
@@ -880,7 +987,7 @@ static int sift_enqueue_rest(SiftJob& J, hipStream_t st, std::string& err) {
     orient_kernel<<<4096, 64, 0, st>>>(J.d_pyr, J.d_surv, J.d_cnt + 2, kCandCap, J.d_kp, J.d_cnt + 1, kKpCap);
     kp_post_kernel<<<1, 1024, 0, st>>>(J.d_kp, J.d_cnt + 1, kKpCap, J.d_mask, J.cols, J.d_kp2, J.d_cnt + 3);
     SCHK(grow(J.w->desc, J.w->desc_cap, sizeof(float) * 128 * (size_t)kSortCap));
-    descr_kernel<<<4096, 64, 0, st>>>(J.d_pyr, J.d_kp2, J.d_cnt + 3, kSortCap, (float*)J.w->desc);
+    descr_kernel<<<4096, kDescrT, 0, st>>>(J.d_pyr, J.d_kp2, J.d_cnt + 3, kSortCap, (float*)J.w->desc);
     SCHK(hipGetLastError());
     SCHK(hipMemcpyAsync(J.h_cnt, J.d_cnt, 4 * sizeof(int), hipMemcpyDeviceToHost, st));
     return 0;
@@ -922,7 +1029,7 @@ static int sift_describe_host(SiftJob& J, hipStream_t st, std::string& err) {
     SCHK(hipMemcpyAsync(J.d_kp, k.data(), sizeof(mim_keypoint) * n, hipMemcpyHostToDevice, st));
     SCHK(grow(J.w->desc, J.w->desc_cap, sizeof(float) * 128 * (size_t)n));
     SCHK(hipMemcpyAsync(J.d_cnt + 3, &n, sizeof(int), hipMemcpyHostToDevice, st));
-    descr_kernel<<<4096, 64, 0, st>>>(J.d_pyr, J.d_kp, J.d_cnt + 3, n, (float*)J.w->desc);
+    descr_kernel<<<4096, kDescrT, 0, st>>>(J.d_pyr, J.d_kp, J.d_cnt + 3, n, (float*)J.w->desc);
     SCHK(hipGetLastError());
     SCHK(hipMemcpyAsync(J.desc, J.w->desc, sizeof(float) * 128 * (size_t)n, hipMemcpyDeviceToHost, st));
     std::copy(k.begin(), k.begin() + n, J.kps);

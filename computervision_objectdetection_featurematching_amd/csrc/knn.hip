@@ -411,68 +411,6 @@ __global__ __launch_bounds__(kThreads, MIM_KNN_OCC) void knn2_i8_kernel(  // OCC
         }
     };
 
-#ifdef MIM_KNN_PIPE
-    // Late tiles, software-pipelined over the 32-row blocks of a stage (two register sets): block
-    // j + 1's LDS reads and block j - 1's filter are issued while block j's MFMAs run, so a wave
-    // no longer waits on an LDS round trip before each MFMA group and on each group's results
-    // before the next one starts (round 3 ISA: three lgkmcnt(0) stalls and an MFMA drain per block)
-    auto load_blk = [&](const unsigned char* tb, int u2, i32x16& sd, i32x4 (&af)[4], unsigned& pw) {
-        const i32x4* A = reinterpret_cast<const i32x4*>(tb);
-        const int* tn = reinterpret_cast<const int*>(tb + kTileBytes);
-        const int* tnu = tn + 32 * u2 + 4 * h;
-#pragma unroll
-        for (int gg = 0; gg < 4; ++gg) {
-            const i32x4 n = *reinterpret_cast<const i32x4*>(tnu + 8 * gg);
-            sd[4 * gg + 0] = n.x; sd[4 * gg + 1] = n.y; sd[4 * gg + 2] = n.z; sd[4 * gg + 3] = n.w;
-        }
-#pragma unroll
-        for (int s2 = 0; s2 < 4; ++s2) af[s2] = A[(u2 * 4 + s2) * 64 + lane];
-        pw = (unsigned)tn[64 + u2] >> (4 * h);
-    };
-    auto mfma_blk = [&](const i32x16& sd, const i32x4 (&af)[4], i32x16 (&acc)[QT]) {
-#pragma unroll
-        for (int u = 0; u < QT; ++u) acc[u] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[0], B[u][0], sd, 0, 0, 0);
-#pragma unroll
-        for (int s2 = 1; s2 < 4; ++s2)
-#pragma unroll
-            for (int u = 0; u < QT; ++u) acc[u] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[s2], B[u][s2], acc[u], 0, 0, 0);
-    };
-    auto filter_blk = [&](const i32x16 (&acc)[QT], unsigned pw, int row0) {
-        int mn[QT];
-        bool hit = false;
-#pragma unroll
-        for (int u = 0; u < QT; ++u) {
-            const i32x16& p = acc[u];
-            int m = min(min(p[0], p[1]), p[2]);
-#pragma unroll
-            for (int g = 3; g < 15; g += 2) m = min(min(m, p[g]), p[g + 1]);
-            mn[u] = min(m, p[15]);
-            hit |= mn[u] <= T[u];
-        }
-        if (__builtin_expect(__ballot(hit) != 0, 0)) {
-#pragma unroll
-            for (int u = 0; u < QT; ++u) {
-                if (__ballot(mn[u] <= T[u])) {
-                    unsigned long long hm[16];
-#pragma unroll
-                    for (int g = 0; g < 16; ++g) hm[g] = __ballot(acc[u][g] <= T[u]);
-#pragma unroll
-                    for (int g = 0; g < 16; ++g) {
-                        if (__builtin_expect(hm[g] != 0, 0))
-                            sel_push(st[u], dval(acc[u][g], (pw >> ((g & 3) + 8 * (g >> 2))) & 1),
-                                     row0 + (g & 3) + 8 * (g >> 2));
-                    }
-#ifdef MIM_KNN_EXACT_PAIR
-                    T[u] = sel_filter(st[u]);
-#else
-                    T[u] = min(max(st[u].m1, o1c[u]), min(st[u].m2, o2c[u])) >> 1;
-#endif
-                }
-            }
-        }
-    };
-#endif
-
     const int tile_e = min(w.tile1, w.tile0 + (kEarlyTiles + kStage - 1) / kStage * kStage);
     int stage = w.tile0;
     for (; stage < tile_e; stage += kStage) {
@@ -503,33 +441,10 @@ __global__ __launch_bounds__(kThreads, MIM_KNN_OCC) void knn2_i8_kernel(  // OCC
             T[u] = min(max(st[u].m1, o1c[u]), min(st[u].m2, o2c[u])) >> 1;
 #endif
         }
-#ifdef MIM_KNN_PIPE
-        {
-            const int nts = min(kStage, w.tile1 - stage);
-            i32x16 sd0, sd1, acc0[QT], acc1[QT];
-            i32x4 af0[4], af1[4];
-            unsigned pw0, pw1, pa1 = 0;
-            load_blk(sb, 0, sd0, af0, pw0);
-            for (int ts = 0; ts < nts; ++ts) {
-                const unsigned char* tb = sb + ts * kLdsTile;
-                const int row = (stage + ts) * 64;
-                mfma_blk(sd0, af0, acc0);
-                const unsigned pa0 = pw0;
-                load_blk(tb, 1, sd1, af1, pw1);
-                if (ts > 0) filter_blk(acc1, pa1, row - 32);
-                mfma_blk(sd1, af1, acc1);
-                pa1 = pw1;
-                load_blk(ts + 1 < nts ? tb + kLdsTile : tb, 0, sd0, af0, pw0);  // unconditional: no join with loads in flight
-                filter_blk(acc0, pa0, row);
-            }
-            filter_blk(acc1, pa1, (stage + nts - 1) * 64 + 32);
-        }
-#else
         // rolled by default (unrolling measured no faster; the late tile is ~3 KiB of code)
 #pragma unroll MIM_KNN_LATE_UNROLL
         for (int ts = 0; ts < kStage; ++ts)
             if (kStage == 1 || stage + ts < w.tile1) tile_late(sb + ts * kLdsTile, stage + ts);
-#endif
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA into the next buffer landed
         if (!kProbeNoBarrier) __syncthreads();
     }

@@ -131,10 +131,12 @@ constexpr int kBlurTW = 64, kBlurTH = 16;
 __global__ __launch_bounds__(256) void blur_kernel(const float* __restrict__ src, float* __restrict__ dst, int rows,
                                                    int cols, Taps t) {
     extern __shared__ float lds[];
+    __shared__ float tk[64];     // the taps, read per tap from LDS rather than the kernel arguments
     const int a = t.n / 2, W = kBlurTW + 2 * a, H = kBlurTH + 2 * a;
     float* in = lds;             // H x W
     float* mid = lds + H * W;    // H x kBlurTW
     const int x0 = blockIdx.x * kBlurTW, y0 = blockIdx.y * kBlurTH, tid = threadIdx.x;
+    if (tid < 64) tk[tid] = t.k[tid];
     // 8 loads in flight per thread: a launch is one or two rounds of this loop on the small octaves,
     // where one dependent global load per iteration made every blur ~11 us whatever its size
     // (profiles/r03e_kernel_stats_c1img.csv: 1-block launches 13.9 us)
@@ -156,8 +158,8 @@ __global__ __launch_bounds__(256) void blur_kernel(const float* __restrict__ src
     for (int e = tid; e < H * kBlurTW; e += 256) {
         const int r = e / kBlurTW, c = e - r * kBlurTW;
         const float* S = in + r * W + c;
-        float acc = t.k[0] * S[0];
-        for (int i = 1; i < t.n; ++i) acc += t.k[i] * S[i];
+        float acc = tk[0] * S[0];
+        for (int i = 1; i < t.n; ++i) acc += tk[i] * S[i];
         mid[e] = acc;
     }
     __syncthreads();
@@ -165,9 +167,87 @@ __global__ __launch_bounds__(256) void blur_kernel(const float* __restrict__ src
         const int r = e / kBlurTW, c = e - r * kBlurTW, y = y0 + r, x = x0 + c;
         if (y >= rows || x >= cols) continue;
         const float* M = mid + (r + a) * kBlurTW + c;
-        float acc = t.k[a] * M[0] + 0.f;
-        for (int i = 1; i <= a; ++i) acc += t.k[a + i] * (M[i * kBlurTW] + M[-i * kBlurTW]);
+        float acc = tk[a] * M[0] + 0.f;
+        for (int i = 1; i <= a; ++i) acc += tk[a + i] * (M[i * kBlurTW] + M[-i * kBlurTW]);
         dst[(size_t)y * cols + x] = acc;
+    }
+}
+
+// The small octaves (plane <= kSmallPlane) of one image in ONE launch of one 1024-thread block: per
+// octave the down-sample of the previous octave's layer kNOL, the five blurs (row pass into LDS, column
+// pass with reflected rows, the same float operations in the same order as blur_kernel) and the five
+// DoG planes, the layers ping-ponging in LDS and written out for the later kernels.  Replaces ~7
+// launches per small octave (each ~4-14 us whatever its size) by one for all of them.
+#ifndef MIM_SMALL_PLANE
+#define MIM_SMALL_PLANE 8192
+#endif
+constexpr int kSmallPlane = MIM_SMALL_PLANE;  // largest octave plane (pixels) fused
+struct SmallOct {
+    int o0, n_oct;            // octaves o0 .. n_oct - 1 (o0 >= 1)
+    int rows[16], cols[16];
+    long long goff[16], doff[16];
+    Taps t[kNOL + 2];          // blur taps of layers 1 .. kNOL + 2
+};
+
+__global__ __launch_bounds__(1024) void small_octaves_kernel(float* __restrict__ P, SmallOct so) {
+    __shared__ float sm[4 * kSmallPlane];  // 128 KiB
+    __shared__ float taps[kNOL + 2][64];   // the kernel-argument taps, read per tap from LDS
+    float* bufA = sm;                     // current layer
+    float* bufB = sm + kSmallPlane;       // next layer
+    float* tmp = sm + 2 * kSmallPlane;    // row pass
+    float* nxt = sm + 3 * kSmallPlane;    // layer kNOL down-sampled: the next octave's layer 0
+    const int tid = threadIdx.x;
+    if (tid < (kNOL + 2) * 64) taps[tid >> 6][tid & 63] = so.t[tid >> 6].k[tid & 63];
+    for (int o = so.o0; o < so.n_oct; ++o) {
+        const int rows = so.rows[o], cols = so.cols[o], plane = rows * cols;
+        float* G = P + so.goff[o];
+        float* D = P + so.doff[o];
+        // layer 0 = every second pixel of the previous octave's layer kNOL (down2_kernel)
+        if (o == so.o0) {
+            const int pc = so.cols[o - 1];
+            const float* src = P + so.goff[o - 1] + (long long)kNOL * so.rows[o - 1] * pc;
+            for (int e = tid; e < plane; e += 1024) {
+                const int y = e / cols, x = e - y * cols;
+                bufA[e] = src[(long long)(2 * y) * pc + 2 * x];
+            }
+        } else {
+            for (int e = tid; e < plane; e += 1024) bufA[e] = nxt[e];
+        }
+        __syncthreads();
+        for (int e = tid; e < plane; e += 1024) G[e] = bufA[e];
+        for (int i = 1; i < kNOL + 3; ++i) {
+            const float* tk = taps[i - 1];
+            const int tn = so.t[i - 1].n, a = tn / 2;
+            for (int e = tid; e < plane; e += 1024) {  // row pass (reflected columns)
+                const int y = e / cols, x = e - y * cols;
+                const float* S = bufA + y * cols;
+                float acc = tk[0] * S[reflect101(x - a, cols)];
+                for (int j = 1; j < tn; ++j) acc += tk[j] * S[reflect101(x - a + j, cols)];
+                tmp[e] = acc;
+            }
+            __syncthreads();
+            for (int e = tid; e < plane; e += 1024) {  // column pass (reflected rows), DoG
+                const int y = e / cols, x = e - y * cols;
+                float acc = tk[a] * tmp[e] + 0.f;
+                for (int j = 1; j <= a; ++j)
+                    acc += tk[a + j] * (tmp[reflect101(y + j, rows) * cols + x] + tmp[reflect101(y - j, rows) * cols + x]);
+                bufB[e] = acc;
+                G[(long long)i * plane + e] = acc;
+                D[(long long)(i - 1) * plane + e] = acc - bufA[e];
+            }
+            __syncthreads();
+            if (i == kNOL && o + 1 < so.n_oct) {
+                const int nc = so.cols[o + 1], np = so.rows[o + 1] * nc;
+                for (int e = tid; e < np; e += 1024) {
+                    const int y = e / nc, x = e - y * nc;
+                    nxt[e] = bufB[(2 * y) * cols + 2 * x];
+                }
+            }
+            float* sw = bufA;
+            bufA = bufB;
+            bufB = sw;
+            __syncthreads();
+        }
     }
 }
 
@@ -927,7 +1007,11 @@ static int sift_build(SiftJob& J, hipStream_t st, std::string& err) {
         const double sp = pow(kk, (double)(i - 1)) * 1.6, stt = sp * kk;
         sig[i] = sqrt(stt * stt - sp * sp);
     }
-    for (int o = 0; o < n_oct; ++o) {
+    // the small octaves (all after the first whose plane fits kSmallPlane) in one launch
+    int o_small = n_oct;
+    for (int o = 1; o < n_oct; ++o)
+        if ((size_t)orows[o] * ocols[o] <= (size_t)kSmallPlane) { o_small = o; break; }
+    for (int o = 0; o < o_small; ++o) {
         const size_t plane = (size_t)orows[o] * ocols[o];
         float* G = P + goff[o];
         if (o > 0)
@@ -936,6 +1020,20 @@ static int sift_build(SiftJob& J, hipStream_t st, std::string& err) {
         for (int i = 1; i < kNOL + 3; ++i)
             if (!blur(G + (i - 1) * plane, G + i * plane, orows[o], ocols[o], sig[i])) { err = "kernel size"; return -2; }
         dog_kernel<<<dim3((unsigned)((plane + 255) / 256), kNOL + 2), 256, 0, st>>>(G, P + doff[o], plane);
+    }
+    if (o_small < n_oct) {
+        SmallOct so{};
+        so.o0 = o_small;
+        so.n_oct = n_oct;
+        for (int o = 0; o < n_oct; ++o) {
+            so.rows[o] = orows[o];
+            so.cols[o] = ocols[o];
+            so.goff[o] = (long long)goff[o];
+            so.doff[o] = (long long)doff[o];
+        }
+        for (int i = 1; i < kNOL + 3; ++i)
+            if (gauss_taps(sig[i], so.t[i - 1]) < 0) { err = "kernel size"; return -2; }
+        small_octaves_kernel<<<1, 1024, 0, st>>>(P, so);
     }
     SCHK(hipGetLastError());
     // layer table

@@ -179,7 +179,7 @@ __global__ __launch_bounds__(256) void blur_kernel(const float* __restrict__ src
 // DoG planes, the layers ping-ponging in LDS and written out for the later kernels.  Replaces ~7
 // launches per small octave (each ~4-14 us whatever its size) by one for all of them.
 #ifndef MIM_SMALL_PLANE
-#define MIM_SMALL_PLANE 8192
+#define MIM_SMALL_PLANE 512  // measured: 8192 1.81 ms per 640x480 image, 2048 1.54, 512 1.49-1.52 (profiles/r03s_sift_small_plane.txt)
 #endif
 constexpr int kSmallPlane = MIM_SMALL_PLANE;  // largest octave plane (pixels) fused
 struct SmallOct {

@@ -310,11 +310,13 @@ __device__ int run_kernel4(const float* M, const float* m, double* D, double* H)
 constexpr int kJ9G = 36 + 9 + 81;  // doubles of LDS state per group
 
 __device__ __forceinline__ int dpp_row(int v, int ctrl) {
+    // every lane of the row is written (full masks, in-row permutations), so no "old" value is needed:
+    // mov_dpp with bound_ctrl avoids materialising one per DPP move
     switch (ctrl) {  // constant after inlining
-        case 0: return __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false);   // quad_perm 1,0,3,2
-        case 1: return __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, false);   // quad_perm 2,3,0,1
-        case 2: return __builtin_amdgcn_update_dpp(0, v, 0x141, 0xF, 0xF, false);  // row_half_mirror
-        default: return __builtin_amdgcn_update_dpp(0, v, 0x140, 0xF, 0xF, false); // row_mirror
+        case 0: return __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, true);   // quad_perm 1,0,3,2
+        case 1: return __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, true);   // quad_perm 2,3,0,1
+        case 2: return __builtin_amdgcn_mov_dpp(v, 0x141, 0xF, 0xF, true);  // row_half_mirror
+        default: return __builtin_amdgcn_mov_dpp(v, 0x140, 0xF, 0xF, true); // row_mirror
     }
 }
 
@@ -3123,6 +3125,12 @@ __device__ double inv_diag_max8(const double (&w)[8], const int (&perm)[8], cons
     return maxval;
 }
 
+#ifdef MIM_REFINE_PROF  // debug build: phase times (shader cycles) of problem 0's refine
+#define RPROF(name) do { const long long t_ = (long long)__builtin_amdgcn_s_memtime(); \
+    if (p == 0 && tid == 0) printf("[refine-prof] %s %lld\n", name, t_ - rp_t0); } while (0)
+#else
+#define RPROF(name) do { } while (0)
+#endif
 struct RefineShared {  // one per wave (problem)
     double red[2];
     double lt[45];
@@ -3238,6 +3246,10 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
 #endif
             wsync();
             const int k = sh.n_inl;
+#ifdef MIM_REFINE_PROF
+            const long long rp_t0 = (long long)__builtin_amdgcn_s_memtime();
+            if (p == 0 && tid == 0) printf("[refine-prof] inliers %d\n", k);
+#endif
             if (k > 0) {
                 // ---- refit: runKernel over all inliers, OpenCV's sequential sums (fundam.cpp) ----
                 if (tid < 4) {  // centroids cm (scene), cM (object): one sequential sum each
@@ -3293,7 +3305,9 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                     const double Hnorm2[9] = {sMx, 0, -cMx * sMx, 0, sMy, -cMy * sMy, 0, 0, 1};
                     if (tid < 16) {  // the Jacobi of runKernel, one 16-lane group (bit-identical)
                         double Hl[9];
+                        RPROF("refit_sums");
                         dlt_finish_group(sh.lt, sh.J9, invHnorm, Hnorm2, Hl);
+                        RPROF("refit_jacobi9");
                         if (tid == 0)
                             for (int i = 0; i < 9; ++i) sh.H[i] = Hl[i];
                     }
@@ -3308,6 +3322,7 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                 for (int i = 0; i < 8; ++i) x[i] = sh.x[i];
                 double rinf;
                 lm_normal(X, k, x, sh.lm, sh.nrm, rinf);
+                RPROF("lm_normal0");
                 if (tid == 0) {
                     int e = 0;
                     for (int a = 0; a < 8; ++a)
@@ -3326,7 +3341,9 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                         __builtin_amdgcn_wave_barrier();
                         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
                         double dl[8];
+                        RPROF("iter_start");
                         solve_eig8(sh.Ap, sh.v, dl, sh.J9, ew, eperm);
+                        RPROF("eig8");
                         if (tid == 0) {
                             double dinf = 0;
                             for (int i = 0; i < 8; ++i) {
@@ -3341,6 +3358,7 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                     double xd[8];
                     for (int i = 0; i < 8; ++i) xd[i] = sh.xd[i];
                     const double Sd = lm_cost(X, k, xd, sh.lm, sh.red);
+                    RPROF("lm_cost");
                     if (tid < 16) {  // every slot evaluates the same update; slot 0 stores it
                         const double Rlo = 0.25, Rhi = 0.75;
                         double lambda = sh.lambda, lc = sh.lc;
@@ -3383,6 +3401,7 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                     if (sh.accept) {
                         for (int i = 0; i < 8; ++i) x[i] = sh.x[i];
                         lm_normal(X, k, x, sh.lm, sh.nrm, rinf);
+                        RPROF("lm_normal");
                         if (tid == 0) {
                             int e = 0;
                             for (int a = 0; a < 8; ++a)
@@ -3398,6 +3417,7 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                     wsync();
                     if (!proceed) break;
                 }
+                RPROF("lm_done");
                 if (tid < 8) sh.H[tid] = sh.x[tid];
                 wsync();
             } else if (tid == 0) {

@@ -496,10 +496,8 @@ static mim_status build_tables(mim_ctx* c, const mim_problem* problems, int n, i
     // Placement: workgroups are dispatched round-robin over the 8 XCDs (block b on XCD b % 8), and
     // XCD x gets the x-th eighth of the sub-chunks.  MIM_KNN_SUB = 0: segments of <= chunk tiles, one
     // round; < 0: whole query-block sweeps, one round.
-    static const int sub_target = [] {
-        const char* e = getenv("MIM_KNN_SUB");
-        return e ? atoi(e) : kKnnSubTiles;
-    }();
+    const char* sub_env = getenv("MIM_KNN_SUB");  // read per batch (tests switch it)
+    const int sub_target = sub_env ? atoi(sub_env) : kKnnSubTiles;
     const long long G = c->knn_grid;
     const long long chunk = std::max<long long>(kKnnMinChunk, (units + G - 1) / G);
     const long long R = (sub_target > 0 && chunk > sub_target) ? (chunk + sub_target - 1) / sub_target : 1;

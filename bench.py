@@ -95,6 +95,9 @@ def parse():
                          "round-robin, so a batch's latency-bound RANSAC tail overlaps the next batch's kNN "
                          "(0: 12, c1 3; with GPU_MAX_HW_QUEUES=16 their streams, torch's and RCCL's each get a "
                          "hardware queue)")
+    ap.add_argument("--shard-of", type=int, default=0,
+                    help="diagnostic (N = 1 only, sharded configs): run rank 0's shard of an N-rank run, the "
+                         "per-GPU workload of strong-scaling point N (value = this GPU's rate on it)")
     ap.add_argument("--hw-queues", type=int, default=16,
                     help="GPU_MAX_HW_QUEUES for this process and the ranks it launches (set before HIP initialises)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
@@ -558,9 +561,12 @@ def main():
     knn_only = bool(cfg.get("knn_only"))
     sharded = bool(cfg.get("sharded"))
     if sharded:  # one global batch: this rank's contiguous block of its scenes (same data at any N)
-        ids = shard.shard_range(cfg["n_scenes"], world, rank)
+        # --shard-of N (diagnostic, one process): rank 0's shard of an N-rank run, i.e. the per-GPU
+        # workload of the strong-scaling point N; `value` is then this GPU's rate on it
+        w_eff = args.shard_of if (args.shard_of > 0 and world == 1) else world
+        ids = shard.shard_range(cfg["n_scenes"], w_eff, rank)
         ds = make_config_dataset(args.config, seed=SEED_BASE, scene_ids=ids)
-        global_batch = cfg["n_scenes"] * cfg["n_models"]
+        global_batch = cfg["n_scenes"] * cfg["n_models"] if w_eff == world else len(ids) * cfg["n_models"]
     else:  # every rank: the same models, its own scenes (seeded by rank)
         ds = make_config_dataset(args.config, seed=SEED_BASE + 1000 * rank)
         global_batch = world * len(ds.problems)
@@ -721,6 +727,9 @@ def main():
                        "parallelism": f"dp{world}", "batches_in_flight": nf, "dist_backend": args.dist_backend,
                        "hw_queues": int(os.environ["GPU_MAX_HW_QUEUES"])},
         }
+        if sharded and args.shard_of > 0 and world == 1:
+            out["config"]["emulated_shard"] = (f"rank 0's shard of a {args.shard_of}-rank run ({n_probs} problems): "
+                                               f"per-GPU rate at that strong-scaling point, not a whole-job value")
         if warm_note := ("" if n_warm == args.warmup else f"--warmup {args.warmup} raised to {n_warm}: every one of "
                                                             f"the {nf} contexts runs once before the timed region"):
             out["warmup_note"] = warm_note

@@ -25,7 +25,7 @@
 namespace mim {
 void launch_prep_batch(const PrepJob* jobs, int njobs, int total_tiles, hipStream_t st);
 void launch_knn(const ProbDev* probs, const KnnWork* works, int n_works, const int* seg_start, int n_blocks, Top2* parts,
-                hipStream_t st);
+                int* dyn_ctr, hipStream_t st);
 int knn_blocks_per_cu();
 void launch_ratio(const ProbDev* probs, int n_probs, const Top2* parts, float ratio, int32_t* good_q,
                   int32_t* good_t, float4* pts, int* n_good, int32_t* knn_idx, float* knn_dist,
@@ -172,7 +172,7 @@ struct mim_ctx {
     Arena arena;
     std::vector<SetRec> sets;
     // batch workspace
-    DevBuf probs, works, parts, good_q, good_t, pts, n_good, results, masks, knn_idx, knn_dist, inl_tab, inl_out;
+    DevBuf probs, works, parts, good_q, good_t, pts, n_good, results, masks, knn_idx, knn_dist, inl_tab, inl_out, knn_ctr;
     RansacWs rws;
     std::vector<ProbDev> h_probs;
     int n_works = 0;  // distance segments of the current batch (works, then the per-block segment starts)
@@ -199,6 +199,7 @@ struct mim_ctx {
     int exact_all = 0;
     int knn_grid = 0;      // resident distance-kernel blocks on the device (first batch)
     int n_knn_blocks = 0;  // distance-kernel blocks of the current batch (<= knn_grid)
+    bool knn_dyn = false;  // current batch's distance work as 8 per-XCD lists pulled dynamically
     hipStream_t cur = nullptr;  // stream the enqueue helpers launch on
     // sampler stream (RansacBufs::s2): the next chunk's getSubset replay beside this chunk's
     // selection kernels (MIM_SAMPLER_STREAM=0: one stream)
@@ -296,7 +297,7 @@ void mim_ctx_destroy(mim_ctx* c) {
     c->prep_stage.destroy();
     c->arena.release();
     for (DevBuf* b : {&c->probs, &c->works, &c->parts, &c->good_q, &c->good_t, &c->pts, &c->n_good,
-                      &c->results, &c->masks, &c->knn_idx, &c->knn_dist, &c->inl_tab, &c->inl_out, &c->rws.state, &c->rws.samples,
+                      &c->results, &c->masks, &c->knn_idx, &c->knn_dist, &c->inl_tab, &c->inl_out, &c->knn_ctr, &c->rws.state, &c->rws.samples,
                       &c->rws.hyp, &c->rws.counts, &c->rws.bounds, &c->rws.flags, &c->rws.irr, &c->rws.irr_cnt, &c->rws.pass_bits, &c->rws.chains, &c->rws.best_h, &c->rws.cand, &c->rws.ncand, &c->rws.cex, &c->rws.cH, &c->rws.stream, &c->rws.scratch, &c->rws.inl, &c->rws.tiles, &c->rws.err, &c->prep_jobs})
         b->release();
     if (c->own) (void)hipStreamDestroy(c->own);
@@ -498,6 +499,17 @@ static mim_status build_tables(mim_ctx* c, const mim_problem* problems, int n, i
     // round; < 0: whole query-block sweeps, one round.
     const char* sub_env = getenv("MIM_KNN_SUB");  // read per batch (tests switch it)
     const int sub_target = sub_env ? atoi(sub_env) : kKnnSubTiles;
+    // Dynamic mode (whole sweeps pulled from per-XCD lists) when the batch has at least one query-block
+    // sweep per resident block: fewer pieces (no early tiles and prologue per split) and a block that
+    // starts late under other batches' kernels takes less (measured: C3 isolated kNN 1.39 -> 1.32 ms,
+    // pipelined C3 +2.5 %, 32-problem shards +3.8 %, C4 even; profiles/r03_knn_variants.txt, r03ac).
+    // Fewer sweeps than blocks (C5's one problem, a scene's small views): the static balanced chunks.
+    // MIM_KNN_DYN=0 / 1 forces either.
+    long long n_sweeps = 0;
+    for (int i = 0; i < n; ++i)
+        n_sweeps += (c->sets[problems[i].query_set].d.n + kKnnBlockQ - 1) / kKnnBlockQ;
+    const char* dyn_env = getenv("MIM_KNN_DYN");
+    const bool dyn = dyn_env ? atoi(dyn_env) != 0 : n_sweeps >= c->knn_grid;
     const long long G = c->knn_grid;
     const long long chunk = std::max<long long>(kKnnMinChunk, (units + G - 1) / G);
     const long long R = (sub_target > 0 && chunk > sub_target) ? (chunk + sub_target - 1) / sub_target : 1;
@@ -556,12 +568,44 @@ static mim_status build_tables(mim_ctx* c, const mim_problem* problems, int n, i
                 blk[last_owner[b]].push_back(KnnWork{i, b * kKnnBlockQ, nt, nt, k});  // empty split
     }
     std::vector<KnnWork> works;
-    std::vector<int> seg(nphys + 1, 0);
-    for (int b = 0; b < nphys; ++b) {
-        seg[b] = (int)works.size();
-        works.insert(works.end(), blk[b].begin(), blk[b].end());
+    std::vector<int> seg;
+    int n_launch = nphys;
+    if (dyn) {
+        // MIM_KNN_DYN=1: whole query-block sweeps (one split per problem), in unit order, as 8 contiguous
+        // lists of about equal work (one per XCD); the resident blocks pull them (knn2_i8_kernel)
+        works.clear();
+        long long total = 0;
+        for (int i = 0; i < n; ++i) {
+            ProbDev& P = c->h_probs[i];
+            const int qb = P.q_pad / kKnnBlockQ;
+            P.nsplit = 1;
+            for (int b = 0; b < qb; ++b) works.push_back(KnnWork{i, b * kKnnBlockQ, 0, P.t.n_tiles, 0});
+            total += (long long)qb * P.t.n_tiles;
+        }
+        // part offsets for one split per problem
+        part = 0;
+        for (int i = 0; i < n; ++i) {
+            c->h_probs[i].part_off = part;
+            part += c->h_probs[i].q_pad;
+        }
+        seg.assign(9, 0);
+        long long acc = 0;
+        int x = 1;
+        for (size_t k = 0; k < works.size() && x < 8; ++k) {
+            acc += c->h_probs[works[k].problem].t.n_tiles;
+            while (x < 8 && acc * 8 >= total * x) seg[x++] = (int)k + 1;
+        }
+        for (; x <= 8; ++x) seg[x] = (int)works.size();
+        n_launch = (int)std::min<long long>(G, std::max<size_t>(works.size(), 8));
+        n_launch = std::max(8, n_launch / 8 * 8);
+    } else {
+        seg.assign(nphys + 1, 0);
+        for (int b = 0; b < nphys; ++b) {
+            seg[b] = (int)works.size();
+            works.insert(works.end(), blk[b].begin(), blk[b].end());
+        }
+        seg[nphys] = (int)works.size();
     }
-    seg[nphys] = (int)works.size();
     HIPCHK(c, c->probs.ensure(sizeof(ProbDev) * std::max(n, 1)));
     HIPCHK(c, c->works.ensure(sizeof(KnnWork) * std::max<size_t>(works.size(), 1) + sizeof(int) * seg.size()));
     HIPCHK(c, c->parts.ensure(sizeof(Top2) * std::max<long long>(part, 1)));
@@ -584,7 +628,9 @@ static mim_status build_tables(mim_ctx* c, const mim_problem* problems, int n, i
     for (int i = 0; i < n; ++i) c->h_good_off[i] = c->h_probs[i].good_off;
     c->last_n = n;
     c->n_works = (int)works.size();
-    c->n_knn_blocks = nphys;
+    c->n_knn_blocks = n_launch;
+    c->knn_dyn = dyn;
+    if (dyn) HIPCHK(c, c->knn_ctr.ensure(8 * sizeof(int)));
     return MIM_OK;
 }
 
@@ -627,7 +673,7 @@ static void ev_collect(mim_ctx* c) {
 static void knn_launch(mim_ctx* c) {
     const KnnWork* w = c->works.as<KnnWork>();
     launch_knn(c->probs.as<ProbDev>(), w, c->n_works, reinterpret_cast<const int*>(w + c->n_works), c->n_knn_blocks,
-               c->parts.as<Top2>(), c->cur);
+               c->parts.as<Top2>(), c->knn_dyn ? c->knn_ctr.as<int>() : nullptr, c->cur);
 }
 
 // distance + ratio kernels of the batch's problems

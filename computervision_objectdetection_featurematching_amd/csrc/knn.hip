@@ -221,11 +221,39 @@ static_assert(kStageChunks * 16 * kThreads == kStage * kTileBytes, "stage split"
 #endif
 __global__ __launch_bounds__(kThreads, MIM_KNN_OCC) void knn2_i8_kernel(  // OCC = waves per SIMD
     const ProbDev* __restrict__ probs, const KnnWork* __restrict__ works, const int* __restrict__ seg_start,
-    Top2* __restrict__ parts) {
+    Top2* __restrict__ parts, int* __restrict__ dyn_ctr) {
     constexpr int QT = kKnnQT;
     __shared__ __attribute__((aligned(16))) unsigned char smem[2 * kStage * kLdsTile];
-  for (int si = seg_start[blockIdx.x]; si < seg_start[blockIdx.x + 1]; ++si) {
+    __shared__ int s_item;
+    // static: block b runs works[seg_start[b] .. seg_start[b + 1]); dynamic (dyn_ctr != null): the works
+    // are 8 lists (seg_start[0..8]), block b pulls items from list b mod 8 (its XCD's) with an atomic
+    // counter, then from the other lists, so a block that starts late (its CU held by another batch's
+    // kernel) takes less
+    int si = dyn_ctr ? 0 : seg_start[blockIdx.x];
+    const int si_end = dyn_ctr ? 0 : seg_start[blockIdx.x + 1];
+    int list = blockIdx.x & 7, lists_done = 0;
+  for (;;) {
+    if (dyn_ctr) {
+        int idx = -1;
+        while (lists_done < 8) {
+            if (threadIdx.x == 0) s_item = atomicAdd(dyn_ctr + list, 1);
+            __syncthreads();
+            const int k = s_item;
+            __syncthreads();
+            if (k < seg_start[list + 1] - seg_start[list]) {
+                idx = seg_start[list] + k;
+                break;
+            }
+            list = (list + 1) & 7;
+            ++lists_done;
+        }
+        if (idx < 0) break;
+        si = idx;
+    } else if (si >= si_end) {
+        break;
+    }
     const KnnWork w = works[si];
+    ++si;
     const ProbDev* P = probs + w.problem;
     if (*P->q.flags | *P->t.flags) continue;  // not integer-valued: generic kernel handles it
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, h = lane >> 5, r = lane & 31;
@@ -753,9 +781,10 @@ int knn_blocks_per_cu() {
 }
 
 void launch_knn(const ProbDev* probs, const KnnWork* works, int n_works, const int* seg_start, int n_blocks,
-                Top2* parts, hipStream_t st) {
+                Top2* parts, int* dyn_ctr, hipStream_t st) {
     if (n_works <= 0) return;
-    knn2_i8_kernel<<<n_blocks, kThreads, 0, st>>>(probs, works, seg_start, parts);
+    if (dyn_ctr) (void)hipMemsetAsync(dyn_ctr, 0, 8 * sizeof(int), st);
+    knn2_i8_kernel<<<n_blocks, kThreads, 0, st>>>(probs, works, seg_start, parts, dyn_ctr);
     knn2_rescan_kernel<<<n_works, 256, 0, st>>>(probs, works, parts);
     knn2_f32_kernel<<<std::min(n_works, 2048), 256, 0, st>>>(probs, works, parts, n_works);
 }

@@ -36,8 +36,9 @@ typedef const __attribute__((address_space(1))) int gint;
 // v_mfma_i32_32x32x32_i8 (query and train use the same k order, so the product is k-order free);
 // one 1 KiB wave load = one fragment, fully coalesced.
 // Norm block per tile (kNormWords): [64] floor(n2/2), [2] the 64 values n2 & 1 as a bit mask + [62]
-// zero (the train side, staged to LDS as is), [64] c (the query side); padded rows floor(n2/2) =
-// 2^30 - 1, n2 & 1 = 1, so D = INT_MAX.
+// zero (the train side, staged to LDS as is), [64] c (the query side), [64] the early-phase key
+// addends K = 2^28 + 128 (n2 & 1) + row (train side, staged for the early tiles only); padded rows
+// floor(n2/2) = 2^30 - 1, n2 & 1 = 1, so D = INT_MAX, and K = 255, so their early key is UINT_MAX.
 // ------------------------------------------------------------------------------------------------
 __device__ __forceinline__ void prep_tile(const float* __restrict__ src, int n, int8_t* __restrict__ frag,
                                           int* __restrict__ norm, int* __restrict__ flags, int tile) {
@@ -82,6 +83,7 @@ __device__ __forceinline__ void prep_tile(const float* __restrict__ src, int n, 
         const unsigned long long pm = __ballot(row < n ? n2 & 1 : 1);  // tid < 64: wave 0, all lanes
         nb[64 + tid] = tid < 2 ? (int)(uint32_t)(pm >> (32 * tid)) : 0;
         nb[128 + tid] = n2 + 2 * sum;
+        nb[192 + tid] = row < n ? (1 << 28) + ((n2 & 1) << 7) + tid : 255;
     }
     if (__any(bad) && (tid & 63) == 0) atomicOr(flags, 1);
 }
@@ -203,6 +205,13 @@ __device__ __forceinline__ int sel_filter(const LaneSel& s) {
 
 __device__ __forceinline__ int dval(int R, int p) { return (R << 1) | p; }  // v_lshl_or_b32
 
+// v_med3_u32 (the compiler rewrites the max/min form of a top-2 update into a max and two mins)
+__device__ __forceinline__ unsigned med3_u32(unsigned a, unsigned b, unsigned c) {
+    unsigned r;
+    asm("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
 // ------------------------------------------------------------------------------------------------
 // Exact distance kernel.  Block = kKnnWaves waves = kKnnBlockQ queries (each wave: kKnnQT 32-query
 // MFMA column tiles, their q' fragments held in VGPRs for the whole sweep).  Train rows stream
@@ -210,7 +219,7 @@ __device__ __forceinline__ int dval(int R, int p) { return (R << 1) | p; }  // v
 // per tile a wave reads the 8 KiB of fragments as 8 conflict-free ds_read_b128 and issues 8 kKnnQT
 // i8 MFMAs.
 // ------------------------------------------------------------------------------------------------
-constexpr int kLdsTile = kTileBytes + 512;  // fragments + the train half of the norm block
+constexpr int kLdsTile = kTileBytes + 768;  // fragments + the train half of the norm block + the key addends
 constexpr int kStage = kKnnStage;
 constexpr int kThreads = 64 * kKnnWaves;
 constexpr int kStageChunks = kStage * kTileBytes / 16 / kThreads;  // 16-B fragment chunks per thread
@@ -301,7 +310,7 @@ __global__ __launch_bounds__(kThreads, MIM_KNN_OCC) void knn2_i8_kernel(  // OCC
 #ifdef MIM_KNN_PRIO  // A/B: the second-dispatched half of the block wins issue arbitration (MI355X_MICROARCH.md, 2 waves per SIMD item 4)
     if (wv >= kKnnWaves / 2) __builtin_amdgcn_s_setprio(1);
 #endif
-    auto stage_dma = [&](int t0, int buf) {
+    auto stage_dma = [&](int t0, int buf, bool keys) {
         unsigned char* base = smem + buf * kStage * kLdsTile;
 #pragma unroll
         for (int c = 0; c < kStageChunks; ++c) {
@@ -319,9 +328,18 @@ __global__ __launch_bounds__(kThreads, MIM_KNN_OCC) void knn2_i8_kernel(  // OCC
                                                  (__attribute__((address_space(3))) void*)(base + tt * kLdsTile + kTileBytes + 256 * (p & 1)),
                                                  4, 0, 0);
         }
+        if (keys) {  // early stages: the key addends (norm words 192..255) of each tile
+#pragma unroll
+            for (int tt = wv; tt < kStage; tt += kKnnWaves)
+                if (kStage == 1 || t0 + tt < w.tile1)
+                    __builtin_amdgcn_global_load_lds((const void*)(tnorm + (size_t)(t0 + tt) * kNormWords + 192 + lane),
+                                                     (__attribute__((address_space(3))) void*)(base + tt * kLdsTile + kTileBytes + 512),
+                                                     4, 0, 0);
+        }
     };
 
-    if (w.tile0 < w.tile1) stage_dma(w.tile0, 0);
+    const int tile_e = min(w.tile1, w.tile0 + (kEarlyTiles + kStage - 1) / kStage * kStage);
+    if (w.tile0 < w.tile1) stage_dma(w.tile0, 0, w.tile0 < tile_e);
     // retire every prologue load (q' fragments included) here: with one still pending at the loop
     // entry the waitcnt pass keeps a vmcnt(0) in the loop
     __builtin_amdgcn_s_waitcnt(0);
@@ -345,24 +363,44 @@ __global__ __launch_bounds__(kThreads, MIM_KNN_OCC) void knn2_i8_kernel(  // OCC
             for (int u = 0; u < QT; ++u) acc[u] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, B[u][s], acc[u], 0, 0, 0);
         }
     };
-    // early tiles: every value inserted branch-free
+    // early tiles: every value enters a branch-free top-2 of 32-bit keys
+    //   key = (R << 8) + K = 128 D + row + 2^28  (K = 2^28 + 128 (n2 & 1) + row from the tile's norm block)
+    // ordered as (D, row): R in [-2^20.1, 2^22] keeps real keys in (0, 2^31); a padded row (R = 2^30 - 1,
+    // K = 255) wraps to exactly UINT_MAX and never enters.  Three VALU per value (v_lshl_add_u32,
+    // v_med3_u32, v_min_u32); the tile's two keys per lane and column tile are decoded and merged into the
+    // (D, index) lists at the tile's end.
     auto tile_early = [&](const unsigned char* tb, int tile) {
-        const int* tn = reinterpret_cast<const int*>(tb + kTileBytes);
+        const int* tk = reinterpret_cast<const int*>(tb + kTileBytes + 512) + 4 * h;
+        unsigned k1[QT], k2[QT];
+#pragma unroll
+        for (int u = 0; u < QT; ++u) k1[u] = k2[u] = 0xFFFFFFFFu;
 #pragma unroll
         for (int u2 = 0; u2 < 2; ++u2) {
-            const int row0 = tile * 64 + 32 * u2;
-            const unsigned pw = (unsigned)tn[64 + u2] >> (4 * h);  // bit 8gg + k: n2 & 1 of the lane's row
             i32x16 acc[QT];
             block_mfma(tb, u2, acc);
 #pragma unroll
             for (int gg = 0; gg < 4; ++gg) {
+                const i32x4 kv = *reinterpret_cast<const i32x4*>(tk + 32 * u2 + 8 * gg);
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
-                    const int pk = (pw >> (8 * gg + k)) & 1;
 #pragma unroll
-                    for (int u = 0; u < QT; ++u) sel_push(st[u], dval(acc[u][4 * gg + k], pk), row0 + k + 8 * gg);
+                    for (int u = 0; u < QT; ++u) {
+                        const unsigned key = ((unsigned)acc[u][4 * gg + k] << 8) + (unsigned)kv[k];
+                        k2[u] = med3_u32(k1[u], k2[u], key);  // = max(k1, min(k2, key)) as k1 <= k2
+                        k1[u] = min(k1[u], key);
+                    }
                 }
             }
+        }
+#pragma unroll
+        for (int u = 0; u < QT; ++u) {
+            LaneSel t;
+            // D = (key - 2^28) >> 7, row = key & 127 (with the lane's 4h, which the lists store without)
+            t.m1 = k1[u] == 0xFFFFFFFFu ? INT_MAX : (int)(k1[u] - (1u << 28)) >> 7;
+            t.i1 = k1[u] == 0xFFFFFFFFu ? INT_MAX : tile * 64 + (int)(k1[u] & 127) - 4 * h;
+            t.m2 = k2[u] == 0xFFFFFFFFu ? INT_MAX : (int)(k2[u] - (1u << 28)) >> 7;
+            t.i2 = k2[u] == 0xFFFFFFFFu ? INT_MAX : tile * 64 + (int)(k2[u] & 127) - 4 * h;
+            st[u] = sel_merge(st[u], t);
         }
     };
     // late tiles: one min over a lane's 16 R per column tile against its threshold, the exact
@@ -439,12 +477,11 @@ __global__ __launch_bounds__(kThreads, MIM_KNN_OCC) void knn2_i8_kernel(  // OCC
         }
     };
 
-    const int tile_e = min(w.tile1, w.tile0 + (kEarlyTiles + kStage - 1) / kStage * kStage);
     int stage = w.tile0;
     for (; stage < tile_e; stage += kStage) {
         const int buf = ((stage - w.tile0) / kStage) & 1;
         const bool more = stage + kStage < w.tile1;
-        if (more && !kProbeNoDma) stage_dma(stage + kStage, buf ^ 1);
+        if (more && !kProbeNoDma) stage_dma(stage + kStage, buf ^ 1, stage + kStage < tile_e);
         const unsigned char* sb = smem + buf * kStage * kLdsTile;
 #pragma unroll
         for (int ts = 0; ts < kStage; ++ts)
@@ -455,7 +492,7 @@ __global__ __launch_bounds__(kThreads, MIM_KNN_OCC) void knn2_i8_kernel(  // OCC
     for (; stage < w.tile1; stage += kStage) {
         const int buf = ((stage - w.tile0) / kStage) & 1;
         const bool more = stage + kStage < w.tile1;
-        if (more && !kProbeNoDma) stage_dma(stage + kStage, buf ^ 1);
+        if (more && !kProbeNoDma) stage_dma(stage + kStage, buf ^ 1, false);
         const unsigned char* sb = smem + buf * kStage * kLdsTile;
 #pragma unroll
         for (int u = 0; u < QT; ++u) {

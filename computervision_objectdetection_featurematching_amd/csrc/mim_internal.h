@@ -9,7 +9,7 @@ namespace mim {
 constexpr int kDim = 128;          // SIFT descriptor length (TestsDetector.cpp:60 operands)
 constexpr int kTileRows = 64;      // descriptor rows per staged tile
 constexpr int kTileBytes = kTileRows * kDim;  // 8 KiB of i8 per tile
-constexpr int kNormWords = 3 * kTileRows;      // norm block per tile (knn.hip prep_tile)
+constexpr int kNormWords = 4 * kTileRows;      // norm block per tile (knn.hip prep_tile)
 constexpr int kWave = 64;
 #ifndef MIM_KNN_QT
 #define MIM_KNN_QT 2
@@ -35,7 +35,7 @@ constexpr int kKnnBlockQ = kKnnWaves * 32 * kKnnQT;  // queries per distance-ker
 // (TestsDetector.cpp:104-106), resident in HBM.
 struct SetDev {
     const int8_t* frag;    // 127 - d as i8, "fragment-major" tiles: [tile][u 0..1][kstep 0..3][lane 0..63][16]
-    const int* norm;       // per tile kNormWords: floor(n2/2), n2 & 1, c (knn.hip prep_tile)
+    const int* norm;       // per tile kNormWords: floor(n2/2), n2 & 1, c, early-phase key addends (knn.hip prep_tile)
     const float* f32;      // row-major n x 128 fp32 (the caller's CV_32F rows)
     const float2* kp;      // KeyPoint::pt per row
     int n;

@@ -430,7 +430,7 @@ __global__ __launch_bounds__(kThreads, MIM_KNN_OCC) void knn2_i8_kernel(  // OCC
             continue;
 #endif
             int mn[QT];
-            bool hit = false;
+            unsigned long long bm[QT], any = 0;  // wave masks of the lanes with a candidate (SGPR pairs)
 #pragma unroll
             for (int u = 0; u < QT; ++u) {
                 const i32x16& p = acc[u];
@@ -438,19 +438,22 @@ __global__ __launch_bounds__(kThreads, MIM_KNN_OCC) void knn2_i8_kernel(  // OCC
 #pragma unroll
                 for (int g = 3; g < 15; g += 2) m = min(min(m, p[g]), p[g + 1]);
                 mn[u] = min(m, p[15]);
-                hit |= mn[u] <= T[u];
+                bm[u] = __ballot(mn[u] <= T[u]);
+                any |= bm[u];
             }
 #ifdef MIM_KNN_NOHIT  // timing probe only (results invalid): the late-tile filter without insertions
-            if (__ballot(hit) != 0) {
+            if (any != 0) {
 #pragma unroll
                 for (int u = 0; u < QT; ++u) st[u].m2 = min(st[u].m2, mn[u]);
             }
             continue;
 #endif
-            if (__builtin_expect(__ballot(hit) != 0, 0)) {  // ~1 insertion per wave and half tile
+            // the masks are tested on the scalar unit (re-evaluating the compare as a ballot made the
+            // compiler rebuild each one with a v_cndmask + v_cmp pair per event)
+            if (__builtin_expect(any != 0, 0)) {  // ~1 insertion per wave and half tile
 #pragma unroll
                 for (int u = 0; u < QT; ++u) {
-                    if (__ballot(mn[u] <= T[u])) {
+                    if (bm[u] != 0) {
                         // per row: one compare (the ballot) and, if some lane has the row under its
                         // threshold, an unconditional insertion in every lane (the lane lists stay the
                         // exact top-2 of the rows pushed, a superset of the filtered ones)
@@ -494,18 +497,21 @@ __global__ __launch_bounds__(kThreads, MIM_KNN_OCC) void knn2_i8_kernel(  // OCC
         const bool more = stage + kStage < w.tile1;
         if (more && !kProbeNoDma) stage_dma(stage + kStage, buf ^ 1, false);
         const unsigned char* sb = smem + buf * kStage * kLdsTile;
+        auto refresh = [&]() {  // thresholds from the partner lane's current m1, m2 (every tile: slower, r03bd)
 #pragma unroll
-        for (int u = 0; u < QT; ++u) {
+            for (int u = 0; u < QT; ++u) {
 #ifdef MIM_KNN_EXACT_PAIR
-            T[u] = sel_filter(st[u]);
+                T[u] = sel_filter(st[u]);
 #else
-            const auto a = __builtin_amdgcn_permlane32_swap(st[u].m1, st[u].m1, false, false);
-            const auto b = __builtin_amdgcn_permlane32_swap(st[u].m2, st[u].m2, false, false);
-            o1c[u] = (tid & 32) ? (int)a[0] : (int)a[1];
-            o2c[u] = (tid & 32) ? (int)b[0] : (int)b[1];
-            T[u] = min(max(st[u].m1, o1c[u]), min(st[u].m2, o2c[u])) >> 1;
+                const auto a = __builtin_amdgcn_permlane32_swap(st[u].m1, st[u].m1, false, false);
+                const auto b = __builtin_amdgcn_permlane32_swap(st[u].m2, st[u].m2, false, false);
+                o1c[u] = (tid & 32) ? (int)a[0] : (int)a[1];
+                o2c[u] = (tid & 32) ? (int)b[0] : (int)b[1];
+                T[u] = min(max(st[u].m1, o1c[u]), min(st[u].m2, o2c[u])) >> 1;
 #endif
-        }
+            }
+        };
+        refresh();
         // rolled by default (unrolling measured no faster; the late tile is ~3 KiB of code)
 #pragma unroll MIM_KNN_LATE_UNROLL
         for (int ts = 0; ts < kStage; ++ts)

@@ -62,3 +62,49 @@ def test_fastmod_from_lemire_constant():
         a = np.concatenate([rng.integers(0, 1 << 32, size=200_000, dtype=np.uint64),
                             np.array([0, 1, n - 1, n, n + 1, (1 << 32) - 1], dtype=np.uint64) % np.uint64(1 << 32)])
         assert np.array_equal(fastmod_from_M(a, n), a % np.uint64(n)), n
+
+
+# ------------------------------------------------------------------------------------------------
+# Early tiles of knn2_i8_kernel (csrc/knn.hip tile_early): a value R = q'.t'' + floor(n2/2) of train
+# row `row` (0..63 within its tile, n2 & 1 = p) becomes the 32-bit key (R << 8) + K, K = 2^28 + 128 p +
+# row (prep_tile's norm words 192..255), so that unsigned key order is (D, row) order with
+# D = 2R + p = d^2 - c(q), decoded as D = (key - 2^28) >> 7 (arithmetic), row = key & 127.  Padded rows
+# (R = 2^30 - 1 exactly, t'' = 0; K = 255) wrap to UINT_MAX and never enter the top-2.
+# ------------------------------------------------------------------------------------------------
+def early_key(R, p, row):
+    K = (1 << 28) + 128 * p.astype(np.int64) + row.astype(np.int64)
+    return ((R.astype(np.int64) << 8) + K) & 0xFFFFFFFF
+
+
+def d_range():
+    # D = d^2 - c(q), c(q) = |q - 128|^2 + 2 sum(q - 128) = sum((q - 127)^2 - 1), q, t in [0, 255]^128
+    d2_max = 128 * 255 * 255
+    c_max = 128 * ((0 - 127) ** 2 - 1)
+    c_min = -128
+    return -c_max, d2_max - c_min
+
+
+def test_early_key_order_and_decode():
+    rng = np.random.default_rng(11)
+    dlo, dhi = d_range()
+    D = np.concatenate([rng.integers(dlo, dhi + 1, 300_000), np.array([dlo, dhi, 0, -1, 1]),
+                        rng.integers(-50, 50, 100_000)])  # many equal D: the row decides
+    row = rng.integers(0, 64, D.size)
+    p = D & 1
+    R = (D - p) >> 1  # floor((D - p) / 2): D = 2R + p
+    key = early_key(R, p, row)
+    assert key.min() > 0 and key.max() < (1 << 31), "real keys stay in (0, 2^31)"
+    # decode
+    k32 = key.astype(np.int64)
+    assert np.array_equal((k32 - (1 << 28)) >> 7, D)
+    assert np.array_equal(k32 & 127, row)
+    # unsigned key order == lexicographic (D, row) order
+    o_key = np.argsort(key, kind="stable")
+    o_lex = np.lexsort((row, D))
+    assert np.array_equal(key[o_key], key[o_lex])
+
+
+def test_early_key_padded_row_is_uint_max():
+    R = np.array([(1 << 30) - 1])
+    K = 255
+    assert ((int(R[0]) << 8) + K) & 0xFFFFFFFF == 0xFFFFFFFF

@@ -42,15 +42,18 @@ typedef const __attribute__((address_space(1))) int gint;
 // ------------------------------------------------------------------------------------------------
 __device__ __forceinline__ void prep_tile(const float* __restrict__ src, int n, int8_t* __restrict__ frag,
                                           int* __restrict__ norm, int* __restrict__ flags, int tile) {
-    const int tid = threadIdx.x;
+    // per row: n2 and sum(t - 128) in 4 partials (one per 32-column block = one per wave), summed by
+    // the first wave; every row is read once, by the fragment pass (integer sums: exact in any order)
+    __shared__ int2 part[4][64];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     int bad = 0;
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
-        const int ci = k * 256 + tid;  // output chunk (16 B) within the tile
-        const int u = ci >> 8, s = (ci >> 6) & 3, lane = ci & 63;
-        const int row = tile * 64 + 32 * u + (lane & 31);
-        const int col = 32 * s + 16 * (lane >> 5);
+        const int ci = k * 256 + tid;  // output chunk (16 B) within the tile: u = k, s = w
+        const int row = tile * 64 + 32 * k + (lane & 31);
+        const int col = 32 * w + 16 * (lane >> 5);
         uint32_t o[4] = {0, 0, 0, 0};
+        int n2 = 0, sum = 0;
         if (row < n) {
             const float4* p = reinterpret_cast<const float4*>(src + (size_t)row * kDim + col);
 #pragma unroll
@@ -60,22 +63,26 @@ __device__ __forceinline__ void prep_tile(const float* __restrict__ src, int n, 
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     bad |= !(v[j] >= 0.f && v[j] <= 255.f && v[j] == rintf(v[j]));
+                    const int d = (int)v[j] - 128;  // garbage for non-integer rows (flagged, unused)
+                    n2 += d * d;
+                    sum += d;
                     o[c] |= (uint32_t)((127 - (int)v[j]) & 0xff) << (8 * j);
                 }
             }
         }
         reinterpret_cast<uint4*>(frag)[(size_t)tile * 512 + ci] = make_uint4(o[0], o[1], o[2], o[3]);
+        n2 += __shfl_xor(n2, 32);  // the other 16 columns of the row's 32-column block
+        sum += __shfl_xor(sum, 32);
+        if (lane < 32) part[w][32 * k + lane] = make_int2(n2, sum);
     }
+    __syncthreads();
     if (tid < 64) {
         const int row = tile * 64 + tid;
         int n2 = 0, sum = 0;
-        if (row < n) {
-            const float* p = src + (size_t)row * kDim;
-            for (int c = 0; c < kDim; ++c) {
-                const int d = (int)p[c] - 128;  // garbage for non-integer rows (flagged, unused)
-                n2 += d * d;
-                sum += d;
-            }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            n2 += part[q][tid].x;
+            sum += part[q][tid].y;
         }
         int* nb = norm + (size_t)tile * kNormWords;
         nb[tid] = row < n ? n2 >> 1 : (1 << 30) - 1;
@@ -273,7 +280,6 @@ __global__ __launch_bounds__(kThreads, MIM_KNN_OCC) void knn2_i8_kernel(  // OCC
     // ---- query fragments q': column tile u = query rows qbase + 32u .. + 31 ----
     const int qbase = w.q0 + wave * 32 * QT;
     i32x4 B[QT][4];
-    int qn[QT];
 #pragma unroll
     for (int u = 0; u < QT; ++u) {
         const int qr = qbase + 32 * u, qt = qr >> 6, qh = (qr >> 5) & 1;
@@ -282,7 +288,6 @@ __global__ __launch_bounds__(kThreads, MIM_KNN_OCC) void knn2_i8_kernel(  // OCC
         const gi32x4* qsrc = (const gi32x4*)(P->q.frag) + (size_t)qtc * 512;
 #pragma unroll
         for (int s = 0; s < 4; ++s) B[u][s] = ~qsrc[(qh * 4 + s) * 64 + lane];  // q' = ~t''
-        qn[u] = ((const gint*)P->q.norm)[(size_t)qtc * kNormWords + 128 + 32 * qh + r];
     }
     LaneSel st[QT];
     int T[QT];  // late-tile thresholds on R
@@ -429,15 +434,21 @@ __global__ __launch_bounds__(kThreads, MIM_KNN_OCC) void knn2_i8_kernel(  // OCC
             }
             continue;
 #endif
-            int mn[QT];
+            // a lane's 16 R as two row groups (g 0-7, 8-15): the group minima cost one v_min more
+            // than a single min chain and let an event compare the rows of the hit groups only
+            int mn[QT], gmn[QT][2];
             unsigned long long bm[QT], any = 0;  // wave masks of the lanes with a candidate (SGPR pairs)
 #pragma unroll
             for (int u = 0; u < QT; ++u) {
                 const i32x16& p = acc[u];
-                int m = min(min(p[0], p[1]), p[2]);
 #pragma unroll
-                for (int g = 3; g < 15; g += 2) m = min(min(m, p[g]), p[g + 1]);
-                mn[u] = min(m, p[15]);
+                for (int i = 0; i < 2; ++i) {
+                    int a = min(min(p[8 * i], p[8 * i + 1]), p[8 * i + 2]);
+                    a = min(min(a, p[8 * i + 3]), p[8 * i + 4]);
+                    a = min(min(a, p[8 * i + 5]), p[8 * i + 6]);
+                    gmn[u][i] = min(a, p[8 * i + 7]);
+                }
+                mn[u] = min(gmn[u][0], gmn[u][1]);
                 bm[u] = __ballot(mn[u] <= T[u]);
                 any |= bm[u];
             }
@@ -454,20 +465,27 @@ __global__ __launch_bounds__(kThreads, MIM_KNN_OCC) void knn2_i8_kernel(  // OCC
 #pragma unroll
                 for (int u = 0; u < QT; ++u) {
                     if (bm[u] != 0) {
-                        // per row: one compare (the ballot) and, if some lane has the row under its
-                        // threshold, an unconditional insertion in every lane (the lane lists stay the
-                        // exact top-2 of the rows pushed, a superset of the filtered ones)
-                        // the 16 row ballots first (independent compares into SGPR pairs, no VALU ->
-                        // VCC -> branch dependency per row), then a not-taken scalar test per row: the
-                        // insertion code sits out of line
-                        unsigned long long hm[16];
+                        // per row of a hit group: one compare (the ballot) and, if some lane has the row
+                        // under its threshold, an unconditional insertion in every lane (the lane lists
+                        // stay the exact top-2 of the rows pushed, a superset of the filtered ones); the
+                        // row ballots of a group first (independent compares into SGPR pairs), then a
+                        // not-taken scalar test per row: the insertion code sits out of line
+                        unsigned long long gb[2];
 #pragma unroll
-                        for (int g = 0; g < 16; ++g) hm[g] = __ballot(acc[u][g] <= T[u]);
+                        for (int i = 0; i < 2; ++i) gb[i] = __ballot(gmn[u][i] <= T[u]);
 #pragma unroll
-                        for (int g = 0; g < 16; ++g) {
-                            if (__builtin_expect(hm[g] != 0, 0))
-                                sel_push(st[u], dval(acc[u][g], (pw >> ((g & 3) + 8 * (g >> 2))) & 1),
-                                         row0 + (g & 3) + 8 * (g >> 2));
+                        for (int i = 0; i < 2; ++i) {
+                            if (gb[i] != 0) {
+                                unsigned long long hm[8];
+#pragma unroll
+                                for (int g = 0; g < 8; ++g) hm[g] = __ballot(acc[u][8 * i + g] <= T[u]);
+#pragma unroll
+                                for (int g = 8 * i; g < 8 * i + 8; ++g) {
+                                    if (__builtin_expect(hm[g - 8 * i] != 0, 0))
+                                        sel_push(st[u], dval(acc[u][g], (pw >> ((g & 3) + 8 * (g >> 2))) & 1),
+                                                 row0 + (g & 3) + 8 * (g >> 2));
+                                }
+                            }
                         }
 #ifdef MIM_KNN_EXACT_PAIR
                         T[u] = sel_filter(st[u]);
@@ -532,7 +550,8 @@ __global__ __launch_bounds__(kThreads, MIM_KNN_OCC) void knn2_i8_kernel(  // OCC
         m = sel_merge(m, o);
         const int q = qbase + 32 * u + r;
         if (h == 0 && q < nq) {
-            const int qq = qn[u];
+            // c(q), read here rather than held in a register for the whole sweep
+            const int qq = ((const gint*)P->q.norm)[(size_t)(q >> 6) * kNormWords + 128 + (q & 63)];
             Top2 t;
             const int d1 = m.m1 + qq, d2 = m.m2 + qq;  // exact d^2 = D + c(q) (< 2^23)
             t.k1 = m.i1 == INT_MAX ? FLT_MAX : sqrtf((float)d1);

@@ -672,7 +672,7 @@ __device__ __forceinline__ float det3xy_f(float x0, float y0, float x1, float y1
 }
 
 __device__ __forceinline__ bool check_subset_fast(const float* s, const float* d) {
-    bool clear = collinear4_clear(s) & collinear4_clear(d);
+    bool clear = (int)collinear4_clear(s) & (int)collinear4_clear(d);  // both evaluated: no branch
     const int tt[4][3] = {{0, 1, 2}, {1, 2, 3}, {0, 2, 3}, {0, 1, 3}};
     int negative = 0;
 #pragma unroll

@@ -326,35 +326,62 @@ __device__ __forceinline__ double dpp_row_d(double v, int ctrl) {
     return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
 }
 
-// max over the 16 lanes of a DPP row (every lane receives it)
-__device__ __forceinline__ double row_max(double v) {
-#pragma unroll
-    for (int c = 0; c < 4; ++c) v = fmax(v, dpp_row_d(v, c));
-    return v;
-}
-
 // lanes of this lane's 16-lane group in a wave ballot, as bits 0..15
 __device__ __forceinline__ unsigned group_bits(unsigned long long m) {
     return (unsigned)(m >> (threadIdx.x & 48)) & 0xFFFFu;
 }
 
+// Max over the 16 lanes of a DPP row of R values that are each >= +0 or -1.0 (every lane receives
+// the R maxima), in two 32-bit passes: the signed max of the high words (doubles >= +0 order as their
+// high words, -1.0's is negative), then the unsigned max of the low words over the lanes holding
+// that high word.  The result is the bits of the maximal element, as fmax gives; the 32-bit maxes
+// take the DPP operand directly (v_max_i32_dpp: no 64-bit moves, no fmax canonicalisation) and the
+// R reductions are interleaved step by step, so one's DPP read hazard is covered by the others.
+template <int R>
+__device__ __forceinline__ void row_max_nn(double (&v)[R]) {
+    int hi[R];
+    unsigned lo[R];
+#pragma unroll
+    for (int j = 0; j < R; ++j) hi[j] = (int)(__double_as_longlong(v[j]) >> 32);
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int j = 0; j < R; ++j) hi[j] = max(hi[j], dpp_row(hi[j], c));
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+        const long long b = __double_as_longlong(v[j]);
+        lo[j] = (int)(b >> 32) == hi[j] ? (unsigned)b : 0u;
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int j = 0; j < R; ++j) lo[j] = max(lo[j], (unsigned)dpp_row((int)lo[j], c));
+#pragma unroll
+    for (int j = 0; j < R; ++j)
+        v[j] = __longlong_as_double((long long)(((unsigned long long)(unsigned)hi[j] << 32) | lo[j]));
+}
+
 // First maximum of |A(idx, i)| over the slots' candidate indices (slots 9..15 carry the rotated
-// values, in increasing index order) plus, optionally, a zero entry at index `zi` (-1: none).
-// The index of the first maximal slot j is recomputed from j (the (j-9)-th index outside {k, l})
-// instead of being fetched from that lane: no LDS round trip.
+// values, in increasing index order) plus, optionally, a zero entry at index `zi` (-1: none), for the
+// four caches of rows/columns k and l at once.  The index of the first maximal slot j is recomputed
+// from j (the (j-9)-th index outside {k, l}) instead of being fetched from that lane: no LDS round trip.
 template <int n>
-__device__ __forceinline__ int refresh_argmax(double val, bool cand, int k, int l, int zi) {
-    const double mx = row_max(cand ? val : -1.0);
-    const unsigned m = group_bits(__ballot(cand & (val == mx)));
-    int first = INT_MAX;
-    if (m) {
-        int im = __builtin_ctz(m) - n;
+__device__ __forceinline__ void refresh_argmax4(const double (&val)[4], const bool (&cand)[4], int k, int l,
+                                                const int (&zi)[4], int (&first)[4]) {
+    double mx[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) mx[j] = cand[j] ? val[j] : -1.0;
+    row_max_nn<4>(mx);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const unsigned m = group_bits(__ballot(cand[j] & (val[j] == mx[j])));
+        int im = __ffs(m) - 1 - n;  // branch-free: m == 0 is selected away below
         im += im >= k;
         im += im >= l;
-        first = im;
+        int f = m ? im : INT_MAX;
+        if (zi[j] >= 0 && !(mx[j] > 0.0)) f = min(f, zi[j]);
+        first[j] = f;
     }
-    if (zi < 0) return first;
-    return mx > 0.0 ? first : min(first, zi);
 }
 
 // A/W/V: this group's LDS state (A packed strict upper, W diagonal) written by the caller.
@@ -393,28 +420,28 @@ __device__ __forceinline__ void jacobi_group(double* __restrict__ A, double* __r
     for (int iters = 0; iters < n * n * 30; iters++) {
         // ---- pivot: OpenCV scans rows 0..7 (A(i, indR[i])) then columns 1..8 (A(indC[i], i)) and
         // keeps the first strict maximum; slot i holds both of its candidates (row first) ----
+        // key = pos << 16 | k | l << 8: positions are distinct over the valid slots, so comparing keys
+        // compares positions (one DPP move per step for both)
         double p = 0.0;
-        int pos = 99, kl = 0;
+        int key = 99 << 16;
         if (slot < n) {
             const double vr = slot < n - 1 ? A[pk<n>(slot, indR)] : 0.0;
             const double vc = slot > 0 ? A[pk<n>(indC, slot)] : 0.0;
             const bool row = slot < n - 1 && (slot == 0 || fabs(vr) >= fabs(vc));
             p = row ? vr : vc;
-            pos = row ? slot : slot + n - 2;
-            kl = row ? (slot | (indR << 8)) : (indC | (slot << 8));
+            key = row ? (slot << 16 | slot | indR << 8) : ((slot + n - 2) << 16 | indC | slot << 8);
         }
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
             const double po = dpp_row_d(p, c);
-            const int poso = dpp_row(pos, c), klo = dpp_row(kl, c);
+            const int keyo = dpp_row(key, c);
             // bitwise: no short-circuit branches
-            const bool take = (int)(fabs(po) > fabs(p)) | ((int)(fabs(po) == fabs(p)) & (int)(poso < pos));
+            const bool take = (int)(fabs(po) > fabs(p)) | ((int)(fabs(po) == fabs(p)) & (int)(keyo < key));
             p = take ? po : p;
-            pos = take ? poso : pos;
-            kl = take ? klo : kl;
+            key = take ? keyo : key;
         }
         if (fabs(p) <= eps) break;
-        const int k = kl & 255, l = kl >> 8;  // k < l
+        const int k = key & 255, l = (key >> 8) & 255;  // k < l
         // ---- the pair of this slot ----
         int im = slot - n;  // slots 9..15: the (slot-9)-th index outside {k, l}
         if (im >= k) ++im;
@@ -452,10 +479,12 @@ __device__ __forceinline__ void jacobi_group(double* __restrict__ A, double* __r
         // slots, plus A(k,l) = 0; row l: nb, plus A(l,k) = 0) ----
         const bool aslot = !vslot && !idle;
         const double va = fabs(na), vb = fabs(nb);
-        const int rk = refresh_argmax<n>(va, aslot & (im > k), k, l, l);
-        const int ck = refresh_argmax<n>(va, aslot & (im < k), k, l, -1);
-        const int rl = refresh_argmax<n>(vb, aslot & (im > l), k, l, -1);
-        const int cl = refresh_argmax<n>(vb, aslot & (im < l), k, l, k);
+        const double rv[4] = {va, va, vb, vb};
+        const bool rc[4] = {aslot && im > k, aslot && im < k, aslot && im > l, aslot && im < l};
+        const int rz[4] = {l, -1, -1, k};
+        int rf[4];
+        refresh_argmax4<n>(rv, rc, k, l, rz, rf);
+        const int rk = rf[0], ck = rf[1], rl = rf[2], cl = rf[3];
         if (slot == k) {
             if (k < n - 1) indR = rk;
             if (k > 0) indC = ck;

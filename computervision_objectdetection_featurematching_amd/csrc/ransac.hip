@@ -142,10 +142,11 @@ __device__ void jacobi_fast(double* __restrict__ A, double* __restrict__ W, doub
         }
         const double y = (wl - wk) * 0.5;
         double t = fabs(y) + d_hypot(p, y);
-        double s = d_hypot(p, t);
+        const double q = fabs(p) / t;  // hypot(p, t) = t sqrt(1 + q^2) and p / t = ±q (jacobi_group)
+        double s = t * sqrt(1 + q * q);
         const double c = t / s;
         s = p / s;
-        t = (p / t) * p;
+        t = copysign(q, p) * p;
         s = y < 0 ? -s : s;
         t = y < 0 ? -t : t;
         AU(k, l) = 0;
@@ -422,15 +423,15 @@ __device__ __forceinline__ void jacobi_group(double* __restrict__ A, double* __r
         // keeps the first strict maximum; slot i holds both of its candidates (row first) ----
         // key = pos << 16 | k | l << 8: positions are distinct over the valid slots, so comparing keys
         // compares positions (one DPP move per step for both)
-        double p = 0.0;
-        int key = 99 << 16;
-        if (slot < n) {
-            const double vr = slot < n - 1 ? A[pk<n>(slot, indR)] : 0.0;
-            const double vc = slot > 0 ? A[pk<n>(indC, slot)] : 0.0;
-            const bool row = slot < n - 1 && (slot == 0 || fabs(vr) >= fabs(vc));
-            p = row ? vr : vc;
-            key = row ? (slot << 16 | slot | indR << 8) : ((slot + n - 2) << 16 | indC | slot << 8);
-        }
+        // branch-free: every slot reads two entries (slots without that candidate read entry 0)
+        const bool hr = slot < n - 1, hc = slot > 0 && slot < n;
+        const double ar = A[hr ? pk<n>(slot, indR) : 0], ac = A[hc ? pk<n>(indC, slot) : 0];
+        const double vr = hr ? ar : 0.0, vc = hc ? ac : 0.0;
+        const bool row = hr && (slot == 0 || fabs(vr) >= fabs(vc));
+        const double p0 = row ? vr : vc;
+        const int key0 = row ? (slot << 16 | slot | indR << 8) : ((slot + n - 2) << 16 | indC | slot << 8);
+        double p = slot < n ? p0 : 0.0;
+        int key = slot < n ? key0 : 99 << 16;
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
             const double po = dpp_row_d(p, c);
@@ -455,10 +456,14 @@ __device__ __forceinline__ void jacobi_group(double* __restrict__ A, double* __r
         const double wk = W[k], wl = W[l];
         const double y = (wl - wk) * 0.5;
         double t = fabs(y) + d_hypot(p, y);
-        double s = d_hypot(p, t);
+        // hypot(p, t) with t >= hypot(p, y) >= |p| > 0: its larger operand is t and its quotient |p| / t
+        // is p / t up to the sign (IEEE division is sign-symmetric), which OpenCV's update of W divides
+        // again: the same bits with one fp64 division less per rotation
+        const double q = fabs(p) / t;
+        double s = t * sqrt(1 + q * q);
         const double c = t / s;
         s = p / s;
-        t = (p / t) * p;
+        t = copysign(q, p) * p;
         s = y < 0 ? -s : s;
         t = y < 0 ? -t : t;
         const double na = a0 * c - b0 * s;

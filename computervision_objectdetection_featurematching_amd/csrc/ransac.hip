@@ -421,28 +421,28 @@ __device__ __forceinline__ void jacobi_group(double* __restrict__ A, double* __r
     for (int iters = 0; iters < n * n * 30; iters++) {
         // ---- pivot: OpenCV scans rows 0..7 (A(i, indR[i])) then columns 1..8 (A(indC[i], i)) and
         // keeps the first strict maximum; slot i holds both of its candidates (row first) ----
-        // key = pos << 16 | k | l << 8: positions are distinct over the valid slots, so comparing keys
-        // compares positions (one DPP move per step for both)
+        // key = pos << 20 | sign(p) << 16 | l << 8 | k: positions are distinct over the valid slots, so
+        // comparing keys compares positions.  The first maximum of |p| in position order as three 32-bit
+        // DPP passes (row_max_nn's two for |p|, then the smallest key among the lanes holding it); the
+        // winner's p is its |p| bits with the sign bit from the key.
         // branch-free: every slot reads two entries (slots without that candidate read entry 0)
         const bool hr = slot < n - 1, hc = slot > 0 && slot < n;
         const double ar = A[hr ? pk<n>(slot, indR) : 0], ac = A[hc ? pk<n>(indC, slot) : 0];
         const double vr = hr ? ar : 0.0, vc = hc ? ac : 0.0;
         const bool row = hr && (slot == 0 || fabs(vr) >= fabs(vc));
         const double p0 = row ? vr : vc;
-        const int key0 = row ? (slot << 16 | slot | indR << 8) : ((slot + n - 2) << 16 | indC | slot << 8);
-        double p = slot < n ? p0 : 0.0;
-        int key = slot < n ? key0 : 99 << 16;
+        const int key0 = row ? (slot << 20 | indR << 8 | slot) : ((slot + n - 2) << 20 | slot << 8 | indC);
+        const double pv = slot < n ? p0 : 0.0;
+        const unsigned long long pb = (unsigned long long)__double_as_longlong(pv);
+        const int key = (slot < n ? key0 : 99 << 20) | (int)(pb >> 63) << 16;
+        double pm[1] = {fabs(pv)};
+        row_max_nn<1>(pm);
+        int kc = fabs(pv) == pm[0] ? key : INT_MAX;
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            const double po = dpp_row_d(p, c);
-            const int keyo = dpp_row(key, c);
-            // bitwise: no short-circuit branches
-            const bool take = (int)(fabs(po) > fabs(p)) | ((int)(fabs(po) == fabs(p)) & (int)(keyo < key));
-            p = take ? po : p;
-            key = take ? keyo : key;
-        }
+        for (int c = 0; c < 4; ++c) kc = min(kc, dpp_row(kc, c));
+        const double p = (kc >> 16) & 1 ? -pm[0] : pm[0];
         if (fabs(p) <= eps) break;
-        const int k = key & 255, l = (key >> 8) & 255;  // k < l
+        const int k = kc & 255, l = (kc >> 8) & 255;  // k < l
         // ---- the pair of this slot ----
         int im = slot - n;  // slots 9..15: the (slot-9)-th index outside {k, l}
         if (im >= k) ++im;

@@ -18,6 +18,8 @@ gates, /root/reference/src/TestsDetector.cpp:58-95) over one batch of problems. 
       (29 views, SIFT computed once before the timed region as processAllModelsImages does) against one
       test view per step through detectObjects: 5 x (resize + SIFT) on the GPU, the 145 problems as one
       device batch, clustering and boxes on the host (pipeline.detect_objects).
+  dataset  the reference's whole run on its own data: 3 models (89 views) vs its 30 test images, one
+      step = processAllTestImages over the 30 scenes, split round robin over the ranks.
 Inputs (descriptors + keypoints) are resident in HBM before the timed region; each step registers
 the sets (the i8 layout prep is inside the step) and runs the batch.  Multi-GPU: one process per GPU
 (`--gpus N` launches N ranks through torch.distributed.run when WORLD_SIZE is unset).  Twelve scene
@@ -80,7 +82,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--config", default="c4", choices=["c1", "c1img", "c2", "c3", "c4", "c5"])
+    ap.add_argument("--config", default="c4", choices=["c1", "c1img", "c2", "c3", "c4", "c5", "dataset"])
     ap.add_argument("--cpu-sample", type=int, default=6,
                     help="problems of the sequential CPU-baseline sample (1 warm-up + the median of the rest; "
                          "0: skip the CPU baseline)")
@@ -152,6 +154,21 @@ def dry_run(args):
     seen = dist.get_world_size() if world > 1 else 1
     if seen != args.gpus:
         raise SystemExit(f"rank {rank}: process group has {seen} ranks, --gpus {args.gpus}")
+    if args.config == "dataset":  # the real-data split: scenes round robin, detections all-gathered
+        mine = list(shard.shard_round_robin(DATASET_SCENES, world, rank))
+        parts = shard.gather_objects([(i, [((i, rank, 1, 1), "stub")]) for i in mine], world)
+        merged = shard.merge_scene_results(parts, DATASET_SCENES)
+        if rank == 0:
+            print(json.dumps({"metric": "dry-run", "value": 0.0, "unit": "problems/s", "n_gpus": world,
+                              "ranks_seen": seen, "steps": 0, "warmup": 0, "ms_per_step": 0.0,
+                              "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dry_run": True,
+                              "config": {"workload": "dataset"},
+                              "scene_ids_covered": sum(d[0][0][0] == i for i, d in enumerate(merged)),
+                              "ranks_of_scenes": [d[0][0][1] for d in merged], "global_batch": DATASET_SCENES}),
+                  flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
     cfg = CONFIGS.get(args.config, {})
     n_scenes = cfg.get("n_scenes", 4) if cfg.get("sharded") else 4 * world
     ids = shard.shard_range(n_scenes, world, rank) if cfg.get("sharded") else range(4 * rank, 4 * rank + 4)
@@ -337,8 +354,14 @@ def run_c1img(args, rank, world, local):
     m = ms[0]
     model = process_model_views(m, "004_sugar_box", [(d[f"view/{n}"], d[f"mask/{n}"]) for n in names])
     models = [model] * nf
-    sid = scenes[rank % len(scenes)]
-    scene = d[f"scene/{sid}"]
+    # the fixture's 10 sugar_box test views: rank r's steps cycle through its round-robin share
+    # (shard_round_robin, as process_all_test_images splits a dataset); the isolated pass, the
+    # latency figures and the CPU baseline use the share's first view
+    from computervision_objectdetection_featurematching_amd.shard import shard_round_robin
+    my_ids = [scenes[i] for i in shard_round_robin(len(scenes), world, rank)] or [scenes[rank % len(scenes)]]
+    my_scenes = [d[f"scene/{s}"] for s in my_ids]
+    sid = my_ids[0]
+    scene = my_scenes[0]
     n_probs = len(SCALES) * len(names)
     for mm, md in zip(ms[1:], models[1:]):
         detect_objects(mm, scene, [md])
@@ -350,8 +373,8 @@ def run_c1img(args, rank, world, local):
     out_dets = [None] * nf
 
     def worker(k):
-        for _ in range(k, args.steps, nf):
-            out_dets[k] = detect_objects(ms[k], scene, [models[k]])
+        for st in range(k, args.steps, nf):
+            out_dets[k] = detect_objects(ms[k], my_scenes[st % len(my_scenes)], [models[k]])
 
     from concurrent.futures import ThreadPoolExecutor
     pool = ThreadPoolExecutor(nf)
@@ -362,7 +385,6 @@ def run_c1img(args, rank, world, local):
     list(pool.map(worker, range(nf)))
     torch.cuda.synchronize()
     pool.shutdown()
-    dets = out_dets[0]
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
@@ -388,6 +410,7 @@ def run_c1img(args, rank, world, local):
         t1 = time.perf_counter()
         run = detect_objects(m, scene, [model], keep=True)
         el_iso += time.perf_counter() - t1
+        dets = run.detections
         for k in names_k:  # each scene's batch collects its own events (match_batch -> batch_results)
             acc[k] += max(m.kernel_ms(k), 0.0)
     scene_ms = 1e3 * el_iso / n_iso
@@ -402,9 +425,10 @@ def run_c1img(args, rank, world, local):
                "steps": args.steps, "warmup": n_warm + nf - 1, "ms_per_step": round(1e3 * el / args.steps, 3),
                "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
                "dtype": "f32 SIFT (OpenCV order), i8-MFMA exact-int distances, fp64 DLT/LM, fp32 reprojection",
-               "data": "reference images: 29 sugar_box model views + masks, test view " + sid,
+               "data": f"reference images: 29 sugar_box model views + masks, test views {', '.join(my_ids)} (rank 0)",
                "config": {"workload": f"c1img: detectObjects of one 640x480 scene against {len(names)} views x "
-                                      f"{len(SCALES)} scales = {n_probs} problems per step per GPU",
+                                      f"{len(SCALES)} scales = {n_probs} problems per step per GPU, the steps "
+                                      f"cycling through the rank's share of the {len(scenes)} test views",
                           "problems_per_gpu": n_probs, "global_batch": world * n_probs, "parallelism": f"dp{world}",
                           "scenes_in_flight": nf},
                "scenes_per_s": round(world * args.steps / el, 3),
@@ -419,7 +443,7 @@ def run_c1img(args, rank, world, local):
                             "kernel_ms_per_scene_isolated": {k: round(v, 4) for k, v in iso.items()},
                             "note": "small problems (Nq ~100-500 x Nt ~1-4k): launch- and latency-bound, the "
                                     "MFMA fraction is not the limiter at this size"},
-               "detections_rank0": [list(b) for b, _ in dets],
+               "detections_rank0": [list(b) for b, _ in dets], "detections_scene": sid,
                "accepted_problems_rank0": int((run.results["status"] == 0).sum())}
         if args.cpu_sample > 0:
             out["cpu_baseline"] = cpu_baseline_c1img(scene, model, run, names)
@@ -427,8 +451,92 @@ def run_c1img(args, rank, world, local):
         print(json.dumps(out), flush=True)
     for mm in ms:
         mm.close()
+
+
+DATASET_SCENES = 30  # tests/golden/dataset_gray.npz: the reference's 30 test images (data/*/test)
+
+
+def run_dataset(args, rank, world, local):
+    """The reference's whole run on its own data (main.cpp:17-33): the 3 objects' 89 model views are
+    described once (processAllModelsImages, untimed, as c1img), then one step = processAllTestImages
+    over the 30 test images (Output.cpp:19-57: detectObjects of every scene against all 3 models, 445
+    problems per scene, plus its results file), the scenes split round robin over the ranks
+    (pipeline.process_all_test_images, detections all-gathered every step).  Strong scaling: 30
+    scenes per step at any N.  Parity: every scene's detections against the restatement's run
+    (tests/golden/dataset_expected.json)."""
+    import tempfile
+
+    import torch
+    import torch.distributed as dist
+
+    from computervision_objectdetection_featurematching_amd import Matcher, build
+    from computervision_objectdetection_featurematching_amd import shard
+    from computervision_objectdetection_featurematching_amd.pipeline import (SCALES, process_all_test_images,
+                                                                               process_model_views)
+
+    build.build()
+    with np.load(os.path.join(ROOT, "tests", "golden", "dataset_gray.npz")) as z:
+        imgs = {k: z[k] for k in z.files}
+    with open(os.path.join(ROOT, "tests", "golden", "dataset_expected.json")) as f:
+        exp = json.load(f)
+    objs = sorted({k.split("/")[0] for k in imgs})
+    scenes = [(obj, k.split("/")[-1] + "-color", imgs[k]) for obj in objs
+              for k in sorted(k for k in imgs if k.startswith(f"{obj}/scene/"))]
+    assert len(scenes) == DATASET_SCENES
+    mine = list(shard.shard_round_robin(len(scenes), world, rank))
+    nf = max(1, min(args.inflight if args.inflight > 0 else 12, len(mine)))
+    ms = [Matcher(local) for _ in range(nf)]
+    models = []
+    for obj in objs:
+        views = sorted(k for k in imgs if k.startswith(f"{obj}/view/"))
+        models.append(process_model_views(ms[0], obj, [(imgs[k], imgs.get(k.replace("/view/", "/mask/")))
+                                                       for k in views]))
+    n_views = sum(len(m.descriptors) for m in models)
+    per_scene = len(SCALES) * n_views
+    out_dir = tempfile.mkdtemp(prefix="mim_dataset_")
+    for k, mm in enumerate(ms):  # every context once (code objects, workspaces, the models' sets)
+        process_all_test_images(mm, [scenes[mine[k % len(mine)]]], models, tempfile.mkdtemp(prefix="mim_warm_"))
+    n_warm = max(args.warmup, 0)
+    for _ in range(n_warm):
+        process_all_test_images(ms, scenes, models, out_dir, rank=rank, world=world)
+    got = None
     if world > 1:
-        dist.destroy_process_group()
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        got = process_all_test_images(ms, scenes, models, out_dir, rank=rank, world=world)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=torch.device("cuda", local))
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    if rank == 0:
+        mism = [f"{f}/{s}" for (f, s), d in got.items()
+                if [[*b, n] for b, n in d] != exp["scenes"][f"{f}/{s[:-6]}"]["detections"]]
+        out = {"metric": "matches+homographies/sec (the reference's dataset: 3 models x 89 views vs its 30 test "
+                         "images, SIFT + match + RANSAC + boxes + results files)",
+               "value": round(len(scenes) * per_scene * args.steps / el, 3), "unit": "problems/s", "n_gpus": world,
+               "steps": args.steps, "warmup": n_warm + nf, "ms_per_step": round(1e3 * el / args.steps, 3),
+               "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+               "dtype": "f32 SIFT (OpenCV order), i8-MFMA exact-int distances, fp64 DLT/LM, fp32 reprojection",
+               "data": "reference images: 3 objects, 89 model views + masks, 30 test images",
+               "config": {"workload": f"dataset: processAllTestImages of {len(scenes)} scenes x {per_scene} problems "
+                                      f"(3 models, {n_views} views, {len(SCALES)} scales), scenes round robin over "
+                                      f"{world} GPU(s)",
+                          "problems_per_step": len(scenes) * per_scene, "scenes_rank0": len(mine),
+                          "parallelism": f"dp{world}", "scenes_in_flight": nf},
+               "scenes_per_s": round(len(scenes) * args.steps / el, 3),
+               "ms_per_scene": round(1e3 * el / (args.steps * len(scenes)), 3),
+               "parity": {"checked": len(got), "mismatch": len(mism), "first": mism[:3],
+                          "reference": "detections of the restatement's run of the same data "
+                                       "(tests/golden/dataset_expected.json; parity vs OpenCV unpinned)"}}
+        print(json.dumps(out), flush=True)
+    for mm in ms:
+        mm.close()
 
 
 def cpu_baseline_c1img(scene, model, run, names):
@@ -539,15 +647,33 @@ def main():
     import torch.distributed as dist
     if args.dist_backend == "gloo":  # rehearsal: every rank on the visible GPU(s), round robin
         local = local % max(torch.cuda.device_count(), 1)
-    if world > 1:
-        torch.cuda.set_device(local)
-        if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    if args.dist_backend == "nccl":
+        # RCCL at every N, N = 1 included: the record gather of every step is the same
+        # all_gather_into_tensor on the contexts' streams whether 1 or 8 ranks run
+        if world == 1:
+            dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1,
+                                    device_id=torch.device("cuda", local))
         else:
-            dist.init_process_group("gloo")
-    if args.config == "c1img":
-        return run_c1img(args, rank, world, local)
-    ranks_seen = dist.get_world_size() if world > 1 else 1
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    elif world > 1:
+        dist.init_process_group("gloo")
+    try:
+        if args.config == "c1img":
+            return run_c1img(args, rank, world, local)
+        if args.config == "dataset":
+            return run_dataset(args, rank, world, local)
+        return run_batches(args, rank, world, local)
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def run_batches(args, rank, world, local):
+    """The synthetic configs (c1 surrogate, c2-c5): see the module docstring."""
+    import torch
+    import torch.distributed as dist
+    ranks_seen = dist.get_world_size() if dist.is_initialized() else 1
     if ranks_seen != args.gpus:
         raise SystemExit(f"rank {rank}: {ranks_seen} ranks in the process group, --gpus {args.gpus}")
     dev = torch.device("cuda", local)
@@ -643,11 +769,33 @@ def main():
     # status 5) would have been counted as throughput; batch_results() re-runs such a batch, a device
     # copy cannot, so they are counted here and fail the parity check
     short_timed = 0
+    gather_check = None
     if not knn_only:
-        for gk in gath:
-            if gk is not None:
-                recs = shard.decode(gk)
-                short_timed += int((recs["status"] == 5).sum())
+        # every context's last gathered step: this rank's row must be its own records byte for byte,
+        # and the records of all ranks (each rank's shard, without the padding) are summarised
+        sizes = ([len(shard.shard_range(global_batch, world, r)) for r in range(world)] if sharded
+                 else [n_probs] * world)
+        same, n_ctx, st_counts, it_min, it_max = True, 0, {}, None, None
+        for k, gk in enumerate(gath):
+            if gk is None:
+                continue
+            n_ctx += 1
+            same = same and bool(torch.equal(gk[rank].to(mine[k].device), mine[k]))
+            recs = shard.decode(gk)
+            short_timed += int((recs["status"] == 5).sum())
+            for r in range(world):
+                rr = recs[r, :sizes[r]]
+                for s, c in zip(*np.unique(rr["status"], return_counts=True)):
+                    st_counts[int(s)] = st_counts.get(int(s), 0) + int(c)
+                if len(rr):
+                    lo, hi = int(rr["iters"].min()), int(rr["iters"].max())
+                    it_min = lo if it_min is None else min(it_min, lo)
+                    it_max = hi if it_max is None else max(it_max, hi)
+        gather_check = {"collective": ("all_gather_into_tensor" if dist.is_initialized() else "identity copy"),
+                        "backend": (dist.get_backend() if dist.is_initialized() else None),
+                        "world": world, "contexts_checked": n_ctx, "own_row_identical": same,
+                        "records": int(sum(st_counts.values())), "status_counts": st_counts,
+                        "iters_min": it_min, "iters_max": it_max}
 
     # ---- isolated pass: one context, one batch at a time, kernel timing on (not part of `value`)
     m0 = matchers[0]
@@ -686,10 +834,11 @@ def main():
         if rank == 0 and world == 1 and args.cpu_sample > 0:
             cpu = cpu_baseline_problems(ds, cfg, res, detail, args.cpu_sample, args.cpu_rounds)
             checked, bad = cpu["parity"]["checked"], [cpu["parity"]["first"]] * cpu["parity"]["mismatch"]
-        elif world > 1 and args.parity_sample > 0:
+        elif (world > 1 or args.cpu_sample == 0) and args.parity_sample > 0:
             k = min(args.parity_sample, n_probs)
             checked, bad = parity_sample(ds, cfg, res, detail, [(7 * j + rank) % n_probs for j in range(k)])
-    tot = torch.tensor([checked, len(bad), short_timed], dtype=torch.int64, device=cdev)
+    own_differs = int(gather_check is not None and not gather_check["own_row_identical"])
+    tot = torch.tensor([checked, len(bad), short_timed, own_differs], dtype=torch.int64, device=cdev)
     if world > 1:
         dist.all_reduce(tot)  # every rank's parity sample and cut-short count
 
@@ -746,11 +895,12 @@ def main():
                          "reference": "oracle/ restatement of OpenCV 4.5.4 (parity unpinned vs OpenCV itself)"}
         if int(tot[2]):
             out["parity"]["mismatch"] = int(tot[1]) + int(tot[2])
+        if gather_check is not None:
+            gather_check["ranks_own_row_differs"] = int(tot[3])  # summed over ranks
+            out["gather"] = gather_check
         print(json.dumps(out), flush=True)
     for mm in matchers:
         mm.close()
-    if world > 1:
-        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

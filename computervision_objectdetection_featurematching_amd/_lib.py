@@ -9,7 +9,7 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 SO_PATH = os.environ.get("MIM_LIB") or os.path.join(_HERE, "lib", "libmim.so")  # MIM_LIB: variant builds
 
-MIM_OK, MIM_EINVAL, MIM_ENOMODEL, MIM_EDEVICE, MIM_ENOMEM, MIM_ERANGE = range(6)
+MIM_OK, MIM_EINVAL, MIM_ENOMODEL, MIM_EDEVICE, MIM_ENOMEM, MIM_ERANGE, MIM_ELIMIT = range(7)
 STATUS_NAMES = {0: "accepted", 1: "few_good", 2: "empty_H", 3: "few_inliers", 4: "bad_det", 5: "stream_short"}
 MIM_STREAM_SHORT = 5
 

@@ -850,6 +850,7 @@ mim_status mim_sift_detect_compute(mim_ctx* c, const uint8_t* gray, int32_t rows
     *n_kp = n;
     if (r == -1) return MIM_EDEVICE;
     if (r == -2) return MIM_ERANGE;
+    if (r == -4) return MIM_ELIMIT;
     return MIM_OK;
 }
 
@@ -871,6 +872,7 @@ mim_status mim_sift_detect_compute_scales(mim_ctx* c, const uint8_t* gray, int32
     if (r == -1) return MIM_EDEVICE;
     if (r == -2) return MIM_ERANGE;
     if (r == -3) return MIM_EINVAL;
+    if (r == -4) return MIM_ELIMIT;
     return MIM_OK;
 }
 
@@ -1198,6 +1200,11 @@ mim_status mim_batch_inlier_points(mim_ctx* c, const float* scales, float* out_x
     mim_status fs = finish_batch_locked(c, res);  // waits; re-runs a batch cut short by the RNG stream
     if (fs != MIM_OK) return fs;
     const int n = c->last_n;
+    // the gather reads the scene keypoints through the batch's set table: sets cleared or truncated
+    // since mim_batch_run have had their storage rewound and possibly reused by newer sets
+    if (n > 0 && c->last_gen != c->sets_gen)
+        return fail(c, MIM_EINVAL, "batch_inlier_points: the batch's sets were cleared or truncated since "
+                                   "mim_batch_run");
     offsets[0] = 0;
     for (int i = 0; i < n; ++i)  // TestsDetector.cpp:79-84: only accepted problems contribute
         offsets[i + 1] = offsets[i] + (res[i].status == MIM_ACCEPTED ? res[i].n_inl : 0);

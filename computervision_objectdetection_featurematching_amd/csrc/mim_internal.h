@@ -150,8 +150,9 @@ struct RansacBufs {
 }  // namespace mim
 
 // SIFT detectAndCompute + 8-bit linear resize (sift.hip), driven by mim_sift_detect_compute /
-// mim_resize_linear_u8 (api.cpp).  Return 0, -1 on a HIP error, -2 on a bad argument / capacity;
-// `err` gets the text.
+// mim_resize_linear_u8 (api.cpp).  Return 0, -1 on a HIP error, -2 when the caller's keypoint buffer is
+// too small (the counts are set), -3 on a bad argument, -4 when an internal hard limit is exceeded
+// (image size, candidates, keypoints, Gaussian kernel size); `err` gets the text.
 #include <string>
 #include <vector>
 #include "../../include/mim.h"

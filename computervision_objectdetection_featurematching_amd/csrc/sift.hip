@@ -731,15 +731,16 @@ __device__ __forceinline__ bool kp_greater_d(const mim_keypoint& a, const mim_ke
 }
 
 __global__ __launch_bounds__(1024) void kp_post_kernel(const mim_keypoint* __restrict__ kp, const int* __restrict__ n_kp,
-                                                      int kp_cap, const uint8_t* __restrict__ mask, long long mstep,
-                                                      mim_keypoint* __restrict__ out, int* __restrict__ n_out) {
+                                                      int kp_cap, int sort_cap, const uint8_t* __restrict__ mask,
+                                                      long long mstep, mim_keypoint* __restrict__ out,
+                                                      int* __restrict__ n_out) {
     __shared__ int idx[kSortCap];
     __shared__ unsigned long long skey[kKeySortCap];
     __shared__ int wsum[16];
     __shared__ int carry;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int n = min(*n_kp, kp_cap);
-    if (n > kSortCap) {
+    if (n > sort_cap) {  // sort_cap <= kSortCap
         if (tid == 0) *n_out = -n;
         return;
     }
@@ -956,6 +957,23 @@ struct SiftJob {
 
 constexpr int kCandCap = 1 << 20, kKpCap = 1 << 19;
 
+// Test knobs (environment, read once): MIM_SIFT_CAND_CAP / MIM_SIFT_SORT_CAP lower the candidate
+// capacity (past it: MIM_ELIMIT) and the device post-processing limit (past it: the host path of
+// sift_describe_host), so that small images reach both paths (tests/test_sift_limits_gpu.py)
+static int env_limit(const char* name, int dflt) {
+    const char* e = getenv(name);
+    const int v = e ? atoi(e) : 0;
+    return v > 0 && v < dflt ? v : dflt;
+}
+static int cand_limit() {
+    static const int v = env_limit("MIM_SIFT_CAND_CAP", kCandCap);
+    return v;
+}
+static int sort_limit() {
+    static const int v = env_limit("MIM_SIFT_SORT_CAP", kSortCap);
+    return v;
+}
+
 // Gaussian pyramid, DoG and the scale-space extrema of one image (enqueued; the candidate count is
 // copied to J.h_cnt[0])
 static int sift_build(SiftJob& J, hipStream_t st, std::string& err) {
@@ -965,7 +983,7 @@ static int sift_build(SiftJob& J, hipStream_t st, std::string& err) {
     if (J.n_oct < 1) return 0;  // no octave (sides < 2 px after doubling): no keypoints, as OpenCV
     if (J.n_oct > 16) {
         err = "image too large for SIFT (more than 16 octaves)";
-        return -2;
+        return -4;
     }
     const int n_oct = J.n_oct;
     // pyramid layout: per octave 6 Gaussian + 5 DoG planes
@@ -998,7 +1016,7 @@ static int sift_build(SiftJob& J, hipStream_t st, std::string& err) {
     // createInitialImage
     up2_kernel<<<dim3((C + 255) / 256, R), 256, 0, st>>>((const uint8_t*)w->img, J.rows, J.cols, T0);
     const float sig_diff = sqrtf(std::max(1.6f * 1.6f - 0.5f * 0.5f * 4, 0.01f));
-    if (!blur(T0, P + goff[0], R, C, sig_diff)) { err = "kernel size"; return -2; }
+    if (!blur(T0, P + goff[0], R, C, sig_diff)) { err = "kernel size"; return -4; }
     // buildGaussianPyramid + DoG
     double sig[kNOL + 3];
     sig[0] = 1.6;
@@ -1018,7 +1036,7 @@ static int sift_build(SiftJob& J, hipStream_t st, std::string& err) {
             down2_kernel<<<dim3((ocols[o] + 255) / 256, orows[o]), 256, 0, st>>>(P + goff[o - 1] + kNOL * (size_t)orows[o - 1] * ocols[o - 1],
                                                                                 ocols[o - 1], G, orows[o], ocols[o]);
         for (int i = 1; i < kNOL + 3; ++i)
-            if (!blur(G + (i - 1) * plane, G + i * plane, orows[o], ocols[o], sig[i])) { err = "kernel size"; return -2; }
+            if (!blur(G + (i - 1) * plane, G + i * plane, orows[o], ocols[o], sig[i])) { err = "kernel size"; return -4; }
         dog_kernel<<<dim3((unsigned)((plane + 255) / 256), kNOL + 2), 256, 0, st>>>(G, P + doff[o], plane);
     }
     if (o_small < n_oct) {
@@ -1032,7 +1050,7 @@ static int sift_build(SiftJob& J, hipStream_t st, std::string& err) {
             so.doff[o] = (long long)doff[o];
         }
         for (int i = 1; i < kNOL + 3; ++i)
-            if (gauss_taps(sig[i], so.t[i - 1]) < 0) { err = "kernel size"; return -2; }
+            if (gauss_taps(sig[i], so.t[i - 1]) < 0) { err = "kernel size"; return -4; }
         small_octaves_kernel<<<1, 1024, 0, st>>>(P, so);
     }
     SCHK(hipGetLastError());
@@ -1071,7 +1089,7 @@ static int sift_build(SiftJob& J, hipStream_t st, std::string& err) {
     for (int o = 0; o < n_oct; ++o) {
         if (orows[o] <= 2 * kBorder || ocols[o] <= 2 * kBorder) continue;
         extrema_kernel<<<dim3((ocols[o] - 2 * kBorder + 127) / 128, orows[o] - 2 * kBorder, kNOL), 128, 0, st>>>(
-            P + doff[o], orows[o], ocols[o], o, threshold, d_cand, d_cnt, cand_cap);
+            P + doff[o], orows[o], ocols[o], o, threshold, d_cand, d_cnt, cand_limit());
     }
     return 0;
 }
@@ -1081,9 +1099,10 @@ static int sift_build(SiftJob& J, hipStream_t st, std::string& err) {
 // keypoint count goes to J.h_cnt[3] (negative: more than kSortCap, the host finishes)
 static int sift_enqueue_rest(SiftJob& J, hipStream_t st, std::string& err) {
     if (J.n_oct < 1) return 0;
-    refine_kernel<<<1024, 128, 0, st>>>(J.d_pyr, J.d_cand, J.d_cnt, kCandCap, J.d_surv, J.d_cnt + 2, kCandCap);
+    refine_kernel<<<1024, 128, 0, st>>>(J.d_pyr, J.d_cand, J.d_cnt, cand_limit(), J.d_surv, J.d_cnt + 2, kCandCap);
     orient_kernel<<<4096, 64, 0, st>>>(J.d_pyr, J.d_surv, J.d_cnt + 2, kCandCap, J.d_kp, J.d_cnt + 1, kKpCap);
-    kp_post_kernel<<<1, 1024, 0, st>>>(J.d_kp, J.d_cnt + 1, kKpCap, J.d_mask, J.cols, J.d_kp2, J.d_cnt + 3);
+    kp_post_kernel<<<1, 1024, 0, st>>>(J.d_kp, J.d_cnt + 1, kKpCap, sort_limit(), J.d_mask, J.cols, J.d_kp2,
+                                       J.d_cnt + 3);
     SCHK(grow(J.w->desc, J.w->desc_cap, sizeof(float) * 128 * (size_t)kSortCap));
     descr_kernel<<<4096, kDescrT, 0, st>>>(J.d_pyr, J.d_kp2, J.d_cnt + 3, kSortCap, (float*)J.w->desc);
     SCHK(hipGetLastError());
@@ -1094,7 +1113,7 @@ static int sift_enqueue_rest(SiftJob& J, hipStream_t st, std::string& err) {
 // KeyPointsFilter::removeDuplicatedSorted, the octave -1 rescale, runByPixelsMask on the host, then the
 // descriptors: only for an image with more than kSortCap keypoints (kp_post_kernel's limit)
 static int sift_describe_host(SiftJob& J, hipStream_t st, std::string& err) {
-    if (J.h_cnt[1] > kKpCap) { err = "more than 2^19 SIFT keypoints"; return -2; }
+    if (J.h_cnt[1] > kKpCap) { err = "more than 2^19 SIFT keypoints"; return -4; }
     std::vector<mim_keypoint>& k = J.k;
     k.resize(J.h_cnt[1]);
     if (!k.empty()) SCHK(hipMemcpyAsync(k.data(), J.d_kp, sizeof(mim_keypoint) * k.size(), hipMemcpyDeviceToHost, st));
@@ -1138,6 +1157,12 @@ static int sift_describe_host(SiftJob& J, hipStream_t st, std::string& err) {
 // copies of the first J.cap keypoints / descriptors (enqueued)
 static int sift_fetch(SiftJob& J, hipStream_t st, std::string& err) {
     if (J.n_oct < 1) return 0;
+    // extrema_kernel counts every candidate but stores only the first cand_limit(): more would
+    // silently drop keypoints OpenCV (no cap) keeps
+    if (J.h_cnt[0] > cand_limit()) {
+        err = "more than " + std::to_string(cand_limit()) + " SIFT candidates";
+        return -4;
+    }
     if (J.h_cnt[3] < 0) return sift_describe_host(J, st, err);
     J.n = J.h_cnt[3];
     const int n = std::min(J.n, J.cap);

@@ -142,7 +142,7 @@ def save_detections(path: str, detections) -> None:
 
 
 def process_all_test_images(matcher, scenes, models, output_dir: str, params=None,
-                            box_params: BoxParams | None = None) -> dict:
+                            box_params: BoxParams | None = None, rank: int = 0, world: int = 1) -> dict:
     """Output.cpp:15-57 without the file decoding and drawing: scenes = [(object folder, scene name,
     gray image)]; writes <output_dir>/<folder>/<scene name>_results.txt (scene name = the image stem,
     e.g. "4_0001_000121-color") and returns {(folder, scene name): detections}.
@@ -151,20 +151,30 @@ def process_all_test_images(matcher, scenes, models, output_dir: str, params=Non
     context i mod len, one host thread per context, so a scene's host stages overlap the other
     contexts' GPU work.  The models are host arrays, registered in each context on its first scene.
     Per-scene results are those of the one-context run (the contexts share no device state), and the
-    files and returned dict are the same."""
+    files and returned dict are the same.
+
+    Several GPUs (one process per GPU, `world` ranks): rank r processes the scenes
+    shard.shard_round_robin(len(scenes), world, r) — round robin, since a scene's cost depends on how
+    early its problems terminate — and writes their results files; the detections are then
+    all-gathered (torch.distributed, the process group the caller created), so every rank returns
+    the whole dict, in scene order, and the union of the ranks' files is the one-GPU run's."""
     import os
     from concurrent.futures import ThreadPoolExecutor
+
+    from . import shard
     if isinstance(matcher, Matcher):
         matcher = [matcher]
     if len(matcher) > 1:  # the contexts overlap each other: one stream each (no sampler stream)
         for mm in matcher:
             mm.set_sampler_stream(False)
-    for folder, _, _ in scenes:
-        os.makedirs(os.path.join(output_dir, folder), exist_ok=True)
-    dets = [None] * len(scenes)
+    mine = list(shard.shard_round_robin(len(scenes), world, rank))
+    for i in mine:
+        os.makedirs(os.path.join(output_dir, scenes[i][0]), exist_ok=True)
+    dets = {}
 
     def worker(k):
-        for i in range(k, len(scenes), len(matcher)):
+        for j in range(k, len(mine), len(matcher)):
+            i = mine[j]
             dets[i] = detect_objects(matcher[k], scenes[i][2], models, params=params, box_params=box_params)
 
     if len(matcher) == 1:
@@ -172,11 +182,12 @@ def process_all_test_images(matcher, scenes, models, output_dir: str, params=Non
     else:
         with ThreadPoolExecutor(len(matcher)) as pool:
             list(pool.map(worker, range(len(matcher))))
-    out = {}
-    for (folder, name, _), d in zip(scenes, dets):
-        save_detections(os.path.join(output_dir, folder, f"{name}_results.txt"), d)
-        out[(folder, name)] = d
-    return out
+    for i in mine:
+        folder, name, _ = scenes[i]
+        save_detections(os.path.join(output_dir, folder, f"{name}_results.txt"), dets[i])
+    parts = shard.gather_objects([(i, dets[i]) for i in mine], world) if world > 1 else [[(i, dets[i]) for i in mine]]
+    all_dets = shard.merge_scene_results(parts, len(scenes))
+    return {(folder, name): d for (folder, name, _), d in zip(scenes, all_dets)}
 
 
 __all__ = ["ObjectModel", "SCALES", "SceneRun", "default_box_params", "detect_boxes", "detect_objects",

@@ -34,7 +34,11 @@ enum {
     MIM_ENOMODEL = 2, /* findHomography found no model: H.empty() at TestsDetector.cpp:79 */
     MIM_EDEVICE = 3,  /* HIP runtime / RCCL error; text in mim_last_error() */
     MIM_ENOMEM = 4,
-    MIM_ERANGE = 5    /* a capacity was exceeded (e.g. RANSAC RNG stream); text in mim_last_error() */
+    MIM_ERANGE = 5,   /* a capacity was exceeded (e.g. RANSAC RNG stream, the caller's keypoint buffer);
+                         text in mim_last_error() */
+    MIM_ELIMIT = 6    /* an internal hard limit of the library was exceeded (SIFT: > 16 octaves, > 2^20
+                         scale-space candidates, > 2^19 keypoints); retrying with a larger buffer does not
+                         help; text in mim_last_error() */
 };
 
 /* Problem outcome codes (mim_result.status), TestsDetector.cpp:74-84 */
@@ -162,7 +166,8 @@ mim_status mim_batch_problem_detail(struct mim_ctx* ctx, int32_t i, int32_t* q_i
  * as one slice.  Waits for the batch (re-running it if the RNG stream was short, as
  * mim_batch_results), then one table copy in, one kernel, one copy out — instead of a
  * mim_batch_problem_detail round trip per accepted problem.  out_xy NULL: offsets only;
- * offsets[n] > cap: MIM_ERANGE (offsets valid, nothing copied). */
+ * offsets[n] > cap: MIM_ERANGE (offsets valid, nothing copied).  MIM_EINVAL if the sets were cleared or
+ * truncated (mim_sets_clear / mim_sets_truncate) after mim_batch_run: the points are read from them. */
 mim_status mim_batch_inlier_points(struct mim_ctx* ctx, const float* scales, float* out_xy, int64_t cap,
                                    int64_t* offsets);
 
@@ -184,7 +189,8 @@ typedef struct {
  * with an empty mask).  gray: host CV_8UC1 rows x cols, row stride `step` bytes; mask: NULL or host
  * CV_8UC1 of the same size, stride mask_step.  Writes min(found, max_kp) keypoints (OpenCV's order:
  * KeypointGreater after removeDuplicatedSorted, then the mask filter) and their 128-float
- * descriptors (row-major); *n_kp = keypoints found (may exceed max_kp).  Synchronous. */
+ * descriptors (row-major); *n_kp = keypoints found (may exceed max_kp: MIM_OK, call again with room
+ * for all).  MIM_ELIMIT past the library's hard limits (nothing written).  Synchronous. */
 mim_status mim_sift_detect_compute(struct mim_ctx* ctx, const uint8_t* gray, int32_t rows, int32_t cols,
                                    int64_t step, const uint8_t* mask, int64_t mask_step, int32_t max_kp,
                                    mim_keypoint* kps, float* desc, int32_t* n_kp);
@@ -194,7 +200,7 @@ mim_status mim_sift_detect_compute(struct mim_ctx* ctx, const uint8_t* gray, int
  * synchronisations in all instead of 3 per image plus one per resize).  Results are those of
  * mim_resize_linear_u8 + mim_sift_detect_compute per scale: keypoints / descriptors concatenated in
  * scale order into kps / desc (max_kp rows in all), n_kp[s] = keypoints of scale s.  More than max_kp
- * in all: MIM_ERANGE with the counts set (only the first max_kp written). */
+ * in all: MIM_ERANGE with the counts set (only the first max_kp written); MIM_ELIMIT as above. */
 mim_status mim_sift_detect_compute_scales(struct mim_ctx* ctx, const uint8_t* gray, int32_t rows, int32_t cols,
                                           int64_t step, int32_t n_scales, const float* scales, int32_t max_kp,
                                           mim_keypoint* kps, float* desc, int32_t* n_kp);

@@ -92,9 +92,9 @@ class Detector {
             desc.resize((size_t)cap * 128);
             const mim_status s = mim_sift_detect_compute(ctx_, gray, rows, cols, step, mask, mask_step, cap, kps.data(),
                                                          desc.data(), &n);
-            if (s != MIM_OK && s != MIM_ERANGE) check(s, "mim_sift_detect_compute", ctx_);
+            check(s, "mim_sift_detect_compute", ctx_);  // MIM_ELIMIT etc. throw: a retry cannot help
             if (n <= cap) break;
-            cap = n;  // more keypoints than the buffer: call again with room for all
+            cap = n;  // more keypoints than the buffer (MIM_OK, n > cap): call again with room for all
         }
         kps.resize(n);
         desc.resize((size_t)n * 128);
@@ -114,9 +114,10 @@ class Detector {
             const mim_status s = mim_sift_detect_compute_scales(ctx_, gray, rows, cols, step, ns, scales.data(), cap,
                                                                 k.data(), d.data(), n.data());
             if (s == MIM_OK) break;
-            if (s != MIM_ERANGE) check(s, "mim_sift_detect_compute_scales", ctx_);
             int64_t tot = 0;
             for (int32_t x : n) tot += x;
+            // retry only for a buffer that was too small; anything else (MIM_ELIMIT, ...) throws
+            if (s != MIM_ERANGE || tot <= cap || tot > INT32_MAX) check(s, "mim_sift_detect_compute_scales", ctx_);
             cap = (int32_t)tot;
         }
         kps.assign(ns, {});

@@ -474,7 +474,7 @@ int orc_sift_detect_compute(const uint8_t* img, int rows, int cols, const uint8_
                 }
         }
     /* removeDuplicatedSorted */
-    qsort(kl.v, (size_t)kl.n, sizeof(orc_keypoint), kp_cmp);
+    if (kl.n > 1) qsort(kl.v, (size_t)kl.n, sizeof(orc_keypoint), kp_cmp); /* kl.v is NULL when empty */
     int m = 0;
     for (int j = 0; j < kl.n; ++j) {
         if (m > 0) {

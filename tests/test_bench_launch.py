@@ -70,3 +70,13 @@ def test_c4_shard_data_is_rank_independent():
             for j, s in enumerate(ids):
                 assert np.array_equal(part.scene_desc[j], full.scene_desc[s])
                 assert np.array_equal(part.scene_kp[j], full.scene_kp[s])
+
+
+def test_dataset_scenes_split_round_robin_over_ranks():
+    """The reference's real-data run (bench --config dataset, pipeline.process_all_test_images): its 30
+    test images split round robin over 4 gloo ranks (Output.cpp:19-57 processes every scene once), the
+    per-scene results all-gathered; rank 0 checks every scene came back once, from rank i mod 4."""
+    d = _run(["--gpus", "4", "--dry-run", "--config", "dataset"])
+    assert d["n_gpus"] == 4 and d["ranks_seen"] == 4
+    assert d["scene_ids_covered"] == 30 and d["global_batch"] == 30
+    assert d["ranks_of_scenes"] == [i % 4 for i in range(30)]

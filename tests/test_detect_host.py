@@ -23,12 +23,19 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 DATASET = os.path.join(ROOT, "tests", "golden", "dataset")
 
 
-@pytest.fixture(scope="module")
-def driver(tmp_path_factory):
-    exe = str(tmp_path_factory.mktemp("detect") / "test_detect")
-    subprocess.check_call(["g++", "-std=c++17", "-O2", "-Wall", "-Wextra",
+def build_driver(exe, sanitize=False):
+    """tests/cpp/test_detect.cpp over include/mim_detect.hpp; sanitize: ASan + UBSan, any
+    finding aborts the driver, so every test below fails on it."""
+    san = ["-O1", "-g", "-fsanitize=address,undefined", "-fno-sanitize-recover=all", "-fno-omit-frame-pointer"]
+    subprocess.check_call(["g++", "-std=c++17", *(san if sanitize else ["-O2"]), "-Wall", "-Wextra",
                            os.path.join(ROOT, "tests", "cpp", "test_detect.cpp"), "-o", exe])
     return exe
+
+
+@pytest.fixture(scope="module", params=["plain", "asan+ubsan"])
+def driver(tmp_path_factory, request):
+    exe = str(tmp_path_factory.mktemp("detect") / "test_detect")
+    return build_driver(exe, sanitize=request.param != "plain")
 
 
 def _write_points(path, pts, eps=20.0, min_points=18, merge=250.0, min_area=2500, factor=1.0):

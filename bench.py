@@ -57,7 +57,9 @@ PEAK_F16_MFMA_TFLOPS = 2500.0  # dense f16 MFMA
 # VALU issue peak: 1024 SIMDs x one wave64 instruction per 4 cycles (v_add/v_fma/v_max3 issue cost of one
 # wave's stream on one SIMD, MI355X_MICROARCH.md cycle-constants table) x 2.4 GHz
 PEAK_VALU_WAVE_INSTR_PER_S = 1024 * 0.25 * 2.4e9
-BOUND_VALU_PER_PAIR = 4       # ransac_bound_mfma_kernel tile loop: med3, fma, sub, sign bit per (point, hypothesis)
+# ransac_bound_mfma_kernel tile loop, VALU per (point, hypothesis) pair: chunk 1 (the first 4,096 iterations,
+# 512 when maxIters <= 4,096) box + octagon lower bound 10; chunk 2 the disc test fma, fma, sign bit: 3
+BOUND_VALU_PER_PAIR_C1, BOUND_VALU_PER_PAIR_C2 = 10, 3
 BOUND_MFMA_FLOP_PER_PAIR = 96  # 3 v_mfma_f32_32x32x16_f16 per 32 x 32 (point, hypothesis) pairs
 H_TOL = 1e-4                  # SURVEY.md 8(c) contract item 4 (the GPU tests hold bit identity)
 
@@ -592,15 +594,19 @@ def kernel_rooflines(args, ds, res, iso, iso_step_ms, knn_only):
             "isolated_step_ms": round(iso_step_ms, 3),
             "kernel_ms_per_step_isolated": {k: round(v, 4) for k, v in iso.items()}}
     if not knn_only and iso.get("score", 0) > 0:
-        pairs = float(np.sum(res["iters"].astype(np.float64) * res["n_good"]))
+        it = res["iters"].astype(np.float64)
+        c1 = 4096 if args_max_iters(args) > 4096 else 512
+        pairs = float(np.sum(it * res["n_good"]))
+        pairs1 = float(np.sum(np.minimum(it, c1) * res["n_good"]))
         tb = iso["score"] * 1e-3
-        wi = pairs * BOUND_VALU_PER_PAIR / 64.0
+        wi = (pairs1 * BOUND_VALU_PER_PAIR_C1 + (pairs - pairs1) * BOUND_VALU_PER_PAIR_C2) / 64.0
         roof["others"] = {"bound": {
             "kernel": "ransac_bound_mfma_kernel (closed-form hypotheses, bounded inlier counts), 2 launches per step",
             "bound": "valu", "unit": "VALU wave-instructions/s",
             "achieved": round(wi / tb, 1), "peak": PEAK_VALU_WAVE_INSTR_PER_S,
             "frac": round(wi / tb / PEAK_VALU_WAVE_INSTR_PER_S, 4),
-            "pairs_per_step": pairs, "valu_per_pair": BOUND_VALU_PER_PAIR,
+            "pairs_per_step": pairs, "pairs_chunk1_per_step": pairs1,
+            "valu_per_pair": {"chunk1": BOUND_VALU_PER_PAIR_C1, "chunk2": BOUND_VALU_PER_PAIR_C2},
             "floor_ms": round(wi / PEAK_VALU_WAVE_INSTR_PER_S * 1e3, 4), "ms_per_step": round(iso["score"], 4),
             "mfma": {"achieved_TFLOPs": round(pairs * BOUND_MFMA_FLOP_PER_PAIR / tb / 1e12, 1),
                      "peak_TFLOPs": PEAK_F16_MFMA_TFLOPS,
@@ -614,6 +620,11 @@ def kernel_rooflines(args, ds, res, iso, iso_step_ms, knn_only):
         raise SystemExit(f"bench: isolated kernel times {iso} exceed the isolated step {iso_step_ms:.3f} ms")
     roof["kernel_sum_ms_per_step_isolated"] = round(total, 4)
     return roof
+
+
+def args_max_iters(args) -> int:
+    from computervision_objectdetection_featurematching_amd.synthetic import CONFIGS
+    return int(CONFIGS[args.config]["max_iters"])
 
 
 def parity_sample(ds, cfg, res, detail, ids):

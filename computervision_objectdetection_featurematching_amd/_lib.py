@@ -19,8 +19,8 @@ EXPORTS = [
     "mim_ctx_set_stream", "mim_ctx_set_sampler_stream", "mim_ctx_get_stream", "mim_synchronize", "mim_set_create", "mim_sets_clear", "mim_sets_truncate",
     "mim_knn2_l2", "mim_ratio_filter", "mim_find_homography", "mim_batch_run", "mim_batch_results",
     "mim_batch_results_dev", "mim_batch_results_copy", "mim_batch_problem_detail", "mim_batch_inlier_points", "mim_knn2_sets_dev", "mim_last_kernel_ms",
-    "mim_set_timing", "mim_sift_detect_compute", "mim_sift_detect_compute_scales", "mim_resize_linear_u8",
-    "mim_default_box_params", "mim_detect_boxes",
+    "mim_set_timing", "mim_sift_detect_compute", "mim_sift_detect_compute_scales", "mim_sift_scales_sets",
+    "mim_resize_linear_u8", "mim_default_box_params", "mim_detect_boxes",
 ]
 
 
@@ -106,14 +106,15 @@ def load():
     L.mim_sift_detect_compute.argtypes = [vp, u8p, i32, i32, C.c_int64, u8p, C.c_int64, i32, vp, f32p,
                                           C.POINTER(C.c_int32)]
     L.mim_sift_detect_compute_scales.argtypes = [vp, u8p, i32, i32, C.c_int64, i32, vp, i32, vp, f32p, vp]
+    L.mim_sift_scales_sets.argtypes = [vp, u8p, i32, i32, C.c_int64, i32, vp, vp, vp, i32, vp]
     L.mim_resize_linear_u8.argtypes = [vp, u8p, i32, i32, C.c_int64, u8p, i32, i32, C.c_double, C.c_double]
     L.mim_default_box_params.argtypes = [C.POINTER(BoxParams)]
     L.mim_detect_boxes.argtypes = [f32p, i32, C.POINTER(BoxParams), C.POINTER(Rect), i32, C.POINTER(C.c_int32)]
     for name in ("mim_ctx_create", "mim_ctx_set_stream", "mim_synchronize", "mim_set_create", "mim_sets_clear",
                  "mim_sets_truncate", "mim_knn2_l2", "mim_ratio_filter", "mim_find_homography", "mim_batch_run", "mim_batch_results",
                  "mim_batch_problem_detail", "mim_batch_inlier_points", "mim_knn2_sets_dev", "mim_set_timing", "mim_ctx_set_sampler_stream",
-                 "mim_sift_detect_compute", "mim_sift_detect_compute_scales", "mim_resize_linear_u8",
-                 "mim_detect_boxes"):
+                 "mim_sift_detect_compute", "mim_sift_detect_compute_scales", "mim_sift_scales_sets",
+                 "mim_resize_linear_u8", "mim_detect_boxes"):
         getattr(L, name).restype = C.c_int32
     _lib = L
     return L

@@ -876,6 +876,71 @@ mim_status mim_sift_detect_compute_scales(mim_ctx* c, const uint8_t* gray, int32
     return MIM_OK;
 }
 
+mim_status mim_sift_scales_sets(mim_ctx* c, const uint8_t* gray, int32_t rows, int32_t cols, int64_t step,
+                                int32_t n_scales, const float* scales, int32_t* set_ids, int32_t* n_kp, int32_t max_kp,
+                                mim_keypoint* kps) {
+    if (!c) return MIM_EINVAL;
+    if (!gray || !set_ids || !n_kp || !scales || n_scales <= 0 || n_scales > 8 || rows <= 0 || cols <= 0 ||
+        step < cols || max_kp < 0 || (max_kp > 0 && !kps))
+        return fail(c, MIM_EINVAL, "sift_scales_sets: bad arguments");
+    for (int i = 0; i < n_scales; ++i)
+        if (!(scales[i] > 0)) return fail(c, MIM_EINVAL, "sift_scales_sets: scale %d is not > 0", i);
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIPCHK(c, hipSetDevice(c->device));
+    std::vector<mim::SiftDevOut> out(n_scales);
+    const int r = mim::sift_scales_device(c->sift_scales, c->stream, gray, rows, cols, step, n_scales, scales, out.data(),
+                                          c->err);
+    if (r == -1) return MIM_EDEVICE;
+    if (r == -3) return MIM_EINVAL;
+    if (r == -4) return MIM_ELIMIT;
+    if (r != 0) return MIM_ERANGE;
+    // each scale's rows and keypoint positions copied on the device into the set arena (the SIFT
+    // workspaces are overwritten by the next SIFT call), the set registered as by mim_set_create
+    long long total = 0;
+    for (int i = 0; i < n_scales; ++i) {
+        const int n = out[i].n;
+        n_kp[i] = n;
+        total += n;
+        SetRec rec{};
+        rec.mark = c->arena.pos();
+        rec.d.n = n;
+        rec.d.n_tiles = (n + 63) / 64;
+        const size_t tiles = (size_t)std::max(rec.d.n_tiles, 1);
+        void *frag, *norm, *df = nullptr, *dk = nullptr;
+        HIPCHK(c, c->arena.alloc(tiles * kTileBytes, &frag));
+        HIPCHK(c, c->arena.alloc(tiles * kNormWords * sizeof(int), &norm));
+        if (n > 0) {
+            HIPCHK(c, c->arena.alloc((size_t)n * kDim * sizeof(float), &df));
+            HIPCHK(c, c->arena.alloc((size_t)n * 2 * sizeof(float), &dk));
+            HIPCHK(c, hipMemcpyAsync(df, out[i].desc, (size_t)n * kDim * sizeof(float), hipMemcpyDeviceToDevice, c->stream));
+            // KeyPoint::pt of each mim_keypoint (x, y are its first two floats): a strided 2D copy
+            HIPCHK(c, hipMemcpy2DAsync(dk, 2 * sizeof(float), out[i].kp, sizeof(mim_keypoint), 2 * sizeof(float), n,
+                                       hipMemcpyDeviceToDevice, c->stream));
+        }
+        rec.d.frag = (const int8_t*)frag;
+        rec.d.norm = (const int*)norm;
+        rec.d.f32 = (const float*)df;
+        rec.d.kp = (const float2*)dk;
+        rec.d.flags = nullptr;
+        set_ids[i] = (int32_t)c->sets.size();
+        c->pend.push_back(PrepJob{(const float*)df, (int8_t*)frag, (int*)norm, nullptr, n, 0});
+        c->pend_set.push_back(set_ids[i]);
+        c->sets.push_back(rec);
+    }
+    if (kps && max_kp > 0) {  // the keypoints on the host too, concatenated in scale order
+        long long used = 0;
+        for (int i = 0; i < n_scales && used < max_kp; ++i) {
+            const long long m = std::min<long long>(out[i].n, max_kp - used);
+            if (m > 0)
+                HIPCHK(c, hipMemcpyAsync(kps + used, out[i].kp, sizeof(mim_keypoint) * m, hipMemcpyDeviceToHost, c->stream));
+            used += m;
+        }
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+    }
+    if (kps && total > max_kp) return fail(c, MIM_ERANGE, "sift_scales_sets: %lld keypoints, buffer holds %d", total, max_kp);
+    return MIM_OK;
+}
+
 mim_status mim_resize_linear_u8(mim_ctx* c, const uint8_t* src, int32_t rows, int32_t cols, int64_t step,
                                 uint8_t* dst, int32_t drows, int32_t dcols, double fx, double fy) {
     if (!c) return MIM_EINVAL;

@@ -168,4 +168,12 @@ int sift_detect_compute_scales(std::vector<SiftWs*>& ws, hipStream_t st, const u
                                float* desc, int* n_out, std::string& err);
 int sift_resize_u8(SiftWs* w, hipStream_t st, const uint8_t* src, int rows, int cols, long long step, uint8_t* dst,
                    int drows, int dcols, double fx, double fy, std::string& err);
+// the keypoints / descriptors of one image left on the device by sift_scales_device
+struct SiftDevOut {
+    const mim_keypoint* kp;
+    const float* desc;
+    int n;
+};
+int sift_scales_device(std::vector<SiftWs*>& ws, hipStream_t st, const uint8_t* img, int rows, int cols,
+                       long long step, int n_scales, const float* scales, SiftDevOut* out, std::string& err);
 }  // namespace mim

@@ -2472,9 +2472,35 @@ __global__ __launch_bounds__(256) void ransac_bound_mfma_kernel(const RansacStat
         CL = S.sb * sqrtf(fmaxf(tl, 0.f)) * 0.92387953f * (1.f - 1e-6f);
         EL = ((CL + 1.41421357f) * kMfmaErr + 1.41421357f * A) * (1.f + 1e-6f);
     }
+    // chunk 2 (disc test, see above the kernel): L1 = ex - cD W and L2 = ex + cD W in place of ex and W,
+    // so that L1 L2 + ey^2 - ED = ex^2 + ey^2 - cD^2 W^2 - ED is two fma per pair
+    constexpr double kDiscDelta = 0.125;
+    const float cD = C * sqrtf(1.f + (float)kDiscDelta) * (1.f + 1e-5f);
+    float ED = 0.f;
+    if (!kLo) {
+        const float eo = (1.f + cD) * kMfmaErr * (1.f + 1e-6f);  // error bound of one MFMA output
+        const float e3 = eo + 1.41421357f * (A + eo);
+        ED = (float)(1.0 + 1.0 / kDiscDelta) * e3 * e3 * (1.f + 1e-4f);
+    }
     // B-operand fragments of the own hypothesis: k 0-7 (bx, by, bw) and k 8-15 (shared by bx, by)
     h8v fx = {}, fy = {}, fw = {}, fn = {};
-    if (count) {
+    if (count && !kLo) {  // fx = L1, fw = L2 on the X part; the u part (fn) is the same for both
+        _Float16 a, b;
+        const double cd = (double)cD;
+        split_f16(h[0] - cd * h[6], a, b); fx[0] = a; fx[1] = a; fx[2] = b;
+        split_f16(h[1] - cd * h[7], a, b); fx[3] = a; fx[4] = a; fx[5] = b;
+        split_f16(h[2] - cd * h[8], a, b); fx[6] = a; fx[7] = b;
+        split_f16(h[0] + cd * h[6], a, b); fw[0] = a; fw[1] = a; fw[2] = b;
+        split_f16(h[1] + cd * h[7], a, b); fw[3] = a; fw[4] = a; fw[5] = b;
+        split_f16(h[2] + cd * h[8], a, b); fw[6] = a; fw[7] = b;
+        split_f16(h[3], a, b); fy[0] = a; fy[1] = a; fy[2] = b;
+        split_f16(h[4], a, b); fy[3] = a; fy[4] = a; fy[5] = b;
+        split_f16(h[5], a, b); fy[6] = a; fy[7] = b;
+        split_f16(h[6], a, b); fn[0] = -a; fn[1] = -a; fn[2] = -b;
+        split_f16(h[7], a, b); fn[3] = -a; fn[4] = -a; fn[5] = -b;
+        fn[6] = fn[7] = -(_Float16)(float)h[8];  // 2^-e: exact
+    }
+    if (count && kLo) {
         _Float16 a, b;
         split_f16(h[0], a, b); fx[0] = a; fx[1] = a; fx[2] = b;
         split_f16(h[1], a, b); fx[3] = a; fx[4] = a; fx[5] = b;
@@ -2502,12 +2528,14 @@ __global__ __launch_bounds__(256) void ransac_bound_mfma_kernel(const RansacStat
     const uint4 zero4 = make_uint4(0, 0, 0, 0);
     const h8v b0x = __builtin_bit_cast(h8v, lowh ? ux : r1);
     const h8v b0y = __builtin_bit_cast(h8v, lowh ? uy : r1);
-    const h8v b0w = __builtin_bit_cast(h8v, lowh ? uw : zero4);
+    const h8v b0w = __builtin_bit_cast(h8v, lowh ? uw : (kLo ? zero4 : r1));
     const h8v b1x = __builtin_bit_cast(h8v, lowh ? r1 : un);
     const h8v b1y = __builtin_bit_cast(h8v, lowh ? r2 : un);
-    const h8v b1w = __builtin_bit_cast(h8v, lowh ? r3 : zero4);
+    const h8v b1w = __builtin_bit_cast(h8v, lowh ? r3 : (kLo ? zero4 : un));
     const float Cp = __shfl_xor(C, 32), Ep = __shfl_xor(E, 32);
     const float C0 = lowh ? C : Cp, E0 = lowh ? E : Ep, C1 = lowh ? Cp : C, E1 = lowh ? Ep : E;
+    const float EDp = __shfl_xor(ED, 32);
+    const float nED0 = -(lowh ? ED : EDp), nED1 = -(lowh ? EDp : ED);
     float CL0 = 0.f, EL0 = 0.f, CL1 = 0.f, EL1 = 0.f;
     if (kLo) {
         const float CLp = __shfl_xor(CL, 32), ELp = __shfl_xor(EL, 32);
@@ -2560,6 +2588,18 @@ __global__ __launch_bounds__(256) void ransac_bound_mfma_kernel(const RansacStat
             const f16acc ey1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ay, b1y, zc, 0, 0, 0);
             const f16acc w1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ax, b1w, zc, 0, 0, 0);
             unsigned bits0 = 0, bits1 = 0, lb0 = 0, lb1 = 0;
+            if (!kLo) {  // disc: sign bit of L1 L2 - ED + ey^2 set when the point may be in (ex0 = L1, w0 = L2)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const float q0 = fmaf(ey0[r], ey0[r], fmaf(ex0[r], w0[r], nED0));
+                    const float q1 = fmaf(ey1[r], ey1[r], fmaf(ex1[r], w1[r], nED1));
+                    bits0 = __builtin_amdgcn_alignbit(bits0, __float_as_uint(q0), 31);
+                    bits1 = __builtin_amdgcn_alignbit(bits1, __float_as_uint(q1), 31);
+                }
+                out0 += __popc(bits0);  // chunk 2 counts the points that may be in
+                out1 += __popc(bits1);
+                continue;
+            }
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 // sign bit of R - max(|ex|, |ey|), R = C |W| + E: set when the point is out of the box
@@ -2613,7 +2653,10 @@ __global__ __launch_bounds__(256) void ransac_bound_mfma_kernel(const RansacStat
         const unsigned i0 = in0 + __shfl_xor(in0, 32), i1 = in1 + __shfl_xor(in1, 32);
         lo = (int)(lowh ? i0 : i1);  // zero-padded rows (ex = ey = W = 0) give m - R_lo = E_lo > 0: never "in"
     }
-    if (act) bounds[o] = invalid ? make_int2(-1, -1) : (uncertain ? make_int2(0, n) : make_int2(lo, n - outs));
+    // chunk 2 counted the points that may be in, the zero-padded rows of the last tile among them (L1 = L2
+    // = ey = 0 there: q = -ED < 0); chunk 1 the points surely out
+    const int hi = kLo ? n - outs : (wave_counts ? outs - (32 * nt - n) : n);
+    if (act) bounds[o] = invalid ? make_int2(-1, -1) : (uncertain ? make_int2(0, n) : make_int2(lo, hi));
 }
 
 // exact count of one hypothesis (runKernel + computeError + findInliers, bit-exact)

@@ -73,8 +73,42 @@ __device__ __forceinline__ LinCoef lin_coef(int d, int ssize, double scale, bool
     return LinCoef{s, 1.f - f, f};
 }
 
-__global__ void up2_kernel(const uint8_t* __restrict__ src, int rows, int cols, float* __restrict__ dst) {
-    const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
+// Batched launches: every stage of a SIFT call runs ONE launch for all its images (the five scene
+// scales of TestsDetector.cpp:99-106, or one model view).  Image j of a flattened launch owns blocks
+// off[j] .. off[j + 1] - 1, laid out as rows of gx[j] blocks; per-image operands are kernel-argument
+// arrays indexed by the block-uniform j (scalar loads from the kernarg segment).
+constexpr int kMaxImg = 8;
+struct Flat {
+    int n;
+    int off[kMaxImg + 1];
+    int gx[kMaxImg];
+};
+
+__device__ __forceinline__ int flat_job(const Flat& f, int b, int& bx, int& by) {
+    int j = 0;
+#pragma unroll
+    for (int k = 1; k < kMaxImg; ++k) j += (k < f.n && b >= f.off[k]);
+    j = __builtin_amdgcn_readfirstlane(j);
+    const int lb = b - f.off[j];
+    by = lb / f.gx[j];
+    bx = lb - by * f.gx[j];
+    return j;
+}
+
+struct Up2B {
+    Flat f;
+    const uint8_t* src[kMaxImg];
+    int rows[kMaxImg], cols[kMaxImg];
+    float* dst[kMaxImg];
+};
+
+__global__ void up2_kernel(Up2B A) {
+    int bx, y;
+    const int j = flat_job(A.f, blockIdx.x, bx, y);
+    const uint8_t* __restrict__ src = A.src[j];
+    float* __restrict__ dst = A.dst[j];
+    const int rows = A.rows[j], cols = A.cols[j];
+    const int x = bx * blockDim.x + threadIdx.x;
     const int dr = rows * 2, dc = cols * 2;
     if (x >= dc) return;
     const LinCoef cx = lin_coef(x, cols, (double)cols / dc, true), cy = lin_coef(y, rows, (double)rows / dr, false);
@@ -91,9 +125,23 @@ __global__ void up2_kernel(const uint8_t* __restrict__ src, int rows, int cols, 
 
 // resize(INTER_LINEAR) of CV_8UC1: fixed-point weights (x 2048); the vertical pass as OpenCV's
 // 128-bit vector path for columns < (dcols / 16) * 16, the exact rounding shift for the rest
-__global__ void resize_u8_kernel(const uint8_t* __restrict__ src, int rows, int cols, uint8_t* __restrict__ dst,
-                                 int drows, int dcols, double sx, double sy) {
-    const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
+struct ResizeB {
+    Flat f;
+    const uint8_t* src;
+    int rows, cols;
+    uint8_t* dst[kMaxImg];
+    int drows[kMaxImg], dcols[kMaxImg];
+    double sx[kMaxImg], sy[kMaxImg];
+};
+
+__global__ void resize_u8_kernel(ResizeB A) {
+    int bx, y;
+    const int j = flat_job(A.f, blockIdx.x, bx, y);
+    const uint8_t* __restrict__ src = A.src;
+    uint8_t* __restrict__ dst = A.dst[j];
+    const int rows = A.rows, cols = A.cols, dcols = A.dcols[j];
+    const double sx = A.sx[j], sy = A.sy[j];
+    const int x = bx * blockDim.x + threadIdx.x;
     if (x >= dcols) return;
     const LinCoef cx = lin_coef(x, cols, sx, true), cy = lin_coef(y, rows, sy, false);
     const int a0 = cv_round(cx.a0 * 2048.f), a1 = cv_round(cx.a1 * 2048.f);
@@ -128,14 +176,25 @@ struct Taps {
 // filter engine (row: k0 s0 + k1 s1 + ...; column, symmetric kernel: k_a m + sum of k_{a+i} (m_+i + m_-i)).
 constexpr int kBlurTW = 64, kBlurTH = 16;
 
-__global__ __launch_bounds__(256) void blur_kernel(const float* __restrict__ src, float* __restrict__ dst, int rows,
-                                                   int cols, Taps t) {
+struct BlurB {
+    Flat f;
+    const float* src[kMaxImg];
+    float* dst[kMaxImg];
+    int rows[kMaxImg], cols[kMaxImg];
+};
+
+__global__ __launch_bounds__(256) void blur_kernel(BlurB A, Taps t) {
     extern __shared__ float lds[];
     __shared__ float tk[64];     // the taps, read per tap from LDS rather than the kernel arguments
+    int bx, by;
+    const int j = flat_job(A.f, blockIdx.x, bx, by);
+    const float* __restrict__ src = A.src[j];
+    float* __restrict__ dst = A.dst[j];
+    const int rows = A.rows[j], cols = A.cols[j];
     const int a = t.n / 2, W = kBlurTW + 2 * a, H = kBlurTH + 2 * a;
     float* in = lds;             // H x W
     float* mid = lds + H * W;    // H x kBlurTW
-    const int x0 = blockIdx.x * kBlurTW, y0 = blockIdx.y * kBlurTH, tid = threadIdx.x;
+    const int x0 = bx * kBlurTW, y0 = by * kBlurTH, tid = threadIdx.x;
     if (tid < 64) tk[tid] = t.k[tid];
     // 8 loads in flight per thread: a launch is one or two rounds of this loop on the small octaves,
     // where one dependent global load per iteration made every blur ~11 us whatever its size
@@ -182,14 +241,28 @@ __global__ __launch_bounds__(256) void blur_kernel(const float* __restrict__ src
 #define MIM_SMALL_PLANE 512  // measured: 8192 1.81 ms per 640x480 image, 2048 1.54, 512 1.49-1.52 (profiles/r03s_sift_small_plane.txt)
 #endif
 constexpr int kSmallPlane = MIM_SMALL_PLANE;  // largest octave plane (pixels) fused
-struct SmallOct {
-    int o0, n_oct;            // octaves o0 .. n_oct - 1 (o0 >= 1)
-    int rows[16], cols[16];
-    long long goff[16], doff[16];
-    Taps t[kNOL + 2];          // blur taps of layers 1 .. kNOL + 2
+struct Layer {
+    const float* p;
+    int rows, cols;
 };
 
-__global__ __launch_bounds__(1024) void small_octaves_kernel(float* __restrict__ P, SmallOct so) {
+struct Pyr {
+    Layer gauss[16][kNOL + 3];
+    Layer dog[16][kNOL + 2];
+};
+
+// one block per image: octaves o0[j] .. n_oct[j] - 1 (o0 >= 1), geometry and planes from its Pyr table
+struct SmallB {
+    int n;
+    const Pyr* pyr[kMaxImg];
+    int o0[kMaxImg], n_oct[kMaxImg];
+    Taps t[kNOL + 2];          // blur taps of layers 1 .. kNOL + 2 (the same for every image)
+};
+
+__global__ __launch_bounds__(1024) void small_octaves_kernel(SmallB so) {
+    const int jb = blockIdx.x;
+    const Pyr* __restrict__ py = so.pyr[jb];
+    const int o_begin = so.o0[jb], o_end = so.n_oct[jb];
     __shared__ float sm[4 * kSmallPlane];  // 128 KiB
     __shared__ float taps[kNOL + 2][64];   // the kernel-argument taps, read per tap from LDS
     float* bufA = sm;                     // current layer
@@ -198,14 +271,14 @@ __global__ __launch_bounds__(1024) void small_octaves_kernel(float* __restrict__
     float* nxt = sm + 3 * kSmallPlane;    // layer kNOL down-sampled: the next octave's layer 0
     const int tid = threadIdx.x;
     if (tid < (kNOL + 2) * 64) taps[tid >> 6][tid & 63] = so.t[tid >> 6].k[tid & 63];
-    for (int o = so.o0; o < so.n_oct; ++o) {
-        const int rows = so.rows[o], cols = so.cols[o], plane = rows * cols;
-        float* G = P + so.goff[o];
-        float* D = P + so.doff[o];
+    for (int o = o_begin; o < o_end; ++o) {
+        const int rows = py->gauss[o][0].rows, cols = py->gauss[o][0].cols, plane = rows * cols;
+        float* G = const_cast<float*>(py->gauss[o][0].p);  // layers i at G + i * plane
+        float* D = const_cast<float*>(py->dog[o][0].p);
         // layer 0 = every second pixel of the previous octave's layer kNOL (down2_kernel)
-        if (o == so.o0) {
-            const int pc = so.cols[o - 1];
-            const float* src = P + so.goff[o - 1] + (long long)kNOL * so.rows[o - 1] * pc;
+        if (o == o_begin) {
+            const int pc = py->gauss[o - 1][0].cols;
+            const float* src = py->gauss[o - 1][kNOL].p;
             for (int e = tid; e < plane; e += 1024) {
                 const int y = e / cols, x = e - y * cols;
                 bufA[e] = src[(long long)(2 * y) * pc + 2 * x];
@@ -236,8 +309,8 @@ __global__ __launch_bounds__(1024) void small_octaves_kernel(float* __restrict__
                 D[(long long)(i - 1) * plane + e] = acc - bufA[e];
             }
             __syncthreads();
-            if (i == kNOL && o + 1 < so.n_oct) {
-                const int nc = so.cols[o + 1], np = so.rows[o + 1] * nc;
+            if (i == kNOL && o + 1 < o_end) {
+                const int nc = py->gauss[o + 1][0].cols, np = py->gauss[o + 1][0].rows * nc;
                 for (int e = tid; e < np; e += 1024) {
                     const int y = e / nc, x = e - y * nc;
                     nxt[e] = bufB[(2 * y) * cols + 2 * x];
@@ -251,28 +324,63 @@ __global__ __launch_bounds__(1024) void small_octaves_kernel(float* __restrict__
     }
 }
 
-__global__ void down2_kernel(const float* __restrict__ src, int scols, float* __restrict__ dst, int rows, int cols) {
-    const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
+struct DownB {
+    Flat f;
+    const float* src[kMaxImg];
+    int scols[kMaxImg];
+    float* dst[kMaxImg];
+    int cols[kMaxImg];
+};
+
+__global__ void down2_kernel(DownB A) {
+    int bx, y;
+    const int j = flat_job(A.f, blockIdx.x, bx, y);
+    const int x = bx * blockDim.x + threadIdx.x, cols = A.cols[j];
     if (x >= cols) return;
-    dst[(size_t)y * cols + x] = src[(size_t)(2 * y) * scols + 2 * x];
+    A.dst[j][(size_t)y * cols + x] = A.src[j][(size_t)(2 * y) * A.scols[j] + 2 * x];
 }
 
-// the 5 DoG layers of one octave: dog[i] = gauss[i + 1] - gauss[i]
-__global__ void dog_kernel(const float* __restrict__ gauss, float* __restrict__ dog, size_t plane) {
-    const size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+// the 5 DoG layers of one octave (blockIdx.y = layer): dog[i] = gauss[i + 1] - gauss[i]
+struct DogB {
+    Flat f;
+    const float* g[kMaxImg];
+    float* d[kMaxImg];
+    long long plane[kMaxImg];
+};
+
+__global__ void dog_kernel(DogB A) {
+    int bx, by;
+    const int j = flat_job(A.f, blockIdx.x, bx, by);
+    const size_t plane = (size_t)A.plane[j];
+    const size_t p = (size_t)bx * blockDim.x + threadIdx.x;
     const int i = blockIdx.y;
     if (p >= plane) return;
-    dog[i * plane + p] = gauss[(i + 1) * plane + p] - gauss[i * plane + p];
+    A.d[j][i * plane + p] = A.g[j][(i + 1) * plane + p] - A.g[j][i * plane + p];
 }
 
 struct Cand {
     int o, layer, r, c;
 };
 
-// findScaleSpaceExtrema's pixel test over layers 1..3 of one octave (blockIdx.z = layer - 1)
-__global__ void extrema_kernel(const float* __restrict__ dog, int rows, int cols, int octave, int threshold,
-                               Cand* __restrict__ cand, int* __restrict__ n_cand, int cap) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x + kBorder, r = blockIdx.y + kBorder, layer = blockIdx.z + 1;
+// findScaleSpaceExtrema's pixel test over layers 1..3 of one octave (blockIdx.z = layer - 1), every image
+// of the batch with that octave
+struct ExtB {
+    Flat f;
+    const float* dog[kMaxImg];
+    int rows[kMaxImg], cols[kMaxImg];
+    Cand* cand[kMaxImg];
+    int* n_cand[kMaxImg];
+    int octave, threshold, cap;
+};
+
+__global__ void extrema_kernel(ExtB A) {
+    int bx, by;
+    const int j = flat_job(A.f, blockIdx.x, bx, by);
+    const float* __restrict__ dog = A.dog[j];
+    const int rows = A.rows[j], cols = A.cols[j], octave = A.octave, threshold = A.threshold, cap = A.cap;
+    Cand* __restrict__ cand = A.cand[j];
+    int* __restrict__ n_cand = A.n_cand[j];
+    const int c = bx * blockDim.x + threadIdx.x + kBorder, r = by + kBorder, layer = blockIdx.z + 1;
     if (c >= cols - kBorder || r >= rows - kBorder) return;
     const size_t plane = (size_t)rows * cols;
     const float* cur = dog + layer * plane;
@@ -298,16 +406,6 @@ __global__ void extrema_kernel(const float* __restrict__ dog, int rows, int cols
     const int k = atomicAdd(n_cand, 1);
     if (k < cap) cand[k] = Cand{octave, layer, r, c};
 }
-
-struct Layer {
-    const float* p;
-    int rows, cols;
-};
-
-struct Pyr {
-    Layer gauss[16][kNOL + 3];
-    Layer dog[16][kNOL + 2];
-};
 
 #define AT(L, r, c) ((L).p[(size_t)(r) * (L).cols + (c)])
 
@@ -349,9 +447,23 @@ struct Surv {  // an extremum that passed adjustLocalExtrema: its keypoint (angl
 
 // adjustLocalExtrema (<= 5 Newton steps, contrast and edge tests), one thread per candidate; the
 // survivors go to orient_kernel (octave field packed as OpenCV's)
-__global__ void refine_kernel(const Pyr* __restrict__ pyr, const Cand* __restrict__ cand, const int* __restrict__ n_cand,
-                              int cap, Surv* __restrict__ surv, int* __restrict__ n_surv, int surv_cap) {
-  const int n_c = min(*n_cand, cap);
+struct RefB {
+    const Pyr* pyr[kMaxImg];
+    const Cand* cand[kMaxImg];
+    const int* n_cand[kMaxImg];
+    Surv* surv[kMaxImg];
+    int* n_surv[kMaxImg];
+    int cap, surv_cap;
+};
+
+__global__ void refine_kernel(RefB A) {  // blockIdx.y = image
+  const int j = blockIdx.y;
+  const Pyr* __restrict__ pyr = A.pyr[j];
+  const Cand* __restrict__ cand = A.cand[j];
+  Surv* __restrict__ surv = A.surv[j];
+  int* __restrict__ n_surv = A.n_surv[j];
+  const int surv_cap = A.surv_cap;
+  const int n_c = min(*A.n_cand[j], A.cap);
   for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < n_c; t += gridDim.x * blockDim.x) {  // fixed grid
     const float kSigma = 1.6f, kContrast = 0.04f, kEdge = 10.f;
     const float img_scale = 1.f / 255, deriv_scale = img_scale * 0.5f, second_deriv_scale = img_scale;
@@ -425,14 +537,26 @@ __global__ void refine_kernel(const Pyr* __restrict__ pyr, const Cand* __restric
 // 36 bins accumulate in the reference's pixel order: per batch of 64 patch pixels each lane computes
 // one pixel's (bin, weight * magnitude), then the lanes walk the batch in order and lane b adds the
 // values of bin b (one bin per pixel: no reordering).  Keypoints in the doubled image's coordinates.
-__global__ __launch_bounds__(64) void orient_kernel(const Pyr* __restrict__ pyr, const Surv* __restrict__ surv,
-                                                    const int* __restrict__ n_surv, int surv_cap,
-                                                    mim_keypoint* __restrict__ kp, int* __restrict__ n_kp, int kp_cap) {
+struct OriB {
+    const Pyr* pyr[kMaxImg];
+    const Surv* surv[kMaxImg];
+    const int* n_surv[kMaxImg];
+    mim_keypoint* kp[kMaxImg];
+    int* n_kp[kMaxImg];
+    int surv_cap, kp_cap;
+};
+
+__global__ __launch_bounds__(64) void orient_kernel(OriB A) {  // blockIdx.y = image
     __shared__ int rb[64];
     __shared__ float rv[64];
     __shared__ float th[kOriBins + 4];
-    const int lane = threadIdx.x;
-  const int n_s = min(*n_surv, surv_cap);
+    const int lane = threadIdx.x, j = blockIdx.y;
+    const Pyr* __restrict__ pyr = A.pyr[j];
+    const Surv* __restrict__ surv = A.surv[j];
+    mim_keypoint* __restrict__ kp = A.kp[j];
+    int* __restrict__ n_kp = A.n_kp[j];
+    const int kp_cap = A.kp_cap;
+  const int n_s = min(*A.n_surv[j], A.surv_cap);
   for (int t = blockIdx.x; t < n_s; t += gridDim.x) {  // fixed grid, block-uniform loop
     const Surv sv = surv[t];
     mim_keypoint k = sv.k;
@@ -527,8 +651,18 @@ __device__ __forceinline__ int ctz64(unsigned long long m) { return __builtin_ct
 // dependent chain of two LDS reads.)
 constexpr int kDescrT = 256, kDescrWords = kDescrT / 64;
 static_assert(kHistLen <= 2 * kDescrT, "two bins per thread");
-__global__ __launch_bounds__(kDescrT) void descr_kernel(const Pyr* __restrict__ pyr, const mim_keypoint* __restrict__ kp,
-                                                        const int* __restrict__ n_dev, int n_cap, float* __restrict__ desc) {
+struct DescB {
+    const Pyr* pyr[kMaxImg];
+    const mim_keypoint* kp[kMaxImg];
+    const int* n[kMaxImg];
+    int n_cap[kMaxImg];
+    float* desc[kMaxImg];
+};
+
+__global__ __launch_bounds__(kDescrT) void descr_kernel(DescB A) {  // blockIdx.y = image
+    const Pyr* __restrict__ pyr = A.pyr[blockIdx.y];
+    const mim_keypoint* __restrict__ kp = A.kp[blockIdx.y];
+    float* __restrict__ desc = A.desc[blockIdx.y];
     __shared__ float hist[kHistLen];
     __shared__ unsigned long long bm[kHistLen][kDescrWords];  // per bin: the batch's pixels that hit it
     __shared__ unsigned short pre[kHistLen][kDescrWords];      // per bin and word: pixels in earlier words
@@ -538,7 +672,7 @@ __global__ __launch_bounds__(kDescrT) void descr_kernel(const Pyr* __restrict__ 
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     for (int e = tid; e < kHistLen * kDescrWords; e += kDescrT) (&bm[0][0])[e] = 0ull;
     __syncthreads();
-  const int n = min(*n_dev, n_cap);
+  const int n = min(*A.n[blockIdx.y], A.n_cap[blockIdx.y]);
   for (int t = blockIdx.x; t < n; t += gridDim.x) {  // fixed grid, block-uniform loop
     const mim_keypoint p = kp[t];
     int octave = p.octave & 255;
@@ -730,10 +864,24 @@ __device__ __forceinline__ bool kp_greater_d(const mim_keypoint& a, const mim_ke
     return a.octave > b.octave;
 }
 
-__global__ __launch_bounds__(1024) void kp_post_kernel(const mim_keypoint* __restrict__ kp, const int* __restrict__ n_kp,
-                                                      int kp_cap, int sort_cap, const uint8_t* __restrict__ mask,
-                                                      long long mstep, mim_keypoint* __restrict__ out,
-                                                      int* __restrict__ n_out) {
+struct KpB {
+    const mim_keypoint* kp[kMaxImg];
+    const int* n_kp[kMaxImg];
+    const uint8_t* mask[kMaxImg];
+    long long mstep[kMaxImg];
+    mim_keypoint* out[kMaxImg];
+    int* n_out[kMaxImg];
+    int kp_cap, sort_cap;
+};
+
+__global__ __launch_bounds__(1024) void kp_post_kernel(KpB A) {  // blockIdx.y = image
+    const mim_keypoint* __restrict__ kp = A.kp[blockIdx.y];
+    const int* __restrict__ n_kp = A.n_kp[blockIdx.y];
+    const uint8_t* __restrict__ mask = A.mask[blockIdx.y];
+    const long long mstep = A.mstep[blockIdx.y];
+    mim_keypoint* __restrict__ out = A.out[blockIdx.y];
+    int* __restrict__ n_out = A.n_out[blockIdx.y];
+    const int kp_cap = A.kp_cap, sort_cap = A.sort_cap;
     __shared__ int idx[kSortCap];
     __shared__ unsigned long long skey[kKeySortCap];
     __shared__ int wsum[16];
@@ -876,8 +1024,9 @@ struct SiftWs {
     void* tmp = nullptr;   size_t tmp_cap = 0;
     void* aux = nullptr;   size_t aux_cap = 0;  // candidates, keypoints, counters, Pyr table
     void* desc = nullptr;  size_t desc_cap = 0;
-    hipStream_t s = nullptr;  // MIM_SIFT_SCALE_STREAMS=1: the multi-scale call's stream of this scale
-    hipEvent_t ev = nullptr;
+    void* batch = nullptr; size_t batch_cap = 0;  // a call's Pyr tables and counters (batch owner only)
+    Pyr* h_pyr = nullptr;  // pinned staging of the Pyr tables
+    int* h_cnt = nullptr;  // pinned copy of the counters
 };
 
 static hipError_t grow(void*& p, size_t& cap, size_t need) {
@@ -898,11 +1047,10 @@ SiftWs* sift_ws_create() { return new SiftWs(); }
 
 void sift_ws_destroy(SiftWs* w) {
     if (!w) return;
-    if (w->s) (void)hipStreamSynchronize(w->s);
-    for (void* p : {w->img, w->pyr, w->tmp, w->aux, w->desc})
+    for (void* p : {w->img, w->pyr, w->tmp, w->aux, w->desc, w->batch})
         if (p) (void)hipFree(p);
-    if (w->ev) (void)hipEventDestroy(w->ev);
-    if (w->s) (void)hipStreamDestroy(w->s);
+    if (w->h_pyr) (void)hipHostFree(w->h_pyr);
+    if (w->h_cnt) (void)hipHostFree(w->h_cnt);
     delete w;
 }
 
@@ -914,21 +1062,6 @@ void sift_ws_destroy(SiftWs* w) {
             return -1;                                       \
         }                                                    \
     } while (0)
-
-int sift_resize_u8(SiftWs* w, hipStream_t st, const uint8_t* src, int rows, int cols, long long step, uint8_t* dst,
-                   int drows, int dcols, double fx, double fy, std::string& err) {
-    const size_t sb = (size_t)rows * cols, db = (size_t)drows * dcols;
-    SCHK(grow(w->img, w->img_cap, sb + db));
-    uint8_t* ds = (uint8_t*)w->img;
-    uint8_t* dd = ds + sb;
-    SCHK(hipMemcpy2DAsync(ds, cols, src, step, cols, rows, hipMemcpyHostToDevice, st));
-    resize_u8_kernel<<<dim3((dcols + 255) / 256, drows), 256, 0, st>>>(ds, rows, cols, dd, drows, dcols, 1. / (fx > 0 ? fx : (double)dcols / cols),
-                                                                     1. / (fy > 0 ? fy : (double)drows / rows));
-    SCHK(hipGetLastError());
-    SCHK(hipMemcpyAsync(dst, dd, db, hipMemcpyDeviceToHost, st));
-    SCHK(hipStreamSynchronize(st));
-    return 0;
-}
 
 // One image of a SIFT call: its workspace (the 8-bit image already in w->img, rows x cols packed),
 // its mask (host, optional), where its keypoints / descriptors go and their capacity.
@@ -942,16 +1075,21 @@ struct SiftJob {
     float* desc;
     int n = 0;  // keypoints found (may exceed cap: then only cap are written)
     // internal
-    int n_oct = 0;
+    int n_oct = 0, o_small = 0;
+    int orows[16], ocols[16];
+    size_t goff[16], doff[16];
+    float* P = nullptr;   // pyramid: per octave kNOL + 3 Gaussian planes, then kNOL + 2 DoG planes
+    float* T0 = nullptr;  // the doubled image
     Pyr h_pyr{};
-    int* d_cnt = nullptr;
+    Pyr* d_pyr = nullptr;  // in the call's batch buffer
+    int* d_cnt = nullptr;  // [0] candidates, [1] keypoints, [2] survivors, [3] final keypoints (batch buffer)
+    int h_cnt[4] = {0, 0, 0, 0};
     Cand* d_cand = nullptr;
     mim_keypoint* d_kp = nullptr;
     Surv* d_surv = nullptr;
-    Pyr* d_pyr = nullptr;
     mim_keypoint* d_kp2 = nullptr;  // the post-processed keypoints (kp_post_kernel)
     uint8_t* d_mask = nullptr;
-    int h_cnt[4] = {0, 0, 0, 0};  // candidates, keypoints, survivors, final keypoints
+    const mim_keypoint* out_kp = nullptr;  // the final keypoints on the device (d_kp2, or d_kp after the host path)
     std::vector<mim_keypoint> k;
 };
 
@@ -974,144 +1112,75 @@ static int sort_limit() {
     return v;
 }
 
-// Gaussian pyramid, DoG and the scale-space extrema of one image (enqueued; the candidate count is
-// copied to J.h_cnt[0])
-static int sift_build(SiftJob& J, hipStream_t st, std::string& err) {
+// Flattened grid of one batched launch: image j gets gx[j] x gy[j] blocks
+template <class F>
+static int flatten(Flat& f, const std::vector<int>& imgs, F&& dims) {
+    f.n = (int)imgs.size();
+    int tot = 0;
+    for (int k = 0; k < f.n; ++k) {
+        int gx = 0, gy = 0;
+        dims(imgs[k], gx, gy);
+        f.off[k] = tot;
+        f.gx[k] = std::max(gx, 1);
+        tot += std::max(gx, 1) * std::max(gy, 0);
+    }
+    for (int k = f.n; k <= kMaxImg; ++k) f.off[k] = tot;
+    return tot;
+}
+
+// Octave geometry, workspace buffers and the Pyr table of one image (host only)
+static int sift_geometry(SiftJob& J, std::string& err) {
     SiftWs* w = J.w;
     const int R = J.rows * 2, C = J.cols * 2;
     J.n_oct = (int)lrint(log((double)std::min(R, C)) / log(2.) - 2) + 1;
-    if (J.n_oct < 1) return 0;  // no octave (sides < 2 px after doubling): no keypoints, as OpenCV
+    if (J.n_oct < 1) {  // no octave (sides < 2 px after doubling): no keypoints, as OpenCV
+        J.n_oct = 0;
+        return 0;
+    }
     if (J.n_oct > 16) {
         err = "image too large for SIFT (more than 16 octaves)";
         return -4;
     }
-    const int n_oct = J.n_oct;
-    // pyramid layout: per octave 6 Gaussian + 5 DoG planes
-    std::vector<int> orows(n_oct), ocols(n_oct);
-    std::vector<size_t> goff(n_oct), doff(n_oct);
     size_t total = 0;
-    for (int o = 0; o < n_oct; ++o) {
-        orows[o] = o == 0 ? R : orows[o - 1] / 2;
-        ocols[o] = o == 0 ? C : ocols[o - 1] / 2;
-        const size_t plane = (size_t)orows[o] * ocols[o];
-        goff[o] = total;
+    for (int o = 0; o < J.n_oct; ++o) {
+        J.orows[o] = o == 0 ? R : J.orows[o - 1] / 2;
+        J.ocols[o] = o == 0 ? C : J.ocols[o - 1] / 2;
+        const size_t plane = (size_t)J.orows[o] * J.ocols[o];
+        J.goff[o] = total;
         total += plane * (kNOL + 3);
-        doff[o] = total;
+        J.doff[o] = total;
         total += plane * (kNOL + 2);
     }
+    // the small octaves (all after the first whose plane fits kSmallPlane) run in one block
+    J.o_small = J.n_oct;
+    for (int o = 1; o < J.n_oct; ++o)
+        if ((size_t)J.orows[o] * J.ocols[o] <= (size_t)kSmallPlane) { J.o_small = o; break; }
     SCHK(grow(w->pyr, w->pyr_cap, total * sizeof(float)));
     SCHK(grow(w->tmp, w->tmp_cap, (size_t)R * C * sizeof(float)));
-    float* P = (float*)w->pyr;
-    float* T0 = (float*)w->tmp;
-
-    auto blur = [&](const float* s, float* d, int rr, int cc, double sigma) -> bool {
-        Taps t;
-        if (gauss_taps(sigma, t) < 0) return false;
-        const int a = t.n / 2;
-        const size_t lds = sizeof(float) * (size_t)(kBlurTH + 2 * a) * (kBlurTW + 2 * a + kBlurTW);
-        if (lds > 64 * 1024) return false;
-        blur_kernel<<<dim3((cc + kBlurTW - 1) / kBlurTW, (rr + kBlurTH - 1) / kBlurTH), 256, lds, st>>>(s, d, rr, cc, t);
-        return true;
-    };
-    // createInitialImage
-    up2_kernel<<<dim3((C + 255) / 256, R), 256, 0, st>>>((const uint8_t*)w->img, J.rows, J.cols, T0);
-    const float sig_diff = sqrtf(std::max(1.6f * 1.6f - 0.5f * 0.5f * 4, 0.01f));
-    if (!blur(T0, P + goff[0], R, C, sig_diff)) { err = "kernel size"; return -4; }
-    // buildGaussianPyramid + DoG
-    double sig[kNOL + 3];
-    sig[0] = 1.6;
-    const double kk = pow(2., 1. / kNOL);
-    for (int i = 1; i < kNOL + 3; i++) {
-        const double sp = pow(kk, (double)(i - 1)) * 1.6, stt = sp * kk;
-        sig[i] = sqrt(stt * stt - sp * sp);
+    J.P = (float*)w->pyr;
+    J.T0 = (float*)w->tmp;
+    for (int o = 0; o < J.n_oct; ++o) {
+        const size_t plane = (size_t)J.orows[o] * J.ocols[o];
+        for (int i = 0; i < kNOL + 3; ++i) J.h_pyr.gauss[o][i] = Layer{J.P + J.goff[o] + i * plane, J.orows[o], J.ocols[o]};
+        for (int i = 0; i < kNOL + 2; ++i) J.h_pyr.dog[o][i] = Layer{J.P + J.doff[o] + i * plane, J.orows[o], J.ocols[o]};
     }
-    // the small octaves (all after the first whose plane fits kSmallPlane) in one launch
-    int o_small = n_oct;
-    for (int o = 1; o < n_oct; ++o)
-        if ((size_t)orows[o] * ocols[o] <= (size_t)kSmallPlane) { o_small = o; break; }
-    for (int o = 0; o < o_small; ++o) {
-        const size_t plane = (size_t)orows[o] * ocols[o];
-        float* G = P + goff[o];
-        if (o > 0)
-            down2_kernel<<<dim3((ocols[o] + 255) / 256, orows[o]), 256, 0, st>>>(P + goff[o - 1] + kNOL * (size_t)orows[o - 1] * ocols[o - 1],
-                                                                                ocols[o - 1], G, orows[o], ocols[o]);
-        for (int i = 1; i < kNOL + 3; ++i)
-            if (!blur(G + (i - 1) * plane, G + i * plane, orows[o], ocols[o], sig[i])) { err = "kernel size"; return -4; }
-        dog_kernel<<<dim3((unsigned)((plane + 255) / 256), kNOL + 2), 256, 0, st>>>(G, P + doff[o], plane);
-    }
-    if (o_small < n_oct) {
-        SmallOct so{};
-        so.o0 = o_small;
-        so.n_oct = n_oct;
-        for (int o = 0; o < n_oct; ++o) {
-            so.rows[o] = orows[o];
-            so.cols[o] = ocols[o];
-            so.goff[o] = (long long)goff[o];
-            so.doff[o] = (long long)doff[o];
-        }
-        for (int i = 1; i < kNOL + 3; ++i)
-            if (gauss_taps(sig[i], so.t[i - 1]) < 0) { err = "kernel size"; return -4; }
-        small_octaves_kernel<<<1, 1024, 0, st>>>(P, so);
-    }
-    SCHK(hipGetLastError());
-    // layer table
-    Pyr& h_pyr = J.h_pyr;
-    for (int o = 0; o < n_oct; ++o) {
-        const size_t plane = (size_t)orows[o] * ocols[o];
-        for (int i = 0; i < kNOL + 3; ++i) h_pyr.gauss[o][i] = Layer{P + goff[o] + i * plane, orows[o], ocols[o]};
-        for (int i = 0; i < kNOL + 2; ++i) h_pyr.dog[o][i] = Layer{P + doff[o] + i * plane, orows[o], ocols[o]};
-    }
-    const int cand_cap = kCandCap, kp_cap = kKpCap;
     const size_t mask_bytes = J.mask ? ((size_t)J.rows * J.cols + 255) / 256 * 256 : 0;
-    const size_t aux_bytes = sizeof(Pyr) + 256 + sizeof(Cand) * cand_cap + sizeof(mim_keypoint) * kp_cap +
-                             sizeof(Surv) * cand_cap + sizeof(mim_keypoint) * kSortCap + mask_bytes;
+    const size_t aux_bytes = sizeof(Cand) * kCandCap + sizeof(mim_keypoint) * kKpCap + sizeof(Surv) * kCandCap +
+                             sizeof(mim_keypoint) * kSortCap + mask_bytes;
     SCHK(grow(w->aux, w->aux_cap, aux_bytes));
     char* A = (char*)w->aux;
-    Pyr* d_pyr = (Pyr*)A;
-    int* d_cnt = (int*)(A + sizeof(Pyr));  // [0] candidates, [1] keypoints, [2] survivors of adjustLocalExtrema
-    Cand* d_cand = (Cand*)(A + sizeof(Pyr) + 256);
-    mim_keypoint* d_kp = (mim_keypoint*)(d_cand + cand_cap);
-    Surv* d_surv = (Surv*)(d_kp + kp_cap);
-    J.d_pyr = d_pyr;
-    J.d_cnt = d_cnt;
-    J.d_cand = d_cand;
-    J.d_kp = d_kp;
-    J.d_surv = d_surv;
-    J.d_kp2 = (mim_keypoint*)(d_surv + cand_cap);
-    J.d_mask = nullptr;
-    if (J.mask) {  // runByPixelsMask on the device: the mask packed rows x cols
-        J.d_mask = (uint8_t*)(J.d_kp2 + kSortCap);
-        SCHK(hipMemcpy2DAsync(J.d_mask, J.cols, J.mask, J.mstep, J.cols, J.rows, hipMemcpyHostToDevice, st));
-    }
-    SCHK(hipMemcpyAsync(d_pyr, &h_pyr, sizeof(Pyr), hipMemcpyHostToDevice, st));
-    SCHK(hipMemsetAsync(d_cnt, 0, 4 * sizeof(int), st));
-    const int threshold = (int)floor(0.5 * 0.04 / kNOL * 255);
-    for (int o = 0; o < n_oct; ++o) {
-        if (orows[o] <= 2 * kBorder || ocols[o] <= 2 * kBorder) continue;
-        extrema_kernel<<<dim3((ocols[o] - 2 * kBorder + 127) / 128, orows[o] - 2 * kBorder, kNOL), 128, 0, st>>>(
-            P + doff[o], orows[o], ocols[o], o, threshold, d_cand, d_cnt, cand_limit());
-    }
-    return 0;
-}
-
-// adjustLocalExtrema + orientations of the candidates, the keypoint post-processing and the
-// descriptors, all enqueued with device-side counts (fixed grids, grid-stride kernels); the final
-// keypoint count goes to J.h_cnt[3] (negative: more than kSortCap, the host finishes)
-static int sift_enqueue_rest(SiftJob& J, hipStream_t st, std::string& err) {
-    if (J.n_oct < 1) return 0;
-    refine_kernel<<<1024, 128, 0, st>>>(J.d_pyr, J.d_cand, J.d_cnt, cand_limit(), J.d_surv, J.d_cnt + 2, kCandCap);
-    orient_kernel<<<4096, 64, 0, st>>>(J.d_pyr, J.d_surv, J.d_cnt + 2, kCandCap, J.d_kp, J.d_cnt + 1, kKpCap);
-    kp_post_kernel<<<1, 1024, 0, st>>>(J.d_kp, J.d_cnt + 1, kKpCap, sort_limit(), J.d_mask, J.cols, J.d_kp2,
-                                       J.d_cnt + 3);
-    SCHK(grow(J.w->desc, J.w->desc_cap, sizeof(float) * 128 * (size_t)kSortCap));
-    descr_kernel<<<4096, kDescrT, 0, st>>>(J.d_pyr, J.d_kp2, J.d_cnt + 3, kSortCap, (float*)J.w->desc);
-    SCHK(hipGetLastError());
-    SCHK(hipMemcpyAsync(J.h_cnt, J.d_cnt, 4 * sizeof(int), hipMemcpyDeviceToHost, st));
+    J.d_cand = (Cand*)A;
+    J.d_kp = (mim_keypoint*)(J.d_cand + kCandCap);
+    J.d_surv = (Surv*)(J.d_kp + kKpCap);
+    J.d_kp2 = (mim_keypoint*)(J.d_surv + kCandCap);
+    J.d_mask = J.mask ? (uint8_t*)(J.d_kp2 + kSortCap) : nullptr;
+    SCHK(grow(w->desc, w->desc_cap, sizeof(float) * 128 * (size_t)kSortCap));
     return 0;
 }
 
 // KeyPointsFilter::removeDuplicatedSorted, the octave -1 rescale, runByPixelsMask on the host, then the
-// descriptors: only for an image with more than kSortCap keypoints (kp_post_kernel's limit)
+// descriptors: only for an image with more than kSortCap keypoints (kp_post_kernel's limit).  The
+// first min(n, cap) keypoints end in J.d_kp (and J.k), their descriptors in w->desc.
 static int sift_describe_host(SiftJob& J, hipStream_t st, std::string& err) {
     if (J.h_cnt[1] > kKpCap) { err = "more than 2^19 SIFT keypoints"; return -4; }
     std::vector<mim_keypoint>& k = J.k;
@@ -1141,46 +1210,256 @@ static int sift_describe_host(SiftJob& J, hipStream_t st, std::string& err) {
         k.resize(m);
     }
     J.n = (int)k.size();
+    J.out_kp = J.d_kp;
     const int n = std::min(J.n, J.cap);
     if (n <= 0) return 0;
     SCHK(hipMemcpyAsync(J.d_kp, k.data(), sizeof(mim_keypoint) * n, hipMemcpyHostToDevice, st));
     SCHK(grow(J.w->desc, J.w->desc_cap, sizeof(float) * 128 * (size_t)n));
     SCHK(hipMemcpyAsync(J.d_cnt + 3, &n, sizeof(int), hipMemcpyHostToDevice, st));
-    descr_kernel<<<4096, kDescrT, 0, st>>>(J.d_pyr, J.d_kp, J.d_cnt + 3, n, (float*)J.w->desc);
+    DescB D{};
+    D.pyr[0] = J.d_pyr;
+    D.kp[0] = J.d_kp;
+    D.n[0] = J.d_cnt + 3;
+    D.n_cap[0] = n;
+    D.desc[0] = (float*)J.w->desc;
+    descr_kernel<<<dim3(4096, 1), kDescrT, 0, st>>>(D);
     SCHK(hipGetLastError());
-    SCHK(hipMemcpyAsync(J.desc, J.w->desc, sizeof(float) * 128 * (size_t)n, hipMemcpyDeviceToHost, st));
-    std::copy(k.begin(), k.begin() + n, J.kps);
     SCHK(hipStreamSynchronize(st));  // `n` and `k` are host locals of this call
     return 0;
 }
 
-// copies of the first J.cap keypoints / descriptors (enqueued)
-static int sift_fetch(SiftJob& J, hipStream_t st, std::string& err) {
-    if (J.n_oct < 1) return 0;
-    // extrema_kernel counts every candidate but stores only the first cand_limit(): more would
-    // silently drop keypoints OpenCV (no cap) keeps
-    if (J.h_cnt[0] > cand_limit()) {
-        err = "more than " + std::to_string(cand_limit()) + " SIFT candidates";
-        return -4;
+// Every stage of every image of `jobs` enqueued as one batched launch per stage, then ONE host
+// synchronisation for the counts.  `bw` holds the batch buffer (the Pyr tables and counters of the
+// images, one upload and one download).  Afterwards J.n / J.out_kp / J.w->desc hold each image's
+// final keypoints and descriptors on the device (the host path already ran for an image past
+// kp_post_kernel's limit).
+static int sift_batch(std::vector<SiftJob>& jobs, SiftWs* bw, hipStream_t st, std::string& err) {
+    const int nj = (int)jobs.size();
+    if (nj > kMaxImg) {
+        err = "sift: more than 8 images in one call";
+        return -3;
     }
-    if (J.h_cnt[3] < 0) return sift_describe_host(J, st, err);
-    J.n = J.h_cnt[3];
-    const int n = std::min(J.n, J.cap);
-    if (n <= 0) return 0;
-    SCHK(hipMemcpyAsync(J.kps, J.d_kp2, sizeof(mim_keypoint) * n, hipMemcpyDeviceToHost, st));
-    SCHK(hipMemcpyAsync(J.desc, J.w->desc, sizeof(float) * 128 * (size_t)n, hipMemcpyDeviceToHost, st));
+    for (auto& J : jobs)
+        if (int r = sift_geometry(J, err)) return r;
+    // taps (the same for every image): the initial blur, then layers 1 .. kNOL + 2
+    Taps t0;
+    const float sig_diff = sqrtf(std::max(1.6f * 1.6f - 0.5f * 0.5f * 4, 0.01f));
+    if (gauss_taps(sig_diff, t0) < 0) { err = "kernel size"; return -4; }
+    double sig[kNOL + 3];
+    sig[0] = 1.6;
+    const double kk = pow(2., 1. / kNOL);
+    for (int i = 1; i < kNOL + 3; i++) {
+        const double sp = pow(kk, (double)(i - 1)) * 1.6, stt = sp * kk;
+        sig[i] = sqrt(stt * stt - sp * sp);
+    }
+    Taps tl[kNOL + 2];
+    for (int i = 1; i < kNOL + 3; ++i)
+        if (gauss_taps(sig[i], tl[i - 1]) < 0) { err = "kernel size"; return -4; }
+    // batch buffer: Pyr tables, then 4 counters per image
+    const size_t pyr_bytes = sizeof(Pyr) * nj;
+    SCHK(grow(bw->batch, bw->batch_cap, pyr_bytes + 256));
+    if (!bw->h_pyr) SCHK(hipHostMalloc((void**)&bw->h_pyr, sizeof(Pyr) * kMaxImg, hipHostMallocDefault));
+    if (!bw->h_cnt) SCHK(hipHostMalloc((void**)&bw->h_cnt, sizeof(int) * 4 * kMaxImg, hipHostMallocDefault));
+    Pyr* d_pyr = (Pyr*)bw->batch;
+    int* d_cnt = (int*)((char*)bw->batch + pyr_bytes);
+    std::vector<int> live;  // images with at least one octave
+    for (int j = 0; j < nj; ++j) {
+        SiftJob& J = jobs[j];
+        J.d_pyr = d_pyr + j;
+        J.d_cnt = d_cnt + 4 * j;
+        bw->h_pyr[j] = J.h_pyr;
+        if (J.n_oct > 0) live.push_back(j);
+        if (J.d_mask) SCHK(hipMemcpy2DAsync(J.d_mask, J.cols, J.mask, J.mstep, J.cols, J.rows, hipMemcpyHostToDevice, st));
+    }
+    SCHK(hipMemcpyAsync(d_pyr, bw->h_pyr, pyr_bytes, hipMemcpyHostToDevice, st));
+    SCHK(hipMemsetAsync(d_cnt, 0, sizeof(int) * 4 * nj, st));
+    if (!live.empty()) {
+        // createInitialImage: x2 INTER_LINEAR, then the initial blur into octave 0 layer 0
+        {
+            Up2B A{};
+            const int nb = flatten(A.f, live, [&](int j, int& gx, int& gy) {
+                gx = (jobs[j].cols * 2 + 255) / 256;
+                gy = jobs[j].rows * 2;
+            });
+            for (int k = 0; k < A.f.n; ++k) {
+                const SiftJob& J = jobs[live[k]];
+                A.src[k] = (const uint8_t*)J.w->img;
+                A.rows[k] = J.rows;
+                A.cols[k] = J.cols;
+                A.dst[k] = J.T0;
+            }
+            up2_kernel<<<nb, 256, 0, st>>>(A);
+        }
+        auto blur = [&](const std::vector<int>& imgs, int o, int layer, bool init, const Taps& t) -> bool {
+            BlurB A{};
+            const int nb = flatten(A.f, imgs, [&](int j, int& gx, int& gy) {
+                gx = (jobs[j].ocols[o] + kBlurTW - 1) / kBlurTW;
+                gy = (jobs[j].orows[o] + kBlurTH - 1) / kBlurTH;
+            });
+            for (int k = 0; k < A.f.n; ++k) {
+                const SiftJob& J = jobs[imgs[k]];
+                const size_t plane = (size_t)J.orows[o] * J.ocols[o];
+                A.src[k] = init ? J.T0 : J.P + J.goff[o] + (layer - 1) * plane;
+                A.dst[k] = J.P + J.goff[o] + layer * plane;
+                A.rows[k] = J.orows[o];
+                A.cols[k] = J.ocols[o];
+            }
+            const int a = t.n / 2;
+            const size_t lds = sizeof(float) * (size_t)(kBlurTH + 2 * a) * (kBlurTW + 2 * a + kBlurTW);
+            if (lds > 64 * 1024) return false;
+            blur_kernel<<<nb, 256, lds, st>>>(A, t);
+            return true;
+        };
+        if (!blur(live, 0, 0, true, t0)) { err = "kernel size"; return -4; }
+        // buildGaussianPyramid + DoG of the large octaves, all images with octave o at once
+        int o_max = 0;
+        for (int j : live) o_max = std::max(o_max, jobs[j].o_small);
+        for (int o = 0; o < o_max; ++o) {
+            std::vector<int> imgs;
+            for (int j : live)
+                if (o < jobs[j].o_small) imgs.push_back(j);
+            if (o > 0) {
+                DownB A{};
+                const int nb = flatten(A.f, imgs, [&](int j, int& gx, int& gy) {
+                    gx = (jobs[j].ocols[o] + 255) / 256;
+                    gy = jobs[j].orows[o];
+                });
+                for (int k = 0; k < A.f.n; ++k) {
+                    const SiftJob& J = jobs[imgs[k]];
+                    A.src[k] = J.P + J.goff[o - 1] + kNOL * (size_t)J.orows[o - 1] * J.ocols[o - 1];
+                    A.scols[k] = J.ocols[o - 1];
+                    A.dst[k] = J.P + J.goff[o];
+                    A.cols[k] = J.ocols[o];
+                }
+                down2_kernel<<<nb, 256, 0, st>>>(A);
+            }
+            for (int i = 1; i < kNOL + 3; ++i)
+                if (!blur(imgs, o, i, false, tl[i - 1])) { err = "kernel size"; return -4; }
+            DogB A{};
+            const int nb = flatten(A.f, imgs, [&](int j, int& gx, int& gy) {
+                gx = (int)(((size_t)jobs[j].orows[o] * jobs[j].ocols[o] + 255) / 256);
+                gy = 1;
+            });
+            for (int k = 0; k < A.f.n; ++k) {
+                const SiftJob& J = jobs[imgs[k]];
+                A.g[k] = J.P + J.goff[o];
+                A.d[k] = J.P + J.doff[o];
+                A.plane[k] = (long long)J.orows[o] * J.ocols[o];
+            }
+            dog_kernel<<<dim3(nb, kNOL + 2), 256, 0, st>>>(A);
+        }
+        {  // the small octaves: one block per image
+            SmallB A{};
+            for (int j : live)
+                if (jobs[j].o_small < jobs[j].n_oct) {
+                    A.pyr[A.n] = jobs[j].d_pyr;
+                    A.o0[A.n] = jobs[j].o_small;
+                    A.n_oct[A.n] = jobs[j].n_oct;
+                    ++A.n;
+                }
+            for (int i = 0; i < kNOL + 2; ++i) A.t[i] = tl[i];
+            if (A.n > 0) small_octaves_kernel<<<A.n, 1024, 0, st>>>(A);
+        }
+        // findScaleSpaceExtrema's pixel test, per octave all images at once
+        const int threshold = (int)floor(0.5 * 0.04 / kNOL * 255);
+        int oct_max = 0;
+        for (int j : live) oct_max = std::max(oct_max, jobs[j].n_oct);
+        for (int o = 0; o < oct_max; ++o) {
+            std::vector<int> imgs;
+            for (int j : live)
+                if (o < jobs[j].n_oct && jobs[j].orows[o] > 2 * kBorder && jobs[j].ocols[o] > 2 * kBorder) imgs.push_back(j);
+            if (imgs.empty()) continue;
+            ExtB A{};
+            const int nb = flatten(A.f, imgs, [&](int j, int& gx, int& gy) {
+                gx = (jobs[j].ocols[o] - 2 * kBorder + 127) / 128;
+                gy = jobs[j].orows[o] - 2 * kBorder;
+            });
+            for (int k = 0; k < A.f.n; ++k) {
+                const SiftJob& J = jobs[imgs[k]];
+                A.dog[k] = J.P + J.doff[o];
+                A.rows[k] = J.orows[o];
+                A.cols[k] = J.ocols[o];
+                A.cand[k] = J.d_cand;
+                A.n_cand[k] = J.d_cnt;
+            }
+            A.octave = o;
+            A.threshold = threshold;
+            A.cap = cand_limit();
+            extrema_kernel<<<dim3(nb, 1, kNOL), 128, 0, st>>>(A);
+        }
+        // adjustLocalExtrema, orientations, keypoint post-processing, descriptors: grids of (X, images)
+        RefB Rf{};
+        OriB Or{};
+        KpB Kp{};
+        DescB Ds{};
+        const int nl = (int)live.size();
+        for (int k = 0; k < nl; ++k) {
+            SiftJob& J = jobs[live[k]];
+            Rf.pyr[k] = J.d_pyr;
+            Rf.cand[k] = J.d_cand;
+            Rf.n_cand[k] = J.d_cnt;
+            Rf.surv[k] = J.d_surv;
+            Rf.n_surv[k] = J.d_cnt + 2;
+            Or.pyr[k] = J.d_pyr;
+            Or.surv[k] = J.d_surv;
+            Or.n_surv[k] = J.d_cnt + 2;
+            Or.kp[k] = J.d_kp;
+            Or.n_kp[k] = J.d_cnt + 1;
+            Kp.kp[k] = J.d_kp;
+            Kp.n_kp[k] = J.d_cnt + 1;
+            Kp.mask[k] = J.d_mask;
+            Kp.mstep[k] = J.cols;
+            Kp.out[k] = J.d_kp2;
+            Kp.n_out[k] = J.d_cnt + 3;
+            Ds.pyr[k] = J.d_pyr;
+            Ds.kp[k] = J.d_kp2;
+            Ds.n[k] = J.d_cnt + 3;
+            Ds.n_cap[k] = kSortCap;
+            Ds.desc[k] = (float*)J.w->desc;
+        }
+        Rf.cap = cand_limit();
+        Rf.surv_cap = kCandCap;
+        Or.surv_cap = kCandCap;
+        Or.kp_cap = kKpCap;
+        Kp.kp_cap = kKpCap;
+        Kp.sort_cap = sort_limit();
+        refine_kernel<<<dim3(std::max(1024 / nl, 128), nl), 128, 0, st>>>(Rf);
+        orient_kernel<<<dim3(std::max(4096 / nl, 512), nl), 64, 0, st>>>(Or);
+        kp_post_kernel<<<dim3(1, nl), 1024, 0, st>>>(Kp);
+        descr_kernel<<<dim3(std::max(4096 / nl, 1024), nl), kDescrT, 0, st>>>(Ds);
+        SCHK(hipGetLastError());
+    }
+    SCHK(hipMemcpyAsync(bw->h_cnt, d_cnt, sizeof(int) * 4 * nj, hipMemcpyDeviceToHost, st));
+    SCHK(hipStreamSynchronize(st));
+    for (int j = 0; j < nj; ++j) {
+        SiftJob& J = jobs[j];
+        for (int q = 0; q < 4; ++q) J.h_cnt[q] = bw->h_cnt[4 * j + q];
+        J.n = 0;
+        J.out_kp = J.d_kp2;
+        if (J.n_oct < 1) continue;
+        // extrema_kernel counts every candidate but stores only the first cand_limit(): more would
+        // silently drop keypoints OpenCV (no cap) keeps
+        if (J.h_cnt[0] > cand_limit()) {
+            err = "more than " + std::to_string(cand_limit()) + " SIFT candidates";
+            return -4;
+        }
+        if (J.h_cnt[3] < 0) {
+            if (int r = sift_describe_host(J, st, err)) return r;
+        } else {
+            J.n = J.h_cnt[3];
+        }
+    }
     return 0;
 }
 
-// every stage of all images enqueued, then two synchronisations per call: the counts, the copies
-static int sift_run(std::vector<SiftJob>& jobs, hipStream_t st, std::string& err) {
-    for (auto& J : jobs)
-        if (int r = sift_build(J, st, err)) return r;
-    for (auto& J : jobs)
-        if (int r = sift_enqueue_rest(J, st, err)) return r;
-    SCHK(hipStreamSynchronize(st));
-    for (auto& J : jobs)
-        if (int r = sift_fetch(J, st, err)) return r;
+// copies of the first J.cap keypoints / descriptors of every image, one synchronisation
+static int sift_fetch(std::vector<SiftJob>& jobs, hipStream_t st, std::string& err) {
+    for (auto& J : jobs) {
+        const int n = std::min(J.n, J.cap);
+        if (n <= 0) continue;
+        SCHK(hipMemcpyAsync(J.kps, J.out_kp, sizeof(mim_keypoint) * n, hipMemcpyDeviceToHost, st));
+        SCHK(hipMemcpyAsync(J.desc, J.w->desc, sizeof(float) * 128 * (size_t)n, hipMemcpyDeviceToHost, st));
+    }
     SCHK(hipStreamSynchronize(st));
     return 0;
 }
@@ -1201,38 +1480,32 @@ int sift_detect_compute(SiftWs* w, hipStream_t st, const uint8_t* img, int rows,
     J.cap = max_kp;
     J.kps = kps;
     J.desc = desc;
-    const int r = sift_run(jobs, st, err);
+    int r = sift_batch(jobs, w, st, err);
+    if (!r) r = sift_fetch(jobs, st, err);
     *n_out = J.n;
     return r;
 }
 
-// TestsDetector.cpp:99-107 for one scene: resize(scene, scaled, Size(), s, s, INTER_LINEAR) and
-// detectAndCompute(scaled) at every scale, all in one call (the scene uploaded once, the resizes on
-// the device, 4 synchronisations in all).  Keypoints / descriptors of the scales are concatenated in
-// scale order into kps / desc (capacity max_kp in all); n_out[s] = the keypoints of scale s.
-int sift_detect_compute_scales(std::vector<SiftWs*>& ws, hipStream_t st, const uint8_t* img, int rows, int cols,
-                               long long step, int n_scales, const float* scales, int max_kp, mim_keypoint* kps,
-                               float* desc, int* n_out, std::string& err) {
+// resize(scene, scaled, Size(), s, s, INTER_LINEAR) of every scale into its workspace, one launch
+static int sift_scale_images(std::vector<SiftWs*>& ws, hipStream_t st, const uint8_t* img, int rows, int cols,
+                             long long step, int n_scales, const float* scales, std::vector<SiftJob>& jobs,
+                             std::string& err) {
+    if (n_scales > kMaxImg) {
+        err = "sift scales: more than 8 scales";
+        return -3;
+    }
     while ((int)ws.size() < n_scales + 1) ws.push_back(sift_ws_create());
-    // MIM_SIFT_SCALE_STREAMS=1: each scale on its workspace's stream (forked after the upload, joined
-    // back into st).  Off by default: measured slower on the MI355X (c1img single scene 17.95 -> 25.3 ms,
-    // 12 scenes in flight 168 -> 107 scenes/s; profiles/r03e_bench_c1img_streams.log), the scales' short
-    // launches then queue behind each other's cross-stream waits instead of running back to back
-    static const bool fork = [] {
-        const char* e = getenv("MIM_SIFT_SCALE_STREAMS");
-        return e && atoi(e) != 0;
-    }();
-    if (fork)
-        for (SiftWs* w : ws) {
-            if (!w->s) SCHK(hipStreamCreateWithFlags(&w->s, hipStreamNonBlocking));
-            if (!w->ev) SCHK(hipEventCreateWithFlags(&w->ev, hipEventDisableTiming));
-        }
-    SiftWs* src = ws[n_scales];  // the scene itself
+    SiftWs* src = ws[n_scales];  // the scene itself, and the batch buffer
     SCHK(grow(src->img, src->img_cap, (size_t)rows * cols));
     SCHK(hipMemcpy2DAsync(src->img, cols, img, step, cols, rows, hipMemcpyHostToDevice, st));
-    if (fork) SCHK(hipEventRecord(src->ev, st));
-    std::vector<SiftJob> jobs(n_scales);
+    jobs.assign(n_scales, SiftJob{});
+    ResizeB A{};
+    A.src = (const uint8_t*)src->img;
+    A.rows = rows;
+    A.cols = cols;
+    std::vector<int> all(n_scales);
     for (int i = 0; i < n_scales; ++i) {
+        all[i] = i;
         const double f = (double)scales[i];
         const int dc = (int)lrint(cols * f), dr = (int)lrint(rows * f);  // Size() + fx: saturate_cast<int>
         if (dc <= 0 || dr <= 0) { err = "sift scales: a scale leaves no pixels"; return -3; }
@@ -1243,37 +1516,88 @@ int sift_detect_compute_scales(std::vector<SiftWs*>& ws, hipStream_t st, const u
         J.mask = nullptr;
         J.mstep = 0;
         J.cap = 0;
-        hipStream_t si = fork ? J.w->s : st;
-        if (fork) SCHK(hipStreamWaitEvent(si, src->ev, 0));
         SCHK(grow(J.w->img, J.w->img_cap, (size_t)dr * dc));
-        resize_u8_kernel<<<dim3((dc + 255) / 256, dr), 256, 0, si>>>((const uint8_t*)src->img, rows, cols,
-                                                                   (uint8_t*)J.w->img, dr, dc, 1. / f, 1. / f);
-        SCHK(hipGetLastError());
-        if (int r = sift_build(J, si, err)) return r;
-        if (int r = sift_enqueue_rest(J, si, err)) return r;
-        if (fork) {
-            SCHK(hipEventRecord(J.w->ev, si));
-            SCHK(hipStreamWaitEvent(st, J.w->ev, 0));
-        }
+        A.dst[i] = (uint8_t*)J.w->img;
+        A.drows[i] = dr;
+        A.dcols[i] = dc;
+        A.sx[i] = A.sy[i] = 1. / f;
     }
-    SCHK(hipStreamSynchronize(st));
+    const int nb = flatten(A.f, all, [&](int i, int& gx, int& gy) {
+        gx = (jobs[i].cols + 255) / 256;
+        gy = jobs[i].rows;
+    });
+    resize_u8_kernel<<<nb, 256, 0, st>>>(A);
+    SCHK(hipGetLastError());
+    return 0;
+}
+
+// TestsDetector.cpp:99-107 for one scene: resize(scene, scaled, Size(), s, s, INTER_LINEAR) and
+// detectAndCompute(scaled) at every scale, all in one call (the scene uploaded once, one launch per
+// stage for all scales, 2 synchronisations in all).  Keypoints / descriptors of the scales are
+// concatenated in scale order into kps / desc (capacity max_kp in all); n_out[s] = the keypoints of
+// scale s.
+int sift_detect_compute_scales(std::vector<SiftWs*>& ws, hipStream_t st, const uint8_t* img, int rows, int cols,
+                               long long step, int n_scales, const float* scales, int max_kp, mim_keypoint* kps,
+                               float* desc, int* n_out, std::string& err) {
+    std::vector<SiftJob> jobs;
+    if (int r = sift_scale_images(ws, st, img, rows, cols, step, n_scales, scales, jobs, err)) return r;
+    for (auto& J : jobs) J.cap = INT_MAX;  // the host path describes every keypoint: copies come below
+    if (int r = sift_batch(jobs, ws[n_scales], st, err)) return r;
     int used = 0;
     for (int i = 0; i < n_scales; ++i) {
         SiftJob& J = jobs[i];
         J.cap = std::max(0, max_kp - used);
         J.kps = kps + used;
         J.desc = desc + (size_t)128 * used;
-        if (int r = sift_fetch(J, st, err)) return r;
         n_out[i] = J.n;
         used += std::min(J.n, J.cap);
     }
-    SCHK(hipStreamSynchronize(st));
+    if (int r = sift_fetch(jobs, st, err)) return r;
     int total = 0;
     for (int i = 0; i < n_scales; ++i) total += n_out[i];
     if (total > max_kp) {
         err = "sift scales: more keypoints than max_kp";
         return -2;
     }
+    return 0;
+}
+
+// The same on the device only: out[i] = scale i's keypoints / descriptors in the workspaces (valid until
+// the next SIFT call on them), one synchronisation (the counts)
+int sift_scales_device(std::vector<SiftWs*>& ws, hipStream_t st, const uint8_t* img, int rows, int cols,
+                       long long step, int n_scales, const float* scales, SiftDevOut* out, std::string& err) {
+    std::vector<SiftJob> jobs;
+    if (int r = sift_scale_images(ws, st, img, rows, cols, step, n_scales, scales, jobs, err)) return r;
+    for (auto& J : jobs) J.cap = INT_MAX;
+    if (int r = sift_batch(jobs, ws[n_scales], st, err)) return r;
+    for (int i = 0; i < n_scales; ++i) out[i] = SiftDevOut{jobs[i].out_kp, (const float*)jobs[i].w->desc, jobs[i].n};
+    return 0;
+}
+
+int sift_resize_u8(SiftWs* w, hipStream_t st, const uint8_t* src, int rows, int cols, long long step, uint8_t* dst,
+                   int drows, int dcols, double fx, double fy, std::string& err) {
+    const size_t sb = (size_t)rows * cols, db = (size_t)drows * dcols;
+    SCHK(grow(w->img, w->img_cap, sb + db));
+    uint8_t* ds = (uint8_t*)w->img;
+    uint8_t* dd = ds + sb;
+    SCHK(hipMemcpy2DAsync(ds, cols, src, step, cols, rows, hipMemcpyHostToDevice, st));
+    ResizeB A{};
+    A.src = ds;
+    A.rows = rows;
+    A.cols = cols;
+    A.dst[0] = dd;
+    A.drows[0] = drows;
+    A.dcols[0] = dcols;
+    A.sx[0] = 1. / (fx > 0 ? fx : (double)dcols / cols);
+    A.sy[0] = 1. / (fy > 0 ? fy : (double)drows / rows);
+    const int nb = flatten(A.f, std::vector<int>{0}, [&](int, int& gx, int& gy) {
+        gx = (dcols + 255) / 256;
+        gy = drows;
+    });
+    resize_u8_kernel<<<nb, 256, 0, st>>>(A);
+    SCHK(hipGetLastError());
+    SCHK(hipMemcpyAsync(dst, dd, db, hipMemcpyDeviceToHost, st));
+    SCHK(hipStreamSynchronize(st));
     return 0;
 }
 

@@ -221,6 +221,31 @@ class Matcher:
             o += int(c)
         return out
 
+    def sift_scales_to_sets(self, gray, scales, keypoints: bool = False, max_kp: int = 1 << 18):
+        """resize + detectAndCompute at every scale (TestsDetector.cpp:99-107) with the descriptors left
+        on the device, each scale registered as a set (mim_sift_scales_sets).  Returns (set ids, n_kp
+        per scale, [keypoints per scale] or None); the sets' rows are what sift_detect_compute_scales
+        returns, without the round trip through host memory."""
+        g = np.ascontiguousarray(gray, np.uint8)
+        if g.ndim != 2:
+            raise ValueError("sift_scales_to_sets: a single-channel image is required")
+        sc = np.ascontiguousarray(scales, np.float32).reshape(-1)
+        ids = np.zeros(len(sc), np.int32)
+        n = np.zeros(len(sc), np.int32)
+        kps = np.zeros(max(max_kp, 1), KEYPOINT_DTYPE) if keypoints else None
+        self._check(self.L.mim_sift_scales_sets(
+            self._ctx, C.c_void_p(g.ctypes.data), g.shape[0], g.shape[1], g.strides[0], len(sc),
+            C.c_void_p(sc.ctypes.data), C.c_void_p(ids.ctypes.data), C.c_void_p(n.ctypes.data),
+            max_kp if keypoints else 0, C.c_void_p(kps.ctypes.data) if keypoints else None))
+        self._n_sets = int(ids[-1]) + 1
+        out = None
+        if keypoints:
+            out, o = [], 0
+            for c in n:
+                out.append(kps[o:o + c].copy())
+                o += int(c)
+        return [int(i) for i in ids], [int(c) for c in n], out
+
     def resize_linear(self, src, dsize=None, fx: float = 0.0, fy: float = 0.0):
         """cv::resize(src, dst, dsize, fx, fy, INTER_LINEAR) of a CV_8UC1 image.
 

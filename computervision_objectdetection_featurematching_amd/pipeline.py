@@ -99,23 +99,24 @@ def _model_sets(matcher: Matcher, models: list[ObjectModel]) -> list[list[int]]:
 class SceneRun:
     """detect_objects' intermediate products (for tests and benches)."""
     scene_kp: list      # per scale: KEYPOINT_DTYPE
-    scene_desc: list    # per scale: (n, 128) float32
+    scene_desc: list    # per scale: (n, 128) float32 (the same SIFT run again through host memory)
     results: np.ndarray  # RESULT_DTYPE per problem, problems in (model, scale, view) order
     points: list        # per model: allUnfilteredScenePts (n, 2) float32
     detections: list    # [((x, y, w, h), name)]
 
 
 def detect_objects(matcher: Matcher, scene_gray, models: list[ObjectModel], scales=SCALES, params=None,
-                   box_params: BoxParams | None = None, keep: bool = False):
+                   box_params: BoxParams | None = None, keep: bool = False, keep_descriptors: bool = False):
     """detectObjects(scene, models, detector) (TestsDetector.cpp:32-251) on a grayscale scene.
 
-    Returns [((x, y, w, h), name)], or the SceneRun when keep=True."""
+    Returns [((x, y, w, h), name)], or the SceneRun when keep=True (its scene_desc only with
+    keep_descriptors: the scene's descriptors never leave the device on the detection path, so they
+    are computed a second time through host memory for the caller)."""
     params = params or default_params()
-    per_scale = matcher.sift_detect_compute_scales(scene_gray, scales)  # :99-107, all scales in one call
-    scene_kp = [k for k, _ in per_scale]
-    scene_desc = [d for _, d in per_scale]
     view_ids = _model_sets(matcher, models)
-    scene_ids = [matcher.add_set(d, np.stack([k["x"], k["y"]], 1)) for k, d in zip(scene_kp, scene_desc)]
+    # :99-107, all scales in one call, the scene's descriptors registered as sets on the device
+    scene_ids, _, scene_kp = matcher.sift_scales_to_sets(scene_gray, scales, keypoints=keep)
+    scene_desc = [d for _, d in matcher.sift_detect_compute_scales(scene_gray, scales)] if keep_descriptors else None
     tags = [(mi, si, vi) for mi in range(len(models)) for si in range(len(scales)) for vi in range(len(view_ids[mi]))]
     res = matcher.match_batch([(view_ids[mi][vi], scene_ids[si]) for mi, si, vi in tags], params)
     # :87-94 inlier scene points of the accepted problems (:74, :79, :81, :84), /scale when scale != 1,

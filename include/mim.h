@@ -205,6 +205,16 @@ mim_status mim_sift_detect_compute_scales(struct mim_ctx* ctx, const uint8_t* gr
                                           int64_t step, int32_t n_scales, const float* scales, int32_t max_kp,
                                           mim_keypoint* kps, float* desc, int32_t* n_kp);
 
+/* TestsDetector.cpp:99-107 with the results left on the device: resize + SIFT at every scale exactly as
+ * mim_sift_detect_compute_scales (n_scales <= 8), then each scale's descriptors and keypoint positions
+ * registered as a set of this ctx (as mim_set_create would, but copied on the device: no descriptor
+ * leaves the GPU).  set_ids[s] = the set of scale s, n_kp[s] its keypoints.  kps (nullable; max_kp
+ * rows) receives the keypoints concatenated in scale order; more than max_kp: MIM_ERANGE after the
+ * sets were registered (only the first max_kp written).  One host synchronisation (the counts), two
+ * with kps.  The sets follow the rules of mim_set_create (dropped by mim_sets_clear / _truncate). */
+mim_status mim_sift_scales_sets(struct mim_ctx* ctx, const uint8_t* gray, int32_t rows, int32_t cols, int64_t step,
+                                int32_t n_scales, const float* scales, int32_t* set_ids, int32_t* n_kp, int32_t max_kp,
+                                mim_keypoint* kps);
 
 /* cv::resize(src, dst, dsize, fx, fy, INTER_LINEAR) of a CV_8UC1 image (TestsDetector.cpp:102, the
  * scene scales).  fx, fy > 0: resize(src, dst, Size(), fx, fy) — the caller passes

@@ -51,7 +51,7 @@ def test_detect_objects_matches_oracle(matcher, model, c1):
     scenes = sorted(k[8:] for k in c1 if k.startswith("exp/res/"))
     assert len(scenes) >= 3
     for sid in scenes:
-        run = detect_objects(matcher, c1[f"scene/{sid}"], [m], keep=True)
+        run = detect_objects(matcher, c1[f"scene/{sid}"], [m], keep=True, keep_descriptors=True)
         for s, k, d in zip(SCALES, run.scene_kp, run.scene_desc):
             assert np.array_equal(sift_hash(k, d), c1[f"exp/sift/{sid}/{s}"]), (sid, s)
         r = run.results

@@ -46,12 +46,12 @@ def test_host_postprocess_path_matches_oracle(tmp_path):
     img = blobs(7, 240, 320, n=60, noise=8.0)
     mask = np.zeros_like(img)
     mask[30:200, 40:290] = 255
-    got = _run_child(tmp_path, {"MIM_SIFT_SORT_CAP": "64"}, [(img, None), (img, mask)])
+    got = _run_child(tmp_path, {"MIM_SIFT_SORT_CAP": "16"}, [(img, None), (img, mask)])
     for j, m in enumerate((None, mask)):
         assert int(got[f"status{j}"]) == 0, got.get(f"err{j}")
         ok, od = O.sift_detect_compute(img, m)
-        if m is None:  # the device limit (64, before dedupe and mask) is exceeded: the host path ran
-            assert len(ok) > 64
+        if m is None:  # the device limit (16, before dedupe and mask) is exceeded: the host path ran
+            assert len(ok) > 16
         compare_sift(got[f"kp{j}"], got[f"desc{j}"], ok, od, f"host path mask={m is not None}")
 
 

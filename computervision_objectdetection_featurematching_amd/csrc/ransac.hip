@@ -941,6 +941,9 @@ __device__ __forceinline__ int redraw_len(const unsigned (&u)[D], int j) {
 // The block's 2048 + 15 draws are staged through LDS with coalesced 16-byte loads (a lane's own 15
 // draws at a 32-byte lane stride would touch 16 cache lines per load instruction, 15 times over).
 constexpr int kAttemptSpan = 256 * kAttemptPerThread;  // window positions per block
+// draws per wanted iteration the sampler grids are sized for (a window is ~4.1 per iteration at
+// n = 2000 and ~4-6 on real views with n >= 128; the flag capacity allows 28: a longer window loops)
+constexpr int kAttemptRateEst = 6;
 
 __global__ __launch_bounds__(256) void ransac_attempt_kernel(const RansacState* __restrict__ st,
                                                              const uint32_t* __restrict__ stream, long long slen,
@@ -952,8 +955,10 @@ __global__ __launch_bounds__(256) void ransac_attempt_kernel(const RansacState* 
     const RansacState S = st[p];
     if (!S.active || S.done || S.fail_iter != -1 || S.n < kSmallMaxN || S.produced >= min(c1, S.niters)) return;
     const int wlen = window_len(S, c1, wcap);  // a multiple of 64
-    const int boff = (blockIdx.x % bpp) * kAttemptSpan;
-    if (boff >= wlen) return;  // uniform over the block
+    // the grid covers the window a typical draw rate implies (kAttemptRateEst), not its capacity; a
+    // longer window (low checkSubset pass rate) is covered by the same blocks looping
+    for (int boff = (blockIdx.x % bpp) * kAttemptSpan; boff < wlen; boff += bpp * kAttemptSpan) {
+    __syncthreads();  // the previous round's reads of sdraw are done
     // stream positions fit 32 bits (the stream is capped at 2^28 draws; 64 zero draws pad its end)
     const int qb = (int)S.stream_pos + boff;
     const int start = qb & ~3, shift = qb - start;
@@ -970,7 +975,7 @@ __global__ __launch_bounds__(256) void ransac_attempt_kernel(const RansacState* 
     }
     __syncthreads();
     const int off = boff + threadIdx.x * kAttemptPerThread;
-    if (off >= wlen) return;
+    if (off >= wlen) continue;  // past the window (the next round's barriers are reached from the loop latch)
     const int q0 = qb + threadIdx.x * kAttemptPerThread;
     const unsigned N = (unsigned)S.n, mB = 0xFFFFFFFFu / N;
     const bool big = N > 256 && N < (1u << 24);  // q and n both fit 24 bits
@@ -1020,6 +1025,7 @@ __global__ __launch_bounds__(256) void ransac_attempt_kernel(const RansacState* 
         w[j >> 2] |= (uint32_t)f << (8 * (j & 3));
     }
     *reinterpret_cast<uint2*>(flags + (long long)p * wcap + off) = make_uint2(w[0], w[1]);
+    }
 }
 
 __device__ __forceinline__ int wave_excl_prefix_sum(int v) {
@@ -1075,12 +1081,13 @@ __global__ __launch_bounds__(256) void ransac_irr_kernel(const RansacState* __re
                                                          int c1, int* __restrict__ irr, int* __restrict__ irr_cnt,
                                                          int irr_blocks) {
     __shared__ int wsum[4];
-    const int p = blockIdx.x / bpp, b = blockIdx.x % bpp, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int p = blockIdx.x / bpp, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const RansacState S = st[p];
     if (!S.active || S.done || S.fail_iter != -1 || S.n < kSmallMaxN || S.produced >= min(c1, S.niters)) return;
     const int wlen = window_len(S, c1, wcap);
+    for (int b = blockIdx.x % bpp; b * kIrrBlock < wlen; b += bpp) {
+    __syncthreads();  // wsum of the previous round read
     const int b0 = b * kIrrBlock;
-    if (b0 >= wlen) return;
     const uint8_t* F = flags + (long long)p * wcap;
     const int r0 = b0 + tid * 64;  // 64 positions per thread
     uint32_t wd[16];
@@ -1117,12 +1124,13 @@ __global__ __launch_bounds__(256) void ransac_irr_kernel(const RansacState* __re
     }
     const long long slot = (long long)p * irr_blocks + b;
     if (tid == 0) irr_cnt[slot] = total <= kIrrCap ? total : -1;
-    if (total > kIrrCap) return;
+    if (total > kIrrCap) continue;
     int* L = irr + slot * kIrrCap;
     while (irrm) {
         const int bit = __builtin_ctzll(irrm);
         irrm &= irrm - 1;
         L[base++] = r0 + bit;
+    }
     }
 }
 
@@ -1362,10 +1370,10 @@ __global__ __launch_bounds__(kCheckBlock) void ransac_check_kernel(const ChainSe
     const int p = blockIdx.x / bpp, lane = threadIdx.x & 63;
     const ChainSegs* G = chains + p;
     const int T = G->T;
-    const int b = blockIdx.x % bpp;
-    const int base = b * kCheckBlock * kCheckPer;
-    if (base >= T) return;  // T < 0: nothing this chunk
+    if (T <= 0) return;  // nothing this chunk
     const RansacState S = st[p];
+    for (int b = blockIdx.x % bpp; b * kCheckBlock * kCheckPer < T; b += bpp) {
+    const int base = b * kCheckBlock * kCheckPer;
     // segment data of the block's first kCheckSegs segments in one round of (uniform, scalar) loads
     const int nseg = G->nseg;
     const int bb = base / kCheckBlock;
@@ -1434,6 +1442,7 @@ __global__ __launch_bounds__(kCheckBlock) void ransac_check_kernel(const ChainSe
         const int w0 = (base + r * kCheckBlock + (threadIdx.x & ~63)) >> 5;  // 2 words per wave
         if (lane == 0 && w0 * 32 < T) PB[w0] = (uint32_t)m;
         if (lane == 32 && (w0 + 1) * 32 < T) PB[w0 + 1] = (uint32_t)(m >> 32);
+    }
     }
 }
 
@@ -2472,35 +2481,9 @@ __global__ __launch_bounds__(256) void ransac_bound_mfma_kernel(const RansacStat
         CL = S.sb * sqrtf(fmaxf(tl, 0.f)) * 0.92387953f * (1.f - 1e-6f);
         EL = ((CL + 1.41421357f) * kMfmaErr + 1.41421357f * A) * (1.f + 1e-6f);
     }
-    // chunk 2 (disc test, see above the kernel): L1 = ex - cD W and L2 = ex + cD W in place of ex and W,
-    // so that L1 L2 + ey^2 - ED = ex^2 + ey^2 - cD^2 W^2 - ED is two fma per pair
-    constexpr double kDiscDelta = 0.125;
-    const float cD = C * sqrtf(1.f + (float)kDiscDelta) * (1.f + 1e-5f);
-    float ED = 0.f;
-    if (!kLo) {
-        const float eo = (1.f + cD) * kMfmaErr * (1.f + 1e-6f);  // error bound of one MFMA output
-        const float e3 = eo + 1.41421357f * (A + eo);
-        ED = (float)(1.0 + 1.0 / kDiscDelta) * e3 * e3 * (1.f + 1e-4f);
-    }
     // B-operand fragments of the own hypothesis: k 0-7 (bx, by, bw) and k 8-15 (shared by bx, by)
     h8v fx = {}, fy = {}, fw = {}, fn = {};
-    if (count && !kLo) {  // fx = L1, fw = L2 on the X part; the u part (fn) is the same for both
-        _Float16 a, b;
-        const double cd = (double)cD;
-        split_f16(h[0] - cd * h[6], a, b); fx[0] = a; fx[1] = a; fx[2] = b;
-        split_f16(h[1] - cd * h[7], a, b); fx[3] = a; fx[4] = a; fx[5] = b;
-        split_f16(h[2] - cd * h[8], a, b); fx[6] = a; fx[7] = b;
-        split_f16(h[0] + cd * h[6], a, b); fw[0] = a; fw[1] = a; fw[2] = b;
-        split_f16(h[1] + cd * h[7], a, b); fw[3] = a; fw[4] = a; fw[5] = b;
-        split_f16(h[2] + cd * h[8], a, b); fw[6] = a; fw[7] = b;
-        split_f16(h[3], a, b); fy[0] = a; fy[1] = a; fy[2] = b;
-        split_f16(h[4], a, b); fy[3] = a; fy[4] = a; fy[5] = b;
-        split_f16(h[5], a, b); fy[6] = a; fy[7] = b;
-        split_f16(h[6], a, b); fn[0] = -a; fn[1] = -a; fn[2] = -b;
-        split_f16(h[7], a, b); fn[3] = -a; fn[4] = -a; fn[5] = -b;
-        fn[6] = fn[7] = -(_Float16)(float)h[8];  // 2^-e: exact
-    }
-    if (count && kLo) {
+    if (count) {
         _Float16 a, b;
         split_f16(h[0], a, b); fx[0] = a; fx[1] = a; fx[2] = b;
         split_f16(h[1], a, b); fx[3] = a; fx[4] = a; fx[5] = b;
@@ -2528,14 +2511,12 @@ __global__ __launch_bounds__(256) void ransac_bound_mfma_kernel(const RansacStat
     const uint4 zero4 = make_uint4(0, 0, 0, 0);
     const h8v b0x = __builtin_bit_cast(h8v, lowh ? ux : r1);
     const h8v b0y = __builtin_bit_cast(h8v, lowh ? uy : r1);
-    const h8v b0w = __builtin_bit_cast(h8v, lowh ? uw : (kLo ? zero4 : r1));
+    const h8v b0w = __builtin_bit_cast(h8v, lowh ? uw : zero4);
     const h8v b1x = __builtin_bit_cast(h8v, lowh ? r1 : un);
     const h8v b1y = __builtin_bit_cast(h8v, lowh ? r2 : un);
-    const h8v b1w = __builtin_bit_cast(h8v, lowh ? r3 : (kLo ? zero4 : un));
+    const h8v b1w = __builtin_bit_cast(h8v, lowh ? r3 : zero4);
     const float Cp = __shfl_xor(C, 32), Ep = __shfl_xor(E, 32);
     const float C0 = lowh ? C : Cp, E0 = lowh ? E : Ep, C1 = lowh ? Cp : C, E1 = lowh ? Ep : E;
-    const float EDp = __shfl_xor(ED, 32);
-    const float nED0 = -(lowh ? ED : EDp), nED1 = -(lowh ? EDp : ED);
     float CL0 = 0.f, EL0 = 0.f, CL1 = 0.f, EL1 = 0.f;
     if (kLo) {
         const float CLp = __shfl_xor(CL, 32), ELp = __shfl_xor(EL, 32);
@@ -2588,18 +2569,6 @@ __global__ __launch_bounds__(256) void ransac_bound_mfma_kernel(const RansacStat
             const f16acc ey1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ay, b1y, zc, 0, 0, 0);
             const f16acc w1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ax, b1w, zc, 0, 0, 0);
             unsigned bits0 = 0, bits1 = 0, lb0 = 0, lb1 = 0;
-            if (!kLo) {  // disc: sign bit of L1 L2 - ED + ey^2 set when the point may be in (ex0 = L1, w0 = L2)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const float q0 = fmaf(ey0[r], ey0[r], fmaf(ex0[r], w0[r], nED0));
-                    const float q1 = fmaf(ey1[r], ey1[r], fmaf(ex1[r], w1[r], nED1));
-                    bits0 = __builtin_amdgcn_alignbit(bits0, __float_as_uint(q0), 31);
-                    bits1 = __builtin_amdgcn_alignbit(bits1, __float_as_uint(q1), 31);
-                }
-                out0 += __popc(bits0);  // chunk 2 counts the points that may be in
-                out1 += __popc(bits1);
-                continue;
-            }
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 // sign bit of R - max(|ex|, |ey|), R = C |W| + E: set when the point is out of the box
@@ -2653,10 +2622,7 @@ __global__ __launch_bounds__(256) void ransac_bound_mfma_kernel(const RansacStat
         const unsigned i0 = in0 + __shfl_xor(in0, 32), i1 = in1 + __shfl_xor(in1, 32);
         lo = (int)(lowh ? i0 : i1);  // zero-padded rows (ex = ey = W = 0) give m - R_lo = E_lo > 0: never "in"
     }
-    // chunk 2 counted the points that may be in, the zero-padded rows of the last tile among them (L1 = L2
-    // = ey = 0 there: q = -ED < 0); chunk 1 the points surely out
-    const int hi = kLo ? n - outs : (wave_counts ? outs - (32 * nt - n) : n);
-    if (act) bounds[o] = invalid ? make_int2(-1, -1) : (uncertain ? make_int2(0, n) : make_int2(lo, hi));
+    if (act) bounds[o] = invalid ? make_int2(-1, -1) : (uncertain ? make_int2(0, n) : make_int2(lo, n - outs));
 }
 
 // exact count of one hypothesis (runKernel + computeError + findInliers, bit-exact)
@@ -3592,18 +3558,20 @@ void ransac_enqueue(const RansacParams& prm, int n_probs, const ProbDev* probs, 
         // falls back to inline evaluation past the window
         // (a multiple of 64: flags are read as 16-byte vectors, pass bits as 32-bit words)
         const int wcap = (int)(std::min<long long>((long long)(c1 - c0) * 28 + 4096, b.flag_cap / std::max(n_probs, 1)) & ~63LL);
-        const int bppw = (wcap + kAttemptSpan - 1) / kAttemptSpan;
+        // grids for the window a typical draw rate implies (the kernels loop over a longer one)
+        const int west = (int)std::min<long long>(wcap, (long long)(c1 - c0) * kAttemptRateEst + 4096);
+        const int bppw = (west + kAttemptSpan - 1) / kAttemptSpan;
         ransac_attempt_kernel<<<n_probs * bppw, 256, 0, ss>>>(b.state, b.stream, b.stream_len, b.flags, wcap, bppw, c1);
         mark(mark_ctx, "attempt", ss);
         if (use_chain) {
             ChainSegs* chains = reinterpret_cast<ChainSegs*>(b.chains);
-            const int bpp_irr = (wcap + kIrrBlock - 1) / kIrrBlock;
+            const int bpp_irr = (west + kIrrBlock - 1) / kIrrBlock;
             ransac_irr_kernel<<<n_probs * bpp_irr, 256, 0, ss>>>(b.state, b.flags, wcap, bpp_irr, c1, b.irr,
                                                                b.irr_cnt, b.irr_blocks);
             ransac_walk_kernel<<<n_probs, kChainThreads, 0, ss>>>(b.state, b.flags, wcap, c1, b.irr, b.irr_cnt,
                                                                  b.irr_blocks, chains);
             mark(mark_ctx, "chain", ss);
-            const int bpp_chk = (wcap / 4 + kCheckBlock * kCheckPer) / (kCheckBlock * kCheckPer);  // T <= wlen / 4 + 1
+            const int bpp_chk = (west / 4 + kCheckBlock * kCheckPer) / (kCheckBlock * kCheckPer);  // T ~ wlen / 4
             ransac_check_kernel<<<n_probs * bpp_chk, kCheckBlock, 0, ss>>>(chains, probs, pts, b.state, b.stream,
                                                                           b.stream_len, b.pass_bits, wcap, bpp_chk);
             mark(mark_ctx, "check", ss);

@@ -9,7 +9,8 @@
 //     not once per scale per model: SIFT is deterministic, so every model sees
 //     the keypoints/descriptors the reference computes for it;
 //   * with MIM_GPU_SIFT (CMake -DMIM_GPU_SIFT=ON) the five resizes and SIFT runs of :102,106 happen on
-//     the device in one call (mim_sift_detect_compute_scales: the scene uploaded once), and
+//     the device in one call whose descriptors stay there as the batch's scene sets
+//     (mim::Detector::detect_scene_gray over mim_sift_scales_sets: the scene uploaded once), and
 //     adapter/opencv/ModelsDetector.cpp describes the model views on the device too
 //     (ModelsDetector.cpp:75).  libmim's SIFT is SIFT::create() with its defaults (main.cpp:17), which is
 //     the detector the reference always passes; `detector` is then not called;
@@ -80,21 +81,20 @@ std::vector<std::pair<cv::Rect, std::string>> detectObjects(const cv::Mat& scene
     const mim::BoxParams box_params;  // TestsDetector.cpp:26-30
     const cv::Mat preprocessed = preprocessImage(scene);
 
-    // :99-107, once per scale for all models
+    // :38-109 for every model at once: one device batch of all (model, scale, view) problems, the
+    // scene described once per scale for all models (:99-107)
     const std::vector<float> scales = {0.7f, 0.85f, 1.0f, 1.15f, 1.3f};
-    std::vector<std::vector<mim::Point2f>> scene_kp(scales.size());
-    std::vector<std::vector<float>> scene_desc(scales.size());
+    std::vector<const mim::ModelViews*> mv;
+    for (const ObjectModel& m : models) mv.push_back(&views_of(m));
+    std::vector<std::vector<mim::Point2f>> all_pts;  // allUnfilteredScenePts per model (:39)
 #ifdef MIM_GPU_SIFT
     (void)detector;  // SIFT::create() defaults, on the device
     CV_Assert(preprocessed.type() == CV_8UC1);
-    {
-        std::vector<std::vector<mim_keypoint>> kps;
-        mim_device().sift_scales(preprocessed.data, preprocessed.rows, preprocessed.cols, (int64_t)preprocessed.step[0],
-                                 scales, kps, scene_desc);
-        for (size_t s = 0; s < scales.size(); ++s)
-            for (const mim_keypoint& k : kps[s]) scene_kp[s].push_back({k.x, k.y});
-    }
+    mim_device().detect_scene_gray(mv, preprocessed.data, preprocessed.rows, preprocessed.cols,
+                                   (int64_t)preprocessed.step[0], scales, all_pts);
 #else
+    std::vector<std::vector<mim::Point2f>> scene_kp(scales.size());
+    std::vector<std::vector<float>> scene_desc(scales.size());
     for (size_t s = 0; s < scales.size(); ++s) {
         cv::Mat scaled;
         cv::resize(preprocessed, scaled, cv::Size(), scales[s], scales[s]);
@@ -108,15 +108,10 @@ std::vector<std::pair<cv::Rect, std::string>> detectObjects(const cv::Mat& scene
             scene_desc[s].assign(dc.ptr<float>(), dc.ptr<float>() + dc.total());
         }
     }
-#endif
-
-    // :38-109 for every model at once: one device batch of all (model, scale, view) problems
-    std::vector<const mim::ModelViews*> mv;
-    for (const ObjectModel& m : models) mv.push_back(&views_of(m));
     std::vector<mim::Detector::ScaledScene> ss;
     for (size_t s = 0; s < scales.size(); ++s) ss.push_back({&scene_kp[s], &scene_desc[s], scales[s]});
-    std::vector<std::vector<mim::Point2f>> all_pts;  // allUnfilteredScenePts per model (:39)
     mim_device().detect_scene(mv, ss, all_pts);
+#endif
 
     // :111-248 per model, in model order
     mim::Detections dets;

@@ -15,7 +15,10 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 # x86-64 build has no FMA), see DESIGN.md "Floating-point contract".
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-Wall",
          "-Wno-unused-result", "-Wno-unused-function"]
-# extra defines for diagnostic builds (e.g. MIM_EXTRA_FLAGS=-DMIM_SAMPLER_PROF)
+# debug build (MIM_DEBUG=1): the in-kernel checks of csrc/mim_debug.h; extra defines for variant
+# builds (tuning knobs of csrc/mim_internal.h, e.g. MIM_EXTRA_FLAGS=-DMIM_KNN_QT=4)
+if os.environ.get("MIM_DEBUG") == "1":
+    FLAGS.append("-DMIM_DEBUG")
 FLAGS += os.environ.get("MIM_EXTRA_FLAGS", "").split()
 # per-source flags: the RANSAC kernels are scalar fp32/fp64 code; v2f32 packing (v_pk_fma_f32 issues
 # at half rate on gfx950 and needs SGPR-pair shuffles for uniform operands) only costs there; MFMA
@@ -31,7 +34,7 @@ def needs_build() -> bool:
     if not os.path.exists(SO):
         return True
     t = os.path.getmtime(SO)
-    deps = sources() + [os.path.join(CSRC, "mim_internal.h"),
+    deps = sources() + [os.path.join(CSRC, "mim_internal.h"), os.path.join(CSRC, "mim_debug.h"),
                         os.path.join(HERE, "..", "include", "mim.h")]
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 

@@ -179,18 +179,6 @@ constexpr int kRescan = -2;  // Top2::i2 marker: the split's top-2 needs the exa
 #define MIM_KNN_EARLY 4
 #endif
 constexpr int kEarlyTiles = MIM_KNN_EARLY;
-// timing probes only (results invalid): MIM_KNN_NODMA = stages past the first never re-staged (the loop
-// reads stale LDS: isolates the LDS-DMA issue cost), MIM_KNN_NOBAR = no per-stage barrier either
-#ifdef MIM_KNN_NODMA
-constexpr bool kProbeNoDma = true;
-#else
-constexpr bool kProbeNoDma = false;
-#endif
-#ifdef MIM_KNN_NOBAR
-constexpr bool kProbeNoBarrier = true;
-#else
-constexpr bool kProbeNoBarrier = false;
-#endif
 #ifndef MIM_KNN_LATE_UNROLL
 #define MIM_KNN_LATE_UNROLL 1
 #endif
@@ -201,15 +189,11 @@ constexpr bool kProbeNoBarrier = false;
 // row can enter that top-2 only if D <= Dc, the 2nd smallest of the pair's four D (an equal D may
 // still win on the lower index), and a row that does enters its own lane's list, so the filter
 // keeps the invariant.  D = 2R + p with p in {0,1} gives R <= floor(Dc/2).
-__device__ __forceinline__ int sel_filter(const LaneSel& s) {
-    const auto a = __builtin_amdgcn_permlane32_swap(s.m1, s.m1, false, false);
-    const auto b = __builtin_amdgcn_permlane32_swap(s.m2, s.m2, false, false);
-    const bool hi = threadIdx.x & 32;
-    const int o1 = hi ? (int)a[0] : (int)a[1], o2 = hi ? (int)b[0] : (int)b[1];
-    const int dc = min(max(s.m1, o1), min(s.m2, o2));  // 2nd smallest of {m1 <= m2, o1 <= o2}
-    return dc >> 1;
+// o1 <= o2: the partner lane's m1, m2 (exchanged by permlane32_swap once per stage; the partner's
+// values only decrease, so a stale copy gives a threshold >= the exact one: still a superset).
+__device__ __forceinline__ int late_threshold(const LaneSel& s, int o1, int o2) {
+    return min(max(s.m1, o1), min(s.m2, o2)) >> 1;  // 2nd smallest of {m1 <= m2, o1 <= o2}, halved
 }
-
 __device__ __forceinline__ int dval(int R, int p) { return (R << 1) | p; }  // v_lshl_or_b32
 
 // v_med3_u32 (the compiler rewrites the max/min form of a top-2 update into a max and two mins)
@@ -291,12 +275,10 @@ __global__ __launch_bounds__(kThreads, MIM_KNN_OCC) void knn2_i8_kernel(  // OCC
     }
     LaneSel st[QT];
     int T[QT];  // late-tile thresholds on R
-#ifndef MIM_KNN_EXACT_PAIR
     // the partner lane's (l ^ 32) m1, m2 as of the last refresh (every stage): between refreshes an
     // insertion recomputes the threshold from its own fresh pair and these (the partner's values only
     // decrease, so a stale copy gives a threshold >= the exact one: a superset, no exchange per event)
     int o1c[QT], o2c[QT];
-#endif
 #pragma unroll
     for (int u = 0; u < QT; ++u) {
         sel_init(st[u]);
@@ -312,9 +294,6 @@ __global__ __launch_bounds__(kThreads, MIM_KNN_OCC) void knn2_i8_kernel(  // OCC
     // seeds read as a struct type the waitcnt pass could not tell them from the DMA's target and
     // waited for the next stage's DMA before each tile.)
     const int wv = __builtin_amdgcn_readfirstlane(wave);
-#ifdef MIM_KNN_PRIO  // A/B: the second-dispatched half of the block wins issue arbitration (MI355X_MICROARCH.md, 2 waves per SIMD item 4)
-    if (wv >= kKnnWaves / 2) __builtin_amdgcn_s_setprio(1);
-#endif
     auto stage_dma = [&](int t0, int buf, bool keys) {
         unsigned char* base = smem + buf * kStage * kLdsTile;
 #pragma unroll
@@ -421,19 +400,6 @@ __global__ __launch_bounds__(kThreads, MIM_KNN_OCC) void knn2_i8_kernel(  // OCC
             // the parity word is read with the seeds (its LDS latency hidden behind the MFMAs), not
             // inside the rare insertion path where the compiler would sink it: one LDS round trip per event
             asm volatile("" ::"v"(pw));
-#ifdef MIM_KNN_NOSEL  // timing probe only: MFMA loop without the selection (results invalid)
-#pragma unroll
-            for (int u = 0; u < QT; ++u) {
-                int x = acc[u][0];
-#ifndef MIM_KNN_MFMAONLY  // (MFMAONLY: one accumulator read per column tile, no filter-sized VALU work)
-#pragma unroll
-                for (int g = 1; g < 16; ++g) x ^= acc[u][g];
-#endif
-                st[u].m1 = min(st[u].m1, x);
-                st[u].i1 = 0;  // a valid row: the indices feed the RANSAC gathers
-            }
-            continue;
-#endif
             // a lane's 16 R as two row groups (g 0-7, 8-15): the group minima cost one v_min more
             // than a single min chain and let an event compare the rows of the hit groups only
             int mn[QT], gmn[QT][2];
@@ -452,13 +418,6 @@ __global__ __launch_bounds__(kThreads, MIM_KNN_OCC) void knn2_i8_kernel(  // OCC
                 bm[u] = __ballot(mn[u] <= T[u]);
                 any |= bm[u];
             }
-#ifdef MIM_KNN_NOHIT  // timing probe only (results invalid): the late-tile filter without insertions
-            if (any != 0) {
-#pragma unroll
-                for (int u = 0; u < QT; ++u) st[u].m2 = min(st[u].m2, mn[u]);
-            }
-            continue;
-#endif
             // the masks are tested on the scalar unit (re-evaluating the compare as a ballot made the
             // compiler rebuild each one with a v_cndmask + v_cmp pair per event)
             if (__builtin_expect(any != 0, 0)) {  // ~1 insertion per wave and half tile
@@ -487,11 +446,7 @@ __global__ __launch_bounds__(kThreads, MIM_KNN_OCC) void knn2_i8_kernel(  // OCC
                                 }
                             }
                         }
-#ifdef MIM_KNN_EXACT_PAIR
-                        T[u] = sel_filter(st[u]);
-#else
-                        T[u] = min(max(st[u].m1, o1c[u]), min(st[u].m2, o2c[u])) >> 1;
-#endif
+                        T[u] = late_threshold(st[u], o1c[u], o2c[u]);
                     }
                 }
             }
@@ -502,31 +457,27 @@ __global__ __launch_bounds__(kThreads, MIM_KNN_OCC) void knn2_i8_kernel(  // OCC
     for (; stage < tile_e; stage += kStage) {
         const int buf = ((stage - w.tile0) / kStage) & 1;
         const bool more = stage + kStage < w.tile1;
-        if (more && !kProbeNoDma) stage_dma(stage + kStage, buf ^ 1, stage + kStage < tile_e);
+        if (more) stage_dma(stage + kStage, buf ^ 1, stage + kStage < tile_e);
         const unsigned char* sb = smem + buf * kStage * kLdsTile;
 #pragma unroll
         for (int ts = 0; ts < kStage; ++ts)
             if (kStage == 1 || stage + ts < w.tile1) tile_early(sb + ts * kLdsTile, stage + ts);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA into the next buffer landed
-        if (!kProbeNoBarrier) __syncthreads();
+        __syncthreads();
     }
     for (; stage < w.tile1; stage += kStage) {
         const int buf = ((stage - w.tile0) / kStage) & 1;
         const bool more = stage + kStage < w.tile1;
-        if (more && !kProbeNoDma) stage_dma(stage + kStage, buf ^ 1, false);
+        if (more) stage_dma(stage + kStage, buf ^ 1, false);
         const unsigned char* sb = smem + buf * kStage * kLdsTile;
         auto refresh = [&]() {  // thresholds from the partner lane's current m1, m2 (every tile: slower, r03bd)
 #pragma unroll
             for (int u = 0; u < QT; ++u) {
-#ifdef MIM_KNN_EXACT_PAIR
-                T[u] = sel_filter(st[u]);
-#else
                 const auto a = __builtin_amdgcn_permlane32_swap(st[u].m1, st[u].m1, false, false);
                 const auto b = __builtin_amdgcn_permlane32_swap(st[u].m2, st[u].m2, false, false);
                 o1c[u] = (tid & 32) ? (int)a[0] : (int)a[1];
                 o2c[u] = (tid & 32) ? (int)b[0] : (int)b[1];
-                T[u] = min(max(st[u].m1, o1c[u]), min(st[u].m2, o2c[u])) >> 1;
-#endif
+                T[u] = late_threshold(st[u], o1c[u], o2c[u]);
             }
         };
         refresh();
@@ -535,7 +486,7 @@ __global__ __launch_bounds__(kThreads, MIM_KNN_OCC) void knn2_i8_kernel(  // OCC
         for (int ts = 0; ts < kStage; ++ts)
             if (kStage == 1 || stage + ts < w.tile1) tile_late(sb + ts * kLdsTile, stage + ts);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA into the next buffer landed
-        if (!kProbeNoBarrier) __syncthreads();
+        __syncthreads();
     }
 
     // ---- merge the two lane halves (disjoint train rows of the same query), keys ----

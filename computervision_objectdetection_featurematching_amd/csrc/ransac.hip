@@ -27,6 +27,7 @@
 #include <vector>
 
 #include "../../include/mim.h"
+#include "mim_debug.h"
 #include "mim_internal.h"
 
 namespace mim {
@@ -705,7 +706,8 @@ __device__ __forceinline__ float det3xy_f(float x0, float y0, float x1, float y1
     return x0 * (y1 - y2) - y0 * (x1 - x2) + (x1 * y2 - x2 * y1);
 }
 
-__device__ __forceinline__ bool check_subset_fast(const float* s, const float* d) {
+// the fp32 decision and whether it is the fp64 one (clear); !clear: check_subset decides
+__device__ __forceinline__ bool check_subset_fp32(const float* s, const float* d, bool& clear_out) {
     bool clear = (int)collinear4_clear(s) & (int)collinear4_clear(d);  // both evaluated: no branch
     const int tt[4][3] = {{0, 1, 2}, {1, 2, 3}, {0, 2, 3}, {0, 1, 3}};
     int negative = 0;
@@ -722,7 +724,7 @@ __device__ __forceinline__ bool check_subset_fast(const float* s, const float* d
         clear &= fabsf(dB) > mB * mB * 0x1p-18f;
         negative += (dA < 0.f) != (dB < 0.f);
     }
-    if (__builtin_expect(!clear, 0)) return check_subset(s, d);
+    clear_out = clear;
     return !(negative != 0 && negative != 4);
 }
 
@@ -889,6 +891,12 @@ __device__ __forceinline__ int length_flag(long long q, const uint32_t* __restri
 // position, and checkSubset runs later for the chain's attempts only (ransac_check_kernel).
 // kPassUnknown marks such a flag: bits 1..6 valid, bit 0 not evaluated.
 constexpr int kPassUnknown = 0x80;
+// The attempt kernel only marks a position whose first 4 draws repeat an index (kNeedLen: pass bit
+// set with kPassUnknown, a combination no evaluated flag has); ransac_irr_kernel resolves the redraw
+// length of every marked position in place before anything reads the flags (and a walker that
+// meets one unresolved evaluates it, as any kPassUnknown flag).  Resolving in the attempt kernel made
+// every wave with one repeated index among its 512 positions (~80 % of them) run the redraw code.
+constexpr int kNeedLen = kPassUnknown | 1;
 
 __device__ __forceinline__ int length_flag(long long q, const uint32_t* __restrict__ stream, long long slen,
                                            unsigned N, unsigned long long M) {
@@ -915,31 +923,8 @@ __device__ __forceinline__ unsigned mod_barrett(unsigned a, unsigned m, unsigned
 
 constexpr int kAttemptPerThread = 8;  // window positions per thread (11 draws reduced for 8 attempts)
 
-constexpr int kAttemptExtra = 4;      // redraws resolved from registers (more: resolve_at)
-
-// getSubset's draw loop for the attempt whose first draw is u[j] (ptsetreg.cpp: redraw while the
-// index repeats an earlier one of the sample), over the reduced draws held in registers.  Returns
-// the draws consumed, or 0 if more than the D - j registers would be needed.
-template <int D>
-__device__ __forceinline__ int redraw_len(const unsigned (&u)[D], int j) {
-    unsigned a0 = u[j], a1 = 0, a2 = 0;
-    int c = 1, len = 0;
-#pragma unroll
-    for (int k = 1; k < D; ++k) {
-        if (k <= j) continue;
-        const unsigned v = u[k];
-        const bool dup = v == a0 || (c > 1 && v == a1) || (c > 2 && v == a2);
-        const bool take = len == 0 && !dup;
-        a1 = take && c == 1 ? v : a1;
-        a2 = take && c == 2 ? v : a2;
-        len = take && c == 3 ? k - j + 1 : len;
-        c += take ? 1 : 0;
-    }
-    return len;
-}
-
-// The block's 2048 + 15 draws are staged through LDS with coalesced 16-byte loads (a lane's own 15
-// draws at a 32-byte lane stride would touch 16 cache lines per load instruction, 15 times over).
+// The block's 2048 + 3 draws are staged through LDS with coalesced 16-byte loads (a lane's own 11
+// draws at a 32-byte lane stride would touch 12 cache lines per load instruction, 11 times over).
 constexpr int kAttemptSpan = 256 * kAttemptPerThread;  // window positions per block
 // draws per wanted iteration the sampler grids are sized for (a window is ~4.1 per iteration at
 // n = 2000 and ~4-6 on real views with n >= 128; the flag capacity allows 28: a longer window loops)
@@ -948,7 +933,7 @@ constexpr int kAttemptRateEst = 6;
 __global__ __launch_bounds__(256) void ransac_attempt_kernel(const RansacState* __restrict__ st,
                                                              const uint32_t* __restrict__ stream, long long slen,
                                                              uint8_t* __restrict__ flags, int wcap, int bpp, int c1) {
-    constexpr int D = kAttemptPerThread + 3 + kAttemptExtra;
+    constexpr int D = kAttemptPerThread + 3;  // the first 4 draws of the thread's 8 attempts
     constexpr int kStageWords = kAttemptSpan + 16;
     __shared__ __attribute__((aligned(16))) unsigned sdraw[kStageWords];
     const int p = blockIdx.x / bpp;
@@ -999,29 +984,18 @@ __global__ __launch_bounds__(256) void ransac_attempt_kernel(const RansacState* 
         for (int k = 0; k < D; ++k) u[k] = mod_barrett<false>(u[k], mB, N);
     }
     // repeated index among the 4 draws of position j: pairs at distance 1, 2, 3, each tested once
-    constexpr int D0 = kAttemptPerThread + 3;
-    bool d1[D0 - 1], d2[D0 - 2], d3[D0 - 3];
+    bool d1[D - 1], d2[D - 2], d3[D - 3];
 #pragma unroll
-    for (int k = 0; k < D0 - 1; ++k) d1[k] = u[k] == u[k + 1];
+    for (int k = 0; k < D - 1; ++k) d1[k] = u[k] == u[k + 1];
 #pragma unroll
-    for (int k = 0; k < D0 - 2; ++k) d2[k] = u[k] == u[k + 2];
+    for (int k = 0; k < D - 2; ++k) d2[k] = u[k] == u[k + 2];
 #pragma unroll
-    for (int k = 0; k < D0 - 3; ++k) d3[k] = u[k] == u[k + 3];
+    for (int k = 0; k < D - 3; ++k) d3[k] = u[k] == u[k + 3];
     uint32_t w[2] = {0, 0};
 #pragma unroll
     for (int j = 0; j < kAttemptPerThread; ++j) {
         const bool rep = d1[j] | d1[j + 1] | d1[j + 2] | d2[j] | d2[j + 1] | d3[j];
-        int f = kPassUnknown;
-        if (q0 + j + 4 > (int)slen) {
-            f = kAttemptSerial;
-        } else if (rep) {
-            int len = redraw_len(u, j);
-            if (len == 0 || q0 + j + len > (int)slen) {  // long redraw run or near the stream end
-                int idx[4];
-                len = resolve_at(q0 + j, stream, slen, N, S.modM, idx);
-            }
-            f = (len == 0 || len > 67) ? kAttemptSerial : (((len - 4) << 1) | kPassUnknown);
-        }
+        const int f = q0 + j + 4 > (int)slen ? kAttemptSerial : (rep ? kNeedLen : kPassUnknown);
         w[j >> 2] |= (uint32_t)f << (8 * (j & 3));
     }
     *reinterpret_cast<uint2*>(flags + (long long)p * wcap + off) = make_uint2(w[0], w[1]);
@@ -1077,9 +1051,10 @@ __device__ __forceinline__ int mbcnt64(unsigned long long m) {
 // attempt-by-attempt walker (ransac_sample_kernel), which resumes from the state it stores.
 // ------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void ransac_irr_kernel(const RansacState* __restrict__ st,
-                                                         const uint8_t* __restrict__ flags, int wcap, int bpp,
+                                                         uint8_t* __restrict__ flags, int wcap, int bpp,
                                                          int c1, int* __restrict__ irr, int* __restrict__ irr_cnt,
-                                                         int irr_blocks) {
+                                                         int irr_blocks, const uint32_t* __restrict__ stream,
+                                                         long long slen) {
     __shared__ int wsum[4];
     const int p = blockIdx.x / bpp, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const RansacState S = st[p];
@@ -1088,7 +1063,7 @@ __global__ __launch_bounds__(256) void ransac_irr_kernel(const RansacState* __re
     for (int b = blockIdx.x % bpp; b * kIrrBlock < wlen; b += bpp) {
     __syncthreads();  // wsum of the previous round read
     const int b0 = b * kIrrBlock;
-    const uint8_t* F = flags + (long long)p * wcap;
+    uint8_t* F = flags + (long long)p * wcap;
     const int r0 = b0 + tid * 64;  // 64 positions per thread
     uint32_t wd[16];
 #pragma unroll
@@ -1099,14 +1074,23 @@ __global__ __launch_bounds__(256) void ransac_irr_kernel(const RansacState* __re
     }
     // irregular: a repeated-index redraw (len > 4) or resolved by the walker (0xFF); positions past
     // wlen (a partial last vector) read as regular: the chain kernels never walk past wlen
-    uint64_t irrm = 0;
+    uint64_t irrm = 0, marked = 0;
 #pragma unroll
     for (int k = 0; k < 16; ++k)
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            const uint32_t f = (wd[k] >> (8 * j)) & 0x7F;
-            irrm |= (uint64_t)(f >= 2) << (4 * k + j);
+            const uint32_t f = (wd[k] >> (8 * j)) & 0xFF;
+            irrm |= (uint64_t)((f & 0x7F) >= 2) << (4 * k + j);
+            marked |= (uint64_t)(f == kNeedLen) << (4 * k + j);
         }
+    // the redraw lengths of the positions the attempt kernel marked (a repeated index: irregular)
+    for (uint64_t m = marked; m; m &= m - 1) {
+        const int bit = __builtin_ctzll(m);
+        int idx[4];
+        const int len = resolve_at(S.stream_pos + r0 + bit, stream, slen, (unsigned)S.n, S.modM, idx);
+        F[r0 + bit] = (uint8_t)((len == 0 || len > 67) ? kAttemptSerial : (((len - 4) << 1) | kPassUnknown));
+    }
+    irrm |= marked;
     const int c = __popcll(irrm);
     int incl = c;
 #pragma unroll
@@ -1367,6 +1351,9 @@ __global__ __launch_bounds__(kCheckBlock) void ransac_check_kernel(const ChainSe
                                                                    const RansacState* __restrict__ st,
                                                                    const uint32_t* __restrict__ stream, long long slen,
                                                                    uint32_t* __restrict__ pass_bits, int wcap, int bpp) {
+    __shared__ uint32_t words[kCheckBlock * kCheckPer / 32];  // the round's pass bits
+    __shared__ int def_t[kCheckBlock * kCheckPer], def_q[kCheckBlock * kCheckPer];
+    __shared__ int n_def;
     const int p = blockIdx.x / bpp, lane = threadIdx.x & 63;
     const ChainSegs* G = chains + p;
     const int T = G->T;
@@ -1387,6 +1374,7 @@ __global__ __launch_bounds__(kCheckBlock) void ransac_check_kernel(const ChainSe
         segQ[k] = G->seg_q[min(j0 + k, max(nseg - 1, 0))];
     }
     const unsigned N = (unsigned)S.n;
+    if (threadIdx.x == 0) n_def = 0;
     int q[kCheckPer];
     bool irr[kCheckPer], valid[kCheckPer];
 #pragma unroll
@@ -1419,30 +1407,56 @@ __global__ __launch_bounds__(kCheckBlock) void ransac_check_kernel(const ChainSe
     }
     int idx[kCheckPer][4];
 #pragma unroll
-    for (int r = 0; r < kCheckPer; ++r) {
+    for (int r = 0; r < kCheckPer; ++r)
 #pragma unroll
         for (int k = 0; k < 4; ++k) idx[r][k] = valid[r] ? (int)fastmod(raw[r][k], S.modM, N) : 0;
-        if (irr[r]) resolve_at(q[r], stream, slen, N, S.modM, idx[r]);  // the walk only listed resolvable ones
-    }
     const float4* P = pts + probs[p].good_off;
     float4 g[kCheckPer][4];
 #pragma unroll
     for (int r = 0; r < kCheckPer; ++r)
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            g[r][k] = P[idx[r][k]];
-        }
-    uint32_t* PB = pass_bits + (long long)p * (wcap / 32);
+        for (int k = 0; k < 4; ++k) g[r][k] = P[idx[r][k]];
+    __syncthreads();  // n_def reset
 #pragma unroll
     for (int r = 0; r < kCheckPer; ++r) {
         const float s4[8] = {g[r][0].x, g[r][0].y, g[r][1].x, g[r][1].y, g[r][2].x, g[r][2].y, g[r][3].x, g[r][3].y};
         const float t4[8] = {g[r][0].z, g[r][0].w, g[r][1].z, g[r][1].w, g[r][2].z, g[r][2].w, g[r][3].z, g[r][3].w};
-        const bool pass = valid[r] && check_subset_fast(s4, t4);  // fp64 check_subset: 0.392 -> 0.355 ms (C3)
-        const unsigned long long m = __ballot(pass);
-        const int w0 = (base + r * kCheckBlock + (threadIdx.x & ~63)) >> 5;  // 2 words per wave
-        if (lane == 0 && w0 * 32 < T) PB[w0] = (uint32_t)m;
-        if (lane == 32 && (w0 + 1) * 32 < T) PB[w0 + 1] = (uint32_t)(m >> 32);
+        bool clear;
+        const bool pass32 = check_subset_fp32(s4, t4, clear);
+        // deferred to the block's second pass: the redraw attempts (their indices need the walk over the
+        // stream) and the samples fp32 cannot decide; in place they made most waves run both slow paths
+        const bool defer = valid[r] && (irr[r] || !clear);
+        const unsigned long long m = __ballot(valid[r] && !defer && pass32);
+        const int wl = (r * kCheckBlock + (threadIdx.x & ~63)) >> 5;  // the wave's 2 words of the block's
+        if (lane == 0) words[wl] = (uint32_t)m;
+        if (lane == 32) words[wl + 1] = (uint32_t)(m >> 32);
+        if (defer) {
+            const int slot = atomicAdd(&n_def, 1);
+            def_t[slot] = r * kCheckBlock + threadIdx.x;
+            def_q[slot] = irr[r] ? -q[r] - 1 : q[r];
+        }
     }
+    __syncthreads();
+    for (int e = threadIdx.x; e < n_def; e += kCheckBlock) {  // one deferred attempt per thread
+        const int tl = def_t[e], qe = def_q[e];
+        const long long qq = qe < 0 ? -(long long)qe - 1 : qe;
+        int ix[4];
+        if (qe < 0) {
+            resolve_at(qq, stream, slen, N, S.modM, ix);  // the walk only listed resolvable ones
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) ix[k] = (int)fastmod(stream[qq + k], S.modM, N);
+        }
+        const float4 a = P[ix[0]], bp = P[ix[1]], c = P[ix[2]], d = P[ix[3]];
+        const float s4[8] = {a.x, a.y, bp.x, bp.y, c.x, c.y, d.x, d.y};
+        const float t4[8] = {a.z, a.w, bp.z, bp.w, c.z, c.w, d.z, d.w};
+        if (check_subset(s4, t4)) atomicOr(&words[tl >> 5], 1u << (tl & 31));
+    }
+    __syncthreads();
+    uint32_t* PB = pass_bits + (long long)p * (wcap / 32);
+    if (threadIdx.x < kCheckBlock * kCheckPer / 32 && (base + 32 * (int)threadIdx.x) < T)
+        PB[(base >> 5) + threadIdx.x] = words[threadIdx.x];
+    __syncthreads();  // words / n_def reused by the next round
     }
 }
 
@@ -2465,12 +2479,6 @@ __global__ __launch_bounds__(256) void ransac_bound_mfma_kernel(const RansacStat
     const double aw = (fabs(Hd[6]) + fabs(Hd[7])) * mx + 1.0;
     const float A = (float)(gam * (ax + (mu + 6.0) * aw) * S.sb * sc * (1.0 + 1e-6));
     const float E = (1.f + C) * kMfmaErr * (1.f + 1e-6f) + A;
-#ifdef MIM_BOUND_DEBUG_IT
-    if (act && it == MIM_BOUND_DEBUG_IT)
-        printf("[mim] hyp it=%d e=%d sa=%g sb=%g C=%.9g A=%.9g E=%.9g eta=%g eta_model=%g count=%d h'=%.9g %.9g %.9g %.9g %.9g %.9g %.9g %.9g %.9g\n",
-               it, e, (double)S.sa, (double)S.sb, (double)C, (double)A, (double)E, (double)eta, eta_model, (int)count,
-               h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], h[8]);
-#endif
     float CL = 0.f, EL = 0.f;
     if (kLo) {
         float tl = thr2 - fmaf(1e-7f * S.smax, S.smax, 0.5f);
@@ -2522,13 +2530,6 @@ __global__ __launch_bounds__(256) void ransac_bound_mfma_kernel(const RansacStat
         const float CLp = __shfl_xor(CL, 32), ELp = __shfl_xor(EL, 32);
         CL0 = lowh ? CL : CLp; EL0 = lowh ? EL : ELp; CL1 = lowh ? CLp : CL; EL1 = lowh ? ELp : EL;
     }
-#ifdef MIM_BOUND_DEBUG_IT
-    if (act && it == MIM_BOUND_DEBUG_IT)
-        printf("[mim] frag it=%d lane=%d fy=%g %g %g %g %g %g %g %g fn=%g %g %g %g %g %g %g %g b0y=%g %g %g %g %g %g %g %g\n", it, lane,
-               (double)fy[0], (double)fy[1], (double)fy[2], (double)fy[3], (double)fy[4], (double)fy[5], (double)fy[6], (double)fy[7],
-               (double)fn[0], (double)fn[1], (double)fn[2], (double)fn[3], (double)fn[4], (double)fn[5], (double)fn[6], (double)fn[7],
-               (double)b0y[0], (double)b0y[1], (double)b0y[2], (double)b0y[3], (double)b0y[4], (double)b0y[5], (double)b0y[6], (double)b0y[7]);
-#endif
     const bool wave_counts = __any(count);
     float big = INFINITY;
     asm volatile("" : "+v"(big));
@@ -2554,13 +2555,6 @@ __global__ __launch_bounds__(256) void ransac_bound_mfma_kernel(const RansacStat
           for (int t = 0; t < tc; ++t) {
             const h8v ax = __builtin_bit_cast(h8v, lt[buf][t * 128 + lane]);
             const h8v ay = __builtin_bit_cast(h8v, lt[buf][t * 128 + 64 + lane]);
-#ifdef MIM_BOUND_DEBUG_IT
-            if (((t0 + t) * 32 + (lane & 31)) == MIM_BOUND_DEBUG_PT && kb == (MIM_BOUND_DEBUG_IT - c0) / 256 &&
-                (tid >> 6) == ((MIM_BOUND_DEBUG_IT - c0) % 256) / 64)
-                printf("[mim] tile pt=%d lane=%d ax=%g %g %g %g %g %g %g %g ay=%g %g %g %g %g %g %g %g\n", MIM_BOUND_DEBUG_PT, lane,
-                       (double)ax[0], (double)ax[1], (double)ax[2], (double)ax[3], (double)ax[4], (double)ax[5], (double)ax[6], (double)ax[7],
-                       (double)ay[0], (double)ay[1], (double)ay[2], (double)ay[3], (double)ay[4], (double)ay[5], (double)ay[6], (double)ay[7]);
-#endif
             const f16acc zc = {};
             const f16acc ex0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ax, b0x, zc, 0, 0, 0);
             const f16acc ey0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ay, b0y, zc, 0, 0, 0);
@@ -2580,20 +2574,6 @@ __global__ __launch_bounds__(256) void ransac_bound_mfma_kernel(const RansacStat
                 const float d1 = fmaf(C1, fabsf(w1[r]), E1) - m1;
                 bits0 = __builtin_amdgcn_alignbit(bits0, __float_as_uint(d0), 31);
                 bits1 = __builtin_amdgcn_alignbit(bits1, __float_as_uint(d1), 31);
-#ifdef MIM_BOUND_DEBUG_IT  // debug build: the box test of one (iteration, point)
-                {
-                    const int row = (t0 + t) * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-                    const int itb = c0 + kb * 256 + (tid & ~63);  // the wave's first iteration
-                    for (int cb = 0; cb < 2; ++cb) {
-                        const int itc = itb + 32 * cb + (lane & 31);
-                        if (itc == MIM_BOUND_DEBUG_IT && row == MIM_BOUND_DEBUG_PT)
-                            printf("[mim] box it=%d pt=%d ex=%.9g ey=%.9g W=%.9g C=%.9g E=%.9g d=%.9g\n", itc, row,
-                                   (double)(cb ? ex1[r] : ex0[r]), (double)(cb ? ey1[r] : ey0[r]),
-                                   (double)(cb ? w1[r] : w0[r]), (double)(cb ? C1 : C0), (double)(cb ? E1 : E0),
-                                   (double)(cb ? d1 : d0));
-                    }
-                }
-#endif
                 if (kLo) {  // sign bit of max(|ex|, |ey|, (|ex| + |ey|) / sqrt 2) - R_lo: set when surely in
                     const float o0 = __builtin_amdgcn_fmed3f(m0, (fabsf(ex0[r]) + fabsf(ey0[r])) * 0.70710677f, big);
                     const float o1 = __builtin_amdgcn_fmed3f(m1, (fabsf(ex1[r]) + fabsf(ey1[r])) * 0.70710677f, big);
@@ -3168,12 +3148,6 @@ __device__ double inv_diag_max8(const double (&w)[8], const int (&perm)[8], cons
     return maxval;
 }
 
-#ifdef MIM_REFINE_PROF  // debug build: phase times (shader cycles) of problem 0's refine
-#define RPROF(name) do { const long long t_ = (long long)__builtin_amdgcn_s_memtime(); \
-    if (p == 0 && tid == 0) printf("[refine-prof] %s %lld\n", name, t_ - rp_t0); } while (0)
-#else
-#define RPROF(name) do { } while (0)
-#endif
 struct RefineShared {  // one per wave (problem)
     double red[2];
     double lt[45];
@@ -3281,18 +3255,11 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                 base += __popcll(bal);
             }
             if (tid == 0) sh.n_inl = base;
-#ifdef MIM_REFINE_DEBUG  // debug build: the best model's mask must hold maxGoodCount inliers
-            if (tid == 0 && base != S.max_good)
-                printf("[refine] p=%d n=%d max_good=%d mask=%d best_iter=%d niters=%d produced=%d fail=%d from_best_h=%d\n",
-                       p, S.n, S.max_good, base, S.best_iter, S.niters, S.produced, S.fail_iter,
-                       (int)(!exact_all && best_h[(long long)p * 9 + 8] != 0.0));
-#endif
+            if (tid == 0)  // the best model's mask holds maxGoodCount inliers
+                MIM_DEBUG_CHECK(base == S.max_good, "[refine] p=%d n=%d max_good=%d mask=%d best_iter=%d niters=%d\n",
+                                p, S.n, S.max_good, base, S.best_iter, S.niters);
             wsync();
             const int k = sh.n_inl;
-#ifdef MIM_REFINE_PROF
-            const long long rp_t0 = (long long)__builtin_amdgcn_s_memtime();
-            if (p == 0 && tid == 0) printf("[refine-prof] inliers %d\n", k);
-#endif
             if (k > 0) {
                 // ---- refit: runKernel over all inliers, OpenCV's sequential sums (fundam.cpp) ----
                 if (tid < 4) {  // centroids cm (scene), cM (object): one sequential sum each
@@ -3348,9 +3315,7 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                     const double Hnorm2[9] = {sMx, 0, -cMx * sMx, 0, sMy, -cMy * sMy, 0, 0, 1};
                     if (tid < 16) {  // the Jacobi of runKernel, one 16-lane group (bit-identical)
                         double Hl[9];
-                        RPROF("refit_sums");
                         dlt_finish_group(sh.lt, sh.J9, invHnorm, Hnorm2, Hl);
-                        RPROF("refit_jacobi9");
                         if (tid == 0)
                             for (int i = 0; i < 9; ++i) sh.H[i] = Hl[i];
                     }
@@ -3365,7 +3330,6 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                 for (int i = 0; i < 8; ++i) x[i] = sh.x[i];
                 double rinf;
                 lm_normal(X, k, x, sh.lm, sh.nrm, rinf);
-                RPROF("lm_normal0");
                 if (tid == 0) {
                     int e = 0;
                     for (int a = 0; a < 8; ++a)
@@ -3384,9 +3348,7 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                         __builtin_amdgcn_wave_barrier();
                         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
                         double dl[8];
-                        RPROF("iter_start");
                         solve_eig8(sh.Ap, sh.v, dl, sh.J9, ew, eperm);
-                        RPROF("eig8");
                         if (tid == 0) {
                             double dinf = 0;
                             for (int i = 0; i < 8; ++i) {
@@ -3401,7 +3363,6 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                     double xd[8];
                     for (int i = 0; i < 8; ++i) xd[i] = sh.xd[i];
                     const double Sd = lm_cost(X, k, xd, sh.lm, sh.red);
-                    RPROF("lm_cost");
                     if (tid < 16) {  // every slot evaluates the same update; slot 0 stores it
                         const double Rlo = 0.25, Rhi = 0.75;
                         double lambda = sh.lambda, lc = sh.lc;
@@ -3444,7 +3405,6 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                     if (sh.accept) {
                         for (int i = 0; i < 8; ++i) x[i] = sh.x[i];
                         lm_normal(X, k, x, sh.lm, sh.nrm, rinf);
-                        RPROF("lm_normal");
                         if (tid == 0) {
                             int e = 0;
                             for (int a = 0; a < 8; ++a)
@@ -3460,7 +3420,6 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                     wsync();
                     if (!proceed) break;
                 }
-                RPROF("lm_done");
                 if (tid < 8) sh.H[tid] = sh.x[tid];
                 wsync();
             } else if (tid == 0) {
@@ -3567,7 +3526,7 @@ void ransac_enqueue(const RansacParams& prm, int n_probs, const ProbDev* probs, 
             ChainSegs* chains = reinterpret_cast<ChainSegs*>(b.chains);
             const int bpp_irr = (west + kIrrBlock - 1) / kIrrBlock;
             ransac_irr_kernel<<<n_probs * bpp_irr, 256, 0, ss>>>(b.state, b.flags, wcap, bpp_irr, c1, b.irr,
-                                                               b.irr_cnt, b.irr_blocks);
+                                                               b.irr_cnt, b.irr_blocks, b.stream, b.stream_len);
             ransac_walk_kernel<<<n_probs, kChainThreads, 0, ss>>>(b.state, b.flags, wcap, c1, b.irr, b.irr_cnt,
                                                                  b.irr_blocks, chains);
             mark(mark_ctx, "chain", ss);

@@ -76,6 +76,20 @@ class Detector {
     // All (model, scale, view) problems of one scene in one device batch.
     // out[m] receives model m's allUnfilteredScenePts in the reference's order: scales outer,
     // views inner (TestsDetector.cpp:100 wraps :58).
+    // TestsDetector.cpp:99-107 and the scene's batch from the grayscale scene itself (CV_8UC1 rows x cols,
+    // row stride `step`): resize + SIFT of every scale on the device, the scene's descriptors registered
+    // there as sets (mim_sift_scales_sets: they never leave the GPU), then detect_scene's batch.
+    void detect_scene_gray(const std::vector<const ModelViews*>& models, const uint8_t* gray, int rows, int cols,
+                           int64_t step, const std::vector<float>& scales, std::vector<std::vector<Point2f>>& out) {
+        out.assign(models.size(), {});
+        register_models(models);
+        std::vector<int32_t> ids(scales.size()), n(scales.size());
+        check(mim_sift_scales_sets(ctx_, gray, rows, cols, step, (int32_t)scales.size(), scales.data(), ids.data(),
+                                   n.data(), 0, nullptr),
+              "mim_sift_scales_sets", ctx_);
+        run_sets(models, ids, scales, out);
+    }
+
     void detect_scene(const std::vector<const ModelViews*>& models, const std::vector<ScaledScene>& scales,
                       std::vector<std::vector<Point2f>>& out) {
         out.assign(models.size(), {});
@@ -135,31 +149,57 @@ class Detector {
         if (s != MIM_OK) throw Error(s, std::string(what) + ": " + (c ? mim_last_error(c) : "failed"));
     }
 
-    void run(const std::vector<const ModelViews*>& models, const std::vector<ScaledScene>& scales,
-             std::vector<std::vector<Point2f>>& out) {
+    // The model views stay registered across scenes (the models are loaded once, main.cpp:22): a call
+    // with the same models (same objects, view counts and descriptor storage) drops only the previous
+    // scene's sets (mim_sets_truncate) instead of re-uploading and re-preparing every view.
+    void register_models(const std::vector<const ModelViews*>& models) {
+        std::vector<RegKey> key;
+        for (const ModelViews* m : models)
+            key.push_back({m, m->views.size(), m->views.empty() ? nullptr : m->views[0].descriptors.data()});
+        if (reg_n_ >= 0 && key == reg_key_) {
+            check(mim_sets_truncate(ctx_, reg_n_), "mim_sets_truncate", ctx_);
+            return;
+        }
         check(mim_sets_clear(ctx_), "mim_sets_clear", ctx_);
-        std::vector<std::vector<int32_t>> view_ids(models.size());
+        reg_ids_.assign(models.size(), {});
+        reg_n_ = 0;
         for (size_t m = 0; m < models.size(); ++m)
             for (const View& v : models[m]->views) {
                 int32_t id;
                 check(mim_set_create(ctx_, v.descriptors.data(), v.keypoints.empty() ? nullptr : &v.keypoints[0].x,
                                      v.size(), 128, 0, &id),
                       "mim_set_create", ctx_);
-                view_ids[m].push_back(id);
+                reg_ids_[m].push_back(id);
+                reg_n_ = id + 1;
             }
+        reg_key_ = key;
+    }
+
+    void run(const std::vector<const ModelViews*>& models, const std::vector<ScaledScene>& scales,
+             std::vector<std::vector<Point2f>>& out) {
+        register_models(models);
         std::vector<int32_t> scene_ids;
+        std::vector<float> sv;
         for (const ScaledScene& s : scales) {
             int32_t id;
             check(mim_set_create(ctx_, s.desc->data(), s.kp->empty() ? nullptr : &(*s.kp)[0].x, (int32_t)s.kp->size(),
                                  128, 0, &id),
                   "mim_set_create", ctx_);
             scene_ids.push_back(id);
+            sv.push_back(s.scale);
         }
+        run_sets(models, scene_ids, sv, out);
+    }
+
+    // one batch over every (model, scale, view) problem: the registered views against the scene's sets
+    void run_sets(const std::vector<const ModelViews*>& models, const std::vector<int32_t>& scene_ids,
+                  const std::vector<float>& scale_of, std::vector<std::vector<Point2f>>& out) {
+        const std::vector<std::vector<int32_t>>& view_ids = reg_ids_;
         struct Tag { size_t m, s, v; };
         std::vector<mim_problem> probs;
         std::vector<Tag> tags;
         for (size_t m = 0; m < models.size(); ++m)
-            for (size_t s = 0; s < scales.size(); ++s)
+            for (size_t s = 0; s < scene_ids.size(); ++s)
                 for (size_t v = 0; v < view_ids[m].size(); ++v) {
                     probs.push_back({view_ids[m][v], scene_ids[s]});
                     tags.push_back({m, s, v});
@@ -172,7 +212,7 @@ class Detector {
         // when it is not 1, gathered on the device in batch order (one copy); model m's problems are
         // contiguous in the batch, so its points are one slice
         std::vector<float> sc(probs.size());
-        for (size_t i = 0; i < probs.size(); ++i) sc[i] = scales[tags[i].s].scale;
+        for (size_t i = 0; i < probs.size(); ++i) sc[i] = scale_of[tags[i].s];
         std::vector<int64_t> offs(probs.size() + 1);
         check(mim_batch_inlier_points(ctx_, sc.data(), nullptr, 0, offs.data()), "mim_batch_inlier_points", ctx_);
         std::vector<Point2f> pts((size_t)offs.back());
@@ -183,9 +223,18 @@ class Detector {
             out[tags[i].m].insert(out[tags[i].m].end(), pts.begin() + offs[i], pts.begin() + offs[i + 1]);
     }
 
+    struct RegKey {
+        const ModelViews* m;
+        size_t n_views;
+        const float* first_desc;
+        bool operator==(const RegKey& o) const { return m == o.m && n_views == o.n_views && first_desc == o.first_desc; }
+    };
     mim_ctx* ctx_ = nullptr;
     mim_params params_;
     std::vector<mim_result> results_;
+    std::vector<RegKey> reg_key_;  // the models whose views are the ctx's first reg_n_ sets
+    std::vector<std::vector<int32_t>> reg_ids_;
+    int32_t reg_n_ = -1;
 };
 
 }  // namespace mim

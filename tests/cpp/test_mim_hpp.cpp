@@ -85,8 +85,82 @@ int main() {
             std::printf("FAIL at %zu\n", i);
             return 1;
         }
+    // the same scene again: the model's views stay registered (mim_sets_truncate), same points
+    std::vector<std::vector<mim::Point2f>> again;
+    det.detect_scene({&model}, {{&skp[0], &sdesc[0], scales[0]}, {&skp[1], &sdesc[1], scales[1]}}, again);
+    if (again.size() != 1 || again[0].size() != out[0].size()) {
+        std::printf("FAIL repeat size\n");
+        return 1;
+    }
+    for (size_t i = 0; i < out[0].size(); ++i)
+        if (again[0][i].x != out[0][i].x || again[0][i].y != out[0][i].y) {
+            std::printf("FAIL repeat at %zu\n", i);
+            return 1;
+        }
     std::printf("OK %zu inlier points, statuses:", ref.size());
     for (auto& r : det.last_results()) std::printf(" %d/%d/%d", r.n_good, r.n_inl, r.status);
     std::printf("\n");
-    return ref.empty() ? 1 : 0;
+    if (ref.empty()) return 1;
+
+    // detect_scene_gray (SIFT of the scales left on the device as the batch's sets) equals
+    // detect_scene on the host copies of the same SIFT: a smooth synthetic scene and two model views
+    // described from crops of it
+    const int R = 240, Cc = 320;
+    std::vector<uint8_t> img((size_t)R * Cc);
+    std::mt19937 g2(3);
+    std::uniform_real_distribution<double> ur(0, 1);
+    std::vector<double> acc((size_t)R * Cc, 110.0);
+    for (int b = 0; b < 60; ++b) {
+        const double cy = ur(g2) * R, cx = ur(g2) * Cc, sg = 1.5 + ur(g2) * 18, a = (ur(g2) - 0.5) * 180;
+        for (int y = 0; y < R; ++y)
+            for (int x = 0; x < Cc; ++x) acc[(size_t)y * Cc + x] += a * std::exp(-((y - cy) * (y - cy) + (x - cx) * (x - cx)) / (2 * sg * sg));
+    }
+    for (size_t i = 0; i < img.size(); ++i) img[i] = (uint8_t)std::min(255.0, std::max(0.0, std::rint(acc[i] + (ur(g2) - 0.5) * 6)));
+    mim::ModelViews crops{"crops", {}};
+    for (int v = 0; v < 2; ++v) {
+        const int y0 = 20 + 60 * v, x0 = 30 + 90 * v, h = 140, w = 160;
+        std::vector<uint8_t> crop((size_t)h * w);
+        for (int y = 0; y < h; ++y)
+            for (int x = 0; x < w; ++x) crop[(size_t)y * w + x] = img[(size_t)(y0 + y) * Cc + x0 + x];
+        std::vector<mim_keypoint> kk;
+        mim::View view;
+        det.sift(crop.data(), h, w, w, nullptr, 0, kk, view.descriptors);
+        for (auto& k : kk) view.keypoints.push_back({k.x, k.y});
+        crops.views.push_back(std::move(view));
+    }
+    const std::vector<float> sc5 = {0.7f, 0.85f, 1.0f, 1.15f, 1.3f};
+    std::vector<std::vector<mim_keypoint>> hk;
+    std::vector<std::vector<float>> hd;
+    det.sift_scales(img.data(), R, Cc, Cc, sc5, hk, hd);
+    std::vector<std::vector<mim::Point2f>> hkp(sc5.size());
+    std::vector<mim::Detector::ScaledScene> ss;
+    for (size_t s = 0; s < sc5.size(); ++s) {
+        for (auto& k : hk[s]) hkp[s].push_back({k.x, k.y});
+        ss.push_back({&hkp[s], &hd[s], sc5[s]});
+    }
+    std::vector<std::vector<mim::Point2f>> host_pts, dev_pts;
+    det.detect_scene({&crops}, ss, host_pts);
+    const std::vector<mim_result> host_res = det.last_results();
+    det.detect_scene_gray({&crops}, img.data(), R, Cc, Cc, sc5, dev_pts);
+    const std::vector<mim_result>& dev_res = det.last_results();
+    if (host_res.size() != dev_res.size() || host_pts[0].size() != dev_pts[0].size()) {
+        std::printf("FAIL gray path: %zu/%zu problems, %zu/%zu points\n", host_res.size(), dev_res.size(),
+                    host_pts[0].size(), dev_pts[0].size());
+        return 1;
+    }
+    for (size_t i = 0; i < host_res.size(); ++i)
+        if (host_res[i].n_good != dev_res[i].n_good || host_res[i].n_inl != dev_res[i].n_inl ||
+            host_res[i].status != dev_res[i].status || host_res[i].iters != dev_res[i].iters) {
+            std::printf("FAIL gray path record %zu\n", i);
+            return 1;
+        }
+    for (size_t i = 0; i < host_pts[0].size(); ++i)
+        if (host_pts[0][i].x != dev_pts[0][i].x || host_pts[0][i].y != dev_pts[0][i].y) {
+            std::printf("FAIL gray path point %zu\n", i);
+            return 1;
+        }
+    int accepted = 0;
+    for (auto& r : dev_res) accepted += r.status == 0;
+    std::printf("OK gray path: %zu problems, %d accepted, %zu points\n", dev_res.size(), accepted, dev_pts[0].size());
+    return accepted > 0 ? 0 : 1;
 }

@@ -30,4 +30,4 @@ def test_cpp_host_matches_reference_loop(tmp_path):
     r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
     print(r.stdout, r.stderr)
     assert r.returncode == 0, r.stdout + r.stderr
-    assert r.stdout.startswith("OK")
+    assert r.stdout.startswith("OK") and "OK gray path" in r.stdout

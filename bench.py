@@ -83,7 +83,7 @@ def pmc_traffic(kernel, config):
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=60)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="c4", choices=["c1", "c1img", "c2", "c3", "c4", "c5", "dataset"])
     ap.add_argument("--cpu-sample", type=int, default=6,

@@ -891,12 +891,6 @@ __device__ __forceinline__ int length_flag(long long q, const uint32_t* __restri
 // position, and checkSubset runs later for the chain's attempts only (ransac_check_kernel).
 // kPassUnknown marks such a flag: bits 1..6 valid, bit 0 not evaluated.
 constexpr int kPassUnknown = 0x80;
-// The attempt kernel only marks a position whose first 4 draws repeat an index (kNeedLen: pass bit
-// set with kPassUnknown, a combination no evaluated flag has); ransac_irr_kernel resolves the redraw
-// length of every marked position in place before anything reads the flags (and a walker that
-// meets one unresolved evaluates it, as any kPassUnknown flag).  Resolving in the attempt kernel made
-// every wave with one repeated index among its 512 positions (~80 % of them) run the redraw code.
-constexpr int kNeedLen = kPassUnknown | 1;
 
 __device__ __forceinline__ int length_flag(long long q, const uint32_t* __restrict__ stream, long long slen,
                                            unsigned N, unsigned long long M) {
@@ -908,6 +902,31 @@ __device__ __forceinline__ int length_flag(long long q, const uint32_t* __restri
         return kPassUnknown;
     const int len = resolve_at(q, stream, slen, N, M, idx);
     return (len == 0 || len > 67) ? kAttemptSerial : (((len - 4) << 1) | kPassUnknown);
+}
+
+// getSubset's redraw loop for the attempt at q with its draws from draw(i) = stream[q + i]: the draws
+// consumed (> 67: resolve serially; 0: the stream ends first), as resolve_at
+template <class Draw>
+__device__ __forceinline__ int redraw_len(Draw&& draw, long long q, long long slen, unsigned N, unsigned long long M) {
+    int idx[4] = {0, 0, 0, 0};
+    int r = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        for (;;) {
+            if (q + r >= slen) return 0;
+            if (r > 67) return r;
+            const int v = (int)fastmod(draw(r), M, N);
+            ++r;
+            bool dup = false;
+#pragma unroll
+            for (int j = 0; j < i; ++j) dup |= idx[j] == v;
+            if (!dup) {
+                idx[i] = v;
+                break;
+            }
+        }
+    }
+    return r;
 }
 
 // RNG::uniform(0, n) = next() % n by Barrett reduction: m = floor((2^32 - 1) / n) >= 2^32/n - 1, so
@@ -936,6 +955,9 @@ __global__ __launch_bounds__(256) void ransac_attempt_kernel(const RansacState* 
     constexpr int D = kAttemptPerThread + 3;  // the first 4 draws of the thread's 8 attempts
     constexpr int kStageWords = kAttemptSpan + 16;
     __shared__ __attribute__((aligned(16))) unsigned sdraw[kStageWords];
+    __shared__ int rep_pos[kAttemptSpan];
+    __shared__ uint8_t rep_flag[kAttemptSpan];
+    __shared__ int n_rep;
     const int p = blockIdx.x / bpp;
     const RansacState S = st[p];
     if (!S.active || S.done || S.fail_iter != -1 || S.n < kSmallMaxN || S.produced >= min(c1, S.niters)) return;
@@ -960,8 +982,8 @@ __global__ __launch_bounds__(256) void ransac_attempt_kernel(const RansacState* 
     }
     __syncthreads();
     const int off = boff + threadIdx.x * kAttemptPerThread;
-    if (off >= wlen) continue;  // past the window (the next round's barriers are reached from the loop latch)
-    const int q0 = qb + threadIdx.x * kAttemptPerThread;
+    const int q0 = qb + threadIdx.x * kAttemptPerThread;  // (a thread past the window computes and stores nothing
+                                                          // but joins the block's barriers)
     const unsigned N = (unsigned)S.n, mB = 0xFFFFFFFFu / N;
     const bool big = N > 256 && N < (1u << 24);  // q and n both fit 24 bits
     unsigned u[D];
@@ -991,14 +1013,42 @@ __global__ __launch_bounds__(256) void ransac_attempt_kernel(const RansacState* 
     for (int k = 0; k < D - 2; ++k) d2[k] = u[k] == u[k + 2];
 #pragma unroll
     for (int k = 0; k < D - 3; ++k) d3[k] = u[k] == u[k + 3];
+    // repeated index among the first 4 draws (~0.3 % of positions at n = 2000): the redraw length is
+    // resolved after the block's pass, the block's such positions one per thread from the staged draws
+    // (resolved in place, every wave holding one of them, ~80 % of the waves, ran the redraw loop)
     uint32_t w[2] = {0, 0};
+    unsigned repm = 0;
 #pragma unroll
     for (int j = 0; j < kAttemptPerThread; ++j) {
         const bool rep = d1[j] | d1[j + 1] | d1[j + 2] | d2[j] | d2[j + 1] | d3[j];
-        const int f = q0 + j + 4 > (int)slen ? kAttemptSerial : (rep ? kNeedLen : kPassUnknown);
-        w[j >> 2] |= (uint32_t)f << (8 * (j & 3));
+        const bool tail = q0 + j + 4 > (int)slen;
+        repm |= (unsigned)(rep && !tail && off < wlen) << j;
+        w[j >> 2] |= (uint32_t)(tail ? kAttemptSerial : kPassUnknown) << (8 * (j & 3));
     }
-    *reinterpret_cast<uint2*>(flags + (long long)p * wcap + off) = make_uint2(w[0], w[1]);
+    if (threadIdx.x == 0) n_rep = 0;
+    __syncthreads();
+    int my_slot = 0;
+    if (repm) my_slot = atomicAdd(&n_rep, __popc(repm));
+    __syncthreads();
+    const int nr = min(n_rep, kAttemptSpan);
+    if (nr > 0) {
+        // each thread's repeated positions take consecutive slots from my_slot, in position order
+        for (unsigned m = repm, sl = my_slot; m; m &= m - 1, ++sl) rep_pos[sl] = threadIdx.x * kAttemptPerThread + __builtin_ctz(m);
+        __syncthreads();
+        for (int e = threadIdx.x; e < nr; e += 256) {
+            const int lp = rep_pos[e];  // block-local position: its draws at sdraw[lp ..]
+            const long long q = qb + lp;
+            const int len = redraw_len([&](int i) { return lp + i < kStageWords ? sdraw[lp + i] : stream[min(q + i, slen - 1)]; },
+                                       q, slen, N, S.modM);
+            rep_flag[e] = (uint8_t)((len == 0 || len > 67) ? kAttemptSerial : (((len - 4) << 1) | kPassUnknown));
+        }
+        __syncthreads();
+        for (unsigned m = repm, sl = my_slot; m; m &= m - 1, ++sl) {
+            const int j = __builtin_ctz(m);
+            w[j >> 2] = (w[j >> 2] & ~(0xFFu << (8 * (j & 3)))) | ((uint32_t)rep_flag[sl] << (8 * (j & 3)));
+        }
+    }
+    if (off < wlen) *reinterpret_cast<uint2*>(flags + (long long)p * wcap + off) = make_uint2(w[0], w[1]);
     }
 }
 
@@ -1051,10 +1101,9 @@ __device__ __forceinline__ int mbcnt64(unsigned long long m) {
 // attempt-by-attempt walker (ransac_sample_kernel), which resumes from the state it stores.
 // ------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void ransac_irr_kernel(const RansacState* __restrict__ st,
-                                                         uint8_t* __restrict__ flags, int wcap, int bpp,
+                                                         const uint8_t* __restrict__ flags, int wcap, int bpp,
                                                          int c1, int* __restrict__ irr, int* __restrict__ irr_cnt,
-                                                         int irr_blocks, const uint32_t* __restrict__ stream,
-                                                         long long slen) {
+                                                         int irr_blocks) {
     __shared__ int wsum[4];
     const int p = blockIdx.x / bpp, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const RansacState S = st[p];
@@ -1063,7 +1112,7 @@ __global__ __launch_bounds__(256) void ransac_irr_kernel(const RansacState* __re
     for (int b = blockIdx.x % bpp; b * kIrrBlock < wlen; b += bpp) {
     __syncthreads();  // wsum of the previous round read
     const int b0 = b * kIrrBlock;
-    uint8_t* F = flags + (long long)p * wcap;
+    const uint8_t* F = flags + (long long)p * wcap;
     const int r0 = b0 + tid * 64;  // 64 positions per thread
     uint32_t wd[16];
 #pragma unroll
@@ -1074,23 +1123,11 @@ __global__ __launch_bounds__(256) void ransac_irr_kernel(const RansacState* __re
     }
     // irregular: a repeated-index redraw (len > 4) or resolved by the walker (0xFF); positions past
     // wlen (a partial last vector) read as regular: the chain kernels never walk past wlen
-    uint64_t irrm = 0, marked = 0;
+    uint64_t irrm = 0;
 #pragma unroll
     for (int k = 0; k < 16; ++k)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const uint32_t f = (wd[k] >> (8 * j)) & 0xFF;
-            irrm |= (uint64_t)((f & 0x7F) >= 2) << (4 * k + j);
-            marked |= (uint64_t)(f == kNeedLen) << (4 * k + j);
-        }
-    // the redraw lengths of the positions the attempt kernel marked (a repeated index: irregular)
-    for (uint64_t m = marked; m; m &= m - 1) {
-        const int bit = __builtin_ctzll(m);
-        int idx[4];
-        const int len = resolve_at(S.stream_pos + r0 + bit, stream, slen, (unsigned)S.n, S.modM, idx);
-        F[r0 + bit] = (uint8_t)((len == 0 || len > 67) ? kAttemptSerial : (((len - 4) << 1) | kPassUnknown));
-    }
-    irrm |= marked;
+        for (int j = 0; j < 4; ++j) irrm |= (uint64_t)((((wd[k] >> (8 * j)) & 0x7F)) >= 2) << (4 * k + j);
     const int c = __popcll(irrm);
     int incl = c;
 #pragma unroll
@@ -3526,7 +3563,7 @@ void ransac_enqueue(const RansacParams& prm, int n_probs, const ProbDev* probs, 
             ChainSegs* chains = reinterpret_cast<ChainSegs*>(b.chains);
             const int bpp_irr = (west + kIrrBlock - 1) / kIrrBlock;
             ransac_irr_kernel<<<n_probs * bpp_irr, 256, 0, ss>>>(b.state, b.flags, wcap, bpp_irr, c1, b.irr,
-                                                               b.irr_cnt, b.irr_blocks, b.stream, b.stream_len);
+                                                               b.irr_cnt, b.irr_blocks);
             ransac_walk_kernel<<<n_probs, kChainThreads, 0, ss>>>(b.state, b.flags, wcap, c1, b.irr, b.irr_cnt,
                                                                  b.irr_blocks, chains);
             mark(mark_ctx, "chain", ss);

@@ -766,7 +766,8 @@ __device__ __forceinline__ int resolve_at(long long q, const uint32_t* __restric
     long long bq = q, r = q;
 #pragma unroll
     for (int k = 0; k < 8; ++k) buf[k] = stream[min(q + k, slen - 1)];  // unconditional: one latency
-    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {  // unrolled: idx stays in registers
         for (;;) {
             if (r >= slen) return 0;
             if (r >= bq + 8) {
@@ -780,6 +781,7 @@ __device__ __forceinline__ int resolve_at(long long q, const uint32_t* __restric
             ++r;
             const int v = (int)fastmod(raw, M, N);
             bool dup = false;
+#pragma unroll
             for (int j = 0; j < i; ++j) dup |= idx[j] == v;
             if (!dup) {
                 idx[i] = v;
@@ -904,31 +906,6 @@ __device__ __forceinline__ int length_flag(long long q, const uint32_t* __restri
     return (len == 0 || len > 67) ? kAttemptSerial : (((len - 4) << 1) | kPassUnknown);
 }
 
-// getSubset's redraw loop for the attempt at q with its draws from draw(i) = stream[q + i]: the draws
-// consumed (> 67: resolve serially; 0: the stream ends first), as resolve_at
-template <class Draw>
-__device__ __forceinline__ int redraw_len(Draw&& draw, long long q, long long slen, unsigned N, unsigned long long M) {
-    int idx[4] = {0, 0, 0, 0};
-    int r = 0;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        for (;;) {
-            if (q + r >= slen) return 0;
-            if (r > 67) return r;
-            const int v = (int)fastmod(draw(r), M, N);
-            ++r;
-            bool dup = false;
-#pragma unroll
-            for (int j = 0; j < i; ++j) dup |= idx[j] == v;
-            if (!dup) {
-                idx[i] = v;
-                break;
-            }
-        }
-    }
-    return r;
-}
-
 // RNG::uniform(0, n) = next() % n by Barrett reduction: m = floor((2^32 - 1) / n) >= 2^32/n - 1, so
 // q = mulhi(a, m) is the quotient or one less and a - q*n lies in [0, 2n); one unsigned min folds it
 // into [0, n).  For n > 256 the quotient fits 24 bits and q*n is the full-rate v_mul_u32_u24 (the
@@ -949,55 +926,58 @@ constexpr int kAttemptSpan = 256 * kAttemptPerThread;  // window positions per b
 // n = 2000 and ~4-6 on real views with n >= 128; the flag capacity allows 28: a longer window loops)
 constexpr int kAttemptRateEst = 6;
 
+// Positions whose first 4 draws repeat an index (~0.3 % at n = 2000, ~5 % at n = 128) are listed in LDS
+// over all of the block's rounds and their redraw lengths resolved once at the block's end, one per
+// thread (resolved in place, every wave holding one of them, ~80 % of the waves, ran the redraw loop).
+constexpr int kAttemptRepCap = 2048;
+
 __global__ __launch_bounds__(256) void ransac_attempt_kernel(const RansacState* __restrict__ st,
                                                              const uint32_t* __restrict__ stream, long long slen,
                                                              uint8_t* __restrict__ flags, int wcap, int bpp, int c1) {
     constexpr int D = kAttemptPerThread + 3;  // the first 4 draws of the thread's 8 attempts
-    constexpr int kStageWords = kAttemptSpan + 16;
-    __shared__ __attribute__((aligned(16))) unsigned sdraw[kStageWords];
-    __shared__ int rep_pos[kAttemptSpan];
-    __shared__ uint8_t rep_flag[kAttemptSpan];
+    constexpr int kStageVecs = kAttemptSpan / 4 + 4;  // 16-byte vectors: the span, its 3 extra draws, alignment
+    __shared__ __attribute__((aligned(16))) unsigned sdraw[4 * kStageVecs];
+    __shared__ int rep_pos[kAttemptRepCap];
     __shared__ int n_rep;
     const int p = blockIdx.x / bpp;
     const RansacState S = st[p];
     if (!S.active || S.done || S.fail_iter != -1 || S.n < kSmallMaxN || S.produced >= min(c1, S.niters)) return;
     const int wlen = window_len(S, c1, wcap);  // a multiple of 64
+    uint8_t* __restrict__ F = flags + (long long)p * wcap;
+    const unsigned N = (unsigned)S.n, mB = 0xFFFFFFFFu / N;
+    const bool big = N > 256 && N < (1u << 24);  // q and n both fit 24 bits
+    if (threadIdx.x == 0) n_rep = 0;
     // the grid covers the window a typical draw rate implies (kAttemptRateEst), not its capacity; a
     // longer window (low checkSubset pass rate) is covered by the same blocks looping
     for (int boff = (blockIdx.x % bpp) * kAttemptSpan; boff < wlen; boff += bpp * kAttemptSpan) {
-    __syncthreads();  // the previous round's reads of sdraw are done
-    // stream positions fit 32 bits (the stream is capped at 2^28 draws; 64 zero draws pad its end)
+    __syncthreads();  // the previous round's reads of sdraw are done (and n_rep's reset seen)
+    // stream positions fit 32 bits (the stream is capped at 2^28 draws; 64 zero draws pad its end);
+    // the stage starts at the 16-byte vector holding qb: draw qb + e is sdraw[shift + e]
     const int qb = (int)S.stream_pos + boff;
-    const int start = qb & ~3, shift = qb - start;
+    const int shift = qb & 3;
     const int nvec = ((int)slen + 64) >> 2;  // 16-byte vectors in the padded stream buffer
     const uint4* __restrict__ sv = reinterpret_cast<const uint4*>(stream);
-    for (int i = threadIdx.x; i * 4 < kStageWords + 4; i += 256) {
-        const uint4 v = sv[min((start >> 2) + i, nvec - 1)];
-        const unsigned vv[4] = {v.x, v.y, v.z, v.w};
+    uint4* sd4 = reinterpret_cast<uint4*>(sdraw);
+    {
+        uint4 v[(kStageVecs + 255) / 256];  // every load in flight before the first LDS write
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            const int e = 4 * i + c - shift;
-            if (e >= 0 && e < kStageWords) sdraw[e] = vv[c];
+        for (int k = 0; k < (kStageVecs + 255) / 256; ++k) {  // unconditional (clamped) loads
+            const int i = min((int)threadIdx.x + 256 * k, kStageVecs - 1);
+            v[k] = sv[min((qb >> 2) + i, nvec - 1)];
+        }
+#pragma unroll
+        for (int k = 0; k < (kStageVecs + 255) / 256; ++k) {
+            const int i = threadIdx.x + 256 * k;
+            if (i < kStageVecs) sd4[i] = v[k];
         }
     }
     __syncthreads();
     const int off = boff + threadIdx.x * kAttemptPerThread;
-    const int q0 = qb + threadIdx.x * kAttemptPerThread;  // (a thread past the window computes and stores nothing
-                                                          // but joins the block's barriers)
-    const unsigned N = (unsigned)S.n, mB = 0xFFFFFFFFu / N;
-    const bool big = N > 256 && N < (1u << 24);  // q and n both fit 24 bits
+    if (off < wlen) {
+    const int q0 = qb + threadIdx.x * kAttemptPerThread;
     unsigned u[D];
-    {
-        const uint4* L = reinterpret_cast<const uint4*>(sdraw + threadIdx.x * kAttemptPerThread);
 #pragma unroll
-        for (int k4 = 0; k4 < (D + 3) / 4; ++k4) {
-            const uint4 v = L[k4];
-            const unsigned vv[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-            for (int c = 0; c < 4; ++c)
-                if (4 * k4 + c < D) u[4 * k4 + c] = vv[c];
-        }
-    }
+    for (int k = 0; k < D; ++k) u[k] = sdraw[shift + threadIdx.x * kAttemptPerThread + k];
     if (big) {
 #pragma unroll
         for (int k = 0; k < D; ++k) u[k] = mod_barrett<true>(u[k], mB, N);
@@ -1013,42 +993,41 @@ __global__ __launch_bounds__(256) void ransac_attempt_kernel(const RansacState* 
     for (int k = 0; k < D - 2; ++k) d2[k] = u[k] == u[k + 2];
 #pragma unroll
     for (int k = 0; k < D - 3; ++k) d3[k] = u[k] == u[k + 3];
-    // repeated index among the first 4 draws (~0.3 % of positions at n = 2000): the redraw length is
-    // resolved after the block's pass, the block's such positions one per thread from the staged draws
-    // (resolved in place, every wave holding one of them, ~80 % of the waves, ran the redraw loop)
-    uint32_t w[2] = {0, 0};
+    unsigned long long w = 0;  // the 8 flag bytes (one 64-bit word: indexed by a runtime j below)
     unsigned repm = 0;
 #pragma unroll
     for (int j = 0; j < kAttemptPerThread; ++j) {
         const bool rep = d1[j] | d1[j + 1] | d1[j + 2] | d2[j] | d2[j + 1] | d3[j];
         const bool tail = q0 + j + 4 > (int)slen;
-        repm |= (unsigned)(rep && !tail && off < wlen) << j;
-        w[j >> 2] |= (uint32_t)(tail ? kAttemptSerial : kPassUnknown) << (8 * (j & 3));
+        repm |= (unsigned)(rep && !tail) << j;
+        w |= (unsigned long long)(tail ? kAttemptSerial : kPassUnknown) << (8 * j);
     }
-    if (threadIdx.x == 0) n_rep = 0;
-    __syncthreads();
-    int my_slot = 0;
-    if (repm) my_slot = atomicAdd(&n_rep, __popc(repm));
-    __syncthreads();
-    const int nr = min(n_rep, kAttemptSpan);
-    if (nr > 0) {
-        // each thread's repeated positions take consecutive slots from my_slot, in position order
-        for (unsigned m = repm, sl = my_slot; m; m &= m - 1, ++sl) rep_pos[sl] = threadIdx.x * kAttemptPerThread + __builtin_ctz(m);
-        __syncthreads();
-        for (int e = threadIdx.x; e < nr; e += 256) {
-            const int lp = rep_pos[e];  // block-local position: its draws at sdraw[lp ..]
-            const long long q = qb + lp;
-            const int len = redraw_len([&](int i) { return lp + i < kStageWords ? sdraw[lp + i] : stream[min(q + i, slen - 1)]; },
-                                       q, slen, N, S.modM);
-            rep_flag[e] = (uint8_t)((len == 0 || len > 67) ? kAttemptSerial : (((len - 4) << 1) | kPassUnknown));
-        }
-        __syncthreads();
-        for (unsigned m = repm, sl = my_slot; m; m &= m - 1, ++sl) {
+    if (repm) {  // rare: list them (a full list: resolved here, from the stream)
+        const int sl = atomicAdd(&n_rep, __popc(repm));
+        int k = 0;
+        for (unsigned m = repm; m; m &= m - 1, ++k) {
             const int j = __builtin_ctz(m);
-            w[j >> 2] = (w[j >> 2] & ~(0xFFu << (8 * (j & 3)))) | ((uint32_t)rep_flag[sl] << (8 * (j & 3)));
+            if (sl + k < kAttemptRepCap) {
+                rep_pos[sl + k] = off + j;
+            } else {
+                int idx[4];
+                const int len = resolve_at(q0 + j, stream, slen, N, S.modM, idx);
+                const unsigned long long f = (len == 0 || len > 67) ? kAttemptSerial : (((len - 4) << 1) | kPassUnknown);
+                w = (w & ~(0xFFull << (8 * j))) | (f << (8 * j));
+            }
         }
     }
-    if (off < wlen) *reinterpret_cast<uint2*>(flags + (long long)p * wcap + off) = make_uint2(w[0], w[1]);
+    *reinterpret_cast<uint2*>(F + off) = make_uint2((uint32_t)w, (uint32_t)(w >> 32));
+    }
+    }
+    // the listed positions' redraw lengths, one per thread, over the flag bytes just written (same block)
+    __syncthreads();
+    const int nr = min(n_rep, kAttemptRepCap);
+    for (int e = threadIdx.x; e < nr; e += 256) {
+        const int pos = rep_pos[e];
+        int idx[4];
+        const int len = resolve_at(S.stream_pos + pos, stream, slen, N, S.modM, idx);
+        F[pos] = (uint8_t)((len == 0 || len > 67) ? kAttemptSerial : (((len - 4) << 1) | kPassUnknown));
     }
 }
 

@@ -676,29 +676,34 @@ __device__ __forceinline__ bool check_subset(const float* s, const float* d) {
 
 // checkSubset decided in fp32 where fp32 cannot disagree with the fp64 reference, else fp64.
 // Collinearity: dx, dy are floats (the reference subtracts in float), so the fp64 cross product is
-// round_d(dx2 dy1 - dy2 dx1) of an exact difference; c = fma(dx2, dy1, -rn(dy2 dx1)) is within
-// 2^-24 (|rn(dy2 dx1)| + |c|) of the exact value, and the fp64 right side is at most
-// FLT_EPSILON (|dx1| + |dy1| + |dx2| + |dy2|) (1 + 2^-52) <= the fp32 one (1 + 2^-20).  A pair is
-// "clearly not collinear" when |c| minus twice that error still exceeds the right side with margin.
+// X (1 + d), |d| <= 2^-53, X = dx2 dy1 - dy2 dx1 exact; c = fma(dx2, dy1, -rn(dy2 dx1)) is within
+// 2^-24 (|c| + |rn(dy2 dx1)|) of X, and the fp64 right side is at most 2^-23 S (1 + 2^-51), S =
+// |dx1| + |dy1| + |dx2| + |dy2| <= 4 M, M = the pair's largest |delta|.  |c| > 2^-21 M (M + 4)
+// (the bound evaluated in fp32: two roundings) gives |X| >= |c| (1 - 2^-24) - 2^-24 M^2 (1 + 2^-24)
+// > 2^-19 M (1 - 2^-22), four times the fp64 right side (<= 2^-21 M (1 + 2^-51)): the pair is
+// "clearly not collinear".
 // Orientation: |det| of a point triple in fp32 and in fp64 are both within 22 2^-24 M^2 of the exact
-// value (M = the triple's largest |coordinate|); with |det32| > 2^-18 M^2 the fp64 determinant has
-// the same sign, so dA dB < 0 is decided by the signs.  Anything not clear (near-collinear samples,
-// tiny triangles, duplicated points) runs the fp64 check: same result as check_subset always.
+// value (M = the triple's largest |coordinate|); with |det32| > 2^-18 M^2 = (2^-9 M)^2 (the same fp32
+// value: power-of-two scaling commutes with rounding) the fp64 determinant has the same sign, so
+// dA dB < 0 is decided by the signs.  Anything not clear (near-collinear samples, tiny triangles,
+// duplicated points) runs the fp64 check: same result as check_subset always.
 __device__ __forceinline__ bool collinear4_clear(const float* xy) {
-    bool clear = true;
+    float dx[3], dy[3], m[3], m21[3];
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
-        const float dx1 = xy[2 * j] - xy[6], dy1 = xy[2 * j + 1] - xy[7];
+        dx[j] = xy[2 * j] - xy[6];
+        dy[j] = xy[2 * j + 1] - xy[7];
+        m[j] = fmaxf(fabsf(dx[j]), fabsf(dy[j]));
+        m21[j] = m[j] * 0x1p-21f;
+    }
+    bool clear = true;
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
 #pragma unroll
         for (int k = 0; k < j; ++k) {
-            const float dx2 = xy[2 * k] - xy[6], dy2 = xy[2 * k + 1] - xy[7];
-            const float p1 = dy2 * dx1;
-            const float c = fmaf(dx2, dy1, -p1);
-            const float err = (fabsf(p1) + fabsf(c)) * 0x1p-23f;
-            const float rhs = FLT_EPSILON * (fabsf(dx1) + fabsf(dy1) + fabsf(dx2) + fabsf(dy2)) * (1.f + 0x1p-19f);
-            clear &= fabsf(c) - err > rhs;
+            const float c = fmaf(dx[k], dy[j], -(dy[k] * dx[j]));
+            clear &= fabsf(c) > fmaxf(m21[j], m21[k]) * (fmaxf(m[j], m[k]) + 4.f);
         }
-    }
     return clear;
 }
 
@@ -709,6 +714,12 @@ __device__ __forceinline__ float det3xy_f(float x0, float y0, float x1, float y1
 // the fp32 decision and whether it is the fp64 one (clear); !clear: check_subset decides
 __device__ __forceinline__ bool check_subset_fp32(const float* s, const float* d, bool& clear_out) {
     bool clear = (int)collinear4_clear(s) & (int)collinear4_clear(d);  // both evaluated: no branch
+    float ps[4], pd[4];  // 2^-9 max(|x|, |y|) per point
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        ps[k] = fmaxf(fabsf(s[2 * k]), fabsf(s[2 * k + 1])) * 0x1p-9f;
+        pd[k] = fmaxf(fabsf(d[2 * k]), fabsf(d[2 * k + 1])) * 0x1p-9f;
+    }
     const int tt[4][3] = {{0, 1, 2}, {1, 2, 3}, {0, 2, 3}, {0, 1, 3}};
     int negative = 0;
 #pragma unroll
@@ -716,12 +727,9 @@ __device__ __forceinline__ bool check_subset_fp32(const float* s, const float* d
         const int a = tt[i][0], b = tt[i][1], c = tt[i][2];
         const float dA = det3xy_f(s[2 * a], s[2 * a + 1], s[2 * b], s[2 * b + 1], s[2 * c], s[2 * c + 1]);
         const float dB = det3xy_f(d[2 * a], d[2 * a + 1], d[2 * b], d[2 * b + 1], d[2 * c], d[2 * c + 1]);
-        const float mA = fmaxf(fmaxf(fmaxf(fabsf(s[2 * a]), fabsf(s[2 * a + 1])), fmaxf(fabsf(s[2 * b]), fabsf(s[2 * b + 1]))),
-                               fmaxf(fabsf(s[2 * c]), fabsf(s[2 * c + 1])));
-        const float mB = fmaxf(fmaxf(fmaxf(fabsf(d[2 * a]), fabsf(d[2 * a + 1])), fmaxf(fabsf(d[2 * b]), fabsf(d[2 * b + 1]))),
-                               fmaxf(fabsf(d[2 * c]), fabsf(d[2 * c + 1])));
-        clear &= fabsf(dA) > mA * mA * 0x1p-18f;
-        clear &= fabsf(dB) > mB * mB * 0x1p-18f;
+        const float mA = fmaxf(fmaxf(ps[a], ps[b]), ps[c]), mB = fmaxf(fmaxf(pd[a], pd[b]), pd[c]);
+        clear &= fabsf(dA) > mA * mA;
+        clear &= fabsf(dB) > mB * mB;
         negative += (dA < 0.f) != (dB < 0.f);
     }
     clear_out = clear;
@@ -1369,6 +1377,7 @@ __global__ __launch_bounds__(kCheckBlock) void ransac_check_kernel(const ChainSe
                                                                    uint32_t* __restrict__ pass_bits, int wcap, int bpp) {
     __shared__ uint32_t words[kCheckBlock * kCheckPer / 32];  // the round's pass bits
     __shared__ int def_t[kCheckBlock * kCheckPer], def_q[kCheckBlock * kCheckPer];
+    __shared__ int4 seg_tab[kCheckSegs];
     __shared__ int n_def;
     const int p = blockIdx.x / bpp, lane = threadIdx.x & 63;
     const ChainSegs* G = chains + p;
@@ -1381,16 +1390,19 @@ __global__ __launch_bounds__(kCheckBlock) void ransac_check_kernel(const ChainSe
     const int nseg = G->nseg;
     const int bb = base / kCheckBlock;
     const int j0 = bb < kChainBlk ? G->blk_seg[bb] : chain_seg(G, base);
-    int segA[kCheckSegs + 1], segS[kCheckSegs], segQ[kCheckSegs];
-#pragma unroll
-    for (int k = 0; k <= kCheckSegs; ++k) segA[k] = G->A[min(j0 + k, nseg + 1)];
-#pragma unroll
-    for (int k = 0; k < kCheckSegs; ++k) {
-        segS[k] = G->seg_s[min(j0 + k, nseg)];
-        segQ[k] = G->seg_q[min(j0 + k, max(nseg - 1, 0))];
+    // {A[j], A[j + 1], seg_s[j], seg_q[j]} of segments j0 .. j0 + kCheckSegs - 1 in LDS (one 16-byte read
+    // per attempt once its segment is known); the segment starts for the count in scalar registers
+    if (threadIdx.x < kCheckSegs) {
+        const int j = j0 + threadIdx.x;
+        seg_tab[threadIdx.x] = make_int4(G->A[min(j, nseg + 1)], G->A[min(j + 1, nseg + 1)], G->seg_s[min(j, nseg)],
+                                         G->seg_q[min(j, max(nseg - 1, 0))]);
     }
+    int segA[kCheckSegs];
+#pragma unroll
+    for (int k = 1; k < kCheckSegs; ++k) segA[k] = j0 + k <= nseg ? G->A[j0 + k] : INT_MAX;
     const unsigned N = (unsigned)S.n;
     if (threadIdx.x == 0) n_def = 0;
+    __syncthreads();  // seg_tab
     int q[kCheckPer];
     bool irr[kCheckPer], valid[kCheckPer];
 #pragma unroll
@@ -1399,15 +1411,16 @@ __global__ __launch_bounds__(kCheckBlock) void ransac_check_kernel(const ChainSe
         valid[r] = t < T;
         int k = 0;
 #pragma unroll
-        for (int i = 1; i < kCheckSegs; ++i) k += (j0 + i <= nseg) && t >= segA[i];
+        for (int i = 1; i < kCheckSegs; ++i) k += t >= segA[i];
+        const int4 e = seg_tab[k];
         int j = j0 + k, pos;
         bool irregular;
-        if (j < nseg && t >= segA[k + 1]) {  // past the preloaded segments (rare)
+        if (j < nseg && t >= e.y) {  // past the preloaded segments (rare)
             while (j < nseg && t >= G->A[j + 1]) ++j;
             pos = chain_pos(G, j, t, irregular);
         } else {
-            irregular = j < nseg && t == segA[k + 1] - 1;
-            pos = irregular ? segQ[k] : segS[k] + 4 * (t - segA[k]);
+            irregular = j < nseg && t == e.y - 1;
+            pos = irregular ? e.w : e.z + 4 * (t - e.x);
         }
         q[r] = valid[r] ? (int)(G->wbase + pos) : 0;
         irr[r] = valid[r] && irregular;

@@ -2439,9 +2439,9 @@ __global__ __launch_bounds__(256) void ransac_tiles_kernel(RansacState* __restri
 
 // Upper bounds of the inlier counts of 256 consecutive iterations per block (64 per wave: two
 // column blocks of 32 hypotheses), the point tiles staged through LDS and shared by the 4 waves.
-// kLo (first chunk): also a lower bound from the octagon inscribed in the inner disc,
-//   max(|ex|, |ey|, (|ex| + |ey|)/sqrt 2) < C_lo |W| - (C_lo + sqrt 2) kMfmaErr - sqrt 2 A,
-//   C_lo = sb sqrt(thr2 - d_max (- widening)) cos(pi/8),
+// kLo (first chunk): also a lower bound from the square inscribed in the inner disc,
+//   max(|ex|, |ey|) < C_lo |W| - (C_lo + 1) kMfmaErr - A,
+//   C_lo = sb sqrt(thr2 - d_max (- widening)) / sqrt 2,
 // which implies ex^2 + ey^2 < (thr2 - d) W^2 for every point's margin d <= d_max.
 // A (both bounds): absolute slack on |X - uW|, |Y - vW| for OpenCV's own fp32 evaluation of
 // computeError and the closed-form/eigenvector disagreement, which the relative margin d cannot
@@ -2512,11 +2512,11 @@ __global__ __launch_bounds__(256) void ransac_bound_mfma_kernel(const RansacStat
     if (kLo) {
         float tl = thr2 - fmaf(1e-7f * S.smax, S.smax, 0.5f);
         if (eta > 0.f) tl -= S.smax * fmaf(eta * eta, S.smax, 10.2f * eta);
-        // octagon inscribed in the disc of radius sqrt(tl): apothem h = sqrt(tl) cos(pi/8),
-        // max(|ex|, |ey|) <= h |W| and (|ex| + |ey|) / sqrt(2) <= h |W|; the sum carries twice the
-        // error of one coordinate, hence sqrt(2) (kMfmaErr + A) beside h kMfmaErr from |W|
-        CL = S.sb * sqrtf(fmaxf(tl, 0.f)) * 0.92387953f * (1.f - 1e-6f);
-        EL = ((CL + 1.41421357f) * kMfmaErr + 1.41421357f * A) * (1.f + 1e-6f);
+        // square inscribed in the disc of radius sqrt(tl): half side h = sqrt(tl) / sqrt(2),
+        // max(|ex|, |ey|) <= h |W|, the box test's own form (one coordinate's error kMfmaErr + A beside
+        // h kMfmaErr from |W|), so it shares the upper bound's max(|ex|, |ey|)
+        CL = S.sb * sqrtf(fmaxf(tl, 0.f)) * 0.70710677f * (1.f - 1e-6f);
+        EL = ((CL + 1.f) * kMfmaErr + A) * (1.f + 1e-6f);
     }
     // B-operand fragments of the own hypothesis: k 0-7 (bx, by, bw) and k 8-15 (shared by bx, by)
     h8v fx = {}, fy = {}, fw = {}, fn = {};
@@ -2603,11 +2603,9 @@ __global__ __launch_bounds__(256) void ransac_bound_mfma_kernel(const RansacStat
                 const float d1 = fmaf(C1, fabsf(w1[r]), E1) - m1;
                 bits0 = __builtin_amdgcn_alignbit(bits0, __float_as_uint(d0), 31);
                 bits1 = __builtin_amdgcn_alignbit(bits1, __float_as_uint(d1), 31);
-                if (kLo) {  // sign bit of max(|ex|, |ey|, (|ex| + |ey|) / sqrt 2) - R_lo: set when surely in
-                    const float o0 = __builtin_amdgcn_fmed3f(m0, (fabsf(ex0[r]) + fabsf(ey0[r])) * 0.70710677f, big);
-                    const float o1 = __builtin_amdgcn_fmed3f(m1, (fabsf(ex1[r]) + fabsf(ey1[r])) * 0.70710677f, big);
-                    const float l0 = o0 - fmaf(CL0, fabsf(w0[r]), -EL0);
-                    const float l1 = o1 - fmaf(CL1, fabsf(w1[r]), -EL1);
+                if (kLo) {  // sign bit of max(|ex|, |ey|) - R_lo: set when surely in
+                    const float l0 = m0 - fmaf(CL0, fabsf(w0[r]), -EL0);
+                    const float l1 = m1 - fmaf(CL1, fabsf(w1[r]), -EL1);
                     lb0 = __builtin_amdgcn_alignbit(lb0, __float_as_uint(l0), 31);
                     lb1 = __builtin_amdgcn_alignbit(lb1, __float_as_uint(l1), 31);
                 }

@@ -930,8 +930,10 @@ constexpr int kAttemptPerThread = 8;  // window positions per thread (11 draws r
 // The block's 2048 + 3 draws are staged through LDS with coalesced 16-byte loads (a lane's own 11
 // draws at a 32-byte lane stride would touch 12 cache lines per load instruction, 11 times over).
 constexpr int kAttemptSpan = 256 * kAttemptPerThread;  // window positions per block
-// draws per wanted iteration the sampler grids are sized for (a window is ~4.1 per iteration at
-// n = 2000 and ~4-6 on real views with n >= 128; the flag capacity allows 28: a longer window loops)
+// draws per wanted iteration the sampler grids are sized for.  Measured windows (profiles/
+// r04_sampler_probe.txt): ~21 draws per iteration on C4 (checkSubset passes ~1 attempt in 5 on 92 %
+// outliers), 29 with the window's margin; the flag capacity allows 28.  The grid is sized for 6: a C4
+// chunk launches ~35 k attempt blocks (and ~18 k check blocks), each looping over ~4 rounds.
 constexpr int kAttemptRateEst = 6;
 
 // Positions whose first 4 draws repeat an index (~0.3 % at n = 2000, ~5 % at n = 128) are listed in LDS
@@ -951,6 +953,9 @@ __global__ __launch_bounds__(256) void ransac_attempt_kernel(const RansacState* 
     const RansacState S = st[p];
     if (!S.active || S.done || S.fail_iter != -1 || S.n < kSmallMaxN || S.produced >= min(c1, S.niters)) return;
     const int wlen = window_len(S, c1, wcap);  // a multiple of 64
+    MIM_DEBUG_PRINT(threadIdx.x == 0 && blockIdx.x % bpp == 0 && (p == 0 || p == 100),
+                    "[attempt] p=%d c1=%d wlen=%d bpp=%d produced=%d stream_pos=%lld n=%d\n", p, c1, wlen, bpp, S.produced,
+                    (long long)S.stream_pos, S.n);
     uint8_t* __restrict__ F = flags + (long long)p * wcap;
     const unsigned N = (unsigned)S.n, mB = 0xFFFFFFFFu / N;
     const bool big = N > 256 && N < (1u << 24);  // q and n both fit 24 bits
@@ -1466,6 +1471,8 @@ __global__ __launch_bounds__(kCheckBlock) void ransac_check_kernel(const ChainSe
         }
     }
     __syncthreads();
+    MIM_DEBUG_PRINT(threadIdx.x == 0 && (p == 0 || p == 100), "[check] p=%d b=%d bpp=%d T=%d nseg=%d n_def=%d wlen=%d\n",
+                    p, b, bpp, T, nseg, n_def, G->wlen);
     for (int e = threadIdx.x; e < n_def; e += kCheckBlock) {  // one deferred attempt per thread
         const int tl = def_t[e], qe = def_q[e];
         const long long qq = qe < 0 ? -(long long)qe - 1 : qe;

@@ -1,6 +1,5 @@
 # Round 4 closing tree, part 2: three runs each of C5, c1img and the reference's whole dataset run, then
-# the rocprofv3 kernel traces and HBM counter passes of C4, C3, C5 (tools/prof_round.sh) and c1img, and
-# the distance and bound kernels' SQ counters on C4 (two passes).
+# the rocprofv3 kernel traces and HBM counter passes of C4 and C3 (tools/prof_round.sh).
 set -e
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
@@ -10,11 +9,4 @@ for c in c5 c1img dataset; do
   for i in 1 2 3; do timeout -k 10 300 python -u bench.py --config $c --cpu-sample 0 > $O/bench_${c}_$i.log 2>&1; done
 done
 for f in $O/bench_c5_*.log $O/bench_c1img_*.log $O/bench_dataset_*.log; do echo "$f $(tail -1 $f | cut -c1-120)"; done
-for c in c4 c3 c5 c1img; do timeout -k 10 900 bash tools/prof_round.sh $c; done
-K='knn2_i8|ransac_bound_mfma'
-i=0
-for C in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_SALU SQ_INSTS_LDS SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE" "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_LDS"; do
-  i=$((i+1))
-  timeout -s KILL 200 rocprofv3 --pmc $C --kernel-trace --output-format csv --kernel-include-regex "$K" \
-     -d $O/pmc_sq$i -o run -- python3 bench.py --inflight 1 --steps 2 --warmup 1 --iso-steps 1 --cpu-sample 0 > $O/pmc_sq$i.log 2>&1
-done
+for c in c4 c3; do timeout -k 10 900 bash tools/prof_round.sh $c; done

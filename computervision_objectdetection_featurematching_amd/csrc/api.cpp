@@ -193,6 +193,8 @@ struct mim_ctx {
     long long sets_gen = 0, last_gen = -1;
     // MIM_CAND_CAP: candidate-list capacity override (test knob for the replay's overflow rescan)
     int cand_cap = 0;
+    // MIM_ATTEMPT_REP_CAP: the attempt kernel's redraw-list capacity (test knob for its in-place path)
+    int rep_cap = 0;
     // MIM_STREAM_DRAWS: initial RNG stream length (test knob for the grow-and-re-run path)
     long long stream_draws = 0;
     // MIM_RANSAC_EXACT=1: evaluate every hypothesis exactly (reference mode for cross-checks)
@@ -274,6 +276,8 @@ mim_status mim_ctx_create(int device, mim_ctx** out) {
     c->exact_all = (ex && ex[0] == '1') ? 1 : 0;
     const char* cc = getenv("MIM_CAND_CAP");
     c->cand_cap = cc ? std::max(1, atoi(cc)) : 0;
+    const char* rc = getenv("MIM_ATTEMPT_REP_CAP");
+    c->rep_cap = rc ? std::max(1, atoi(rc)) : 0;
     const char* sd = getenv("MIM_STREAM_DRAWS");
     c->stream_draws = sd ? std::max(4096LL, atoll(sd)) : 0;
     *out = c;
@@ -1111,6 +1115,7 @@ static mim_status ransac_prepare(mim_ctx* c, int n, const mim_params* prm, Ransa
     rp.det_lo = prm->det_lo;
     rp.det_hi = prm->det_hi;
     rp.cand_cap = c->cand_cap;
+    rp.rep_cap = c->rep_cap;
     return MIM_OK;
 }
 

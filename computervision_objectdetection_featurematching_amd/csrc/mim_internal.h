@@ -108,6 +108,7 @@ struct RansacParams {
     int min_good, min_inliers;
     double det_lo, det_hi;
     int cand_cap;    // candidate-list capacity per problem and chunk (0: kCandPerProblem)
+    int rep_cap;     // attempt kernel's list of repeated-index positions per block (0: kAttemptRepCap)
 };
 
 }  // namespace mim

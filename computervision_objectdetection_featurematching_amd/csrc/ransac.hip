@@ -853,10 +853,10 @@ __global__ void ransac_init_kernel(RansacState* __restrict__ st, const int* __re
 }
 
 // ------------------------------------------------------------------------------------------------
-// attempt: the outcome of a getSubset attempt that starts at stream position q, for every q of a
-// window ahead of each problem's current position — fully parallel over the GPU.  The sampler
-// below then only walks the chain of attempt start positions.  flag: 0 checkSubset fails,
-// 1 passes, 2 an index repeats (resolved serially by the walker), 3 beyond the RNG stream.
+// attempt: the draws a getSubset attempt that starts at stream position q consumes, for every q of a
+// window ahead of each problem's current position — fully parallel over the GPU (one flag byte per
+// position: kPassUnknown | (draws - 4) << 1, or kAttemptSerial).  The chain kernels then walk the
+// attempt start positions and ransac_check_kernel evaluates checkSubset for the chain's attempts.
 // attempts precomputed ahead of the walker: the expected draws of the remaining iterations of the
 // chunk (draws per iteration measured so far, 28 before any) + 6 % (25 % unmeasured) + 4096, capped by the buffer
 // problems with fewer points are replayed by ransac_small_kernel from the stream alone (no window)
@@ -943,7 +943,8 @@ constexpr int kAttemptRepCap = 2048;
 
 __global__ __launch_bounds__(256) void ransac_attempt_kernel(const RansacState* __restrict__ st,
                                                              const uint32_t* __restrict__ stream, long long slen,
-                                                             uint8_t* __restrict__ flags, int wcap, int bpp, int c1) {
+                                                             uint8_t* __restrict__ flags, int wcap, int bpp, int c1,
+                                                             int rep_cap) {
     constexpr int D = kAttemptPerThread + 3;  // the first 4 draws of the thread's 8 attempts
     constexpr int kStageVecs = kAttemptSpan / 4 + 4;  // 16-byte vectors: the span, its 3 extra draws, alignment
     __shared__ __attribute__((aligned(16))) unsigned sdraw[4 * kStageVecs];
@@ -1020,7 +1021,7 @@ __global__ __launch_bounds__(256) void ransac_attempt_kernel(const RansacState* 
         int k = 0;
         for (unsigned m = repm; m; m &= m - 1, ++k) {
             const int j = __builtin_ctz(m);
-            if (sl + k < kAttemptRepCap) {
+            if (sl + k < rep_cap) {
                 rep_pos[sl + k] = off + j;
             } else {
                 int idx[4];
@@ -1035,7 +1036,7 @@ __global__ __launch_bounds__(256) void ransac_attempt_kernel(const RansacState* 
     }
     // the listed positions' redraw lengths, one per thread, over the flag bytes just written (same block)
     __syncthreads();
-    const int nr = min(n_rep, kAttemptRepCap);
+    const int nr = min(n_rep, rep_cap);
     for (int e = threadIdx.x; e < nr; e += 256) {
         const int pos = rep_pos[e];
         int idx[4];
@@ -3554,7 +3555,10 @@ void ransac_enqueue(const RansacParams& prm, int n_probs, const ProbDev* probs, 
         // grids for the window a typical draw rate implies (the kernels loop over a longer one)
         const int west = (int)std::min<long long>(wcap, (long long)(c1 - c0) * kAttemptRateEst + 4096);
         const int bppw = (west + kAttemptSpan - 1) / kAttemptSpan;
-        ransac_attempt_kernel<<<n_probs * bppw, 256, 0, ss>>>(b.state, b.stream, b.stream_len, b.flags, wcap, bppw, c1);
+        // (MIM_ATTEMPT_REP_CAP < kAttemptRepCap: test knob forcing the in-place redraw resolution)
+        const int rep_cap = prm.rep_cap > 0 ? std::min(prm.rep_cap, kAttemptRepCap) : kAttemptRepCap;
+        ransac_attempt_kernel<<<n_probs * bppw, 256, 0, ss>>>(b.state, b.stream, b.stream_len, b.flags, wcap, bppw, c1,
+                                                             rep_cap);
         mark(mark_ctx, "attempt", ss);
         if (use_chain) {
             ChainSegs* chains = reinterpret_cast<ChainSegs*>(b.chains);

@@ -417,3 +417,41 @@ def test_sampler_stream_identical(mode):
     for (ha, ma, ra), (hb, mb, rb) in zip(f0, f1):
         np.testing.assert_array_equal(ma, mb)
         assert ra == rb
+
+
+def _small_sets(seed=99):
+    """Point sets of 128-300 matches (the chain sampler's range, n >= 128) whose getSubset redraws a
+    repeated index every ~20-50 positions, with 20-40 % inliers of a mild homography."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for n in (128, 150, 200, 300):
+        src = np.c_[rng.uniform(0, 640, n), rng.uniform(0, 480, n)].astype(np.float32)
+        dst = np.c_[rng.uniform(0, 640, n), rng.uniform(0, 480, n)].astype(np.float32)
+        k = int(n * rng.uniform(0.2, 0.4))
+        dst[:k] = src[:k] * np.float32(1.05) + np.float32(7) + rng.uniform(-0.5, 0.5, (k, 2)).astype(np.float32)
+        out.append((src, dst))
+    return out
+
+
+def test_attempt_redraw_list_overflow_equals_walker(oracle):
+    """MIM_ATTEMPT_REP_CAP=1: the attempt kernel's per-block list of repeated-index positions holds one
+    entry, so nearly every redraw length is resolved in place (the list-overflow path); masks, records
+    and H must equal the attempt-by-attempt walker (MIM_SAMPLER_WALK=1) and the oracle."""
+    import os
+    from computervision_objectdetection_featurematching_amd import Matcher
+    sets = _small_sets()
+    outs = []
+    for env in ({"MIM_ATTEMPT_REP_CAP": "1"}, {"MIM_SAMPLER_WALK": "1"}):
+        os.environ.update(env)
+        m = Matcher(0)
+        try:
+            outs.append([m.find_homography(s_, d_, 5.0, 2000) + (m.batch_results(1).tobytes(),) for s_, d_ in sets])
+        finally:
+            m.close()
+            for k in env:
+                os.environ.pop(k)
+    for (ha, ma, ra), (hb, mb, rb), (s_, d_) in zip(outs[0], outs[1], sets):
+        np.testing.assert_array_equal(ma, mb)
+        assert ra == rb
+        r = oracle.ransac(s_, d_, 5.0, 0.995, 2000)
+        np.testing.assert_array_equal(ma, r["mask"])

@@ -43,7 +43,10 @@ def build(force: bool = False, verbose: bool = False) -> str:
     if not force and not needs_build():
         return SO
     os.makedirs(LIBDIR, exist_ok=True)
-    odir = os.environ.get("MIM_BUILD_DIR", LIBDIR)  # objects (variant builds run in parallel: own dirs)
+    # objects in a directory of this process's own and the library renamed into place, so processes
+    # that build at the same time (the ranks of a multi-GPU bench) cannot mix each other's files
+    import tempfile
+    odir = os.environ.get("MIM_BUILD_DIR") or tempfile.mkdtemp(prefix="mim_build_")
     os.makedirs(odir, exist_ok=True)
     objs = []
     for src in sources():
@@ -54,11 +57,14 @@ def build(force: bool = False, verbose: bool = False) -> str:
         subprocess.check_call(cmd)
         objs.append(obj)
     os.makedirs(os.path.dirname(os.path.abspath(SO)), exist_ok=True)
-    cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", SO + ".tmp", *objs]
+    tmp = f"{SO}.tmp{os.getpid()}"
+    cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", tmp, *objs]
     subprocess.check_call(cmd)
-    os.replace(SO + ".tmp", SO)
+    os.replace(tmp, SO)
     for o in objs:
         os.remove(o)
+    if not os.environ.get("MIM_BUILD_DIR"):
+        os.rmdir(odir)
     return SO
 
 

@@ -678,48 +678,51 @@ __device__ __forceinline__ bool check_subset(const float* s, const float* d) {
 // Collinearity: dx, dy are floats (the reference subtracts in float), so the fp64 cross product is
 // X (1 + d), |d| <= 2^-53, X = dx2 dy1 - dy2 dx1 exact; c = fma(dx2, dy1, -rn(dy2 dx1)) is within
 // 2^-24 (|c| + |rn(dy2 dx1)|) of X, and the fp64 right side is at most 2^-23 S (1 + 2^-51), S =
-// |dx1| + |dy1| + |dx2| + |dy2| <= 4 M, M = the pair's largest |delta|.  |c| > 2^-21 M (M + 4)
-// (the bound evaluated in fp32: two roundings) gives |X| >= |c| (1 - 2^-24) - 2^-24 M^2 (1 + 2^-24)
-// > 2^-19 M (1 - 2^-22), four times the fp64 right side (<= 2^-21 M (1 + 2^-51)): the pair is
-// "clearly not collinear".
-// Orientation: |det| of a point triple in fp32 and in fp64 are both within 22 2^-24 M^2 of the exact
-// value (M = the triple's largest |coordinate|); with |det32| > 2^-18 M^2 = (2^-9 M)^2 (the same fp32
-// value: power-of-two scaling commutes with rounding) the fp64 determinant has the same sign, so
-// dA dB < 0 is decided by the signs.  Anything not clear (near-collinear samples, tiny triangles,
-// duplicated points) runs the fp64 check: same result as check_subset always.
+// |dx1| + |dy1| + |dx2| + |dy2| <= 4 M, M >= every |delta| of the pair (here: the largest |delta| of
+// the set's three).  |c| > 2^-21 M (M + 4) (the bound evaluated in fp32: two roundings) gives
+// |X| >= |c| (1 - 2^-24) - 2^-24 M^2 (1 + 2^-24) > 2^-19 M (1 - 2^-22), four times the fp64 right
+// side (<= 2^-21 M (1 + 2^-51)): the pair is "clearly not collinear".
+// Orientation: |det| of a point triple in fp32 (three fma, three roundings fewer than the plain
+// form: within 17 2^-24 M^2) and in fp64 are both within 22 2^-24 M^2 of the exact value (M >= the
+// triple's largest |coordinate|; here the set's largest); with |det32| > 2^-18 M^2 = (2^-9 M)^2 (the
+// same fp32 value: power-of-two scaling commutes with rounding) the fp64 determinant has the same
+// sign, so dA dB < 0 is decided by the signs.  Anything not clear (near-collinear samples, tiny
+// triangles, duplicated points) runs the fp64 check: same result as check_subset always.  (One M
+// per set instead of per pair or triple: 4 of the 4-point sample's bounds instead of 14, and "not
+// clear" stays ~0.3 % of the attempts, profiles/r04_sampler_probe.txt.)
 __device__ __forceinline__ bool collinear4_clear(const float* xy) {
-    float dx[3], dy[3], m[3], m21[3];
+    float dx[3], dy[3];
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
         dx[j] = xy[2 * j] - xy[6];
         dy[j] = xy[2 * j + 1] - xy[7];
-        m[j] = fmaxf(fabsf(dx[j]), fabsf(dy[j]));
-        m21[j] = m[j] * 0x1p-21f;
     }
+    const float m = fmaxf(fmaxf(fmaxf(fabsf(dx[0]), fabsf(dy[0])), fmaxf(fabsf(dx[1]), fabsf(dy[1]))),
+                          fmaxf(fabsf(dx[2]), fabsf(dy[2])));
+    const float bound = m * 0x1p-21f * (m + 4.f);
     bool clear = true;
 #pragma unroll
     for (int j = 0; j < 3; ++j)
 #pragma unroll
-        for (int k = 0; k < j; ++k) {
-            const float c = fmaf(dx[k], dy[j], -(dy[k] * dx[j]));
-            clear &= fabsf(c) > fmaxf(m21[j], m21[k]) * (fmaxf(m[j], m[k]) + 4.f);
-        }
+        for (int k = 0; k < j; ++k) clear &= fabsf(fmaf(dx[k], dy[j], -(dy[k] * dx[j]))) > bound;
     return clear;
 }
 
+// x0 (y1 - y2) - y0 (x1 - x2) + (x1 y2 - x2 y1), the fp32 decision's form (fma: fewer roundings)
 __device__ __forceinline__ float det3xy_f(float x0, float y0, float x1, float y1, float x2, float y2) {
-    return x0 * (y1 - y2) - y0 * (x1 - x2) + (x1 * y2 - x2 * y1);
+    return fmaf(-y0, x1 - x2, fmaf(x0, y1 - y2, fmaf(x1, y2, -(x2 * y1))));
+}
+
+__device__ __forceinline__ float max_abs8(const float* v) {
+    return fmaxf(fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))),
+                 fmaxf(fmaxf(fabsf(v[4]), fabsf(v[5])), fmaxf(fabsf(v[6]), fabsf(v[7]))));
 }
 
 // the fp32 decision and whether it is the fp64 one (clear); !clear: check_subset decides
 __device__ __forceinline__ bool check_subset_fp32(const float* s, const float* d, bool& clear_out) {
     bool clear = (int)collinear4_clear(s) & (int)collinear4_clear(d);  // both evaluated: no branch
-    float ps[4], pd[4];  // 2^-9 max(|x|, |y|) per point
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        ps[k] = fmaxf(fabsf(s[2 * k]), fabsf(s[2 * k + 1])) * 0x1p-9f;
-        pd[k] = fmaxf(fabsf(d[2 * k]), fabsf(d[2 * k + 1])) * 0x1p-9f;
-    }
+    const float ms = max_abs8(s) * 0x1p-9f, md = max_abs8(d) * 0x1p-9f;
+    const float ts = ms * ms, td = md * md;
     const int tt[4][3] = {{0, 1, 2}, {1, 2, 3}, {0, 2, 3}, {0, 1, 3}};
     int negative = 0;
 #pragma unroll
@@ -727,9 +730,8 @@ __device__ __forceinline__ bool check_subset_fp32(const float* s, const float* d
         const int a = tt[i][0], b = tt[i][1], c = tt[i][2];
         const float dA = det3xy_f(s[2 * a], s[2 * a + 1], s[2 * b], s[2 * b + 1], s[2 * c], s[2 * c + 1]);
         const float dB = det3xy_f(d[2 * a], d[2 * a + 1], d[2 * b], d[2 * b + 1], d[2 * c], d[2 * c + 1]);
-        const float mA = fmaxf(fmaxf(ps[a], ps[b]), ps[c]), mB = fmaxf(fmaxf(pd[a], pd[b]), pd[c]);
-        clear &= fabsf(dA) > mA * mA;
-        clear &= fabsf(dB) > mB * mB;
+        clear &= fabsf(dA) > ts;
+        clear &= fabsf(dB) > td;
         negative += (dA < 0.f) != (dB < 0.f);
     }
     clear_out = clear;

@@ -59,6 +59,11 @@ class Detector {
     // Per-view outcome of the last call (same order as the views).
     const std::vector<mim_result>& last_results() const { return results_; }
 
+    // The model views registered by the last detect_* call are reused while the next call passes the
+    // same ModelViews objects with the same view counts and descriptor storage.  A caller that rewrites
+    // a view's descriptors or keypoints in place calls this first, so the next call registers them anew.
+    void invalidate_models() { reg_n_ = -1; }
+
     // TestsDetector.cpp:58-95 for one model at one scale.
     void detect_at_scale(const ModelViews& model, const std::vector<Point2f>& scene_kp,
                          const std::vector<float>& scene_desc, float scale, std::vector<Point2f>& out_pts) {

@@ -97,6 +97,27 @@ int main() {
             std::printf("FAIL repeat at %zu\n", i);
             return 1;
         }
+    // a view rewritten in place (its keypoints moved): after invalidate_models() the next call registers
+    // the views anew and equals a fresh Detector's result on the changed model
+    {
+        for (auto& v : model.views)
+            for (auto& k : v.keypoints) k.x += 3.0f;
+        det.invalidate_models();
+        std::vector<std::vector<mim::Point2f>> moved, fresh;
+        det.detect_scene({&model}, {{&skp[0], &sdesc[0], scales[0]}, {&skp[1], &sdesc[1], scales[1]}}, moved);
+        mim::Detector det2(0);
+        det2.detect_scene({&model}, {{&skp[0], &sdesc[0], scales[0]}, {&skp[1], &sdesc[1], scales[1]}}, fresh);
+        bool same = moved.size() == fresh.size() && moved[0].size() == fresh[0].size();
+        for (size_t i = 0; same && i < fresh[0].size(); ++i)
+            same = moved[0][i].x == fresh[0][i].x && moved[0][i].y == fresh[0][i].y;
+        if (!same) {
+            std::printf("FAIL invalidate_models\n");
+            return 1;
+        }
+        for (auto& v : model.views)
+            for (auto& k : v.keypoints) k.x -= 3.0f;
+        det.invalidate_models();
+    }
     std::printf("OK %zu inlier points, statuses:", ref.size());
     for (auto& r : det.last_results()) std::printf(" %d/%d/%d", r.n_good, r.n_inl, r.status);
     std::printf("\n");

@@ -95,6 +95,13 @@ def _model_sets(matcher: Matcher, models: list[ObjectModel]) -> list[list[int]]:
     return ids
 
 
+def forget_models(matcher: Matcher) -> None:
+    """Drop the registered-models cache of _model_sets: call it after rewriting a model's view arrays in
+    place (the cache recognises the views by array identity), so the next detect_objects registers them
+    anew (mim.hpp's Detector::invalidate_models)."""
+    matcher._pipeline_models = None
+
+
 @dataclass
 class SceneRun:
     """detect_objects' intermediate products (for tests and benches)."""
@@ -192,4 +199,4 @@ def process_all_test_images(matcher, scenes, models, output_dir: str, params=Non
 
 
 __all__ = ["ObjectModel", "SCALES", "SceneRun", "default_box_params", "detect_boxes", "detect_objects",
-           "process_all_test_images", "process_model_views", "save_detections", "DIM"]
+           "forget_models", "process_all_test_images", "process_model_views", "save_detections", "DIM"]

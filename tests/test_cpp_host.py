@@ -31,3 +31,45 @@ def test_cpp_host_matches_reference_loop(tmp_path):
     print(r.stdout, r.stderr)
     assert r.returncode == 0, r.stdout + r.stderr
     assert r.stdout.startswith("OK") and "OK gray path" in r.stdout
+
+
+def _compile_real(out):
+    from computervision_objectdetection_featurematching_amd import build
+    build.build()
+    cmd = ["g++", "-std=c++17", "-O2", os.path.join(ROOT, "tests", "cpp", "detector_real.cpp"), "-o", out,
+           "-I" + os.path.join(ROOT, "include"), "-L" + LIBDIR, "-lmim", "-Wl,-rpath," + LIBDIR]
+    subprocess.check_call(cmd)
+
+
+def test_cpp_detector_real_compiles(tmp_path):
+    _compile_real(str(tmp_path / "d"))
+
+
+@pytest.mark.gpu
+def test_cpp_detector_on_reference_images(tmp_path):
+    """The C++ drop-in path (Detector::sift per model view with its mask, detect_scene_gray per scene,
+    mim_detect.hpp's boxes) on the reference's sugar_box images: every labelled scene's
+    allUnfilteredScenePts and detections equal the restatement's (tests/golden/c1_sugar_box.npz, the
+    same outputs test_pipeline_gpu.py holds the Python path to)."""
+    import numpy as np
+    with np.load(os.path.join(ROOT, "tests", "golden", "c1_sugar_box.npz")) as z:
+        c1 = {k: z[k] for k in z.files}
+    names = sorted(k[5:] for k in c1 if k.startswith("view/"))
+    scenes = sorted(k[8:] for k in c1 if k.startswith("exp/res/"))
+    rows, cols = c1[f"view/{names[0]}"].shape
+    for i, n in enumerate(names):
+        np.ascontiguousarray(c1[f"view/{n}"], np.uint8).tofile(str(tmp_path / f"view_{i}.u8"))
+        np.ascontiguousarray(c1[f"mask/{n}"], np.uint8).tofile(str(tmp_path / f"mask_{i}.u8"))
+    for sid in scenes:
+        np.ascontiguousarray(c1[f"scene/{sid}"], np.uint8).tofile(str(tmp_path / f"scene_{sid}.u8"))
+    exe = str(tmp_path / "d")
+    _compile_real(exe)
+    r = subprocess.run([exe, str(tmp_path), str(rows), str(cols), str(len(names)), *scenes], capture_output=True,
+                       text=True, timeout=300)
+    print(r.stdout, r.stderr)
+    assert r.returncode == 0, r.stdout + r.stderr
+    for sid in scenes:
+        pts = np.fromfile(str(tmp_path / f"pts_{sid}.f32"), np.float32).reshape(-1, 2)
+        np.testing.assert_array_equal(pts, c1[f"exp/pts/{sid}"], err_msg=sid)
+        boxes = np.fromfile(str(tmp_path / f"boxes_{sid}.i32"), np.int32).reshape(-1, 4)
+        np.testing.assert_array_equal(boxes, c1[f"exp/boxes/{sid}"], err_msg=sid)

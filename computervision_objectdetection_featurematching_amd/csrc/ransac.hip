@@ -2348,10 +2348,10 @@ __device__ __forceinline__ void bound_hypothesis(const float4* __restrict__ P, i
 //   (ay, by: v and h3 h4 h5; W = ax . [h6h h6h h6l h7h h7h h7l h8 0 | 0 ...]).
 // Error of each computed quantity (|factors| <= 1, f16 split 2^-22 per factor and 2^-22 per dropped
 // al*bl, fp32 products u'x' 2^-24, fp32 accumulation of <= 16 terms of total magnitude <= 6):
-// < 1e-5 in these units; kMfmaErr = 2^-15 = 3.05e-5.  A point is out of the box only if
-//   max(|ex|, |ey|) > C |W| + (1 + C) kMfmaErr,  C = sb sqrt(thr2 + d_max (+ widening)) (1 + 1e-6)
+// < 1e-5 in these units; kMfmaErr = 2^-15 = 3.05e-5.  A point is outside only if
+//   |ex| + |ey| > C |W| + (2 + C) kMfmaErr,  C = sqrt 2 sb sqrt(thr2 + d_max (+ widening)) (1 + 1e-6)
 // with d_max the largest per-point margin of the problem, so the count of the rest bounds the
-// exact inlier count from above exactly as the fp32 box test does ("Bounds").
+// exact inlier count from above ("Exactness of the filtered RANSAC").
 // MI355X MFMA keeps f16 subnormal operands (tools/probe/f16_probe.hip).
 // ------------------------------------------------------------------------------------------------
 typedef _Float16 h8v __attribute__((ext_vector_type(8)));
@@ -2449,9 +2449,14 @@ __global__ __launch_bounds__(256) void ransac_tiles_kernel(RansacState* __restri
 
 // Upper bounds of the inlier counts of 256 consecutive iterations per block (64 per wave: two
 // column blocks of 32 hypotheses), the point tiles staged through LDS and shared by the 4 waves.
-// kLo (first chunk): also a lower bound from the square inscribed in the inner disc,
-//   max(|ex|, |ey|) < C_lo |W| - (C_lo + 1) kMfmaErr - A,
-//   C_lo = sb sqrt(thr2 - d_max (- widening)) / sqrt 2,
+// Both bounds test the L1 norm |ex| + |ey| (a diamond: the same area as the box max(|ex|, |ey|) of
+// rounds 2-4 around the same disc, so as tight, and v_add/v_sub with |.| operands issue at the
+// fp32 rate where the max / med3 issues ~1.5x slower, tools/probe/valu_rate_probe.hip).
+// Upper bound: a point can be an inlier only if
+//   |ex| + |ey| <= C |W| + (C + 2) kMfmaErr + 2 A,  C = sqrt 2 sb sqrt(thr2 + d_max (+ widening)),
+// since (|ex| - A, |ey| - A) lies in the disc of radius C |W| / sqrt 2 and each MFMA output is
+// within kMfmaErr.  kLo (first chunk) also a lower bound from the diamond inscribed in the inner
+// disc, |ex| + |ey| < C_lo |W| - (C_lo + 2) kMfmaErr - 2 A, C_lo = sb sqrt(thr2 - d_max (- widening)),
 // which implies ex^2 + ey^2 < (thr2 - d) W^2 for every point's margin d <= d_max.
 // A (both bounds): absolute slack on |X - uW|, |Y - vW| for OpenCV's own fp32 evaluation of
 // computeError and the closed-form/eigenvector disagreement, which the relative margin d cannot
@@ -2509,7 +2514,7 @@ __global__ __launch_bounds__(256) void ransac_bound_mfma_kernel(const RansacStat
     // per-hypothesis box constants (d_max and, for poorly conditioned samples, the widening at smax)
     float tt = thr2 + fmaf(1e-7f * S.smax, S.smax, 0.5f);
     if (eta > 0.f) tt += S.smax * fmaf(eta * eta, S.smax, 10.2f * eta);
-    const float C = S.sb * sqrtf(tt) * (1.f + 1e-6f);
+    const float C = S.sb * sqrtf(tt) * 1.41421366f * (1.f + 1e-6f);  // sqrt 2 rounded up
     // near-horizon slack A (pixel units, |x|, |y| < 1/sa and |u|, |v| < 1/sb), in the scaled units of
     // the MFMA outputs, with the sample's modelled closed-form/eigenvector disagreement eta_model
     const double mx = 1.0 / S.sa, mu = 1.0 / S.sb;
@@ -2517,16 +2522,16 @@ __global__ __launch_bounds__(256) void ransac_bound_mfma_kernel(const RansacStat
     const double ax = fmax((fabs(Hd[0]) + fabs(Hd[1])) * mx + fabs(Hd[2]), (fabs(Hd[3]) + fabs(Hd[4])) * mx + fabs(Hd[5]));
     const double aw = (fabs(Hd[6]) + fabs(Hd[7])) * mx + 1.0;
     const float A = (float)(gam * (ax + (mu + 6.0) * aw) * S.sb * sc * (1.0 + 1e-6));
-    const float E = (1.f + C) * kMfmaErr * (1.f + 1e-6f) + A;
+    const float E = ((2.f + C) * kMfmaErr + 2.f * A) * (1.f + 1e-6f);
     float CL = 0.f, EL = 0.f;
     if (kLo) {
         float tl = thr2 - fmaf(1e-7f * S.smax, S.smax, 0.5f);
         if (eta > 0.f) tl -= S.smax * fmaf(eta * eta, S.smax, 10.2f * eta);
-        // square inscribed in the disc of radius sqrt(tl): half side h = sqrt(tl) / sqrt(2),
-        // max(|ex|, |ey|) <= h |W|, the box test's own form (one coordinate's error kMfmaErr + A beside
-        // h kMfmaErr from |W|), so it shares the upper bound's max(|ex|, |ey|)
-        CL = S.sb * sqrtf(fmaxf(tl, 0.f)) * 0.70710677f * (1.f - 1e-6f);
-        EL = ((CL + 1.f) * kMfmaErr + A) * (1.f + 1e-6f);
+        // diamond inscribed in the disc of radius sqrt(tl): |ex| + |ey| <= sqrt(tl) |W| (two
+        // coordinates' errors 2 (kMfmaErr + A) beside C_lo kMfmaErr from |W|), sharing the upper
+        // bound's |ex| + |ey|
+        CL = S.sb * sqrtf(fmaxf(tl, 0.f)) * (1.f - 1e-6f);
+        EL = ((CL + 2.f) * kMfmaErr + 2.f * A) * (1.f + 1e-6f);
     }
     // B-operand fragments of the own hypothesis: k 0-7 (bx, by, bw) and k 8-15 (shared by bx, by)
     h8v fx = {}, fy = {}, fw = {}, fn = {};
@@ -2570,8 +2575,6 @@ __global__ __launch_bounds__(256) void ransac_bound_mfma_kernel(const RansacStat
         CL0 = lowh ? CL : CLp; EL0 = lowh ? EL : ELp; CL1 = lowh ? CLp : CL; EL1 = lowh ? ELp : EL;
     }
     const bool wave_counts = __any(count);
-    float big = INFINITY;
-    asm volatile("" : "+v"(big));
     const uint4* __restrict__ T = tiles + (go >> 5) * 128;
     const int nt = (n + 31) >> 5;
     unsigned out0 = 0, out1 = 0, in0 = 0, in1 = 0;
@@ -2604,20 +2607,27 @@ __global__ __launch_bounds__(256) void ransac_bound_mfma_kernel(const RansacStat
             unsigned bits0 = 0, bits1 = 0, lb0 = 0, lb1 = 0;
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                // sign bit of R - max(|ex|, |ey|), R = C |W| + E: set when the point is out of the box
-                // (med3(a, b, big) = max(a, b) without the NaN canonicalisation of fmaxf; big is
-                // opaque so the compiler cannot turn the med3 back into a max)
-                const float m0 = __builtin_amdgcn_fmed3f(fabsf(ex0[r]), fabsf(ey0[r]), big);
-                const float m1 = __builtin_amdgcn_fmed3f(fabsf(ex1[r]), fabsf(ey1[r]), big);
-                const float d0 = fmaf(C0, fabsf(w0[r]), E0) - m0;
-                const float d1 = fmaf(C1, fabsf(w1[r]), E1) - m1;
-                bits0 = __builtin_amdgcn_alignbit(bits0, __float_as_uint(d0), 31);
-                bits1 = __builtin_amdgcn_alignbit(bits1, __float_as_uint(d1), 31);
-                if (kLo) {  // sign bit of max(|ex|, |ey|) - R_lo: set when surely in
-                    const float l0 = m0 - fmaf(CL0, fabsf(w0[r]), -EL0);
-                    const float l1 = m1 - fmaf(CL1, fabsf(w1[r]), -EL1);
+                // sign bit of R - |ex| - |ey|, R = C |W| + E: set when the point is outside the
+                // diamond (fma, two subtractions with |.| operands, alignbit; the rounding of R -
+                // |ex| moves the sign only where |ex| + |ey| is within 2^-24 R of R, inside C's and
+                // E's 1e-6 relative slack)
+                if (kLo) {  // the lower bound shares s = |ex| + |ey|
+                    const float s0 = fabsf(ex0[r]) + fabsf(ey0[r]);
+                    const float s1 = fabsf(ex1[r]) + fabsf(ey1[r]);
+                    const float d0 = fmaf(C0, fabsf(w0[r]), E0) - s0;
+                    const float d1 = fmaf(C1, fabsf(w1[r]), E1) - s1;
+                    bits0 = __builtin_amdgcn_alignbit(bits0, __float_as_uint(d0), 31);
+                    bits1 = __builtin_amdgcn_alignbit(bits1, __float_as_uint(d1), 31);
+                    // sign bit of s - R_lo: set when surely in
+                    const float l0 = s0 - fmaf(CL0, fabsf(w0[r]), -EL0);
+                    const float l1 = s1 - fmaf(CL1, fabsf(w1[r]), -EL1);
                     lb0 = __builtin_amdgcn_alignbit(lb0, __float_as_uint(l0), 31);
                     lb1 = __builtin_amdgcn_alignbit(lb1, __float_as_uint(l1), 31);
+                } else {
+                    const float d0 = (fmaf(C0, fabsf(w0[r]), E0) - fabsf(ex0[r])) - fabsf(ey0[r]);
+                    const float d1 = (fmaf(C1, fabsf(w1[r]), E1) - fabsf(ex1[r])) - fabsf(ey1[r]);
+                    bits0 = __builtin_amdgcn_alignbit(bits0, __float_as_uint(d0), 31);
+                    bits1 = __builtin_amdgcn_alignbit(bits1, __float_as_uint(d1), 31);
                 }
             }
             out0 += __popc(bits0);
@@ -2637,7 +2647,7 @@ __global__ __launch_bounds__(256) void ransac_bound_mfma_kernel(const RansacStat
     int lo = 0;
     if (kLo) {
         const unsigned i0 = in0 + __shfl_xor(in0, 32), i1 = in1 + __shfl_xor(in1, 32);
-        lo = (int)(lowh ? i0 : i1);  // zero-padded rows (ex = ey = W = 0) give m - R_lo = E_lo > 0: never "in"
+        lo = (int)(lowh ? i0 : i1);  // zero-padded rows (ex = ey = W = 0) give s - R_lo = E_lo > 0: never "in"
     }
     if (act) bounds[o] = invalid ? make_int2(-1, -1) : (uncertain ? make_int2(0, n) : make_int2(lo, n - outs));
 }

@@ -58,8 +58,8 @@ PEAK_F16_MFMA_TFLOPS = 2500.0  # dense f16 MFMA
 # wave's stream on one SIMD, MI355X_MICROARCH.md cycle-constants table) x 2.4 GHz
 PEAK_VALU_WAVE_INSTR_PER_S = 1024 * 0.25 * 2.4e9
 # ransac_bound_mfma_kernel tile loop, VALU per (point, hypothesis) pair: chunk 1 (the first 4,096 iterations,
-# 512 when maxIters <= 4,096) box upper bound + inscribed-square lower bound 7; later chunks the box alone (med3,
-# fma, sub, sign bit) 4
+# 512 when maxIters <= 4,096) diamond upper bound + inscribed-diamond lower bound 7 (|ex| + |ey| shared); later
+# chunks the upper bound alone (fma, two subtractions with |.| operands, sign bit) 4
 BOUND_VALU_PER_PAIR_C1, BOUND_VALU_PER_PAIR_C2 = 7, 4
 BOUND_MFMA_FLOP_PER_PAIR = 96  # 3 v_mfma_f32_32x32x16_f16 per 32 x 32 (point, hypothesis) pairs
 H_TOL = 1e-4                  # SURVEY.md 8(c) contract item 4 (the GPU tests hold bit identity)

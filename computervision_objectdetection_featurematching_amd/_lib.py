@@ -16,7 +16,7 @@ MIM_STREAM_SHORT = 5
 # every symbol include/mim.h declares (checked by tests/test_abi.py)
 EXPORTS = [
     "mim_version", "mim_default_params", "mim_ctx_create", "mim_ctx_destroy", "mim_last_error",
-    "mim_ctx_set_stream", "mim_ctx_set_sampler_stream", "mim_ctx_get_stream", "mim_synchronize", "mim_set_create", "mim_sets_clear", "mim_sets_truncate",
+    "mim_ctx_set_stream", "mim_ctx_set_sampler_stream", "mim_ctx_get_stream", "mim_synchronize", "mim_set_create", "mim_sets_clear", "mim_sets_truncate", "mim_sets_info", "mim_set_rows",
     "mim_knn2_l2", "mim_ratio_filter", "mim_find_homography", "mim_batch_run", "mim_batch_results",
     "mim_batch_results_dev", "mim_batch_results_copy", "mim_batch_problem_detail", "mim_batch_inlier_points", "mim_knn2_sets_dev", "mim_last_kernel_ms",
     "mim_set_timing", "mim_sift_detect_compute", "mim_sift_detect_compute_scales", "mim_sift_scales_sets",
@@ -87,6 +87,8 @@ def load():
     L.mim_set_create.argtypes = [vp, f32p, f32p, i32, i32, i32, C.POINTER(C.c_int32)]
     L.mim_sets_clear.argtypes = [vp]
     L.mim_sets_truncate.argtypes = [vp, i32]
+    L.mim_sets_info.argtypes = [vp, C.POINTER(C.c_int32), C.POINTER(C.c_int64)]
+    L.mim_set_rows.argtypes = [vp, i32, i32, f32p, f32p, C.POINTER(C.c_int32)]
     L.mim_knn2_l2.argtypes = [vp, f32p, i32, f32p, i32, i32, i32p, f32p]
     L.mim_ratio_filter.argtypes = [vp, i32p, f32p, i32, C.c_float, i32p, i32p, C.POINTER(C.c_int32)]
     L.mim_find_homography.argtypes = [vp, f32p, f32p, i32, C.c_double, i32, C.c_double, f64p, u8p]

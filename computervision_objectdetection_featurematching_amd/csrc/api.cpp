@@ -191,6 +191,8 @@ struct mim_ctx {
     std::vector<mim_problem> last_problems;
     mim_params last_params{};
     long long sets_gen = 0, last_gen = -1;
+    // the last batch is mim_find_homography's one record (no set table: no inlier points to gather)
+    bool last_fh = false;
     // MIM_CAND_CAP: candidate-list capacity override (test knob for the replay's overflow rescan)
     int cand_cap = 0;
     // MIM_ATTEMPT_REP_CAP: the attempt kernel's redraw-list capacity (test knob for its in-place path)
@@ -434,13 +436,9 @@ mim_status mim_sets_clear(mim_ctx* c) {
     return MIM_OK;
 }
 
-mim_status mim_sets_truncate(mim_ctx* c, int32_t n_keep) {
-    if (!c) return MIM_EINVAL;
-    std::lock_guard<std::mutex> lk(c->mu);
-    if (n_keep < 0 || n_keep > (int)c->sets.size())
-        return fail(c, MIM_EINVAL, "sets_truncate: %d sets registered, %d to keep", (int)c->sets.size(), n_keep);
-    if (n_keep == (int)c->sets.size()) return MIM_OK;
-    HIPCHK(c, hipSetDevice(c->device));
+// drops the sets with ids >= n_keep (0 <= n_keep <= sets.size(), checked by the callers) and
+// rewinds the arena to the first dropped set's storage; with the lock held
+static void sets_truncate_locked(mim_ctx* c, int n_keep) {
     // the dropped sets' pending preps go; their storage (and prep flags blocks that cover only dropped
     // sets) is reused by later sets, ordered on the ctx stream after the work already enqueued, as
     // for mim_sets_clear
@@ -461,6 +459,42 @@ mim_status mim_sets_truncate(mim_ctx* c, int32_t n_keep) {
     c->arena.seek(target);
     c->sets.resize(n_keep);
     ++c->sets_gen;
+}
+
+mim_status mim_sets_truncate(mim_ctx* c, int32_t n_keep) {
+    if (!c) return MIM_EINVAL;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (n_keep < 0 || n_keep > (int)c->sets.size())
+        return fail(c, MIM_EINVAL, "sets_truncate: %d sets registered, %d to keep", (int)c->sets.size(), n_keep);
+    if (n_keep == (int)c->sets.size()) return MIM_OK;
+    HIPCHK(c, hipSetDevice(c->device));
+    sets_truncate_locked(c, n_keep);
+    return MIM_OK;
+}
+
+mim_status mim_sets_info(mim_ctx* c, int32_t* n_sets, int64_t* generation) {
+    if (!c) return MIM_EINVAL;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (n_sets) *n_sets = (int32_t)c->sets.size();
+    if (generation) *generation = (int64_t)c->sets_gen;
+    return MIM_OK;
+}
+
+mim_status mim_set_rows(mim_ctx* c, int32_t set_id, int32_t cap, float* desc, float* kp_xy, int32_t* n_rows) {
+    if (!c) return MIM_EINVAL;
+    if (!n_rows || cap < 0) return fail(c, MIM_EINVAL, "set_rows: bad arguments");
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (set_id < 0 || set_id >= (int)c->sets.size())
+        return fail(c, MIM_EINVAL, "set_rows: set %d not registered (%d sets)", set_id, (int)c->sets.size());
+    HIPCHK(c, hipSetDevice(c->device));
+    const SetDev& d = c->sets[set_id].d;
+    *n_rows = d.n;
+    const int m = std::min(d.n, cap);
+    if (m > 0 && desc && d.f32)
+        HIPCHK(c, hipMemcpyAsync(desc, d.f32, sizeof(float) * kDim * m, hipMemcpyDeviceToHost, c->stream));
+    if (m > 0 && kp_xy && d.kp)
+        HIPCHK(c, hipMemcpyAsync(kp_xy, d.kp, sizeof(float2) * m, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
     return MIM_OK;
 }
 
@@ -728,6 +762,7 @@ mim_status mim_knn2_l2(mim_ctx* c, const float* q, int32_t nq, const float* t, i
     c->sets.resize(base);  // arena space is reclaimed at the next mim_sets_clear
     c->last_n = 0;         // no RANSAC records: the previous batch's are invalidated (mim.h)
     c->last_gen = -1;
+    c->last_fh = false;
     return MIM_OK;
 }
 
@@ -780,6 +815,7 @@ mim_status mim_ratio_filter(mim_ctx* c, const int32_t* idx, const float* dist, i
     *n_good = ng;
     c->last_n = 0;
     c->last_gen = -1;
+    c->last_fh = false;
     return MIM_OK;
 }
 
@@ -801,6 +837,7 @@ mim_status mim_knn2_sets_dev(mim_ctx* c, int32_t query_set, int32_t train_set, i
     ev_mark(c, "ratio");
     c->last_n = 0;  // no RANSAC records (mim.h)
     c->last_gen = -1;
+    c->last_fh = false;
     return MIM_OK;
 }
 
@@ -880,27 +917,9 @@ mim_status mim_sift_detect_compute_scales(mim_ctx* c, const uint8_t* gray, int32
     return MIM_OK;
 }
 
-mim_status mim_sift_scales_sets(mim_ctx* c, const uint8_t* gray, int32_t rows, int32_t cols, int64_t step,
-                                int32_t n_scales, const float* scales, int32_t* set_ids, int32_t* n_kp, int32_t max_kp,
-                                mim_keypoint* kps) {
-    if (!c) return MIM_EINVAL;
-    if (!gray || !set_ids || !n_kp || !scales || n_scales <= 0 || n_scales > 8 || rows <= 0 || cols <= 0 ||
-        step < cols || max_kp < 0 || (max_kp > 0 && !kps))
-        return fail(c, MIM_EINVAL, "sift_scales_sets: bad arguments");
-    for (int i = 0; i < n_scales; ++i)
-        if (!(scales[i] > 0)) return fail(c, MIM_EINVAL, "sift_scales_sets: scale %d is not > 0", i);
-    std::lock_guard<std::mutex> lk(c->mu);
-    HIPCHK(c, hipSetDevice(c->device));
-    std::vector<mim::SiftDevOut> out(n_scales);
-    const int r = mim::sift_scales_device(c->sift_scales, c->stream, gray, rows, cols, step, n_scales, scales, out.data(),
-                                          c->err);
-    if (r == -1) return MIM_EDEVICE;
-    if (r == -3) return MIM_EINVAL;
-    if (r == -4) return MIM_ELIMIT;
-    if (r != 0) return MIM_ERANGE;
-    // each scale's rows and keypoint positions copied on the device into the set arena (the SIFT
-    // workspaces are overwritten by the next SIFT call), the set registered as by mim_set_create
-    long long total = 0;
+// mim_sift_scales_sets' registration of the scales as sets (lock held); total = keypoints of all scales
+static mim_status scales_sets_register(mim_ctx* c, const mim::SiftDevOut* out, int n_scales, int32_t* set_ids,
+                                       int32_t* n_kp, long long& total) {
     for (int i = 0; i < n_scales; ++i) {
         const int n = out[i].n;
         n_kp[i] = n;
@@ -930,6 +949,42 @@ mim_status mim_sift_scales_sets(mim_ctx* c, const uint8_t* gray, int32_t rows, i
         c->pend.push_back(PrepJob{(const float*)df, (int8_t*)frag, (int*)norm, nullptr, n, 0});
         c->pend_set.push_back(set_ids[i]);
         c->sets.push_back(rec);
+    }
+    return MIM_OK;
+}
+
+mim_status mim_sift_scales_sets(mim_ctx* c, const uint8_t* gray, int32_t rows, int32_t cols, int64_t step,
+                                int32_t n_scales, const float* scales, int32_t* set_ids, int32_t* n_kp, int32_t max_kp,
+                                mim_keypoint* kps) {
+    if (!c) return MIM_EINVAL;
+    if (!gray || !set_ids || !n_kp || !scales || n_scales <= 0 || n_scales > 8 || rows <= 0 || cols <= 0 ||
+        step < cols || max_kp < 0 || (max_kp > 0 && !kps))
+        return fail(c, MIM_EINVAL, "sift_scales_sets: bad arguments");
+    for (int i = 0; i < n_scales; ++i)
+        if (!(scales[i] > 0)) return fail(c, MIM_EINVAL, "sift_scales_sets: scale %d is not > 0", i);
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIPCHK(c, hipSetDevice(c->device));
+    std::vector<mim::SiftDevOut> out(n_scales);
+    const int r = mim::sift_scales_device(c->sift_scales, c->stream, gray, rows, cols, step, n_scales, scales, out.data(),
+                                          c->err);
+    if (r == -1) return MIM_EDEVICE;
+    if (r == -3) return MIM_EINVAL;
+    if (r == -4) return MIM_ELIMIT;
+    if (r != 0) return MIM_ERANGE;
+    // each scale's rows and keypoint positions copied on the device into the set arena (the SIFT
+    // workspaces are overwritten by the next SIFT call), the set registered as by mim_set_create; a
+    // failure part-way (arena allocation, copy) drops the scales registered so far, so the ctx is left
+    // as before the call
+    const int n0 = (int)c->sets.size();
+    const Arena::Mark mark0 = c->arena.pos();
+    long long total = 0;
+    const mim_status rs = scales_sets_register(c, out.data(), n_scales, set_ids, n_kp, total);
+    if (rs != MIM_OK) {
+        if ((int)c->sets.size() > n0)
+            sets_truncate_locked(c, n0);
+        else
+            c->arena.seek(mark0);
+        return rs;
     }
     if (kps && max_kp > 0) {  // the keypoints on the host too, concatenated in scale order
         long long used = 0;
@@ -1168,6 +1223,7 @@ static mim_status batch_run_locked(mim_ctx* c, const mim_problem* problems, int3
     c->last_problems.assign(problems, problems + n);
     c->last_params = *params;
     c->last_gen = c->sets_gen;
+    c->last_fh = false;
     if (n == 0) { c->last_n = 0; return MIM_OK; }
     mim_status s = build_tables(c, problems, n, std::max(params->max_iters, 1));
     if (s != MIM_OK) return s;
@@ -1272,6 +1328,9 @@ mim_status mim_batch_inlier_points(mim_ctx* c, const float* scales, float* out_x
     const int n = c->last_n;
     // the gather reads the scene keypoints through the batch's set table: sets cleared or truncated
     // since mim_batch_run have had their storage rewound and possibly reused by newer sets
+    if (n > 0 && c->last_fh)
+        return fail(c, MIM_EINVAL, "batch_inlier_points: the last call was mim_find_homography, whose record has "
+                                   "no scene set to gather from (read its mask instead)");
     if (n > 0 && c->last_gen != c->sets_gen)
         return fail(c, MIM_EINVAL, "batch_inlier_points: the batch's sets were cleared or truncated since "
                                    "mim_batch_run");
@@ -1336,6 +1395,7 @@ mim_status mim_find_homography(mim_ctx* c, const float* src, const float* dst, i
     c->h_good_off.assign(1, 0);
     c->last_n = 1;  // mim_batch_results returns this call's record (mim.h)
     c->last_gen = -1;
+    c->last_fh = true;
     c->last_problems.clear();
     mim_result r;
     for (;;) {  // a run out of RNG draws is re-run on a longer stream

@@ -2357,7 +2357,15 @@ __device__ __forceinline__ void bound_hypothesis(const float4* __restrict__ P, i
 typedef _Float16 h8v __attribute__((ext_vector_type(8)));
 typedef float f16acc __attribute__((ext_vector_type(16)));
 constexpr float kMfmaErr = 0x1p-15f;
+// the bound kernel's fragments: points (ransac_tiles_kernel) and hypotheses each times 2^15, so its
+// MFMA outputs are K = 2^30 times the quantities above
+constexpr float kPointScale = 0x1p15f;
+constexpr double kHypScale = 0x1p15;
+constexpr double kOutScale = 0x1p30;
 constexpr int kTileChunk = 8;  // 32-point tiles per LDS stage of the MFMA bound kernel (2 x 16 KiB)
+
+// clamp to [0, 1]: folds into the producing instruction's clamp bit (no NaN reaches it here)
+__device__ __forceinline__ float clamp01(float x) { return __builtin_amdgcn_fmed3f(x, 0.f, 1.f); }
 
 // hi + lo = a to 2^-22 relative, with hi = (f16)a and lo = (f16)(a - hi) taken from the SAME value a.
 // `a` is pinned in a register first: given split_f16(u * x), the compiler otherwise forms
@@ -2421,22 +2429,24 @@ __global__ __launch_bounds__(256) void ransac_tiles_kernel(RansacState* __restri
     }
     uint4* __restrict__ T = tiles + (go >> 5) * 128;
     const int nt = (n + 31) >> 5;
-    const _Float16 one = (_Float16)1.f;
+    // the fragments carry kPointScale = 2^15 (|x'| < 1, so every entry stays below 2^15 in f16)
+    const _Float16 one = (_Float16)kPointScale;
     for (int i = tid; i < nt * 32; i += 256) {
         h8v lo = {}, axh = {}, ayh = {};
         if (i < n) {
             const float4 q = P[i];
             const float x = q.x * sa, y = q.y * sa, u = q.z * sb, v = q.w * sb;
+            const float xk = x * kPointScale, yk = y * kPointScale, uk = u * kPointScale, vk = v * kPointScale;
             _Float16 a, b;
-            split_f16(x, a, b); lo[0] = a; lo[1] = b; lo[2] = a;
-            split_f16(y, a, b); lo[3] = a; lo[4] = b; lo[5] = a;
+            split_f16(xk, a, b); lo[0] = a; lo[1] = b; lo[2] = a;
+            split_f16(yk, a, b); lo[3] = a; lo[4] = b; lo[5] = a;
             lo[6] = one; lo[7] = one;
-            split_f16(u * x, a, b); axh[0] = a; axh[1] = b; axh[2] = a;
-            split_f16(u * y, a, b); axh[3] = a; axh[4] = b; axh[5] = a;
-            split_f16(u, a, b); axh[6] = a; axh[7] = b;
-            split_f16(v * x, a, b); ayh[0] = a; ayh[1] = b; ayh[2] = a;
-            split_f16(v * y, a, b); ayh[3] = a; ayh[4] = b; ayh[5] = a;
-            split_f16(v, a, b); ayh[6] = a; ayh[7] = b;
+            split_f16(u * xk, a, b); axh[0] = a; axh[1] = b; axh[2] = a;
+            split_f16(u * yk, a, b); axh[3] = a; axh[4] = b; axh[5] = a;
+            split_f16(uk, a, b); axh[6] = a; axh[7] = b;
+            split_f16(v * xk, a, b); ayh[0] = a; ayh[1] = b; ayh[2] = a;
+            split_f16(v * yk, a, b); ayh[3] = a; ayh[4] = b; ayh[5] = a;
+            split_f16(vk, a, b); ayh[6] = a; ayh[7] = b;
         }
         uint4* t = T + (i >> 5) * 128;
         const int r = i & 31;
@@ -2451,7 +2461,7 @@ __global__ __launch_bounds__(256) void ransac_tiles_kernel(RansacState* __restri
 // column blocks of 32 hypotheses), the point tiles staged through LDS and shared by the 4 waves.
 // Both bounds test the L1 norm |ex| + |ey| (a diamond: the same area as the box max(|ex|, |ey|) of
 // rounds 2-4 around the same disc, so as tight, and v_add/v_sub with |.| operands issue at the
-// fp32 rate where the max / med3 issues ~1.5x slower, tools/probe/valu_rate_probe.hip).
+// fp32 rate where the max / med3 issues ~1.5x slower, tools/issue_probe.hip).
 // Upper bound: a point can be an inlier only if
 //   |ex| + |ey| <= C |W| + (C + 2) kMfmaErr + 2 A,  C = sqrt 2 sb sqrt(thr2 + d_max (+ widening)),
 // since (|ex| - A, |ey| - A) lies in the disc of radius C |W| / sqrt 2 and each MFMA output is
@@ -2463,6 +2473,17 @@ __global__ __launch_bounds__(256) void ransac_tiles_kernel(RansacState* __restri
 // cover near the hypothesis' horizon (|W| -> 0): X and W each carry an absolute error of
 // gamma * (sum of |terms|), gamma = 4 ulp(1/2) (float cast of H, product, two sums) + eta, so
 // |X_c/W_c - u| moves by <= (err_X + (|u| + 6) err_W) / |W|, i.e. |ex| by <= A.
+// Counting (round 5): the point and the hypothesis fragments each carry a factor 2^15, so every MFMA
+// output is K = kOutScale = 2^30 times the quantity above (X' = K ex, ...; exact: powers of two,
+// every fragment stays below 2^15 in f16, and the split's error only shrinks relative to the
+// outputs), and each (point, hypothesis) pair adds u = clamp(C |W'| + (K E + 1) - |X'| - |Y'|) to a
+// float count: exactly 1 for every point the test keeps (C and E carry 1e-6 relative slack, above the
+// three roundings' 2^-22 of C |W'| + K E + 1 >= 3, so the value cannot fall below 1), 0 past the
+// diamond widened by 1/K (2^-30 in the scaled units: no wider in practice), a fraction only there.
+// That is four fast-rate VALU per pair (fma, sub, sub with clamp, add) where the sign bit took a
+// v_alignbit and a v_bcnt at the slow rate; hi = floor(sum + slack) - padded rows, slack bounding
+// the float sum's rounding.  The lower bound adds clamp(C_lo |W'| - K E_lo - (|X'| + |Y'|)), positive
+// only where the point is surely in, so lo = ceil(sum - slack) never exceeds the exact count.
 template <bool kLo>
 __global__ __launch_bounds__(256) void ransac_bound_mfma_kernel(const RansacState* __restrict__ st,
                                                                 const ProbDev* __restrict__ probs,
@@ -2511,6 +2532,10 @@ __global__ __launch_bounds__(256) void ransac_bound_mfma_kernel(const RansacStat
     const double sc = ldexp(1.0, -e);
 #pragma unroll
     for (int i = 0; i < 9; ++i) h[i] *= sc;
+    // the fragments carry 2^15 on top (|h 2^15| < 2^15: f16 range), h[8] 2^15 = 2^(15 - e) exact
+    double hk[9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) hk[i] = h[i] * kHypScale;
     // per-hypothesis box constants (d_max and, for poorly conditioned samples, the widening at smax)
     float tt = thr2 + fmaf(1e-7f * S.smax, S.smax, 0.5f);
     if (eta > 0.f) tt += S.smax * fmaf(eta * eta, S.smax, 10.2f * eta);
@@ -2537,15 +2562,15 @@ __global__ __launch_bounds__(256) void ransac_bound_mfma_kernel(const RansacStat
     h8v fx = {}, fy = {}, fw = {}, fn = {};
     if (count) {
         _Float16 a, b;
-        split_f16(h[0], a, b); fx[0] = a; fx[1] = a; fx[2] = b;
-        split_f16(h[1], a, b); fx[3] = a; fx[4] = a; fx[5] = b;
-        split_f16(h[2], a, b); fx[6] = a; fx[7] = b;
-        split_f16(h[3], a, b); fy[0] = a; fy[1] = a; fy[2] = b;
-        split_f16(h[4], a, b); fy[3] = a; fy[4] = a; fy[5] = b;
-        split_f16(h[5], a, b); fy[6] = a; fy[7] = b;
-        split_f16(h[6], a, b); fw[0] = a; fw[1] = a; fw[2] = b;
-        split_f16(h[7], a, b); fw[3] = a; fw[4] = a; fw[5] = b;
-        fw[6] = (_Float16)(float)h[8];  // 2^-e: exact
+        split_f16(hk[0], a, b); fx[0] = a; fx[1] = a; fx[2] = b;
+        split_f16(hk[1], a, b); fx[3] = a; fx[4] = a; fx[5] = b;
+        split_f16(hk[2], a, b); fx[6] = a; fx[7] = b;
+        split_f16(hk[3], a, b); fy[0] = a; fy[1] = a; fy[2] = b;
+        split_f16(hk[4], a, b); fy[3] = a; fy[4] = a; fy[5] = b;
+        split_f16(hk[5], a, b); fy[6] = a; fy[7] = b;
+        split_f16(hk[6], a, b); fw[0] = a; fw[1] = a; fw[2] = b;
+        split_f16(hk[7], a, b); fw[3] = a; fw[4] = a; fw[5] = b;
+        fw[6] = (_Float16)(float)hk[8];  // 2^(15 - e): exact
         fn = -fw;
         fn[7] = fn[6];
     }
@@ -2567,17 +2592,19 @@ __global__ __launch_bounds__(256) void ransac_bound_mfma_kernel(const RansacStat
     const h8v b1x = __builtin_bit_cast(h8v, lowh ? r1 : un);
     const h8v b1y = __builtin_bit_cast(h8v, lowh ? r2 : un);
     const h8v b1w = __builtin_bit_cast(h8v, lowh ? r3 : zero4);
-    const float Cp = __shfl_xor(C, 32), Ep = __shfl_xor(E, 32);
-    const float C0 = lowh ? C : Cp, E0 = lowh ? E : Ep, C1 = lowh ? Cp : C, E1 = lowh ? Ep : E;
+    // in output units: K E + 1 (the band outside the upper test) and -K E_lo
+    const float EK = fmaf(E, (float)kOutScale, 1.f), ELK = -EL * (float)kOutScale;
+    const float Cp = __shfl_xor(C, 32), Ep = __shfl_xor(EK, 32);
+    const float C0 = lowh ? C : Cp, E0 = lowh ? EK : Ep, C1 = lowh ? Cp : C, E1 = lowh ? Ep : EK;
     float CL0 = 0.f, EL0 = 0.f, CL1 = 0.f, EL1 = 0.f;
     if (kLo) {
-        const float CLp = __shfl_xor(CL, 32), ELp = __shfl_xor(EL, 32);
-        CL0 = lowh ? CL : CLp; EL0 = lowh ? EL : ELp; CL1 = lowh ? CLp : CL; EL1 = lowh ? ELp : EL;
+        const float CLp = __shfl_xor(CL, 32), ELp = __shfl_xor(ELK, 32);
+        CL0 = lowh ? CL : CLp; EL0 = lowh ? ELK : ELp; CL1 = lowh ? CLp : CL; EL1 = lowh ? ELp : ELK;
     }
     const bool wave_counts = __any(count);
     const uint4* __restrict__ T = tiles + (go >> 5) * 128;
     const int nt = (n + 31) >> 5;
-    unsigned out0 = 0, out1 = 0, in0 = 0, in1 = 0;
+    float keep0 = 0.f, keep1 = 0.f, in0 = 0.f, in1 = 0.f;  // float counts (see above)
     // point tiles through LDS by LDS-DMA in chunks of kTileChunk, double buffered: the next chunk's
     // pieces are in flight while this chunk is scored; one barrier per chunk
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -2604,52 +2631,40 @@ __global__ __launch_bounds__(256) void ransac_bound_mfma_kernel(const RansacStat
             const f16acc ex1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ax, b1x, zc, 0, 0, 0);
             const f16acc ey1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ay, b1y, zc, 0, 0, 0);
             const f16acc w1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ax, b1w, zc, 0, 0, 0);
-            unsigned bits0 = 0, bits1 = 0, lb0 = 0, lb1 = 0;
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                // sign bit of R - |ex| - |ey|, R = C |W| + E: set when the point is outside the
-                // diamond (fma, two subtractions with |.| operands, alignbit; the rounding of R -
-                // |ex| moves the sign only where |ex| + |ey| is within 2^-24 R of R, inside C's and
-                // E's 1e-6 relative slack)
-                if (kLo) {  // the lower bound shares s = |ex| + |ey|
+                if (kLo) {  // the lower bound shares s = |X'| + |Y'|
                     const float s0 = fabsf(ex0[r]) + fabsf(ey0[r]);
                     const float s1 = fabsf(ex1[r]) + fabsf(ey1[r]);
-                    const float d0 = fmaf(C0, fabsf(w0[r]), E0) - s0;
-                    const float d1 = fmaf(C1, fabsf(w1[r]), E1) - s1;
-                    bits0 = __builtin_amdgcn_alignbit(bits0, __float_as_uint(d0), 31);
-                    bits1 = __builtin_amdgcn_alignbit(bits1, __float_as_uint(d1), 31);
-                    // sign bit of s - R_lo: set when surely in
-                    const float l0 = s0 - fmaf(CL0, fabsf(w0[r]), -EL0);
-                    const float l1 = s1 - fmaf(CL1, fabsf(w1[r]), -EL1);
-                    lb0 = __builtin_amdgcn_alignbit(lb0, __float_as_uint(l0), 31);
-                    lb1 = __builtin_amdgcn_alignbit(lb1, __float_as_uint(l1), 31);
+                    keep0 += clamp01(fmaf(C0, fabsf(w0[r]), E0) - s0);
+                    keep1 += clamp01(fmaf(C1, fabsf(w1[r]), E1) - s1);
+                    in0 += clamp01(fmaf(CL0, fabsf(w0[r]), EL0) - s0);
+                    in1 += clamp01(fmaf(CL1, fabsf(w1[r]), EL1) - s1);
                 } else {
-                    const float d0 = (fmaf(C0, fabsf(w0[r]), E0) - fabsf(ex0[r])) - fabsf(ey0[r]);
-                    const float d1 = (fmaf(C1, fabsf(w1[r]), E1) - fabsf(ex1[r])) - fabsf(ey1[r]);
-                    bits0 = __builtin_amdgcn_alignbit(bits0, __float_as_uint(d0), 31);
-                    bits1 = __builtin_amdgcn_alignbit(bits1, __float_as_uint(d1), 31);
+                    keep0 += clamp01((fmaf(C0, fabsf(w0[r]), E0) - fabsf(ex0[r])) - fabsf(ey0[r]));
+                    keep1 += clamp01((fmaf(C1, fabsf(w1[r]), E1) - fabsf(ex1[r])) - fabsf(ey1[r]));
                 }
-            }
-            out0 += __popc(bits0);
-            out1 += __popc(bits1);
-            if (kLo) {
-                in0 += __popc(lb0);
-                in1 += __popc(lb1);
             }
           }
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces of the next chunk landed
         __syncthreads();
     }
-    // rows (points) of a column are split over lanes l and l ^ 32
-    const unsigned o0 = out0 + __shfl_xor(out0, 32), o1 = out1 + __shfl_xor(out1, 32);
-    const int outs = (int)(lowh ? o0 : o1);
+    // rows (points) of a column are split over lanes l and l ^ 32.  Rounding of the float counts: a
+    // lane adds m = 16 nt values in [0, 1], each add off by <= 2^-24 m, plus the add of the two lanes:
+    // |error| <= 2^-24 (2 m^2 + 2 m) <= 2^-24 (32 nt)^2 = slack (0.24 at 2,000 points); an exact
+    // integer count (no value in the band) is unchanged by floor(+ slack) while slack < 1.
+    // Zero-padded rows (ex = ey = W = 0) add exactly 1 to the upper count (K E + 1 >= 1) and 0 to the
+    // lower one (-K E_lo < 0).
+    const float k0 = keep0 + __shfl_xor(keep0, 32), k1 = keep1 + __shfl_xor(keep1, 32);
+    const double slack = 0x1p-24 * (double)(32 * nt) * (double)(32 * nt);
+    const int hi = min(n, max(0, (int)floor((double)(lowh ? k0 : k1) + slack) - (32 * nt - n)));
     int lo = 0;
     if (kLo) {
-        const unsigned i0 = in0 + __shfl_xor(in0, 32), i1 = in1 + __shfl_xor(in1, 32);
-        lo = (int)(lowh ? i0 : i1);  // zero-padded rows (ex = ey = W = 0) give s - R_lo = E_lo > 0: never "in"
+        const float i0 = in0 + __shfl_xor(in0, 32), i1 = in1 + __shfl_xor(in1, 32);
+        lo = min(hi, max(0, (int)ceil((double)(lowh ? i0 : i1) - slack)));
     }
-    if (act) bounds[o] = invalid ? make_int2(-1, -1) : (uncertain ? make_int2(0, n) : make_int2(lo, n - outs));
+    if (act) bounds[o] = invalid ? make_int2(-1, -1) : (uncertain ? make_int2(0, n) : make_int2(lo, hi));
 }
 
 // exact count of one hypothesis (runKernel + computeError + findInliers, bit-exact)

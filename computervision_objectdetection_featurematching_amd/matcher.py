@@ -221,11 +221,12 @@ class Matcher:
             o += int(c)
         return out
 
-    def sift_scales_to_sets(self, gray, scales, keypoints: bool = False, max_kp: int = 1 << 18):
+    def sift_scales_to_sets(self, gray, scales, keypoints: bool = False, max_kp: int = 1 << 20):
         """resize + detectAndCompute at every scale (TestsDetector.cpp:99-107) with the descriptors left
         on the device, each scale registered as a set (mim_sift_scales_sets).  Returns (set ids, n_kp
         per scale, [keypoints per scale] or None); the sets' rows are what sift_detect_compute_scales
-        returns, without the round trip through host memory."""
+        returns, without the round trip through host memory.  With keypoints=True and more than max_kp
+        keypoints in all, this call's sets are dropped and the call made again with room for all."""
         g = np.ascontiguousarray(gray, np.uint8)
         if g.ndim != 2:
             raise ValueError("sift_scales_to_sets: a single-channel image is required")
@@ -233,11 +234,18 @@ class Matcher:
         ids = np.zeros(len(sc), np.int32)
         n = np.zeros(len(sc), np.int32)
         kps = np.zeros(max(max_kp, 1), KEYPOINT_DTYPE) if keypoints else None
-        self._check(self.L.mim_sift_scales_sets(
+        before = self.sets_info()[0]
+        st = self.L.mim_sift_scales_sets(
             self._ctx, C.c_void_p(g.ctypes.data), g.shape[0], g.shape[1], g.strides[0], len(sc),
             C.c_void_p(sc.ctypes.data), C.c_void_p(ids.ctypes.data), C.c_void_p(n.ctypes.data),
-            max_kp if keypoints else 0, C.c_void_p(kps.ctypes.data) if keypoints else None))
-        self._n_sets = int(ids[-1]) + 1
+            max_kp if keypoints else 0, C.c_void_p(kps.ctypes.data) if keypoints else None)
+        # the context's set count, whatever happened (MIM_ERANGE for a short host keypoint buffer comes
+        # after the sets were registered)
+        self._n_sets = self.sets_info()[0]
+        if st == _lib.MIM_ERANGE and keypoints and self._n_sets == before + len(sc) and int(n.sum()) > max_kp:
+            self.truncate_sets(before)  # drop this call's sets, run again with room for all
+            return self.sift_scales_to_sets(gray, scales, True, int(n.sum()))
+        self._check(st)
         out = None
         if keypoints:
             out, o = [], 0
@@ -245,6 +253,24 @@ class Matcher:
                 out.append(kps[o:o + c].copy())
                 o += int(c)
         return [int(i) for i in ids], [int(c) for c in n], out
+
+    def sets_info(self):
+        """(registered set count, sets generation) of the context (mim_sets_info)."""
+        n, gen = C.c_int32(), C.c_int64()
+        self._check(self.L.mim_sets_info(self._ctx, C.byref(n), C.byref(gen)))
+        return n.value, gen.value
+
+    def set_rows(self, set_id: int):
+        """The descriptor rows (n, 128) float32 and keypoint positions (n, 2) of a registered set as the
+        kernels read them (mim_set_rows; a debug/test copy-out, e.g. of mim_sift_scales_sets' sets)."""
+        n = C.c_int32()
+        self._check(self.L.mim_set_rows(self._ctx, int(set_id), 0, None, None, C.byref(n)))
+        desc = np.zeros((n.value, DIM), np.float32)
+        kp = np.zeros((n.value, 2), np.float32)
+        if n.value:
+            self._check(self.L.mim_set_rows(self._ctx, int(set_id), n.value, C.c_void_p(desc.ctypes.data),
+                                            C.c_void_p(kp.ctypes.data), C.byref(n)))
+        return desc, kp
 
     def resize_linear(self, src, dsize=None, fx: float = 0.0, fy: float = 0.0):
         """cv::resize(src, dst, dsize, fx, fy, INTER_LINEAR) of a CV_8UC1 image.

@@ -106,10 +106,17 @@ def forget_models(matcher: Matcher) -> None:
 class SceneRun:
     """detect_objects' intermediate products (for tests and benches)."""
     scene_kp: list      # per scale: KEYPOINT_DTYPE
-    scene_desc: list    # per scale: (n, 128) float32 (the same SIFT run again through host memory)
+    _scene_desc: list   # per scale: (n, 128) float32, copied out of the device sets the batch used
     results: np.ndarray  # RESULT_DTYPE per problem, problems in (model, scale, view) order
     points: list        # per model: allUnfilteredScenePts (n, 2) float32
     detections: list    # [((x, y, w, h), name)]
+
+    @property
+    def scene_desc(self) -> list:
+        if self._scene_desc is None:
+            raise ValueError("SceneRun.scene_desc: detect_objects(..., keep=True) ran without "
+                             "keep_descriptors=True (the scene's descriptors stay on the device)")
+        return self._scene_desc
 
 
 def detect_objects(matcher: Matcher, scene_gray, models: list[ObjectModel], scales=SCALES, params=None,
@@ -117,13 +124,13 @@ def detect_objects(matcher: Matcher, scene_gray, models: list[ObjectModel], scal
     """detectObjects(scene, models, detector) (TestsDetector.cpp:32-251) on a grayscale scene.
 
     Returns [((x, y, w, h), name)], or the SceneRun when keep=True (its scene_desc only with
-    keep_descriptors: the scene's descriptors never leave the device on the detection path, so they
-    are computed a second time through host memory for the caller)."""
+    keep_descriptors: the scene's descriptors never leave the device on the detection path; for the
+    caller they are copied out of the very sets the batch matched against, mim_set_rows)."""
     params = params or default_params()
     view_ids = _model_sets(matcher, models)
     # :99-107, all scales in one call, the scene's descriptors registered as sets on the device
     scene_ids, _, scene_kp = matcher.sift_scales_to_sets(scene_gray, scales, keypoints=keep)
-    scene_desc = [d for _, d in matcher.sift_detect_compute_scales(scene_gray, scales)] if keep_descriptors else None
+    scene_desc = [matcher.set_rows(i)[0] for i in scene_ids] if keep_descriptors else None
     tags = [(mi, si, vi) for mi in range(len(models)) for si in range(len(scales)) for vi in range(len(view_ids[mi]))]
     res = matcher.match_batch([(view_ids[mi][vi], scene_ids[si]) for mi, si, vi in tags], params)
     # :87-94 inlier scene points of the accepted problems (:74, :79, :81, :84), /scale when scale != 1,

@@ -116,6 +116,17 @@ mim_status mim_sets_clear(struct mim_ctx* ctx);
  * enqueued and borrowed pointers.  For a caller that keeps its model views registered across
  * scenes and replaces only the scene scales (TestsDetector.cpp:38-107 recomputes neither). */
 mim_status mim_sets_truncate(struct mim_ctx* ctx, int32_t n_keep);
+/* The registered set count and the sets generation: a counter that every mim_sets_clear and every
+ * mim_sets_truncate that drops a set increments (never mim_set_create).  A caller that caches set ids
+ * across calls (mim.hpp's Detector keeps its model views registered) compares the generation with the
+ * one it saw after its own last clear/truncate: a difference means another user of the ctx dropped
+ * sets, so the cached ids may name reused storage.  Either output may be NULL. */
+mim_status mim_sets_info(struct mim_ctx* ctx, int32_t* n_sets, int64_t* generation);
+/* Debug/test copy-out of set `set_id`: its n float32 descriptor rows (n x 128, row-major) and keypoint
+ * positions (n x 2) as the kernels read them, e.g. the device-registered scene scales of
+ * mim_sift_scales_sets.  Writes min(n, cap) rows (either output may be NULL); *n_rows = n.  Waits for
+ * the ctx stream. */
+mim_status mim_set_rows(struct mim_ctx* ctx, int32_t set_id, int32_t cap, float* desc, float* kp_xy, int32_t* n_rows);
 
 /* ---- primitive ops, host buffers, synchronous ------------------------------------------------
  * Each primitive call replaces the ctx's "last batch": after mim_knn2_l2 / mim_ratio_filter /
@@ -167,7 +178,9 @@ mim_status mim_batch_problem_detail(struct mim_ctx* ctx, int32_t i, int32_t* q_i
  * mim_batch_results), then one table copy in, one kernel, one copy out — instead of a
  * mim_batch_problem_detail round trip per accepted problem.  out_xy NULL: offsets only;
  * offsets[n] > cap: MIM_ERANGE (offsets valid, nothing copied).  MIM_EINVAL if the sets were cleared or
- * truncated (mim_sets_clear / mim_sets_truncate) after mim_batch_run: the points are read from them. */
+ * truncated (mim_sets_clear / mim_sets_truncate) after mim_batch_run: the points are read from them;
+ * MIM_EINVAL too after mim_find_homography, whose one record has no scene set to gather from (use
+ * its mask with the caller's own points). */
 mim_status mim_batch_inlier_points(struct mim_ctx* ctx, const float* scales, float* out_xy, int64_t cap,
                                    int64_t* offsets);
 

@@ -15,6 +15,9 @@
 // With OpenCV present, INTEGRATION.md shows the 20-line patch that swaps the reference's view loop for
 // detect_at_scale; the clustering/box code after the loop (TestsDetector.cpp:111-248) is unchanged.
 #pragma once
+#include <atomic>
+#include <cstdint>
+#include <cstring>
 #include <stdexcept>
 #include <string>
 #include <utility>
@@ -32,9 +35,31 @@ struct View {
     int size() const { return (int)keypoints.size(); }
 };
 
+// An object's identity for the Detector's registered-views cache: every constructed, copied, moved or
+// assigned-to ModelViews gets a fresh value, so an object that reuses a destroyed one's address (or is
+// overwritten by assignment) is never mistaken for it.
+class ObjectIdentity {
+   public:
+    ObjectIdentity() : v_(next()) {}
+    ObjectIdentity(const ObjectIdentity&) : v_(next()) {}
+    ObjectIdentity& operator=(const ObjectIdentity&) {
+        v_ = next();
+        return *this;
+    }
+    uint64_t value() const { return v_; }
+
+   private:
+    static uint64_t next() {
+        static std::atomic<uint64_t> counter{0};
+        return ++counter;
+    }
+    uint64_t v_;
+};
+
 struct ModelViews {
     std::string name;
     std::vector<View> views;  // ObjectModel::descriptors.size() entries
+    ObjectIdentity identity{};
 };
 
 class Error : public std::runtime_error {
@@ -60,8 +85,11 @@ class Detector {
     const std::vector<mim_result>& last_results() const { return results_; }
 
     // The model views registered by the last detect_* call are reused while the next call passes the
-    // same ModelViews objects with the same view counts and descriptor storage.  A caller that rewrites
-    // a view's descriptors or keypoints in place calls this first, so the next call registers them anew.
+    // same ModelViews objects (identity, not address: see ObjectIdentity) whose every view has the same
+    // descriptor and keypoint storage (pointers and sizes) and the same sampled rows (first, middle and
+    // last descriptor row and keypoint), and nobody else has dropped sets of this ctx (mim_sets_info's
+    // generation).  A caller that rewrites view contents in place calls this first, so the next call
+    // registers them anew: the sampled rows catch most rewrites, not all.
     void invalidate_models() { reg_n_ = -1; }
 
     // TestsDetector.cpp:58-95 for one model at one scale.
@@ -159,15 +187,23 @@ class Detector {
     // scene's sets (mim_sets_truncate) instead of re-uploading and re-preparing every view.
     void register_models(const std::vector<const ModelViews*>& models) {
         std::vector<RegKey> key;
-        for (const ModelViews* m : models)
-            key.push_back({m, m->views.size(), m->views.empty() ? nullptr : m->views[0].descriptors.data()});
-        if (reg_n_ >= 0 && key == reg_key_) {
+        for (const ModelViews* m : models) {
+            key.push_back({m, m->identity.value(), m->views.size(), nullptr, 0, nullptr, 0, 0});
+            for (const View& v : m->views)
+                key.push_back({nullptr, 0, 0, v.descriptors.data(), v.descriptors.size(),
+                               v.keypoints.empty() ? nullptr : &v.keypoints[0].x, v.keypoints.size(), sample(v)});
+        }
+        int64_t gen = -1;
+        check(mim_sets_info(ctx_, nullptr, &gen), "mim_sets_info", ctx_);
+        if (reg_n_ >= 0 && gen == reg_gen_ && key == reg_key_) {
             check(mim_sets_truncate(ctx_, reg_n_), "mim_sets_truncate", ctx_);
+            check(mim_sets_info(ctx_, nullptr, &reg_gen_), "mim_sets_info", ctx_);
             return;
         }
+        reg_n_ = -1;
         check(mim_sets_clear(ctx_), "mim_sets_clear", ctx_);
         reg_ids_.assign(models.size(), {});
-        reg_n_ = 0;
+        int32_t n = 0;
         for (size_t m = 0; m < models.size(); ++m)
             for (const View& v : models[m]->views) {
                 int32_t id;
@@ -175,9 +211,26 @@ class Detector {
                                      v.size(), 128, 0, &id),
                       "mim_set_create", ctx_);
                 reg_ids_[m].push_back(id);
-                reg_n_ = id + 1;
+                n = id + 1;
             }
+        check(mim_sets_info(ctx_, nullptr, &reg_gen_), "mim_sets_info", ctx_);
         reg_key_ = key;
+        reg_n_ = n;
+    }
+
+    // FNV-1a over a view's first, middle and last descriptor rows and keypoints
+    static uint64_t sample(const View& v) {
+        uint64_t h = 1469598103934665603ull;
+        auto mix = [&h](const void* p, size_t bytes) {
+            const unsigned char* b = (const unsigned char*)p;
+            for (size_t i = 0; i < bytes; ++i) h = (h ^ b[i]) * 1099511628211ull;
+        };
+        const size_t n = v.keypoints.size(), rows = v.descriptors.size() / 128;
+        for (size_t r : {size_t(0), rows / 2, rows ? rows - 1 : 0})
+            if (r < rows) mix(&v.descriptors[r * 128], 128 * sizeof(float));
+        for (size_t r : {size_t(0), n / 2, n ? n - 1 : 0})
+            if (r < n) mix(&v.keypoints[r], sizeof(Point2f));
+        return h;
     }
 
     void run(const std::vector<const ModelViews*>& models, const std::vector<ScaledScene>& scales,
@@ -228,11 +281,20 @@ class Detector {
             out[tags[i].m].insert(out[tags[i].m].end(), pts.begin() + offs[i], pts.begin() + offs[i + 1]);
     }
 
+    // one entry per model (m, its identity, view count), then one per view (storage and sampled rows)
     struct RegKey {
         const ModelViews* m;
+        uint64_t identity;
         size_t n_views;
-        const float* first_desc;
-        bool operator==(const RegKey& o) const { return m == o.m && n_views == o.n_views && first_desc == o.first_desc; }
+        const float* desc;
+        size_t desc_size;
+        const float* kp;
+        size_t kp_size;
+        uint64_t sampled;
+        bool operator==(const RegKey& o) const {
+            return m == o.m && identity == o.identity && n_views == o.n_views && desc == o.desc &&
+                   desc_size == o.desc_size && kp == o.kp && kp_size == o.kp_size && sampled == o.sampled;
+        }
     };
     mim_ctx* ctx_ = nullptr;
     mim_params params_;
@@ -240,6 +302,7 @@ class Detector {
     std::vector<RegKey> reg_key_;  // the models whose views are the ctx's first reg_n_ sets
     std::vector<std::vector<int32_t>> reg_ids_;
     int32_t reg_n_ = -1;
+    int64_t reg_gen_ = -1;  // the ctx's sets generation after this Detector's last clear/truncate
 };
 
 }  // namespace mim

@@ -118,6 +118,45 @@ int main() {
             for (auto& k : v.keypoints) k.x -= 3.0f;
         det.invalidate_models();
     }
+    // the cache without invalidate_models(): (a) a view's descriptors replaced by copy-assignment (the
+    // vector keeps its buffer, so only the sampled rows differ), (b) the model overwritten by
+    // assignment (fresh identity), (c) the ctx's sets dropped and replaced through det.ctx() (sets
+    // generation): each time the result equals a fresh Detector's
+    auto same_as_fresh = [&](const mim::ModelViews& mv, const char* what) {
+        std::vector<std::vector<mim::Point2f>> a, f;
+        det.detect_scene({&mv}, {{&skp[0], &sdesc[0], scales[0]}, {&skp[1], &sdesc[1], scales[1]}}, a);
+        mim::Detector det2(0);
+        det2.params().max_iters = 2000;
+        det2.detect_scene({&mv}, {{&skp[0], &sdesc[0], scales[0]}, {&skp[1], &sdesc[1], scales[1]}}, f);
+        bool same = a.size() == f.size() && a[0].size() == f[0].size();
+        for (size_t i = 0; same && i < f[0].size(); ++i) same = a[0][i].x == f[0][i].x && a[0][i].y == f[0][i].y;
+        if (!same) std::printf("FAIL registered-views cache: %s (%zu vs %zu points)\n", what, a[0].size(), f[0].size());
+        return same;
+    };
+    {
+        const std::vector<float> keep1 = model.views[1].descriptors;
+        const float* buf = model.views[1].descriptors.data();
+        model.views[1].descriptors = model.views[2].descriptors;
+        if (model.views[1].descriptors.data() != buf) std::printf("note: the copy-assignment reallocated\n");
+        if (!same_as_fresh(model, "view descriptors replaced")) return 1;
+        model.views[1].descriptors = keep1;
+        if (!same_as_fresh(model, "view descriptors restored")) return 1;
+        mim::ModelViews other = model;
+        for (auto& k : other.views[0].keypoints) k.y += 2.0f;
+        model = other;
+        if (!same_as_fresh(model, "model assigned")) return 1;
+        for (auto& k : model.views[0].keypoints) k.y -= 2.0f;
+        det.invalidate_models();
+        if (!same_as_fresh(model, "model restored")) return 1;
+        int32_t junk_id = 0;
+        if (mim_sets_clear(det.ctx()) != MIM_OK ||
+            mim_set_create(det.ctx(), sdesc[0].data(), &skp[0][0].x, nt, 128, 0, &junk_id) != MIM_OK) {
+            std::printf("FAIL external sets calls\n");
+            return 1;
+        }
+        if (!same_as_fresh(model, "sets replaced through ctx()")) return 1;
+        std::printf("OK registered-views cache\n");
+    }
     std::printf("OK %zu inlier points, statuses:", ref.size());
     for (auto& r : det.last_results()) std::printf(" %d/%d/%d", r.n_good, r.n_inl, r.status);
     std::printf("\n");

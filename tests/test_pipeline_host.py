@@ -40,3 +40,12 @@ def test_save_detections_format(tmp_path):
     p = tmp_path / "r.txt"
     save_detections(str(p), [((10, 20, 30, 40), "004_sugar_box"), ((1, 2, 3, 4), "035_power_drill")])
     assert p.read_text() == "004_sugar_box 10 20 40 60\n035_power_drill 1 2 4 6\n"
+
+
+def test_scene_run_descriptors_only_when_kept():
+    from computervision_objectdetection_featurematching_amd.pipeline import SceneRun
+    run = SceneRun([], None, np.zeros(0), [], [])
+    with pytest.raises(ValueError, match="keep_descriptors"):
+        _ = run.scene_desc
+    d = [np.zeros((2, 128), np.float32)]
+    assert SceneRun([], d, np.zeros(0), [], []).scene_desc is d

@@ -736,6 +736,7 @@ def run_batches(args, rank, world, local):
     knn_idx = [torch.empty((nq0, 2), dtype=torch.int32, device=dev) for _ in range(nf)]  # per context
     knn_dist = [torch.empty((nq0, 2), dtype=torch.float32, device=dev) for _ in range(nf)]
     counter = [0]
+    no_gather = os.environ.get("MIM_BENCH_GATHER", "1") == "0"
 
     def step():
         k = counter[0] % nf
@@ -750,8 +751,10 @@ def run_batches(args, rank, world, local):
                 return
             m.match_batch_async([(q_ids[a], t_ids[b]) for a, b in ds.problems], prm)
             m.batch_results_copy_to(mine[k])
-            # RCCL all-gather of the result records (gloo rehearsal: through host memory)
-            gath[k] = shard.gather_results(mine[k] if cdev.type == "cuda" else mine[k].cpu(), world)
+            # RCCL all-gather of the result records (gloo rehearsal: through host memory); MIM_BENCH_GATHER=0
+            # is a diagnostic that leaves it out (the line then says so and is not a contract line)
+            if not no_gather:
+                gath[k] = shard.gather_results(mine[k] if cdev.type == "cuda" else mine[k].cpu(), world)
 
     for mm in matchers:
         mm.set_timing(False)
@@ -910,6 +913,8 @@ def run_batches(args, rank, world, local):
         if gather_check is not None:
             gather_check["ranks_own_row_differs"] = int(tot[3])  # summed over ranks
             out["gather"] = gather_check
+        if os.environ.get("MIM_BENCH_GATHER", "1") == "0":
+            out["diagnostic"] = "MIM_BENCH_GATHER=0: the per-step record gather left out (not a contract line)"
         print(json.dumps(out), flush=True)
     for mm in matchers:
         mm.close()

@@ -610,30 +610,69 @@ static mim_status build_tables(mim_ctx* c, const mim_problem* problems, int n, i
     int n_launch = nphys;
     if (dyn) {
         // MIM_KNN_DYN=1: whole query-block sweeps (one split per problem), in unit order, as 8 contiguous
-        // lists of about equal work (one per XCD); the resident blocks pull them (knn2_i8_kernel)
+        // lists of about equal work (one per XCD); the resident blocks pull them (knn2_i8_kernel).
+        // The tail: when the sweeps do not fill the last round of the G resident blocks (a per-GPU shard
+        // of 32 C4 problems is 640 sweeps over 512 blocks: two rounds, the second a quarter full), the
+        // trailing problems covering that remainder are cut into k train-tile pieces per query block
+        // (k ~ G / their sweeps, <= 8), which every list holds after its whole sweeps: the blocks
+        // that finish early pull pieces and the kernel ends near sweeps / G rounds instead of the
+        // ceiling (each piece repeats the keyed early tiles and the prologue, a few per cent of a
+        // sweep; partial top-2 lists merged by the ratio kernel).  MIM_KNN_TAIL=0: whole sweeps only.
         works.clear();
-        long long total = 0;
+        const char* tail_env = getenv("MIM_KNN_TAIL");
+        const long long rem = n_sweeps % G;
+        int tail_from = n, ksplit = 1;
+        if ((!tail_env || atoi(tail_env) != 0) && n_sweeps > G && rem > 0) {
+            long long ts = 0;
+            while (tail_from > 0 && ts < rem) ts += c->h_probs[--tail_from].q_pad / kKnnBlockQ;
+            ksplit = (int)std::max<long long>(2, std::min<long long>(8, (G + ts / 2) / ts));
+        }
+        long long total = 0, total_t = 0;
         for (int i = 0; i < n; ++i) {
             ProbDev& P = c->h_probs[i];
             const int qb = P.q_pad / kKnnBlockQ;
             P.nsplit = 1;
+            if (i >= tail_from) continue;
             for (int b = 0; b < qb; ++b) works.push_back(KnnWork{i, b * kKnnBlockQ, 0, P.t.n_tiles, 0});
             total += (long long)qb * P.t.n_tiles;
         }
-        // part offsets for one split per problem
+        std::vector<KnnWork> tail;
+        for (int i = tail_from; i < n; ++i) {  // pieces in (problem, tile range, query block) order
+            ProbDev& P = c->h_probs[i];
+            const int qb = P.q_pad / kKnnBlockQ, nt = P.t.n_tiles, k = std::min(ksplit, std::max(nt, 1));
+            P.nsplit = k;
+            for (int j = 0; j < k; ++j)
+                for (int b = 0; b < qb; ++b) tail.push_back(KnnWork{i, b * kKnnBlockQ, j * nt / k, (j + 1) * nt / k, j});
+            total_t += (long long)qb * nt;
+        }
         part = 0;
         for (int i = 0; i < n; ++i) {
             c->h_probs[i].part_off = part;
-            part += c->h_probs[i].q_pad;
+            part += (long long)c->h_probs[i].nsplit * c->h_probs[i].q_pad;
         }
+        // 8 lists, each [its eighth of the whole sweeps | its eighth of the pieces], equal work per part
+        auto cuts = [&](const std::vector<KnnWork>& v, long long tot) {
+            std::vector<int> cut(9, (int)v.size());
+            cut[0] = 0;
+            long long acc = 0;
+            int x = 1;
+            for (size_t k = 0; k < v.size() && x < 8; ++k) {
+                acc += v[k].tile1 - v[k].tile0;
+                while (x < 8 && acc * 8 >= tot * x) cut[x++] = (int)k + 1;
+            }
+            return cut;
+        };
+        const std::vector<int> cw = cuts(works, total), ct = cuts(tail, total_t);
+        std::vector<KnnWork> all;
+        all.reserve(works.size() + tail.size());
         seg.assign(9, 0);
-        long long acc = 0;
-        int x = 1;
-        for (size_t k = 0; k < works.size() && x < 8; ++k) {
-            acc += c->h_probs[works[k].problem].t.n_tiles;
-            while (x < 8 && acc * 8 >= total * x) seg[x++] = (int)k + 1;
+        for (int x = 0; x < 8; ++x) {
+            seg[x] = (int)all.size();
+            all.insert(all.end(), works.begin() + cw[x], works.begin() + cw[x + 1]);
+            all.insert(all.end(), tail.begin() + ct[x], tail.begin() + ct[x + 1]);
         }
-        for (; x <= 8; ++x) seg[x] = (int)works.size();
+        seg[8] = (int)all.size();
+        works.swap(all);
         n_launch = (int)std::min<long long>(G, std::max<size_t>(works.size(), 8));
         n_launch = std::max(8, n_launch / 8 * 8);
     } else {

@@ -937,26 +937,41 @@ constexpr int kAttemptSpan = 256 * kAttemptPerThread;  // window positions per b
 // outliers), 29 with the window's margin; the flag capacity allows 28.  The grid is sized for 6: a C4
 // chunk launches ~35 k attempt blocks (and ~18 k check blocks), each looping over ~4 rounds.
 constexpr int kAttemptRateEst = 6;
+// the sampler grids' floor (blocks in all, ~16 per CU) for batches too small to fill the GPU otherwise
+constexpr int kSamplerMinBlocks = 4096;
 
 // Positions whose first 4 draws repeat an index (~0.3 % at n = 2000, ~5 % at n = 128) are listed in LDS
 // over all of the block's rounds and their redraw lengths resolved once at the block's end, one per
 // thread (resolved in place, every wave holding one of them, ~80 % of the waves, ran the redraw loop).
 constexpr int kAttemptRepCap = 2048;
 
+// Placement (speed only; blocks b and b + 8 share an XCD under round-robin dispatch): the problems share
+// one RNG stream and their windows start near the same position, so block b runs window slice kb of
+// problem p with kb = b mod 8 (mod 8) and the problems in dispatch order: an XCD streams only its
+// slices (1/8 of the window), and consecutive blocks on it read the same slice for different
+// problems from its L2.  bpp is a multiple of 8; the grid is n_probs x bpp.
+__device__ __forceinline__ void sampler_slice_block(int n_probs, int bpp, int& p, int& kb) {
+    const int x = blockIdx.x & 7, j = blockIdx.x >> 3;
+    p = j % n_probs;
+    kb = 8 * (j / n_probs) + x;
+    (void)bpp;
+}
+
 __global__ __launch_bounds__(256) void ransac_attempt_kernel(const RansacState* __restrict__ st,
                                                              const uint32_t* __restrict__ stream, long long slen,
                                                              uint8_t* __restrict__ flags, int wcap, int bpp, int c1,
-                                                             int rep_cap) {
+                                                             int rep_cap, int n_probs) {
     constexpr int D = kAttemptPerThread + 3;  // the first 4 draws of the thread's 8 attempts
     constexpr int kStageVecs = kAttemptSpan / 4 + 4;  // 16-byte vectors: the span, its 3 extra draws, alignment
     __shared__ __attribute__((aligned(16))) unsigned sdraw[4 * kStageVecs];
     __shared__ int rep_pos[kAttemptRepCap];
     __shared__ int n_rep;
-    const int p = blockIdx.x / bpp;
+    int p, kb;
+    sampler_slice_block(n_probs, bpp, p, kb);
     const RansacState S = st[p];
     if (!S.active || S.done || S.fail_iter != -1 || S.n < kSmallMaxN || S.produced >= min(c1, S.niters)) return;
     const int wlen = window_len(S, c1, wcap);  // a multiple of 64
-    MIM_DEBUG_PRINT(threadIdx.x == 0 && blockIdx.x % bpp == 0 && (p == 0 || p == 100),
+    MIM_DEBUG_PRINT(threadIdx.x == 0 && kb == 0 && (p == 0 || p == 100),
                     "[attempt] p=%d c1=%d wlen=%d bpp=%d produced=%d stream_pos=%lld n=%d\n", p, c1, wlen, bpp, S.produced,
                     (long long)S.stream_pos, S.n);
     uint8_t* __restrict__ F = flags + (long long)p * wcap;
@@ -965,7 +980,7 @@ __global__ __launch_bounds__(256) void ransac_attempt_kernel(const RansacState* 
     if (threadIdx.x == 0) n_rep = 0;
     // the grid covers the window a typical draw rate implies (kAttemptRateEst), not its capacity; a
     // longer window (low checkSubset pass rate) is covered by the same blocks looping
-    for (int boff = (blockIdx.x % bpp) * kAttemptSpan; boff < wlen; boff += bpp * kAttemptSpan) {
+    for (int boff = kb * kAttemptSpan; boff < wlen; boff += bpp * kAttemptSpan) {
     __syncthreads();  // the previous round's reads of sdraw are done (and n_rep's reset seen)
     // stream positions fit 32 bits (the stream is capped at 2^28 draws; 64 zero draws pad its end);
     // the stage starts at the 16-byte vector holding qb: draw qb + e is sdraw[shift + e]
@@ -1382,17 +1397,23 @@ __global__ __launch_bounds__(kCheckBlock) void ransac_check_kernel(const ChainSe
                                                                    const float4* __restrict__ pts,
                                                                    const RansacState* __restrict__ st,
                                                                    const uint32_t* __restrict__ stream, long long slen,
-                                                                   uint32_t* __restrict__ pass_bits, int wcap, int bpp) {
+                                                                   uint32_t* __restrict__ pass_bits, int wcap, int bpp,
+                                                                   int n_probs) {
     __shared__ uint32_t words[kCheckBlock * kCheckPer / 32];  // the round's pass bits
     __shared__ int def_t[kCheckBlock * kCheckPer], def_q[kCheckBlock * kCheckPer];
     __shared__ int4 seg_tab[kCheckSegs];
     __shared__ int n_def;
-    const int p = blockIdx.x / bpp, lane = threadIdx.x & 63;
+    // placement (speed only): problem p on XCD p mod 8 (its points stay in one L2), and an XCD's
+    // problems in dispatch order for each chain slice kb (the slice's stream draws read from that L2 by
+    // all of them); grid 8 ceil(n_probs / 8) bpp, blocks past n_probs idle
+    const int x = blockIdx.x & 7, jx = blockIdx.x >> 3, np8 = (n_probs + 7) >> 3;
+    const int p = x + 8 * (jx % np8), kb0 = jx / np8, lane = threadIdx.x & 63;
+    if (p >= n_probs) return;
     const ChainSegs* G = chains + p;
     const int T = G->T;
     if (T <= 0) return;  // nothing this chunk
     const RansacState S = st[p];
-    for (int b = blockIdx.x % bpp; b * kCheckBlock * kCheckPer < T; b += bpp) {
+    for (int b = kb0; b * kCheckBlock * kCheckPer < T; b += bpp) {
     const int base = b * kCheckBlock * kCheckPer;
     // segment data of the block's first kCheckSegs segments in one round of (uniform, scalar) loads
     const int nseg = G->nseg;
@@ -3581,11 +3602,15 @@ void ransac_enqueue(const RansacParams& prm, int n_probs, const ProbDev* probs, 
         const int wcap = (int)(std::min<long long>((long long)(c1 - c0) * 28 + 4096, b.flag_cap / std::max(n_probs, 1)) & ~63LL);
         // grids for the window a typical draw rate implies (the kernels loop over a longer one)
         const int west = (int)std::min<long long>(wcap, (long long)(c1 - c0) * kAttemptRateEst + 4096);
-        const int bppw = (west + kAttemptSpan - 1) / kAttemptSpan;
+        // at least kSamplerMinBlocks blocks in all while the window holds that many slices (a small batch's
+        // first chunk would otherwise leave most of the GPU idle), a multiple of 8 per problem (placement)
+        const int bppw_cap = std::max(1, wcap / kAttemptSpan);
+        const int bppw = (std::max((west + kAttemptSpan - 1) / kAttemptSpan,
+                                   std::min(bppw_cap, (kSamplerMinBlocks + n_probs - 1) / n_probs)) + 7) / 8 * 8;
         // (MIM_ATTEMPT_REP_CAP < kAttemptRepCap: test knob forcing the in-place redraw resolution)
         const int rep_cap = prm.rep_cap > 0 ? std::min(prm.rep_cap, kAttemptRepCap) : kAttemptRepCap;
         ransac_attempt_kernel<<<n_probs * bppw, 256, 0, ss>>>(b.state, b.stream, b.stream_len, b.flags, wcap, bppw, c1,
-                                                             rep_cap);
+                                                             rep_cap, n_probs);
         mark(mark_ctx, "attempt", ss);
         if (use_chain) {
             ChainSegs* chains = reinterpret_cast<ChainSegs*>(b.chains);
@@ -3595,9 +3620,11 @@ void ransac_enqueue(const RansacParams& prm, int n_probs, const ProbDev* probs, 
             ransac_walk_kernel<<<n_probs, kChainThreads, 0, ss>>>(b.state, b.flags, wcap, c1, b.irr, b.irr_cnt,
                                                                  b.irr_blocks, chains);
             mark(mark_ctx, "chain", ss);
-            const int bpp_chk = (west / 4 + kCheckBlock * kCheckPer) / (kCheckBlock * kCheckPer);  // T ~ wlen / 4
-            ransac_check_kernel<<<n_probs * bpp_chk, kCheckBlock, 0, ss>>>(chains, probs, pts, b.state, b.stream,
-                                                                          b.stream_len, b.pass_bits, wcap, bpp_chk);
+            constexpr int kChkSpan = kCheckBlock * kCheckPer;
+            const int bpp_chk = std::max((west / 4 + kChkSpan) / kChkSpan,  // T ~ wlen / 4
+                                         std::min(std::max(1, wcap / 4 / kChkSpan), (kSamplerMinBlocks + n_probs - 1) / n_probs));
+            ransac_check_kernel<<<8 * ((n_probs + 7) / 8) * bpp_chk, kCheckBlock, 0, ss>>>(
+                chains, probs, pts, b.state, b.stream, b.stream_len, b.pass_bits, wcap, bpp_chk, n_probs);
             mark(mark_ctx, "check", ss);
             ransac_count_kernel<<<n_probs, kChainThreads, 0, ss>>>(b.state, probs, chains, b.pass_bits, b.flags, wcap,
                                                                   b.samples, c1);

@@ -54,14 +54,22 @@ sys.path.insert(0, ROOT)
 
 PEAK_I8_TOPS = 5000.0       # MI355X dense i8 MFMA = 2x dense bf16 2.5 PF (MI355X_MICROARCH.md, no sparsity)
 PEAK_F16_MFMA_TFLOPS = 2500.0  # dense f16 MFMA
-# VALU issue peak: 1024 SIMDs x one wave64 instruction per 4 cycles (v_add/v_fma/v_max3 issue cost of one
-# wave's stream on one SIMD, MI355X_MICROARCH.md cycle-constants table) x 2.4 GHz
-PEAK_VALU_WAVE_INSTR_PER_S = 1024 * 0.25 * 2.4e9
-# ransac_bound_mfma_kernel tile loop, VALU per (point, hypothesis) pair: chunk 1 (the first 4,096 iterations,
-# 512 when maxIters <= 4,096) diamond upper bound + inscribed-diamond lower bound 7 (|ex| + |ey| shared); later
-# chunks the upper bound alone (fma, two subtractions with |.| operands, sign bit) 4
+# VALU issue peak: 1024 SIMDs x one wave64 fp32 add/fma per 2 cycles (a SIMD-32 retires a wave64 fp32 op in 2
+# cycles once two or more waves issue: MI355X_MICROARCH.md cycle-constants table; tools/issue_probe.hip measures
+# 1.07-1.21 ns per wave-instruction at 8 waves per SIMD, profiles/r05*_issue_probe.txt) x 2.4 GHz
+PEAK_VALU_WAVE_INSTR_PER_S = 1024 * 0.5 * 2.4e9
+# ransac_bound_mfma_kernel tile loop, VALU per (point, hypothesis) pair, all fp32 add/sub/fma (round 5: a clamped
+# float count instead of the sign bit's v_alignbit): later chunks fma, sub, sub with clamp, add = 4; chunk 1 (the
+# first 4,096 iterations, 512 when maxIters <= 4,096) also the lower bound: add (|X'| + |Y'|, shared), then fma,
+# sub with clamp, add for each bound = 7
 BOUND_VALU_PER_PAIR_C1, BOUND_VALU_PER_PAIR_C2 = 7, 4
 BOUND_MFMA_FLOP_PER_PAIR = 96  # 3 v_mfma_f32_32x32x16_f16 per 32 x 32 (point, hypothesis) pairs
+# issue model of one SIMD (tools/issue_probe.hip at ~2.0-2.1 GHz, profiles/r05b_issue_probe.txt): a fast fp32
+# VALU wave-instruction costs ~1.15 ns, and a v_mfma_f32_32x32x16_f16 takes ~10.5 ns of VALU issue from its SIMD
+# (2 MFMAs + 64 fmas run 20-22 ns longer than the 64 fmas alone, at 2 and 4 waves per SIMD, i.e. about 2/3 of the
+# MFMA's 32 cycles: the matrix pipe and the VALU do not co-execute on one SIMD beyond that, nor with the roles
+# split over two waves, section D)
+ISSUE_NS_VALU, ISSUE_NS_MFMA_F16_32 = 1.15, 10.5
 H_TOL = 1e-4                  # SURVEY.md 8(c) contract item 4 (the GPU tests hold bit identity)
 
 
@@ -612,8 +620,13 @@ def kernel_rooflines(args, ds, res, iso, iso_step_ms, knn_only):
             "mfma": {"achieved_TFLOPs": round(pairs * BOUND_MFMA_FLOP_PER_PAIR / tb / 1e12, 1),
                      "peak_TFLOPs": PEAK_F16_MFMA_TFLOPS,
                      "frac": round(pairs * BOUND_MFMA_FLOP_PER_PAIR / tb / 1e12 / PEAK_F16_MFMA_TFLOPS, 4)},
+            # the SIMDs' issue time the tile loop needs by the probe's costs (test VALU + MFMA), over the kernel time
+            "issue_model": {"valu_ns": ISSUE_NS_VALU, "mfma_ns": ISSUE_NS_MFMA_F16_32,
+                            "floor_ms": round((wi * ISSUE_NS_VALU + pairs * 3 / 1024.0 * ISSUE_NS_MFMA_F16_32) / 1024 * 1e-6, 4),
+                            "frac": round((wi * ISSUE_NS_VALU + pairs * 3 / 1024.0 * ISSUE_NS_MFMA_F16_32) / 1024 * 1e-9 / tb, 4)},
             "note": "pairs = iterations x good matches of every problem (OpenCV scores every hypothesis on every "
-                    "point); VALU peak = 1024 SIMDs x 1 wave64 instruction per 4 cycles x 2.4 GHz"}}
+                    "point); VALU peak = 1024 SIMDs x 1 wave64 fp32 instruction per 2 cycles x 2.4 GHz; issue_model: "
+                    "the tile loop's test VALU and MFMA priced by tools/issue_probe.hip (per SIMD)"}}
     # consistency: one stream, one batch at a time -> the kernels' durations cannot exceed the step
     worst = max(iso.values()) if iso else 0.0
     total = sum(iso.values())

@@ -646,10 +646,33 @@ __device__ __forceinline__ int ctz64(unsigned long long m) { return __builtin_ct
 //      bins b and b + 256 in order, so every bin's sum runs in pixel order: the oracle's float sums,
 //      bit for bit, with independent LDS reads instead of a dependent round trip per contribution.
 // The wrap, the 0.2 clamp and the x 512 normalisation then run on wave 0 in the reference's order.
+// Round 5: only about half the (2 radius + 1)^2 patch can pass the window test (the rotated 5 x 5-cell
+// square inside its circumscribed square), so the batches run over a compacted patch: per row a
+// conservative column range from the window's two linear constraints (in double, widened by a value
+// margin and one pixel, intersected with the image), rows concatenated in order.  The exact float test
+// still decides every pixel, and the excluded pixels are ones it rejects, so the contributions and
+// their pixel order are unchanged.  Patches of more than kDescrRowsMax rows take the full square.
 // (Round 3 history: one wave walking the pixels one at a time, 0.76 ms per call; one wave with 64-bit
 // masks walked by the owners, 0.64 ms; 256 threads with the mask walk, 0.37 ms: each contribution a
 // dependent chain of two LDS reads.)
 constexpr int kDescrT = 256, kDescrWords = kDescrT / 64;
+constexpr int kDescrRowsMax = 512;
+
+// columns j of one patch row with a j + b in (-2.5, 2.5) (c_rot or r_rot of the window test, rbin /
+// cbin in (-1, kDW)), intersected into [lo, hi]: conservative (value margin 1e-3, one pixel each side)
+__device__ __forceinline__ void window_cols(double a, double b, int& lo, int& hi) {
+    constexpr double kM = 2.5 + 1e-3;
+    if (fabs(a) < 1e-30) {
+        if (fabs(b) >= kM) hi = lo - 1;
+        return;
+    }
+    double j0 = (-kM - b) / a, j1 = (kM - b) / a;
+    if (j0 > j1) { const double t = j0; j0 = j1; j1 = t; }
+    j0 = fmax(j0, -1e9);
+    j1 = fmin(j1, 1e9);
+    lo = max(lo, (int)floor(j0));
+    hi = min(hi, (int)ceil(j1));
+}
 static_assert(kHistLen <= 2 * kDescrT, "two bins per thread");
 struct DescB {
     const Pyr* pyr[kMaxImg];
@@ -669,6 +692,7 @@ __global__ __launch_bounds__(kDescrT) void descr_kernel(DescB A) {  // blockIdx.
     __shared__ int seg[kHistLen];                              // per bin: its segment of `sorted`
     __shared__ int wsum[kDescrWords];
     __shared__ float sorted[kDescrT * 8];                      // the batch's values grouped by bin
+    __shared__ int row_off[kDescrRowsMax + 1], row_lo[kDescrRowsMax];  // the compacted patch's rows
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     for (int e = tid; e < kHistLen * kDescrWords; e += kDescrT) (&bm[0][0])[e] = 0ull;
     __syncthreads();
@@ -694,7 +718,42 @@ __global__ __launch_bounds__(kDescrT) void descr_kernel(DescB A) {  // blockIdx.
     cos_t /= hist_width;
     sin_t /= hist_width;
     const int W = 2 * radius + 1;
-    const int P = W * W;
+    const bool compact = W <= kDescrRowsMax;
+    int P = W * W;
+    if (compact) {  // per row: the first column and the count of the conservative range, then offsets
+        int len[2] = {0, 0};
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const int rr = 2 * tid + k;
+            if (rr < W) {
+                const int i = rr - radius, r = py + i;
+                int lo = max(-radius, 1 - px), hi = min(radius, im.cols - 2 - px);
+                if (r <= 0 || r >= im.rows - 1) hi = lo - 1;
+                window_cols((double)sin_t, (double)i * (double)cos_t, lo, hi);  // r_rot = j sin_t + i cos_t
+                window_cols((double)cos_t, -(double)i * (double)sin_t, lo, hi);  // c_rot = j cos_t - i sin_t
+                len[k] = max(0, hi - lo + 1);
+                row_lo[rr] = lo;
+            }
+        }
+        const int mine = len[0] + len[1];
+        int incl = mine;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int y = __shfl_up(incl, d);
+            if (lane >= d) incl += y;
+        }
+        if (lane == 63) wsum[wv] = incl;
+        __syncthreads();
+        int excl = incl - mine;
+#pragma unroll
+        for (int w = 0; w < kDescrWords; ++w) excl += w < wv ? wsum[w] : 0;
+        if (2 * tid < W) row_off[2 * tid] = excl;
+        if (2 * tid + 1 < W) row_off[2 * tid + 1] = excl + len[0];
+        if (tid == kDescrT - 1) row_off[W] = excl + mine;  // the last thread's inclusive sum: the total
+        __syncthreads();
+        P = row_off[W];
+        __syncthreads();  // wsum reused by the batches' scans
+    }
     float h0 = 0.f, h1 = 0.f;  // bins tid, tid + 256
     for (int base = 0; base < P; base += kDescrT) {
         // ---- A: pixel base + tid ----
@@ -703,7 +762,19 @@ __global__ __launch_bounds__(kDescrT) void descr_kernel(DescB A) {  // blockIdx.
         {
             const int q = base + tid;
             if (q < P) {
-                const int i = q / W - radius, j = q % W - radius;
+                int i, j;
+                if (compact) {  // the row holding compacted pixel q: last rr with row_off[rr] <= q
+                    int lo = 0, hi = W - 1;
+                    while (lo < hi) {
+                        const int mid = (lo + hi + 1) >> 1;
+                        if (row_off[mid] <= q) lo = mid; else hi = mid - 1;
+                    }
+                    i = lo - radius;
+                    j = row_lo[lo] + (q - row_off[lo]);
+                } else {
+                    i = q / W - radius;
+                    j = q % W - radius;
+                }
                 const float c_rot = j * cos_t - i * sin_t, r_rot = j * sin_t + i * cos_t;
                 float rbin = r_rot + kDW / 2 - 0.5f, cbin = c_rot + kDW / 2 - 0.5f;
                 const int r = py + i, c = px + j;

@@ -47,6 +47,11 @@
 #define FMA_CLAMP(n) "v_fma_f32 %" #n ", %16, |%" #n "|, %17 clamp\n"
 #define SUB_I32_E64(n) "v_sub_i32 %" #n ", %" #n ", %16\n"
 #define BFE(n) "v_bfe_u32 %" #n ", %" #n ", 31, 1\n"
+#define CND_E32(n) "v_cndmask_b32_e32 %" #n ", %" #n ", %16, vcc\n"
+#define CND_E64(n) "v_cndmask_b32_e64 %" #n ", %" #n ", %16, s[40:41]\n"
+#define MED3I(n) "v_med3_i32 %" #n ", %" #n ", %16, %17\n"
+#define MINI(n) "v_min_i32_e32 %" #n ", %" #n ", %16\n"
+#define MIN3I(n) "v_min3_i32 %" #n ", %" #n ", %16, %17\n"
 
 KERNEL(fma, FMA)
 KERNEL(sub_abs, SUB_ABS)
@@ -69,6 +74,32 @@ KERNEL(mul_legacy, MUL_LEGACY)
 KERNEL(fma_clamp, FMA_CLAMP)
 KERNEL(sub_i32, SUB_I32_E64)
 KERNEL(bfe, BFE)
+KERNEL(med3i, MED3I)
+KERNEL(mini, MINI)
+KERNEL(min3i, MIN3I)
+// v_cndmask with the mask set once before the loop (VCC or an SGPR pair): does the form matter
+#define KERNEL_CND(NAME, OP, SETUP)                                                            \
+    __global__ __launch_bounds__(256) void k_##NAME(float* out, int iters) {                  \
+        float r[16];                                                                           \
+        for (int j = 0; j < 16; ++j) r[j] = 1.f + 1e-3f * (threadIdx.x + j);                   \
+        float c = 1.0001f, d = 0.25f;                                                          \
+        asm volatile("" : "+v"(c), "+v"(d));                                                   \
+        asm volatile(SETUP ::: "vcc", "s40", "s41");                                           \
+        for (int i = 0; i < iters; ++i) asm volatile(R16(OP) : OUTS : "v"(c), "v"(d) : "vcc", "s40", "s41"); \
+        float s = 0.f;                                                                         \
+        for (int j = 0; j < 16; ++j) s += r[j];                                                \
+        out[blockIdx.x * 256 + threadIdx.x] = s;                                               \
+    }
+KERNEL_CND(cnd_e32, CND_E32, "s_mov_b64 vcc, 0x5555\n")
+// compare + select pairs as the compiler emits them: VOPC into VCC + v_cndmask_e32, or VOP3 compare into
+// an SGPR pair (or VCC) + v_cndmask_e64 (reported per pair)
+#define CS_E32(n) "v_cmp_gt_f32_e32 vcc, %" #n ", %16\nv_cndmask_b32_e32 %" #n ", %" #n ", %17, vcc\n"
+#define CS_E64(n) "v_cmp_gt_f32_e64 s[40:41], %" #n ", %16\nv_cndmask_b32_e64 %" #n ", %" #n ", %17, s[40:41]\n"
+#define CS_E64V(n) "v_cmp_gt_f32_e64 vcc, %" #n ", %16\nv_cndmask_b32_e64 %" #n ", %" #n ", %17, vcc\n"
+KERNEL(cs_e32, CS_E32)
+KERNEL(cs_e64, CS_E64)
+KERNEL(cs_e64v, CS_E64V)
+KERNEL_CND(cnd_e64, CND_E64, "s_mov_b64 s[40:41], 0x5555\n")
 
 
 // packed f32: 8 independent 64-bit chains per lane (16 floats), one v_pk_* per pair
@@ -258,7 +289,11 @@ int main() {
         {"v_or_b32_e32", k_orb},           {"v_and_b32_e32", k_andb},        {"v_min_f32_e32", k_minf},
         {"v_cmp_lt_f32_e32 vcc", k_cmp_e32}, {"v_cmp_lt_f32_e64 sgpr", k_cmp_e64}, {"v_addc_co_u32 vcc", k_addc},
         {"v_subrev_co_u32 vcc", k_subrev_co}, {"v_cvt_f32_u32", k_cvt_f32_u32}, {"v_mul_legacy_f32", k_mul_legacy},
-        {"v_fma_f32 clamp", k_fma_clamp},  {"v_sub_i32 (vop3)", k_sub_i32},  {"v_bfe_u32", k_bfe}};
+        {"v_fma_f32 clamp", k_fma_clamp},  {"v_sub_i32 (vop3)", k_sub_i32},  {"v_bfe_u32", k_bfe},
+        {"v_med3_i32", k_med3i},           {"v_min_i32_e32", k_mini},        {"v_min3_i32", k_min3i},
+        {"v_cndmask_b32_e32 (vcc set)", k_cnd_e32}, {"v_cndmask_b32_e64 (sgpr)", k_cnd_e64},
+        {"cmp_e32 vcc + cndmask_e32 (pair)", k_cs_e32}, {"cmp_e64 sgpr + cndmask_e64 (pair)", k_cs_e64},
+        {"cmp_e64 vcc + cndmask_e64 (pair)", k_cs_e64v}};
     // packed forms: 8 instructions per asm block, each doing 2 lanes' worth (reported per instruction)
     const Entry pk[] = {{"v_pk_add_f32", k_pk_add}, {"v_pk_fma_f32", k_pk_fma}, {"v_pk_mul_f32", k_pk_mul},
                         {"v_pk_mov_b32", k_pk_mov}};

@@ -1,6 +1,6 @@
 # Round 5i: where the 32-problem shard (--shard-of 8) loses against the full batch: the same tree with the
 # record gather left out (MIM_BENCH_GATHER=0, diagnostic), 16 / 24 batches in flight, and the whole-sweep
-# distance schedule (MIM_KNN_TAIL=0).
+# distance schedule (MIM_KNN_TAIL=0); then the C4 kernel trace, HBM traffic and SQ counters (co-execution included).
 set -e
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
@@ -16,3 +16,13 @@ done
 timeout -k 10 300 python -u bench.py --cpu-sample 0 --shard-of 8 --steps 240 > $O/s8_steps240.log 2>&1; echo "steps240 $(show $O/s8_steps240.log)"
 timeout -k 10 300 python -u bench.py --cpu-sample 0 > $O/c4_base.log 2>&1; echo "c4 $(show $O/c4_base.log)"
 MIM_BENCH_GATHER=0 timeout -k 10 300 python -u bench.py --cpu-sample 0 > $O/c4_nogather.log 2>&1; echo "c4 nogather $(show $O/c4_nogather.log)"
+# kernel trace + HBM counters of C4 (tools/prof_round.sh), then SQ counters of the distance and bound
+# kernels, the co-execution counter in a pass of its own
+timeout -k 10 900 bash tools/prof_round.sh c4
+K='knn2_i8|ransac_bound_mfma'
+i=0
+for C in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_SALU SQ_INSTS_LDS SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE" "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_LDS" "SQ_VALU_MFMA_COEXEC_CYCLES GRBM_GUI_ACTIVE"; do
+  i=$((i+1))
+  timeout -s KILL 200 rocprofv3 --pmc $C --kernel-trace --output-format csv --kernel-include-regex "$K" \
+     -d $O/pmc_sq$i -o run -- python3 bench.py --inflight 1 --steps 2 --warmup 1 --iso-steps 1 --cpu-sample 0 > $O/pmc_sq$i.log 2>&1 || echo "sq pass $i failed"
+done

@@ -617,12 +617,15 @@ static mim_status build_tables(mim_ctx* c, const mim_problem* problems, int n, i
         // (k ~ G / their sweeps, <= 8), which every list holds after its whole sweeps: the blocks
         // that finish early pull pieces and the kernel ends near sweeps / G rounds instead of the
         // ceiling (each piece repeats the keyed early tiles and the prologue, a few per cent of a
-        // sweep; partial top-2 lists merged by the ratio kernel).  MIM_KNN_TAIL=0: whole sweeps only.
+        // sweep; partial top-2 lists merged by the ratio kernel).  Opt-in (MIM_KNN_TAIL=1): it shortens a
+        // batch alone (32-problem shard: 0.48 -> 0.45 ms) but costs throughput once batches overlap (the
+        // pieces' extra early tiles and merge work: 32-problem shard with 12 in flight 26.8k -> 25.5k
+        // problems/s, profiles/r05i_*), and the bench keeps batches in flight.
         works.clear();
         const char* tail_env = getenv("MIM_KNN_TAIL");
         const long long rem = n_sweeps % G;
         int tail_from = n, ksplit = 1;
-        if ((!tail_env || atoi(tail_env) != 0) && n_sweeps > G && rem > 0) {
+        if (tail_env && atoi(tail_env) != 0 && n_sweeps > G && rem > 0) {
             long long ts = 0;
             while (tail_from > 0 && ts < rem) ts += c->h_probs[--tail_from].q_pad / kKnnBlockQ;
             ksplit = (int)std::max<long long>(2, std::min<long long>(8, (G + ts / 2) / ts));

@@ -108,3 +108,35 @@ def test_knn_small_pool_mass_ties(matcher, oracle):
     q = np.concatenate([pool[rng.integers(0, 24, size=100)], sift_like(rng, 100)])
     gi, _ = _check(matcher, oracle, q, t)
     assert (gi[:100, 0] < gi[:100, 1]).all()  # equal distance: lower index first
+
+
+def test_knn_split_tail_identical(oracle):
+    """MIM_KNN_TAIL=1 (opt-in): when the query-block sweeps leave the last round of resident blocks partly
+    empty, the trailing problems run as train-tile pieces whose partial top-2 lists the ratio kernel
+    merges.  40 problems x 16 sweeps = 640 sweeps over 512 resident blocks: the records and good-match
+    lists equal the whole-sweep schedule's, and a sampled problem equals the oracle."""
+    import os
+
+    from computervision_objectdetection_featurematching_amd import Matcher, default_params
+    ds = make_dataset(1, 40, 8000, 2500, 600, inlier_frac=0.3, seed=77)
+    outs = []
+    for tail in ("0", "1"):
+        os.environ["MIM_KNN_TAIL"] = tail
+        m = Matcher(0)
+        try:
+            q = m.add_set(ds.model_desc[0], ds.model_kp[0])
+            ts = [m.add_set(d, k) for d, k in zip(ds.scene_desc, ds.scene_kp)]
+            res = m.match_batch([(q, t) for t in ts], default_params(max_iters=500))
+            det = [m.problem_detail(i, int(r["n_good"])) for i, r in enumerate(res)]
+        finally:
+            m.close()
+            os.environ.pop("MIM_KNN_TAIL", None)
+        outs.append((res, det))
+    (r0, d0), (r1, d1) = outs
+    assert r0.tobytes() == r1.tobytes()
+    for a, b in zip(d0, d1):
+        for x, y in zip(a, b):
+            np.testing.assert_array_equal(x, y)
+    o = oracle.match_problem(ds.model_desc[0], ds.model_kp[0], ds.scene_desc[39], ds.scene_kp[39],
+                             oracle.default_params(max_iters=500))
+    assert int(r1[39]["n_good"]) == o["n_good"] and np.array_equal(d1[39][0], o["good_q"])

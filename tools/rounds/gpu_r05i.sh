@@ -7,13 +7,14 @@ export TMPDIR=/tmp
 O=gpurun_out/r05i
 mkdir -p $O
 show() { tail -1 $1 | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"], "host", d["host_enqueue_ms_per_step"])'; }
-for i in 1 2; do
+timeout -k 10 120 ./tools/issue_probe > $O/issue_probe.txt 2>&1
+for i in 1; do
   timeout -k 10 300 python -u bench.py --cpu-sample 0 --shard-of 8 > $O/s8_base_$i.log 2>&1; echo "base $(show $O/s8_base_$i.log)"
   MIM_BENCH_GATHER=0 timeout -k 10 300 python -u bench.py --cpu-sample 0 --shard-of 8 > $O/s8_nogather_$i.log 2>&1; echo "nogather $(show $O/s8_nogather_$i.log)"
   MIM_KNN_TAIL=0 timeout -k 10 300 python -u bench.py --cpu-sample 0 --shard-of 8 > $O/s8_notail_$i.log 2>&1; echo "notail $(show $O/s8_notail_$i.log)"
   timeout -k 10 300 python -u bench.py --cpu-sample 0 --shard-of 8 --inflight 24 > $O/s8_if24_$i.log 2>&1; echo "inflight24 $(show $O/s8_if24_$i.log)"
 done
-timeout -k 10 300 python -u bench.py --cpu-sample 0 --shard-of 8 --steps 240 > $O/s8_steps240.log 2>&1; echo "steps240 $(show $O/s8_steps240.log)"
+
 timeout -k 10 300 python -u bench.py --cpu-sample 0 > $O/c4_base.log 2>&1; echo "c4 $(show $O/c4_base.log)"
 MIM_BENCH_GATHER=0 timeout -k 10 300 python -u bench.py --cpu-sample 0 > $O/c4_nogather.log 2>&1; echo "c4 nogather $(show $O/c4_nogather.log)"
 # kernel trace + HBM counters of C4 (tools/prof_round.sh), then SQ counters of the distance and bound

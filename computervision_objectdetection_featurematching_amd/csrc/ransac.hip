@@ -1166,7 +1166,14 @@ __global__ __launch_bounds__(256) void ransac_irr_kernel(const RansacState* __re
 }
 
 constexpr int kChainThreads = 1024;
-constexpr int kChainEntries = 8192;                 // irregular attempts staged in LDS per piece
+#ifndef MIM_WALK_THREADS
+#define MIM_WALK_THREADS 1024
+#endif
+#ifndef MIM_WALK_ENTRIES
+#define MIM_WALK_ENTRIES 8192
+#endif
+constexpr int kWalkThreads = MIM_WALK_THREADS;     // walk kernel block (>= kIrrBlocksMax)
+constexpr int kChainEntries = MIM_WALK_ENTRIES;    // irregular attempts staged in LDS per piece
 constexpr int kIrrBlocksMax = 512;                  // list blocks per window (7.3M positions max)
 constexpr int kChainSegs = 4 * kChainThreads - 2;   // runs (segments) walked per chunk
 constexpr int kNoEvent = INT_MAX;
@@ -1193,10 +1200,13 @@ struct ChainWalkShared {
     int q[kChainEntries];
     uint8_t f[kChainEntries];
     int boff[kIrrBlocksMax + 1];
-    int wred[kChainThreads / 64];
-    int wred2[kChainThreads / 64];
+    int wred[kWalkThreads / 64];
+    int wred2[kWalkThreads / 64];
     int n_entries, limit, nseg, tail, cut, stop;
 };
+static_assert(kWalkThreads >= kIrrBlocksMax, "one thread per irregular-list block");
+static_assert((kChainSegs + 2) % kWalkThreads == 0, "walk: segments per thread");
+constexpr int kWalkSegsPer = (kChainSegs + 2) / kWalkThreads;
 
 __device__ __forceinline__ int block_excl_sum(int v, int* wred, int& total) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
@@ -1252,7 +1262,7 @@ __device__ __forceinline__ int block_min(int v, int* wred) {
 }
 
 // ---- walk: stage the irregular list in LDS, follow the chain over it (one wave) ----
-__global__ __launch_bounds__(kChainThreads) void ransac_walk_kernel(const RansacState* __restrict__ st,
+__global__ __launch_bounds__(kWalkThreads) void ransac_walk_kernel(const RansacState* __restrict__ st,
                                                                     const uint8_t* __restrict__ flags, int wcap,
                                                                     int c1, const int* __restrict__ irr,
                                                                     const int* __restrict__ irr_cnt, int irr_blocks,
@@ -1291,7 +1301,7 @@ __global__ __launch_bounds__(kChainThreads) void ransac_walk_kernel(const Ransac
     const int E = sh.n_entries, cut = sh.cut;
     for (int eb = 0; eb < E; eb += kChainEntries) {
         const int ee = min(E, eb + kChainEntries);
-        for (int e = eb + tid; e < ee; e += kChainThreads) {
+        for (int e = eb + tid; e < ee; e += kWalkThreads) {
             int lo = 0, hi = cut - 1;
             while (lo < hi) {
                 const int mid = (lo + hi + 1) >> 1;
@@ -1349,18 +1359,18 @@ __global__ __launch_bounds__(kChainThreads) void ransac_walk_kernel(const Ransac
     __syncthreads();
     const int nseg = sh.nseg;
     // chain index of every segment start
-    int v[4], sum = 0;
+    int v[kWalkSegsPer], sum = 0;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const int j = 4 * tid + k;
+    for (int k = 0; k < kWalkSegsPer; ++k) {
+        const int j = kWalkSegsPer * tid + k;
         v[k] = j < nseg ? ((G->seg_q[j] - G->seg_s[j]) >> 2) + 1 : (j == nseg ? sh.tail : 0);
         sum += v[k];
     }
     int total;
     int base = block_excl_sum(sum, sh.wred, total);
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const int j = 4 * tid + k;
+    for (int k = 0; k < kWalkSegsPer; ++k) {
+        const int j = kWalkSegsPer * tid + k;
         if (j <= nseg + 1) G->A[j] = base;
         if (j <= nseg)  // the check blocks whose first attempt falls in segment j
             for (int b = (base + kCheckBlock - 1) / kCheckBlock; b * kCheckBlock < base + v[k] && b < kChainBlk; ++b)
@@ -2274,8 +2284,8 @@ __global__ __launch_bounds__(256) void ransac_score_kernel(const RansacState* __
 __device__ __forceinline__ void square_to_quad(const double* x, const double* y, double* Q) {
     const double sx = x[0] - x[1] + x[2] - x[3], sy = y[0] - y[1] + y[2] - y[3];
     const double dx1 = x[1] - x[2], dx2 = x[3] - x[2], dy1 = y[1] - y[2], dy2 = y[3] - y[2];
-    const double den = dx1 * dy2 - dx2 * dy1;
-    const double g = (sx * dy2 - sy * dx2) / den, h = (dx1 * sy - dy1 * sx) / den;
+    const double iden = 1.0 / (dx1 * dy2 - dx2 * dy1);  // one division: g, h within an ulp of the quotients
+    const double g = (sx * dy2 - sy * dx2) * iden, h = (dx1 * sy - dy1 * sx) * iden;
     Q[0] = x[1] - x[0] + g * x[1]; Q[1] = x[3] - x[0] + h * x[3]; Q[2] = x[0];
     Q[3] = y[1] - y[0] + g * y[1]; Q[4] = y[3] - y[0] + h * y[3]; Q[5] = y[0];
     Q[6] = g; Q[7] = h; Q[8] = 1.0;
@@ -2539,10 +2549,11 @@ __global__ __launch_bounds__(256) void ransac_bound_mfma_kernel(const RansacStat
         const int4 s4 = decode_sample(samples[o], stream, (unsigned)n, S.modM);
         bound_hypothesis(P, s4, Hd, invalid, uncertain, eta, eta_model);
     }
-    // H' in scaled coordinates, then scaled by 2^-e into [-1, 1]
-    const double rs = (double)S.sb / (double)S.sa;
+    // H' in scaled coordinates, then scaled by 2^-e into [-1, 1] (sa, sb are powers of two, so their
+    // reciprocals and quotient are exact and the divisions become multiplications, bit for bit)
+    const double isa = ldexp(1.0, -ilogb((double)S.sa)), rs = (double)S.sb * isa;
     double h[9] = {Hd[0] * rs, Hd[1] * rs, Hd[2] * S.sb, Hd[3] * rs, Hd[4] * rs, Hd[5] * S.sb,
-                   Hd[6] / S.sa, Hd[7] / S.sa, 1.0};
+                   Hd[6] * isa, Hd[7] * isa, 1.0};
     double hm = 0;
 #pragma unroll
     for (int i = 0; i < 9; ++i) hm = fmax(hm, fabs(h[i]));
@@ -2563,7 +2574,7 @@ __global__ __launch_bounds__(256) void ransac_bound_mfma_kernel(const RansacStat
     const float C = S.sb * sqrtf(tt) * 1.41421366f * (1.f + 1e-6f);  // sqrt 2 rounded up
     // near-horizon slack A (pixel units, |x|, |y| < 1/sa and |u|, |v| < 1/sb), in the scaled units of
     // the MFMA outputs, with the sample's modelled closed-form/eigenvector disagreement eta_model
-    const double mx = 1.0 / S.sa, mu = 1.0 / S.sb;
+    const double mx = isa, mu = ldexp(1.0, -ilogb((double)S.sb));
     const double gam = 4.0 * 0x1p-24 + fmin(eta_model, 1.0);
     const double ax = fmax((fabs(Hd[0]) + fabs(Hd[1])) * mx + fabs(Hd[2]), (fabs(Hd[3]) + fabs(Hd[4])) * mx + fabs(Hd[5]));
     const double aw = (fabs(Hd[6]) + fabs(Hd[7])) * mx + 1.0;
@@ -3042,7 +3053,10 @@ __global__ __launch_bounds__(64) void ransac_select_kernel(RansacState* __restri
 // ------------------------------------------------------------------------------------------------
 // refine: best mask, refit DLT + LM on the inliers, gates (TestsDetector.cpp:74-84)
 // ------------------------------------------------------------------------------------------------
-constexpr int kRW = 4;        // refine: problems (waves) per block
+#ifndef MIM_REFINE_RW
+#define MIM_REFINE_RW 4
+#endif
+constexpr int kRW = MIM_REFINE_RW;  // refine: problems (waves) per block
 constexpr int kRT = 64 * kRW;  // refine block
 
 // LDS visibility between the lanes of one wave (the refine runs one problem per wave)
@@ -3617,7 +3631,7 @@ void ransac_enqueue(const RansacParams& prm, int n_probs, const ProbDev* probs, 
             const int bpp_irr = (west + kIrrBlock - 1) / kIrrBlock;
             ransac_irr_kernel<<<n_probs * bpp_irr, 256, 0, ss>>>(b.state, b.flags, wcap, bpp_irr, c1, b.irr,
                                                                b.irr_cnt, b.irr_blocks);
-            ransac_walk_kernel<<<n_probs, kChainThreads, 0, ss>>>(b.state, b.flags, wcap, c1, b.irr, b.irr_cnt,
+            ransac_walk_kernel<<<n_probs, kWalkThreads, 0, ss>>>(b.state, b.flags, wcap, c1, b.irr, b.irr_cnt,
                                                                  b.irr_blocks, chains);
             mark(mark_ctx, "chain", ss);
             constexpr int kChkSpan = kCheckBlock * kCheckPer;

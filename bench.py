@@ -106,12 +106,12 @@ def parse():
     ap.add_argument("--inflight", type=int, default=0,
                     help="scene batches in flight: one library context + HIP stream each, steps assigned "
                          "round-robin, so a batch's latency-bound RANSAC tail overlaps the next batch's kNN "
-                         "(0: 12, c1 3; with GPU_MAX_HW_QUEUES=16 their streams, torch's and RCCL's each get a "
-                         "hardware queue)")
+                         "(0: 16 for the C3/C4 batches and shards, 12 for c1img/dataset scenes, c1 3; with "
+                         "GPU_MAX_HW_QUEUES=24 their streams, torch's and RCCL's each get a hardware queue)")
     ap.add_argument("--shard-of", type=int, default=0,
                     help="diagnostic (N = 1 only, sharded configs): run rank 0's shard of an N-rank run, the "
                          "per-GPU workload of strong-scaling point N (value = this GPU's rate on it)")
-    ap.add_argument("--hw-queues", type=int, default=16,
+    ap.add_argument("--hw-queues", type=int, default=24,
                     help="GPU_MAX_HW_QUEUES for this process and the ranks it launches (set before HIP initialises)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (one GPU per rank); gloo = rehearsal of the N-rank path with several "
@@ -660,7 +660,7 @@ def main():
     args = parse()
     # HIP hardware queues per process (read at HIP init, inherited by launched ranks): the batches in
     # flight each keep their own stream, and with HIP's default 4 queues streams past the 4th share a
-    # queue, serialising unrelated batches (same box: 4 queues / 3 batches 23.0k, 16 / 12 25.9k problems/s)
+    # queue, serialising unrelated batches (same box: 4 queues / 3 batches 23.0k, 16 / 12 25.9k problems/s; round 5: 24 / 16, r05p)
     # (the GPU box exports GPU_MAX_HW_QUEUES=4, HIP's default: overridden here, not defaulted)
     os.environ["GPU_MAX_HW_QUEUES"] = str(args.hw_queues)
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -731,9 +731,10 @@ def run_batches(args, rank, world, local):
     skp = [torch.from_numpy(k).to(dev) for k in ds.scene_kp]
     torch.cuda.synchronize()
 
-    # C3/C4: 12 batches in flight (+11 % over 3, same box); the C1 surrogate's small batches: 3 (12: -40 %)
+    # C3/C4: 16 batches in flight on 24 hardware queues (12 on 16: -1 % on C4, -2-3 % on its 32-problem
+    # shard, profiles/r05o_*, r05p_*; 12 was +11 % over 3); the C1 surrogate's small batches: 3 (12: -40 %)
     # C5: 2 (one contraction's set prep overlaps the other's distance kernel)
-    nf = args.inflight if args.inflight > 0 else (2 if knn_only else (3 if args.config == "c1" else 12))
+    nf = args.inflight if args.inflight > 0 else (2 if knn_only else (3 if args.config == "c1" else 16))
     # one stream per context: the sampler stream helps one batch alone (+5 %), not batches already
     # overlapping; with it off the isolated pass's kernels run one after another on one stream, so
     # their HIP-event durations add up to at most the step (checked in kernel_rooflines)

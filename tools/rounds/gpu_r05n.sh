@@ -12,3 +12,5 @@ timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv -d $O/c4 -o run -
 python3 tools/trace_busy.py $O/s8/run_kernel_trace.csv 0.3 > $O/s8_busy.txt || true
 python3 tools/trace_busy.py $O/c4/run_kernel_trace.csv 0.3 > $O/c4_busy.txt || true
 cat $O/s8_busy.txt $O/c4_busy.txt
+python3 tools/trace_busy.py $O/s8/run_kernel_trace.csv --timed 12 80 > $O/s8_timed.txt
+python3 tools/trace_busy.py $O/c4/run_kernel_trace.csv --timed 12 10 > $O/c4_timed.txt

@@ -743,6 +743,13 @@ def run_batches(args, rank, world, local):
     # each context keeps its own non-blocking HIP stream; torch work of a step (the result gather)
     # is ordered on the same stream
     streams = [torch.cuda.ExternalStream(mm.stream_handle(), device=dev) for mm in matchers]
+    # diagnostic (MIM_BENCH_PRIO): contexts on torch streams of mixed priority, every `every`-th one high
+    prio = os.environ.get("MIM_BENCH_PRIO", "")
+    if prio:
+        every = int(prio)
+        streams = [torch.cuda.Stream(device=dev, priority=-1 if k % every == 0 else 0) for k in range(nf)]
+        for mm, st in zip(matchers, streams):
+            mm.set_stream(st.cuda_stream)
     prm = default_params(max_iters=max(cfg["max_iters"], 1))
     mine = [torch.zeros(n_rec * RESULT_DTYPE.itemsize, dtype=torch.uint8, device=dev) for _ in range(nf)]
     gath = [None] * nf

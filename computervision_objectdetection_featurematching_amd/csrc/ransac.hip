@@ -2393,7 +2393,10 @@ constexpr float kMfmaErr = 0x1p-15f;
 constexpr float kPointScale = 0x1p15f;
 constexpr double kHypScale = 0x1p15;
 constexpr double kOutScale = 0x1p30;
-constexpr int kTileChunk = 8;  // 32-point tiles per LDS stage of the MFMA bound kernel (2 x 16 KiB)
+#ifndef MIM_BOUND_CHUNK
+#define MIM_BOUND_CHUNK 8
+#endif
+constexpr int kTileChunk = MIM_BOUND_CHUNK;  // 32-point tiles per LDS stage of the MFMA bound kernel (2 x 16 KiB)
 
 // clamp to [0, 1]: folds into the producing instruction's clamp bit (no NaN reaches it here)
 __device__ __forceinline__ float clamp01(float x) { return __builtin_amdgcn_fmed3f(x, 0.f, 1.f); }

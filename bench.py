@@ -111,8 +111,10 @@ def parse():
     ap.add_argument("--shard-of", type=int, default=0,
                     help="diagnostic (N = 1 only, sharded configs): run rank 0's shard of an N-rank run, the "
                          "per-GPU workload of strong-scaling point N (value = this GPU's rate on it)")
-    ap.add_argument("--hw-queues", type=int, default=24,
-                    help="GPU_MAX_HW_QUEUES for this process and the ranks it launches (set before HIP initialises)")
+    ap.add_argument("--hw-queues", type=int, default=0,
+                    help="GPU_MAX_HW_QUEUES for this process and the ranks it launches (set before HIP initialises); "
+                         "0: 24 for the synthetic batch configs (16 batches in flight), 16 for the scene configs "
+                         "c1img/dataset (12 scenes in flight: 24 queues cost the dataset line 15 %, r05v)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (one GPU per rank); gloo = rehearsal of the N-rank path with several "
                          "ranks on one GPU (the record gather through host memory)")
@@ -662,6 +664,8 @@ def main():
     # flight each keep their own stream, and with HIP's default 4 queues streams past the 4th share a
     # queue, serialising unrelated batches (same box: 4 queues / 3 batches 23.0k, 16 / 12 25.9k problems/s; round 5: 24 / 16, r05p)
     # (the GPU box exports GPU_MAX_HW_QUEUES=4, HIP's default: overridden here, not defaulted)
+    if args.hw_queues <= 0:
+        args.hw_queues = 16 if args.config in ("c1img", "dataset") else 24
     os.environ["GPU_MAX_HW_QUEUES"] = str(args.hw_queues)
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args))  # children only: this process never touches the GPU

@@ -211,24 +211,6 @@ __device__ __forceinline__ unsigned med3_u32(unsigned a, unsigned b, unsigned c)
 // i8 MFMAs.
 // ------------------------------------------------------------------------------------------------
 constexpr int kLdsTile = kTileBytes + 768;  // fragments + the train half of the norm block + the key addends
-#ifndef MIM_KNN_RING
-#define MIM_KNN_RING 0
-#endif
-constexpr int kRingBufs = MIM_KNN_RING ? 3 : 2;  // LDS stage buffers of the distance kernel
-
-// ring counters (MIM_KNN_RING): one lane per wave adds 1; a wait spins on the LDS word (bounded: a
-// counting error ends the spin after ~0.1 s with wrong results, which the tests catch, not a hang)
-__device__ __forceinline__ void ring_signal(int* c, int lane) {
-    if (lane == 0) atomicAdd(c, 1);
-}
-__device__ __forceinline__ void ring_wait(int* c, int target) {
-    for (int it = 0; it < (1 << 21); ++it) {
-        const int v = __builtin_amdgcn_readfirstlane(*(volatile int*)c);
-        if (v >= target) break;
-        __builtin_amdgcn_s_sleep(1);
-    }
-    asm volatile("" ::: "memory");
-}
 constexpr int kStage = kKnnStage;
 constexpr int kThreads = 64 * kKnnWaves;
 constexpr int kStageChunks = kStage * kTileBytes / 16 / kThreads;  // 16-B fragment chunks per thread
@@ -241,11 +223,8 @@ __global__ __launch_bounds__(kThreads, MIM_KNN_OCC) void knn2_i8_kernel(  // OCC
     const ProbDev* __restrict__ probs, const KnnWork* __restrict__ works, const int* __restrict__ seg_start,
     Top2* __restrict__ parts, int* __restrict__ dyn_ctr) {
     constexpr int QT = kKnnQT;
-    __shared__ __attribute__((aligned(16))) unsigned char smem[kRingBufs * kStage * kLdsTile];
+    __shared__ __attribute__((aligned(16))) unsigned char smem[2 * kStage * kLdsTile];
     __shared__ int s_item;
-#if MIM_KNN_RING
-    __shared__ int s_ring[6];  // per ring buffer: waves whose pieces landed [0..2], waves done [3..5]
-#endif
     // static: block b runs works[seg_start[b] .. seg_start[b + 1]); dynamic (dyn_ctr != null): the works
     // are 8 lists (seg_start[0..8]), block b pulls items from list b mod 8 (its XCD's) with an atomic
     // counter, then from the other lists, so a block that starts late (its CU held by another batch's
@@ -344,22 +323,11 @@ __global__ __launch_bounds__(kThreads, MIM_KNN_OCC) void knn2_i8_kernel(  // OCC
     };
 
     const int tile_e = min(w.tile1, w.tile0 + (kEarlyTiles + kStage - 1) / kStage * kStage);
-#if MIM_KNN_RING
-    const int nst = (w.tile1 - w.tile0 + kStage - 1) / kStage;  // stages of this work item
-    __syncthreads();  // every wave is past the previous item's buffers and counters
-    if (tid < 6) s_ring[tid] = 0;
-    __syncthreads();
-    if (nst > 0) stage_dma(w.tile0, 0, w.tile0 < tile_e);
-    if (nst > 1) stage_dma(w.tile0 + kStage, 1, w.tile0 + kStage < tile_e);
-    __builtin_amdgcn_s_waitcnt(0);
-    ring_signal(s_ring + 0, lane);  // this wave's pieces of stage 0 landed
-#else
     if (w.tile0 < w.tile1) stage_dma(w.tile0, 0, w.tile0 < tile_e);
     // retire every prologue load (q' fragments included) here: with one still pending at the loop
     // entry the waitcnt pass keeps a vmcnt(0) in the loop
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
-#endif
 
     // the 32x32 block u2 of a tile: accumulators start at floor(n2/2) (LDS), R = q'.t'' + floor(n2/2)
     auto block_mfma = [&](const unsigned char* tb, int u2, i32x16 (&acc)[QT]) {
@@ -485,48 +453,6 @@ __global__ __launch_bounds__(kThreads, MIM_KNN_OCC) void knn2_i8_kernel(  // OCC
         }
     };
 
-#if MIM_KNN_RING
-    // 3-deep ring of stages, no block barrier per stage: stage j reads buffer j % 3 once every wave's
-    // pieces of it have landed (each wave signals its own after its vmcnt wait), and a wave loads its
-    // pieces of stage j + 2 into buffer (j + 2) % 3 once every wave is done with stage j - 1, so waves
-    // drift up to a stage apart instead of meeting at every stage's end
-    auto refresh = [&]() {
-#pragma unroll
-        for (int u = 0; u < QT; ++u) {
-            const auto a = __builtin_amdgcn_permlane32_swap(st[u].m1, st[u].m1, false, false);
-            const auto b = __builtin_amdgcn_permlane32_swap(st[u].m2, st[u].m2, false, false);
-            o1c[u] = (tid & 32) ? (int)a[0] : (int)a[1];
-            o2c[u] = (tid & 32) ? (int)b[0] : (int)b[1];
-            T[u] = late_threshold(st[u], o1c[u], o2c[u]);
-        }
-    };
-    for (int j = 0; j < nst; ++j) {
-        const int b = j % 3, stage = w.tile0 + j * kStage;
-        ring_wait(s_ring + b, kKnnWaves * (j / 3 + 1));
-        const unsigned char* sb = smem + b * kStage * kLdsTile;
-        if (stage < tile_e) {
-#pragma unroll
-            for (int ts = 0; ts < kStage; ++ts)
-                if (stage + ts < w.tile1) tile_early(sb + ts * kLdsTile, stage + ts);
-        } else {
-            refresh();
-#pragma unroll MIM_KNN_LATE_UNROLL
-            for (int ts = 0; ts < kStage; ++ts)
-                if (stage + ts < w.tile1) tile_late(sb + ts * kLdsTile, stage + ts);
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of buffer b returned
-        ring_signal(s_ring + 3 + b, lane);
-        if (j + 1 < nst) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces of stage j + 1 landed
-            ring_signal(s_ring + (j + 1) % 3, lane);
-        }
-        if (j + 2 < nst) {
-            const int b2 = (j + 2) % 3;
-            if (j >= 1) ring_wait(s_ring + 3 + b2, kKnnWaves * ((j - 1) / 3 + 1));  // stage j - 1 done
-            stage_dma(stage + 2 * kStage, b2, stage + 2 * kStage < tile_e);
-        }
-    }
-#else
     int stage = w.tile0;
     for (; stage < tile_e; stage += kStage) {
         const int buf = ((stage - w.tile0) / kStage) & 1;
@@ -562,8 +488,6 @@ __global__ __launch_bounds__(kThreads, MIM_KNN_OCC) void knn2_i8_kernel(  // OCC
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA into the next buffer landed
         __syncthreads();
     }
-
-#endif
 
     // ---- merge the two lane halves (disjoint train rows of the same query), keys ----
 #pragma unroll

@@ -590,11 +590,19 @@ def kernel_rooflines(args, ds, res, iso, iso_step_ms, knn_only):
     knn_bytes = float(np.sum(512 * (pq + pt) + 16 * pq))
     t = iso["knn"]
     ach = knn_ops / (t * 1e-3) / 1e12
+    # the committed PMC passes profile the config's whole batch on one GPU (bench.py --config C --inflight
+    # 1): a shard's smaller launch (N > 1 or --shard-of) has no measured traffic of its own
+    from computervision_objectdetection_featurematching_amd.synthetic import CONFIGS
+    cfg = CONFIGS.get(args.config, {})
+    full = cfg.get("ragged") or not cfg.get("sharded") or len(ds.problems) == cfg["n_scenes"] * cfg["n_models"]
+    traffic = pmc_traffic("knn2_i8_kernel", args.config) if full else None
     roof = {"kernel": "knn2_i8_kernel (exact-integer distance contraction on v_mfma_i32_32x32x32_i8 + top-2 "
                       "selection), 1 launch per step",
             "bound": "mfma", "achieved": round(ach, 2), "peak": PEAK_I8_TOPS, "unit": "TFLOP/s",
             "frac": round(ach / PEAK_I8_TOPS, 4),
-            "traffic": pmc_traffic("knn2_i8_kernel", args.config),
+            "traffic": traffic,
+            **({} if full else {"traffic_note": f"PMC traffic is measured on the full {args.config} batch; this "
+                                                f"rank's launch holds {len(ds.problems)} problems"}),
             "launch_ms": round(t, 4), "ops_per_launch": knn_ops,
             "ops": "2 * Nq * Nt * 128 integer multiply-adds (i8 operands, i32 accumulate), summed over the batch",
             "algorithmic_bytes_per_launch": knn_bytes,

@@ -2649,13 +2649,16 @@ __global__ __launch_bounds__(256) void ransac_bound_mfma_kernel(const RansacStat
             __builtin_amdgcn_global_load_lds((const void*)(T + (long long)t0 * 128 + i0 + lane),
                                              (__attribute__((address_space(3))) void*)(lt[buf] + i0), 16, 0, 0);
     };
+#ifndef MIM_PROBE_BOUND
+#define MIM_PROBE_BOUND 0  // timing probe only (wrong bounds): 1 = no tile arithmetic, 2 = no tile loop
+#endif
     if (nt > 0) stage(0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    for (int t0 = 0, buf = 0; t0 < nt; t0 += kTileChunk, buf ^= 1) {
+    for (int t0 = 0, buf = 0; t0 < (MIM_PROBE_BOUND == 2 ? 0 : nt); t0 += kTileChunk, buf ^= 1) {
         const int tc = min(kTileChunk, nt - t0);
         if (t0 + kTileChunk < nt) stage(t0 + kTileChunk, buf ^ 1);
-        if (wave_counts) {
+        if (wave_counts && MIM_PROBE_BOUND == 0) {
           for (int t = 0; t < tc; ++t) {
             const h8v ax = __builtin_bit_cast(h8v, lt[buf][t * 128 + lane]);
             const h8v ay = __builtin_bit_cast(h8v, lt[buf][t * 128 + 64 + lane]);

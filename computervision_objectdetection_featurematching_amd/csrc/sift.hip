@@ -655,6 +655,15 @@ __device__ __forceinline__ int ctz64(unsigned long long m) { return __builtin_ct
 // (Round 3 history: one wave walking the pixels one at a time, 0.76 ms per call; one wave with 64-bit
 // masks walked by the owners, 0.64 ms; 256 threads with the mask walk, 0.37 ms: each contribution a
 // dependent chain of two LDS reads.)
+#ifndef MIM_PROBE_DESCR
+#define MIM_PROBE_DESCR 0
+#endif
+#ifndef MIM_DESCR_SPLIT
+#define MIM_DESCR_SPLIT 0  // batched SIFT: one descriptor launch per image instead of one for all
+#endif
+#ifndef MIM_DESCR_GRID
+#define MIM_DESCR_GRID 4096  // descriptor blocks of a batch launch (at least 1024 per image)
+#endif
 constexpr int kDescrT = 256, kDescrWords = kDescrT / 64;
 constexpr int kDescrRowsMax = 512;
 
@@ -781,7 +790,11 @@ __global__ __launch_bounds__(kDescrT) void descr_kernel(DescB A) {  // blockIdx.
                 if (rbin > -1 && rbin < kDW && cbin > -1 && cbin < kDW && r > 0 && r < im.rows - 1 && c > 0 &&
                     c < im.cols - 1) {
                     const float dx = AT(im, r, c + 1) - AT(im, r, c - 1), dy = AT(im, r - 1, c) - AT(im, r + 1, c);
+#if MIM_PROBE_DESCR == 1  // timing probe only (not the reference's weights)
+                    const float w = __expf((c_rot * c_rot + r_rot * r_rot) * exp_scale);
+#else
                     const float w = (float)exp((double)((c_rot * c_rot + r_rot * r_rot) * exp_scale));
+#endif
                     const float o = fast_atan2(dy, dx), m = sqrtf(dx * dx + dy * dy);
                     float obin = (o - ori) * bins_per_rad;
                     const float mag = m * w;
@@ -802,6 +815,10 @@ __global__ __launch_bounds__(kDescrT) void descr_kernel(DescB A) {  // blockIdx.
                 }
             }
         }
+#if MIM_PROBE_DESCR == 2  // timing probe only: phase A alone
+        h0 += vals[0] + vals[1] + vals[2] + vals[3] + vals[4] + vals[5] + vals[6] + vals[7] + (float)idx;
+        continue;
+#endif
         // ---- B: stable counting sort of the batch's contributions by bin, then sequential sums ----
         constexpr int kOff[8] = {0, 1, kDB + 2, kDB + 3, (kDW + 2) * (kDB + 2), (kDW + 2) * (kDB + 2) + 1,
                                  (kDW + 3) * (kDB + 2), (kDW + 3) * (kDB + 2) + 1};
@@ -1497,7 +1514,19 @@ static int sift_batch(std::vector<SiftJob>& jobs, SiftWs* bw, hipStream_t st, st
         refine_kernel<<<dim3(std::max(1024 / nl, 128), nl), 128, 0, st>>>(Rf);
         orient_kernel<<<dim3(std::max(4096 / nl, 512), nl), 64, 0, st>>>(Or);
         kp_post_kernel<<<dim3(1, nl), 1024, 0, st>>>(Kp);
-        descr_kernel<<<dim3(std::max(4096 / nl, 1024), nl), kDescrT, 0, st>>>(Ds);
+#if MIM_DESCR_SPLIT
+        for (int k = 0; k < nl; ++k) {  // one launch per image, in order
+            DescB D1{};
+            D1.pyr[0] = Ds.pyr[k];
+            D1.kp[0] = Ds.kp[k];
+            D1.n[0] = Ds.n[k];
+            D1.n_cap[0] = Ds.n_cap[k];
+            D1.desc[0] = Ds.desc[k];
+            descr_kernel<<<dim3(MIM_DESCR_GRID, 1), kDescrT, 0, st>>>(D1);
+        }
+#else
+        descr_kernel<<<dim3(std::max(MIM_DESCR_GRID / nl, 1024), nl), kDescrT, 0, st>>>(Ds);
+#endif
         SCHK(hipGetLastError());
     }
     SCHK(hipMemcpyAsync(bw->h_cnt, d_cnt, sizeof(int) * 4 * nj, hipMemcpyDeviceToHost, st));

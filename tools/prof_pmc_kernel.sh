@@ -1,5 +1,5 @@
 # Per-kernel SQ/TCC counters (separate --pmc passes, kernel trace only).
-# usage: KREGEX='knn2_bf16' PASSES='A B|C D' bash tools/prof_pmc_kernel.sh
+# usage: KREGEX='knn2_i8' PASSES='A B|C D' bash tools/prof_pmc_kernel.sh
 set -e
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp

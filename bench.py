@@ -778,7 +778,7 @@ def run_batches(args, rank, world, local):
         with torch.cuda.stream(streams[k]):
             m.clear_sets()
             q_ids = [m.add_set(d, kp) for d, kp in zip(mdesc, mkp)]
-            t_ids = [m.add_set(d, kp) for d, kp in zip(sdesc, skp)]
+            t_ids = m.add_sets(zip(sdesc, skp))  # the step's scene sets in one library call
             if knn_only:  # C5: the distance contraction + top-2 alone
                 m.knn_sets_dev(q_ids[0], t_ids[0], knn_idx[k], knn_dist[k])
                 return

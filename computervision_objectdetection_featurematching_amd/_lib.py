@@ -16,7 +16,7 @@ MIM_STREAM_SHORT = 5
 # every symbol include/mim.h declares (checked by tests/test_abi.py)
 EXPORTS = [
     "mim_version", "mim_default_params", "mim_ctx_create", "mim_ctx_destroy", "mim_last_error",
-    "mim_ctx_set_stream", "mim_ctx_set_sampler_stream", "mim_ctx_get_stream", "mim_synchronize", "mim_set_create", "mim_sets_clear", "mim_sets_truncate", "mim_sets_info", "mim_set_rows",
+    "mim_ctx_set_stream", "mim_ctx_set_sampler_stream", "mim_ctx_get_stream", "mim_synchronize", "mim_set_create", "mim_sets_create", "mim_sets_clear", "mim_sets_truncate", "mim_sets_info", "mim_set_rows",
     "mim_knn2_l2", "mim_ratio_filter", "mim_find_homography", "mim_batch_run", "mim_batch_results",
     "mim_batch_results_dev", "mim_batch_results_copy", "mim_batch_problem_detail", "mim_batch_inlier_points", "mim_knn2_sets_dev", "mim_last_kernel_ms",
     "mim_set_timing", "mim_sift_detect_compute", "mim_sift_detect_compute_scales", "mim_sift_scales_sets",
@@ -85,6 +85,7 @@ def load():
     L.mim_ctx_get_stream.restype = vp
     L.mim_synchronize.argtypes = [vp]
     L.mim_set_create.argtypes = [vp, f32p, f32p, i32, i32, i32, C.POINTER(C.c_int32)]
+    L.mim_sets_create.argtypes = [vp, i32, C.POINTER(vp), C.POINTER(vp), i32p, i32, i32, C.POINTER(C.c_int32)]
     L.mim_sets_clear.argtypes = [vp]
     L.mim_sets_truncate.argtypes = [vp, i32]
     L.mim_sets_info.argtypes = [vp, C.POINTER(C.c_int32), C.POINTER(C.c_int64)]
@@ -112,7 +113,7 @@ def load():
     L.mim_resize_linear_u8.argtypes = [vp, u8p, i32, i32, C.c_int64, u8p, i32, i32, C.c_double, C.c_double]
     L.mim_default_box_params.argtypes = [C.POINTER(BoxParams)]
     L.mim_detect_boxes.argtypes = [f32p, i32, C.POINTER(BoxParams), C.POINTER(Rect), i32, C.POINTER(C.c_int32)]
-    for name in ("mim_ctx_create", "mim_ctx_set_stream", "mim_synchronize", "mim_set_create", "mim_sets_clear",
+    for name in ("mim_ctx_create", "mim_ctx_set_stream", "mim_synchronize", "mim_set_create", "mim_sets_create", "mim_sets_clear",
                  "mim_sets_truncate", "mim_knn2_l2", "mim_ratio_filter", "mim_find_homography", "mim_batch_run", "mim_batch_results",
                  "mim_batch_problem_detail", "mim_batch_inlier_points", "mim_knn2_sets_dev", "mim_set_timing", "mim_ctx_set_sampler_stream",
                  "mim_sift_detect_compute", "mim_sift_detect_compute_scales", "mim_sift_scales_sets",

@@ -421,6 +421,27 @@ mim_status mim_set_create(mim_ctx* c, const float* desc, const float* kp, int32_
     return set_create_locked(c, desc, kp, n, dim, on_device, set_id);
 }
 
+static void sets_truncate_locked(mim_ctx* c, int n_keep);
+
+mim_status mim_sets_create(mim_ctx* c, int32_t count, const float* const* desc, const float* const* kp,
+                           const int32_t* rows, int32_t dim, int32_t on_device, int32_t* first_id) {
+    if (!c) return MIM_EINVAL;
+    if (count < 0 || !first_id || (count > 0 && (!desc || !kp || !rows)))
+        return fail(c, MIM_EINVAL, "sets_create: bad arguments");
+    std::lock_guard<std::mutex> lk(c->mu);
+    const int n0 = (int)c->sets.size();
+    for (int i = 0; i < count; ++i) {
+        int32_t id = -1;
+        const mim_status st = set_create_locked(c, desc[i], kp[i], rows[i], dim, on_device, &id);
+        if (st != MIM_OK) {
+            if ((int)c->sets.size() > n0) sets_truncate_locked(c, n0);  // all or nothing
+            return st;
+        }
+    }
+    *first_id = n0;
+    return MIM_OK;
+}
+
 mim_status mim_sets_clear(mim_ctx* c) {
     if (!c) return MIM_EINVAL;
     std::lock_guard<std::mutex> lk(c->mu);

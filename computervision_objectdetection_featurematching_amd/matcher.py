@@ -127,6 +127,55 @@ class Matcher:
         self._n_sets = sid.value + 1
         return sid.value
 
+    def add_sets(self, pairs) -> list[int]:
+        """Register several sets in one library call (mim_sets_create), as add_set in order: every pair
+        (desc, kp) numpy (host) or every pair torch (device), the same rules per pair; all or nothing."""
+        pairs = list(pairs)
+        if not pairs:
+            return []
+        on_dev = int(hasattr(pairs[0][0], "is_cuda") and pairs[0][0].is_cuda)
+        descs, kps = [], []
+        if on_dev:
+            import torch
+            for desc, kp in pairs:
+                for name, t, cols in (("descriptors", desc, DIM), ("keypoints", kp, 2)):
+                    if not (hasattr(t, "is_cuda") and t.is_cuda):
+                        raise ValueError("add_sets: every array must be on the device when the first is")
+                    if t.dtype != torch.float32 or not t.is_contiguous() or t.dim() != 2 or t.shape[1] != cols:
+                        raise ValueError(f"add_sets: {name} must be a contiguous float32 (n, {cols}) tensor, got "
+                                         f"{t.dtype} {tuple(t.shape)} contiguous={t.is_contiguous()}")
+                    if t.device.index != self.device:
+                        raise ValueError(f"add_sets: {name} on {t.device}, matcher on cuda:{self.device}")
+                if kp.shape[0] != desc.shape[0]:
+                    raise ValueError("add_sets: descriptor and keypoint row counts differ")
+                descs.append(desc)
+                kps.append(kp)
+            dev = descs[0].device
+            mine = torch.cuda.ExternalStream(self.stream_handle(), device=dev)
+            cur = torch.cuda.current_stream(dev)
+            if cur.cuda_stream != mine.cuda_stream:
+                mine.wait_stream(cur)
+        else:
+            for desc, kp in pairs:
+                if hasattr(desc, "is_cuda") and desc.is_cuda:
+                    raise ValueError("add_sets: host and device arrays mixed")
+                descs.append(np.ascontiguousarray(desc, np.float32).reshape(-1, DIM))
+                kps.append(np.ascontiguousarray(kp, np.float32).reshape(-1, 2))
+                if kps[-1].shape[0] != descs[-1].shape[0]:
+                    raise ValueError("add_sets: descriptor and keypoint row counts differ")
+        n = len(pairs)
+        dp = (C.c_void_p * n)(*[_lib.ptr(d) for d in descs])
+        kpp = (C.c_void_p * n)(*[_lib.ptr(k) for k in kps])
+        rows = np.array([int(d.shape[0]) for d in descs], np.int32)
+        first = C.c_int32()
+        self._check(self.L.mim_sets_create(self._ctx, n, dp, kpp, C.c_void_p(_lib.ptr(rows)), DIM, on_dev, C.byref(first)))
+        ids = list(range(first.value, first.value + n))
+        if on_dev:
+            for sid, d, k in zip(ids, descs, kps):
+                self._borrowed.append((sid, [d, k]))
+        self._n_sets = first.value + n
+        return ids
+
     @property
     def n_sets(self) -> int:
         return self._n_sets

@@ -110,6 +110,12 @@ mim_status mim_synchronize(struct mim_ctx* ctx);
  * fewer than 2^18 rows (BFMatcher::knnMatchImpl's assertion), checked at mim_batch_run. */
 mim_status mim_set_create(struct mim_ctx* ctx, const float* desc, const float* kp_xy, int32_t n,
                           int32_t dim, int32_t on_device, int32_t* set_id);
+/* count sets in one call, as count mim_set_create calls in order (desc[i], kp_xy[i], rows[i]; one
+ * on_device flag for all): their ids are *first_id .. *first_id + count - 1.  All or nothing: on an
+ * error no set of the call stays registered.  For a caller registering a whole batch of views or
+ * scene sets (processAllModelsImages' views, a batch of scenes) without a call per set. */
+mim_status mim_sets_create(struct mim_ctx* ctx, int32_t count, const float* const* desc, const float* const* kp_xy,
+                           const int32_t* rows, int32_t dim, int32_t on_device, int32_t* first_id);
 mim_status mim_sets_clear(struct mim_ctx* ctx);
 /* Drops the sets registered after the first n_keep (ids >= n_keep) and reuses their device storage;
  * the first n_keep keep their ids and layout.  The same rules as mim_sets_clear for work already

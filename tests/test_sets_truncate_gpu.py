@@ -48,3 +48,43 @@ def test_truncate_bounds(matcher):
     matcher.truncate_sets(1)
     matcher.truncate_sets(0)
     assert matcher.n_sets == 0
+
+
+def test_add_sets_equals_add_set_and_rolls_back(matcher):
+    """mim_sets_create (Matcher.add_sets): the same ids and records as one mim_set_create per set, host
+    and device inputs; a call that fails part way registers nothing (ids and storage as before)."""
+    import ctypes as C
+    import torch
+    from computervision_objectdetection_featurematching_amd import Matcher, default_params
+    from computervision_objectdetection_featurematching_amd._lib import MimError
+    ds = make_dataset(2, 4, 500, 900, 200, inlier_frac=0.3, seed=91)
+    prm = default_params(max_iters=2000)
+    probs = [(a, 2 + b) for a in range(2) for b in range(4)]
+    matcher.clear_sets()
+    q = [matcher.add_set(d, k) for d, k in zip(ds.model_desc, ds.model_kp)]
+    t = [matcher.add_set(d, k) for d, k in zip(ds.scene_desc, ds.scene_kp)]
+    ref = matcher.match_batch([(q[a], t[b - 2]) for a, b in probs], prm).copy()
+    for on_dev in (False, True):
+        m2 = Matcher(0)
+        try:
+            conv = (lambda x: torch.from_numpy(x).cuda()) if on_dev else (lambda x: x)
+            q2 = m2.add_sets([(conv(d), conv(k)) for d, k in zip(ds.model_desc, ds.model_kp)])
+            t2 = m2.add_sets([(conv(d), conv(k)) for d, k in zip(ds.scene_desc, ds.scene_kp)])
+            assert q2 == [0, 1] and t2 == [2, 3, 4, 5]
+            got = m2.match_batch([(q2[a], t2[b - 2]) for a, b in probs], prm)
+            assert got.tobytes() == ref.tobytes()
+            # a failing third set (null rows pointer): nothing of the call stays, ids continue as before
+            n_before, _ = m2.sets_info()
+            d = np.ascontiguousarray(ds.scene_desc[0], np.float32)
+            k = np.ascontiguousarray(ds.scene_kp[0], np.float32)
+            dp = (C.c_void_p * 3)(d.ctypes.data, d.ctypes.data, None)
+            kp = (C.c_void_p * 3)(k.ctypes.data, k.ctypes.data, None)
+            rows = np.array([len(d), len(d), len(d)], np.int32)
+            first = C.c_int32(-1)
+            with pytest.raises(MimError):
+                m2._check(m2.L.mim_sets_create(m2._ctx, 3, dp, kp, C.c_void_p(rows.ctypes.data), 128, 0,
+                                               C.byref(first)))
+            assert m2.sets_info()[0] == n_before
+            assert m2.add_sets([(ds.scene_desc[1], ds.scene_kp[1])]) == [n_before]
+        finally:
+            m2.close()

@@ -175,7 +175,7 @@ def dry_run(args):
             print(json.dumps({"metric": "dry-run", "value": 0.0, "unit": "problems/s", "n_gpus": world,
                               "ranks_seen": seen, "steps": 0, "warmup": 0, "ms_per_step": 0.0,
                               "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dry_run": True,
-                              "config": {"workload": "dataset"},
+                              "config": {"workload": "dataset", "hw_queues": int(os.environ["GPU_MAX_HW_QUEUES"])},
                               "scene_ids_covered": sum(d[0][0][0] == i for i, d in enumerate(merged)),
                               "ranks_of_scenes": [d[0][0][1] for d in merged], "global_batch": DATASET_SCENES}),
                   flush=True)
@@ -209,7 +209,8 @@ def dry_run(args):
         print(json.dumps({"metric": "dry-run", "value": 0.0, "unit": "problems/s", "n_gpus": world,
                           "ranks_seen": seen, "steps": 0, "warmup": 0, "ms_per_step": float(t.item()) * 1e3,
                           "higher_is_better": True, "scaling": "strong" if cfg.get("sharded") else "weak",
-                          "vs_baseline": None, "dry_run": True, "config": {"workload": args.config},
+                          "vs_baseline": None, "dry_run": True,
+                          "config": {"workload": args.config, "hw_queues": int(os.environ["GPU_MAX_HW_QUEUES"])},
                           "scene_ids_covered": int(len(np.unique(got))), "global_batch": n_scenes}),
               flush=True)
     if world > 1:

@@ -32,6 +32,15 @@ def test_single_rank_dry_run():
     assert d["n_gpus"] == 1 and d["ranks_seen"] == 1
 
 
+def test_hw_queue_defaults_per_config_reach_the_ranks():
+    """24 hardware queues for the batch configs, 16 for the scene configs (bench.py main), set before HIP
+    starts and inherited by the launched ranks; --hw-queues overrides."""
+    assert _run(["--dry-run"])["config"]["hw_queues"] == 24
+    assert _run(["--gpus", "2", "--dry-run", "--config", "c4"])["config"]["hw_queues"] == 24
+    assert _run(["--gpus", "2", "--dry-run", "--config", "dataset"])["config"]["hw_queues"] == 16
+    assert _run(["--dry-run", "--hw-queues", "8"])["config"]["hw_queues"] == 8
+
+
 def test_cpu_parity_compare_detects_differences():
     sys.path.insert(0, ROOT)
     import bench

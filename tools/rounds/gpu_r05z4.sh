@@ -4,7 +4,7 @@
 set -e
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
-O=gpurun_out/r05z4
+O=gpurun_out/${R05Z4_OUT:-r05z4}
 mkdir -p $O
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest_gpu_final.log 2>&1 || { tail -40 $O/pytest_gpu_final.log; exit 1; }
 tail -1 $O/pytest_gpu_final.log

@@ -2862,7 +2862,10 @@ __global__ __launch_bounds__(kCandThreads) void ransac_cand_kernel(RansacState* 
 constexpr int kExactGroups = 4;
 constexpr int kExactWaves = kCandCap / kExactGroups;
 
-__global__ __launch_bounds__(64) void ransac_exact_kernel(const RansacState* __restrict__ st,
+#ifndef MIM_EXACT_OCC
+#define MIM_EXACT_OCC 1  // waves per SIMD the exact kernel's register budget is sized for (1: no cap)
+#endif
+__global__ __launch_bounds__(64, MIM_EXACT_OCC) void ransac_exact_kernel(const RansacState* __restrict__ st,
                                                           const ProbDev* __restrict__ probs,
                                                           const float4* __restrict__ pts,
                                                           const int4* __restrict__ samples,

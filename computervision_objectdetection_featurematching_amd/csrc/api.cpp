@@ -158,7 +158,7 @@ struct PinnedStage {
 namespace mim {
 // RANSAC workspace (definition shared with ransac.hip through this layout)
 struct RansacWs {
-    DevBuf state, samples, hyp, counts, bounds, flags, irr, irr_cnt, pass_bits, chains, best_h, cand, ncand, cex, cH, stream,
+    DevBuf state, samples, hyp, counts, bounds, flags, irr, irr_cnt, pass_bits, chains, best_h, cand, ncand, cex, cH, decided, stream,
         scratch, inl, tiles, err;
     long long stream_len = 0;
 };
@@ -304,7 +304,7 @@ void mim_ctx_destroy(mim_ctx* c) {
     c->arena.release();
     for (DevBuf* b : {&c->probs, &c->works, &c->parts, &c->good_q, &c->good_t, &c->pts, &c->n_good,
                       &c->results, &c->masks, &c->knn_idx, &c->knn_dist, &c->inl_tab, &c->inl_out, &c->knn_ctr, &c->rws.state, &c->rws.samples,
-                      &c->rws.hyp, &c->rws.counts, &c->rws.bounds, &c->rws.flags, &c->rws.irr, &c->rws.irr_cnt, &c->rws.pass_bits, &c->rws.chains, &c->rws.best_h, &c->rws.cand, &c->rws.ncand, &c->rws.cex, &c->rws.cH, &c->rws.stream, &c->rws.scratch, &c->rws.inl, &c->rws.tiles, &c->rws.err, &c->prep_jobs})
+                      &c->rws.hyp, &c->rws.counts, &c->rws.bounds, &c->rws.flags, &c->rws.irr, &c->rws.irr_cnt, &c->rws.pass_bits, &c->rws.chains, &c->rws.best_h, &c->rws.cand, &c->rws.ncand, &c->rws.cex, &c->rws.cH, &c->rws.decided, &c->rws.stream, &c->rws.scratch, &c->rws.inl, &c->rws.tiles, &c->rws.err, &c->prep_jobs})
         b->release();
     if (c->own) (void)hipStreamDestroy(c->own);
     delete c;
@@ -1181,6 +1181,7 @@ static mim_status ransac_prepare(mim_ctx* c, int n, const mim_params* prm, Ransa
     HIPCHK(c, c->rws.ncand.ensure(sizeof(int) * 2 * std::max(n, 1)));
     HIPCHK(c, c->rws.cex.ensure(sizeof(int) * cap));
     HIPCHK(c, c->rws.cH.ensure(sizeof(double) * 9 * cap));
+    HIPCHK(c, c->rws.decided.ensure(sizeof(int) * cap));
     HIPCHK(c, c->rws.inl.ensure(sizeof(float4) * good_total));
     HIPCHK(c, c->rws.tiles.ensure(sizeof(uint4) * 128 * ((good_total + 31) / 32)));
     HIPCHK(c, c->rws.err.ensure(sizeof(int) * 4));
@@ -1199,6 +1200,7 @@ static mim_status ransac_prepare(mim_ctx* c, int n, const mim_params* prm, Ransa
     b.ncand = c->rws.ncand.as<int>();
     b.cex = c->rws.cex.as<int>();
     b.cH = c->rws.cH.as<double>();
+    b.decided = c->rws.decided.as<int>();
     b.flag_cap = flag_cap;
     b.irr = c->rws.irr.as<int>();
     b.irr_cnt = c->rws.irr_cnt.as<int>();
@@ -1254,6 +1256,7 @@ static mim_status ransac_enqueue_range(mim_ctx* c, int p0, int np, const RansacB
     g.ncand += 2 * p0;
     g.cex += (long long)p0 * 2 * kCandPerProblem;
     g.cH += 9LL * p0 * 2 * kCandPerProblem;
+    g.decided += (long long)p0 * 2 * kCandPerProblem;
     ransac_enqueue(rp, np, c->probs.as<ProbDev>() + p0, c->pts.as<float4>(), c->n_good.as<int>() + p0, g,
                    c->masks.as<uint8_t>(), c->results.as<mim_result>() + p0, raw, c->cur, mark_cb, c, c->exact_all);
     HIPCHK(c, hipGetLastError());

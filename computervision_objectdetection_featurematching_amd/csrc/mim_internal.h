@@ -130,6 +130,7 @@ struct RansacBufs {
     int* ncand;               // [problem][list] candidates listed (may exceed the capacity)
     int* cex;                 // [problem][list][kCandPerProblem] their exact inlier counts
     double* cH;               // [problem][list][kCandPerProblem][9] their exact models
+    int* decided;             // [problem][list][kCandPerProblem] 1: the prescreen decided the listed candidate
     uint8_t* flags;           // [problem][window] getSubset attempt outcomes ahead of stream_pos
     long long flag_cap;       // bytes of `flags`
     int* irr;                 // [problem][block][kIrrCap] positions of irregular attempts (chain sampler)

@@ -2788,10 +2788,166 @@ constexpr int kCandWaves = 16;                 // exact-evaluation waves per pro
 constexpr int kCandCap = kCandWaves * 64;      // listed candidates per problem and chunk
 static_assert(kCandCap == kCandPerProblem, "candidate list layout shared with api.cpp");
 
+constexpr int kCandThreads = 1024;  // the cand kernel's block
+
+// Candidate prescreen (round 5): before the exact pass, every listed candidate whose count the
+// closed-form hypothesis already decides gets it here, without the eigensolve; the exact kernel's waves
+// take only the rest (flagged undecided in `decided`, in list order).  Decided: a bracket with lo == hi (chunk 1), or no point in
+// the uncertain band of the disc test the bound kernel's diamonds relax, evaluated in fp64 in pixel
+// units: with (X, Y, W) = Hd (x, y, 1), ex = |X - u W|, ey = |Y - v W| and the bound kernel's per-point
+// margins (tt / tl = thr2 -/+ the margin d_max (+ the widening of a poorly conditioned sample), the
+// near-horizon slack A per coordinate),
+//   surely in:  (ex + A)^2 + (ey + A)^2 < tl W^2      surely out:  (ex - A)+^2 + (ey - A)+^2 > tt W^2
+// — the conditions the bound kernel's diamond tests are derived from ("Exactness of the
+// filtered RANSAC"), so the count of surely-in points is the exact count when no point is in between.
+// Samples the conditioning screen rejects (uncertain) are left to the exact kernel.  One wave per
+// candidate (points over the lanes), kPreWaves one-wave blocks per problem.
+__device__ __forceinline__ int wave_isum(int v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+    return v;
+}
+
+constexpr int kPreWaves = 16;  // prescreen blocks (one wave each) per problem
+
+__global__ __launch_bounds__(64) void ransac_prescreen_kernel(const RansacState* __restrict__ st,
+                                                              const ProbDev* __restrict__ probs,
+                                                              const int2* __restrict__ bounds,
+                                                              const float4* __restrict__ pts,
+                                                              const int4* __restrict__ samples,
+                                                              const uint32_t* __restrict__ stream,
+                                                              const int* __restrict__ cand,
+                                                              const int* __restrict__ ncand, int* __restrict__ cex,
+                                                              double* __restrict__ cH, int* __restrict__ decided,
+                                                              float thr2, int L, int cap) {
+    const int p = blockIdx.x / kPreWaves, j = blockIdx.x % kPreWaves, lane = threadIdx.x;
+    const RansacState S = st[p];
+    if (!S.active || S.done) return;
+    const ProbDev PD = probs[p];
+    const int2* Bd = bounds + PD.it_off;
+    const long long lb = (long long)(2 * p + L) * kCandCap;
+    const int nl = min(ncand[2 * p + L], cap);
+    const float4* __restrict__ P = pts + PD.good_off;
+    const int n = S.n;
+    for (int k = j; k < nl; k += kPreWaves) {
+        const int t = cand[lb + k];
+        const int2 bd = Bd[t];
+        int res = 0, cnt = 0;
+        if (bd.x == bd.y) {
+            res = 1;
+            cnt = bd.x;
+        } else {
+            const int4 s4 = decode_sample(samples[PD.it_off + t], stream, (unsigned)n, S.modM);
+            double Hd[8];
+            bool invalid = false, uncertain = false;
+            float eta = 0.f;
+            double eta_model = 0;
+            bound_hypothesis(P, s4, Hd, invalid, uncertain, eta, eta_model);
+            if (!invalid && !uncertain) {
+                float tt = thr2 + fmaf(1e-7f * S.smax, S.smax, 0.5f);
+                float tl = thr2 - fmaf(1e-7f * S.smax, S.smax, 0.5f);
+                if (eta > 0.f) {
+                    const float wd = S.smax * fmaf(eta * eta, S.smax, 10.2f * eta);
+                    tt += wd;
+                    tl -= wd;
+                }
+                // |x|, |y| <= mx and |u|, |v| <= mu (powers of two from the tiles kernel's scales)
+                const double mx = ldexp(1.0, -ilogb((double)S.sa)), mu = ldexp(1.0, -ilogb((double)S.sb));
+                const double gam = 4.0 * 0x1p-24 + fmin(eta_model, 1.0);
+                const double ax = fmax((fabs(Hd[0]) + fabs(Hd[1])) * mx + fabs(Hd[2]),
+                                       (fabs(Hd[3]) + fabs(Hd[4])) * mx + fabs(Hd[5]));
+                const double aw = (fabs(Hd[6]) + fabs(Hd[7])) * mx + 1.0;
+                const double A = gam * (ax + (mu + 6.0) * aw) * (1.0 + 1e-6);
+                const double TT = (double)tt * (1.0 + 1e-9), TL = (double)fmaxf(tl, 0.f) * (1.0 - 1e-9);
+                int in = 0, unc = 0;
+                for (int i = lane; i < n; i += 64) {
+                    const float4 q = P[i];
+                    const double x = q.x, y = q.y;
+                    const double W = fma(Hd[6], x, fma(Hd[7], y, 1.0));
+                    const double X = fma(Hd[0], x, fma(Hd[1], y, Hd[2]));
+                    const double Y = fma(Hd[3], x, fma(Hd[4], y, Hd[5]));
+                    const double ex = fabs(X - (double)q.z * W), ey = fabs(Y - (double)q.w * W);
+                    const double ux = fmax(ex - A, 0.0), uy = fmax(ey - A, 0.0);
+                    const double W2 = W * W;
+                    const bool maybe = ux * ux + uy * uy <= TT * W2;
+                    const bool surely = (ex + A) * (ex + A) + (ey + A) * (ey + A) < TL * W2;
+                    in += surely ? 1 : 0;
+                    unc += (maybe && !surely) ? 1 : 0;
+                }
+                in = wave_isum(in);
+                unc = wave_isum(unc);
+                if (unc == 0) {
+                    res = 1;
+                    cnt = in;
+                }
+            }
+        }
+        if (lane == 0) {
+            decided[lb + k] = res;
+            if (res) {
+                cex[lb + k] = cnt;
+                cH[(lb + k) * 9 + 8] = 0.0;  // H not computed (refine recomputes the best sample's)
+            }
+        }
+    }
+}
+
+// position of the r-th undecided listed candidate (list order), -1 past them: one wave scans the flags
+__device__ __forceinline__ int undecided_position(const int* __restrict__ decided, long long lb, int nl, int r) {
+    const int lane = threadIdx.x & 63;
+    int seen = 0;
+    for (int base = 0; base < nl; base += 64) {
+        const bool u = base + lane < nl && decided[lb + base + lane] == 0;
+        const unsigned long long m = __ballot(u);
+        const int c = __popcll(m);
+        if (r < seen + c) {  // the (r - seen)-th set bit of m
+            const int before = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+            const unsigned long long hit = __ballot(u && before == r - seen);
+            return base + __builtin_ctzll(hit);
+        }
+        seen += c;
+    }
+    return -1;
+}
+
+// Debug check of the prescreen (MIM_CHECK_PRESCREEN=1): every listed candidate the prescreen decided
+// (flagged in `decided`) recounted exactly (runKernel + computeError, one lane each) against its cex.
+__global__ __launch_bounds__(64) void ransac_prescreen_check_kernel(const RansacState* __restrict__ st,
+                                                                    const ProbDev* __restrict__ probs,
+                                                                    const float4* __restrict__ pts,
+                                                                    const int4* __restrict__ samples,
+                                                                    const uint32_t* __restrict__ stream,
+                                                                    const int* __restrict__ cand,
+                                                                    const int* __restrict__ ncand,
+                                                                    const int* __restrict__ cex,
+                                                                    const int* __restrict__ decided,
+                                                                    const int2* __restrict__ bounds, float thr2,
+                                                                    int L, int cap, unsigned long long* stats) {
+    __shared__ double sd[kJ9D * 64];
+    const int p = blockIdx.x / (kCandCap / 64), k = (blockIdx.x % (kCandCap / 64)) * 64 + threadIdx.x;
+    const RansacState S = st[p];
+    if (!S.active || S.done) return;
+    const int nl = min(ncand[2 * p + L], cap);
+    if (k >= nl) return;
+    const long long lb = (long long)(2 * p + L) * kCandCap;
+    if (decided[lb + k] == 0) return;  // undecided: the exact kernel's
+    const int t = cand[lb + k];
+    double H[9];
+    const int ex = exact_count(pts + probs[p].good_off, S.n, decode_sample(samples[probs[p].it_off + t], stream,
+                                                                           (unsigned)S.n, S.modM),
+                               sd + threadIdx.x, thr2, H);
+    atomicAdd(stats + 0, 1ull);
+    if (ex != cex[lb + k]) {
+        atomicAdd(stats + 1, 1ull);
+        const int2 bd = bounds[probs[p].it_off + t];
+        printf("[mim] prescreen mismatch p=%d it=%d exact=%d prescreen=%d lo=%d hi=%d n=%d\n", p, t, ex, cex[lb + k],
+               bd.x, bd.y, S.n);
+    }
+}
+
 // Candidates of one chunk: iteration t is listed iff hi_t > max(3, maxGoodCount, earlier lower
 // bounds) — a prefix maximum over the chunk, computed by a 1024-thread block (contiguous ranges
 // per thread, block max-scan, ordered compaction).
-constexpr int kCandThreads = 1024;
 
 __global__ __launch_bounds__(kCandThreads) void ransac_cand_kernel(RansacState* __restrict__ st,
                                                                    const ProbDev* __restrict__ probs,
@@ -2873,7 +3029,8 @@ __global__ __launch_bounds__(64, MIM_EXACT_OCC) void ransac_exact_kernel(const R
                                                           const int* __restrict__ cand, const int* __restrict__ ncand,
                                                           const int2* __restrict__ bounds,
                                                           int* __restrict__ cex, double* __restrict__ cH, float thr2,
-                                                          int L, int cap) {
+                                                          int L, int cap, const int* __restrict__ decided,
+                                                          int prescreen) {
     __shared__ double sd[kExactGroups * kJ9G];
     // blocks: [list pass][wave][problem]; chunk 1 (L = 0): list 0 of the problems not deferred;
     // chunk 2 (L = 1): list 1 of every problem, then list 0 of the deferred ones.  Problem-minor
@@ -2888,9 +3045,16 @@ __global__ __launch_bounds__(64, MIM_EXACT_OCC) void ransac_exact_kernel(const R
     if (list == 0 && (L == 0) == (S.defer != 0)) return;  // uniform over the block
     const long long lb = (long long)(2 * p + list) * kCandCap;
     const int nc = min(ncand[2 * p + list], cap);
-    if (w * kExactGroups >= nc) return;  // uniform over the wave
-    const bool valid = w * kExactGroups + grp < nc;  // groups past the list only join the counting
-    const int k = min(w * kExactGroups + grp, nc - 1);
+    // with the prescreen, wave w takes the undecided candidates 4w .. 4w + 3 in list order
+    int kg[kExactGroups];
+#pragma unroll
+    for (int g = 0; g < kExactGroups; ++g) {
+        const int r = w * kExactGroups + g;
+        kg[g] = prescreen ? undecided_position(decided, lb, nc, r) : (r < nc ? r : -1);
+    }
+    if (kg[0] < 0) return;  // uniform over the wave
+    const bool valid = kg[grp] >= 0;  // groups past the list only join the counting
+    const int k = valid ? kg[grp] : kg[0];
     const int t = cand[lb + k];
     const long long o = lb + k;
     const int2 bd = bounds[probs[p].it_off + t];
@@ -3617,6 +3781,9 @@ void ransac_enqueue(const RansacParams& prm, int n_probs, const ProbDev* probs, 
     // listed candidates per problem and chunk (MIM_CAND_CAP < 1024: test knob forcing the replay's
     // overflow rescan)
     const int cap = prm.cand_cap > 0 ? std::min(prm.cand_cap, kCandCap) : kCandCap;
+    // candidate prescreen in the cand kernel (MIM_PRESCREEN=0: every listed candidate through the exact kernel)
+    const char* pe = getenv("MIM_PRESCREEN");
+    const int prescreen = (pe && pe[0] == '0') ? 0 : 1;
     while (c0 < max_iters) {
         const int c1 = (int)std::min<long long>((long long)c0 + chunk, max_iters);
         // attempt outcomes for a window of ~28 draws per wanted iteration (pass rate ~1/5), the walk
@@ -3710,19 +3877,45 @@ void ransac_enqueue(const RansacParams& prm, int n_probs, const ProbDev* probs, 
             const int L = c0 == 0 ? 0 : 1;  // candidate list of this chunk (at most two chunks)
             ransac_cand_kernel<<<n_probs, kCandThreads, 0, s>>>(b.state, probs, b.bounds, c1, b.cand, b.ncand, L,
                                                                 cap);
+            if (prescreen)
+                ransac_prescreen_kernel<<<n_probs * kPreWaves, 64, 0, s>>>(b.state, probs, b.bounds, pts, b.samples,
+                                                                          b.stream, b.cand, b.ncand, b.cex, b.cH,
+                                                                          b.decided, thr2, L, cap);
             mark(mark_ctx, "cand", s);
+            if (prescreen && getenv("MIM_CHECK_PRESCREEN")) {  // debug: decided candidates recounted exactly
+                unsigned long long* dst = nullptr;
+                unsigned long long h[2] = {0, 0};
+                if (hipMalloc(&dst, sizeof h) == hipSuccess) {
+                    (void)hipMemsetAsync(dst, 0, sizeof h, s);
+                    ransac_prescreen_check_kernel<<<n_probs * (kCandCap / 64), 64, 0, s>>>(
+                        b.state, probs, pts, b.samples, b.stream, b.cand, b.ncand, b.cex, b.decided, b.bounds,
+                        thr2, L, cap, dst);
+                    (void)hipMemcpyAsync(h, dst, sizeof h, hipMemcpyDeviceToHost, s);
+                    (void)hipStreamSynchronize(s);
+                    (void)hipFree(dst);
+                }
+                fprintf(stderr, "[mim] prescreen check chunk [%d,%d): decided %llu mismatch %llu\n", c0, c1, h[0], h[1]);
+            }
             if (getenv("MIM_DEBUG_NCAND")) {
-                std::vector<int> h(2 * n_probs);
+                std::vector<int> h(2 * n_probs), dec((size_t)2 * n_probs * kCandCap);
                 (void)hipMemcpyAsync(h.data(), b.ncand, sizeof(int) * 2 * n_probs, hipMemcpyDeviceToHost, s);
+                if (prescreen)
+                    (void)hipMemcpyAsync(dec.data(), b.decided, sizeof(int) * dec.size(), hipMemcpyDeviceToHost, s);
                 (void)hipStreamSynchronize(s);
-                long long sum = 0; int mx = 0;
-                for (int i = 0; i < n_probs; ++i) { sum += h[2 * i + L]; mx = std::max(mx, h[2 * i + L]); }
-                fprintf(stderr, "[mim] chunk [%d,%d): candidates mean %.1f max %d\n", c0, c1, (double)sum / n_probs, mx);
+                long long sum = 0, sum2 = 0; int mx = 0;
+                for (int i = 0; i < n_probs; ++i) {
+                    const int nl = std::min(h[2 * i + L], cap);
+                    sum += h[2 * i + L];
+                    mx = std::max(mx, h[2 * i + L]);
+                    for (int k = 0; k < nl; ++k) sum2 += prescreen ? dec[(size_t)(2 * i + L) * kCandCap + k] == 0 : 1;
+                }
+                fprintf(stderr, "[mim] chunk [%d,%d): candidates mean %.1f max %d undecided mean %.1f\n", c0, c1,
+                        (double)sum / n_probs, mx, (double)sum2 / n_probs);
             }
             // chunk 2 also evaluates the list of every problem whose chunk-1 pass was deferred
             ransac_exact_kernel<<<n_probs * kExactWaves * (L + 1), 64, 0, s>>>(b.state, probs, pts, b.samples, b.stream,
                                                                              b.cand, b.ncand, b.bounds, b.cex, b.cH,
-                                                                             thr2, L, cap);
+                                                                             thr2, L, cap, b.decided, prescreen);
             mark(mark_ctx, "exact", s);
             ransac_replay_kernel<<<n_probs, 64, 0, s>>>(b.state, probs, pts, b.samples, b.stream, b.bounds, b.cand,
                                                         b.ncand, b.cex, b.cH, c1, prm.conf, thr2, b.best_h, L,

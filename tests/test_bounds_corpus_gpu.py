@@ -145,3 +145,25 @@ def test_filtered_equals_exact_corpus():
             os.environ.pop("MIM_RANSAC_EXACT", None)
     diff = [a[:2] for a, b in zip(*outs) if a != b]
     assert not diff, diff[:10]
+
+
+def test_prescreen_decisions_recounted_exactly(capfd):
+    """Every candidate the prescreen decides (closed-form disc test, no eigensolve) is recounted by
+    runKernel + computeError (MIM_CHECK_PRESCREEN=1) on the whole corpus: no count differs, and the
+    prescreen does decide some."""
+    from computervision_objectdetection_featurematching_amd import Matcher
+    os.environ["MIM_CHECK_PRESCREEN"] = "1"
+    m = Matcher(0)
+    decided = bad = 0
+    try:
+        for fam, seed, src, dst, iters in _corpus():
+            m.find_homography(src, dst, 5.0, iters, 0.995)
+            for d, b in re.findall(r"prescreen check chunk \[\d+,\d+\): decided (\d+) mismatch (\d+)",
+                                   capfd.readouterr().err):
+                decided += int(d)
+                bad += int(b)
+    finally:
+        m.close()
+        os.environ.pop("MIM_CHECK_PRESCREEN", None)
+    print(f"prescreen corpus: {decided} decided candidates recounted, {bad} differ")
+    assert decided > 0 and bad == 0

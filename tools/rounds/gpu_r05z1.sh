@@ -3,7 +3,7 @@
 set -e
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
-O=gpurun_out/r05z
+O=gpurun_out/${R05Z_OUT:-r05z}
 mkdir -p $O
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { tail -40 $O/pytest_gpu.log; exit 1; }
 tail -1 $O/pytest_gpu.log

@@ -4,7 +4,7 @@
 set -e
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
-O=gpurun_out/r05z
+O=gpurun_out/${R05Z_OUT:-r05z}
 mkdir -p $O
 show() { tail -1 $1 | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"], d.get("single_scene_ms"), d.get("scenes_per_s"))'; }
 timeout -k 10 400 python -u bench.py --config c1img > $O/bench_c1img_3.log 2>&1; echo "c1img $(show $O/bench_c1img_3.log)"

@@ -2892,6 +2892,46 @@ __global__ __launch_bounds__(64) void ransac_prescreen_kernel(const RansacState*
     }
 }
 
+// After the prescreen, in list order (one wave per problem): an undecided candidate whose upper bound
+// does not exceed max(3, maxGoodCount before the chunk, the decided counts listed before it) cannot be
+// a new best wherever the running best stands (it is at least that bar), so it is settled as
+// irrelevant (decided = 2, count 0: the replay's `count > best` test skips it) without the eigensolve.
+// Earlier candidates past the final niters only precede later ones that are past it as well.
+__global__ __launch_bounds__(64) void ransac_settle_kernel(const RansacState* __restrict__ st,
+                                                           const ProbDev* __restrict__ probs,
+                                                           const int2* __restrict__ bounds,
+                                                           const int* __restrict__ cand, const int* __restrict__ ncand,
+                                                           int* __restrict__ cex, double* __restrict__ cH,
+                                                           int* __restrict__ decided, int L, int cap) {
+    const int p = blockIdx.x, lane = threadIdx.x;
+    const RansacState S = st[p];
+    if (!S.active || S.done) return;
+    const long long lb = (long long)(2 * p + L) * kCandCap;
+    const int nl = min(ncand[2 * p + L], cap);
+    const int2* Bd = bounds + probs[p].it_off;
+    int bar = max(S.max_good, 3);
+    for (int base = 0; base < nl; base += 64) {
+        const int k = base + lane;
+        const bool in = k < nl;
+        const int dec = in ? decided[lb + k] : 1;
+        int incl = (in && dec == 1) ? cex[lb + k] : INT_MIN;  // decided counts (exact)
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const int o = __shfl_up(incl, off);
+            if (lane >= off) incl = max(incl, o);
+        }
+        int excl = __shfl_up(incl, 1);
+        if (lane == 0) excl = INT_MIN;
+        const int before = max(bar, excl);
+        if (in && dec == 0 && Bd[cand[lb + k]].y <= before) {
+            decided[lb + k] = 2;
+            cex[lb + k] = 0;
+            cH[(lb + k) * 9 + 8] = 0.0;
+        }
+        bar = max(bar, __shfl(incl, 63));
+    }
+}
+
 // position of the r-th undecided listed candidate (list order), -1 past them: one wave scans the flags
 __device__ __forceinline__ int undecided_position(const int* __restrict__ decided, long long lb, int nl, int r) {
     const int lane = threadIdx.x & 63;
@@ -2930,7 +2970,7 @@ __global__ __launch_bounds__(64) void ransac_prescreen_check_kernel(const Ransac
     const int nl = min(ncand[2 * p + L], cap);
     if (k >= nl) return;
     const long long lb = (long long)(2 * p + L) * kCandCap;
-    if (decided[lb + k] == 0) return;  // undecided: the exact kernel's
+    if (decided[lb + k] != 1) return;  // undecided (the exact kernel's) or settled as irrelevant
     const int t = cand[lb + k];
     double H[9];
     const int ex = exact_count(pts + probs[p].good_off, S.n, decode_sample(samples[probs[p].it_off + t], stream,
@@ -3784,6 +3824,9 @@ void ransac_enqueue(const RansacParams& prm, int n_probs, const ProbDev* probs, 
     // candidate prescreen in the cand kernel (MIM_PRESCREEN=0: every listed candidate through the exact kernel)
     const char* pe = getenv("MIM_PRESCREEN");
     const int prescreen = (pe && pe[0] == '0') ? 0 : 1;
+    // settling irrelevant candidates after the prescreen (MIM_SETTLE=0: off)
+    const char* se = getenv("MIM_SETTLE");
+    const int settle = (se && se[0] == '0') ? 0 : 1;
     while (c0 < max_iters) {
         const int c1 = (int)std::min<long long>((long long)c0 + chunk, max_iters);
         // attempt outcomes for a window of ~28 draws per wanted iteration (pass rate ~1/5), the walk
@@ -3877,10 +3920,14 @@ void ransac_enqueue(const RansacParams& prm, int n_probs, const ProbDev* probs, 
             const int L = c0 == 0 ? 0 : 1;  // candidate list of this chunk (at most two chunks)
             ransac_cand_kernel<<<n_probs, kCandThreads, 0, s>>>(b.state, probs, b.bounds, c1, b.cand, b.ncand, L,
                                                                 cap);
-            if (prescreen)
+            if (prescreen) {
                 ransac_prescreen_kernel<<<n_probs * kPreWaves, 64, 0, s>>>(b.state, probs, b.bounds, pts, b.samples,
                                                                           b.stream, b.cand, b.ncand, b.cex, b.cH,
                                                                           b.decided, thr2, L, cap);
+                if (settle)
+                    ransac_settle_kernel<<<n_probs, 64, 0, s>>>(b.state, probs, b.bounds, b.cand, b.ncand, b.cex, b.cH,
+                                                                b.decided, L, cap);
+            }
             mark(mark_ctx, "cand", s);
             if (prescreen && getenv("MIM_CHECK_PRESCREEN")) {  // debug: decided candidates recounted exactly
                 unsigned long long* dst = nullptr;

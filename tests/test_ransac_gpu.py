@@ -458,16 +458,18 @@ def test_attempt_redraw_list_overflow_equals_walker(oracle):
 
 
 def test_candidate_prescreen_equals_exact_paths(capfd):
-    """The cand kernel's prescreen (closed-form disc test in fp64, MIM_PRESCREEN=1, default) decides a
-    part of the candidates without the eigensolve: records and masks identical to the prescreen off and
-    to the all-exact mode on C4's regime (8 % planted inliers of 2,000 good matches, 50,000 iterations),
+    """The prescreen (closed-form disc test in fp64, MIM_PRESCREEN=1, default) decides a part of the
+    candidates without the eigensolve and the settle pass drops those that cannot beat the decided counts
+    before them: records and masks identical to the prescreen off, the settle pass off and to the all-exact
+    mode on C4's regime (8 % planted inliers of 2,000 good matches, 50,000 iterations),
     and the debug counts show candidates actually decided."""
     import os
     import re
     from computervision_objectdetection_featurematching_amd import Matcher, default_params
     ds = make_dataset(1, 6, 3000, 3000, 2000, inlier_frac=0.08, seed=4242)
     outs = []
-    for env in ({"MIM_PRESCREEN": "1", "MIM_DEBUG_NCAND": "1"}, {"MIM_PRESCREEN": "0"}, {"MIM_RANSAC_EXACT": "1"}):
+    for env in ({"MIM_PRESCREEN": "1", "MIM_DEBUG_NCAND": "1"}, {"MIM_PRESCREEN": "0"}, {"MIM_SETTLE": "0"},
+                {"MIM_RANSAC_EXACT": "1"}):
         os.environ.update(env)
         m = Matcher(0)
         try:

@@ -3266,6 +3266,15 @@ __global__ __launch_bounds__(64) void ransac_select_kernel(RansacState* __restri
 // ------------------------------------------------------------------------------------------------
 // refine: best mask, refit DLT + LM on the inliers, gates (TestsDetector.cpp:74-84)
 // ------------------------------------------------------------------------------------------------
+#ifndef MIM_LM_MERGE
+#define MIM_LM_MERGE 1  // the trial step's cost S(x - d) from the normal-equation pass at x - d (see below)
+#endif
+#ifndef MIM_LTL_STAGE
+#define MIM_LTL_STAGE 1  // the refit's LtL sums read the inliers' L rows from LDS (0: select them in registers)
+#endif
+#ifndef MIM_REFINE_TIMING
+#define MIM_REFINE_TIMING 0  // diagnostic: print the refine phases (wall clock) of the slow problems
+#endif
 #ifndef MIM_REFINE_RW
 #define MIM_REFINE_RW 4
 #endif
@@ -3458,6 +3467,17 @@ __device__ double inv_diag_max8(const double (&w)[8], const int (&perm)[8], cons
     return maxval;
 }
 
+#if MIM_REFINE_TIMING
+#define MIM_RT_MARK(acc)                          \
+    do {                                          \
+        const unsigned long long t_ = wall_clock64(); \
+        acc += t_ - rt_last;                      \
+        rt_last = t_;                             \
+    } while (0)
+#else
+#define MIM_RT_MARK(acc) do {} while (0)
+#endif
+
 struct RefineShared {  // one per wave (problem)
     double red[2];
     double lt[45];
@@ -3496,6 +3516,12 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
     float4* X = inl + go;
     mim_result res{};
     res.n_good = ng;
+#if MIM_REFINE_TIMING
+    unsigned long long rt_last = wall_clock64(), t_mask = 0, t_refit = 0, t_norm0 = 0, t_solve = 0, t_cost = 0,
+                       t_norm = 0;
+    const unsigned long long rt_start = rt_last;
+    int rt_iters = 0;
+#endif
     // ---- gate :74 ----
     if (ng < prm.min_good || ng < 4) {
         res.status = MIM_FEW_GOOD;
@@ -3564,6 +3590,7 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                 if (in) X[base + within] = q;
                 base += __popcll(bal);
             }
+            MIM_RT_MARK(t_mask);
             if (tid == 0) sh.n_inl = base;
             if (tid == 0)  // the best model's mask holds maxGoodCount inliers
                 MIM_DEBUG_CHECK(base == S.max_good, "[refine] p=%d n=%d max_good=%d mask=%d best_iter=%d niters=%d\n",
@@ -3598,6 +3625,47 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                                         fabs(sh.norm[6]) < DBL_EPSILON || fabs(sh.norm[7]) < DBL_EPSILON;
                 if (!degenerate) {
                     const double smx = k / sh.norm[4], smy = k / sh.norm[5], sMx = k / sh.norm[6], sMy = k / sh.norm[7];
+#if MIM_LTL_STAGE
+                    {  // LtL entry (j, kk), kk >= j: one sequential sum over the inliers per lane, the
+                       // inliers' L rows staged in LDS 64 at a time (one point per lane) so each lane
+                       // reads its four entries instead of selecting them from the 18 (same values,
+                       // same expression, same order)
+                        int j = 8, kk = 8;
+                        if (tid < 45) {
+                            int r = tid;
+                            j = 0;
+                            while (r >= 9 - j) { r -= 9 - j; ++j; }
+                            kk = j + r;
+                        }
+                        double acc = 0;
+                        for (int c0 = 0; c0 < k; c0 += kLmChunk) {
+                            const int m = min(kLmChunk, k - c0);
+                            wsync();
+                            if (tid < m) {
+                                const float4 q = X[c0 + tid];
+                                const double x = (q.z - cmx) * smx, y = (q.w - cmy) * smy;
+                                const double Xx = (q.x - cMx) * sMx, Yy = (q.y - cMy) * sMy;
+                                double* lx = sh.lm.rx + tid * kLmRow;
+                                double* ly = sh.lm.ry + tid * kLmRow;
+                                lx[0] = Xx; lx[1] = Yy; lx[2] = 1; lx[3] = 0; lx[4] = 0; lx[5] = 0;
+                                lx[6] = -x * Xx; lx[7] = -x * Yy; lx[8] = -x;
+                                ly[0] = 0; ly[1] = 0; ly[2] = 0; ly[3] = Xx; ly[4] = Yy; ly[5] = 1;
+                                ly[6] = -y * Xx; ly[7] = -y * Yy; ly[8] = -y;
+                            }
+                            wsync();
+                            if (tid < 45) {
+#pragma unroll 4
+                                for (int i = 0; i < m; ++i) {
+                                    const double* lx = sh.lm.rx + i * kLmRow;
+                                    const double* ly = sh.lm.ry + i * kLmRow;
+                                    const double lxj = lx[j], lxk = lx[kk], lyj = ly[j], lyk = ly[kk];
+                                    acc += lxj * lxk + lyj * lyk;
+                                }
+                            }
+                        }
+                        if (tid < 45) sh.lt[tid] = acc;
+                    }
+#else
                     if (tid < 45) {  // LtL entry (j, kk), kk >= j: one sequential sum over the inliers
                         int j = 0, r = tid;
                         while (r >= 9 - j) { r -= 9 - j; ++j; }
@@ -3620,6 +3688,7 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                         }
                         sh.lt[tid] = acc;
                     }
+#endif
                     wsync();
                     const double invHnorm[9] = {1. / smx, 0, cmx, 0, 1. / smy, cmy, 0, 0, 1};
                     const double Hnorm2[9] = {sMx, 0, -cMx * sMx, 0, sMy, -cMy * sMy, 0, 0, 1};
@@ -3633,6 +3702,7 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                     for (int i = 0; i < 9; ++i) sh.H[i] = sh.Hb[i];  // runKernel returned 0: H kept
                 }
                 wsync();
+                MIM_RT_MARK(t_refit);
                 // ---- LMSolverImpl (levmarq.cpp) on H8 = H[0..7], maxIters 10, eps FLT_EPSILON ----
                 if (tid < 8) sh.x[tid] = sh.H[tid];
                 wsync();
@@ -3648,6 +3718,7 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                     sh.S = sh.nrm[44]; sh.rinf = rinf; sh.lambda = 1; sh.lc = 0.75;
                 }
                 wsync();
+                MIM_RT_MARK(t_norm0);
                 int iter = 0;
                 double ew[8];  // the step solve's eigendecomposition (group lanes), for the lambda restart
                 int eperm[8];
@@ -3670,9 +3741,20 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                         }
                     }
                     wsync();
+                    MIM_RT_MARK(t_solve);
                     double xd[8];
                     for (int i = 0; i < 8; ++i) xd[i] = sh.xd[i];
+#if MIM_LM_MERGE
+                    // S(x - d) is the normal pass's S entry at x - d (the same rows, summed in the same
+                    // order as lm_cost), and an accepted step needs that pass's A, v and |r|_inf next:
+                    // one pass over the inliers per iteration instead of two
+                    double rinf_d;
+                    lm_normal(X, k, xd, sh.lm, sh.nrm, rinf_d);
+                    const double Sd = sh.nrm[44];
+#else
                     const double Sd = lm_cost(X, k, xd, sh.lm, sh.red);
+#endif
+                    MIM_RT_MARK(t_cost);
                     if (tid < 16) {  // every slot evaluates the same update; slot 0 stores it
                         const double Rlo = 0.25, Rhi = 0.75;
                         double lambda = sh.lambda, lc = sh.lc;
@@ -3713,8 +3795,12 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                     }
                     wsync();
                     if (sh.accept) {
+#if MIM_LM_MERGE
+                        rinf = rinf_d;
+#else
                         for (int i = 0; i < 8; ++i) x[i] = sh.x[i];
                         lm_normal(X, k, x, sh.lm, sh.nrm, rinf);
+#endif
                         if (tid == 0) {
                             int e = 0;
                             for (int a = 0; a < 8; ++a)
@@ -3723,6 +3809,7 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                             sh.rinf = rinf;
                         }
                     }
+                    MIM_RT_MARK(t_norm);
                     ++iter;
                     if (tid == 0) sh.proceed = iter < 10 && sh.dinf >= FLT_EPSILON && sh.rinf >= FLT_EPSILON;
                     wsync();
@@ -3730,6 +3817,9 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
                     wsync();
                     if (!proceed) break;
                 }
+#if MIM_REFINE_TIMING
+                rt_iters = iter;
+#endif
                 if (tid < 8) sh.H[tid] = sh.x[tid];
                 wsync();
             } else if (tid == 0) {
@@ -3743,6 +3833,15 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
     }
     wsync();
     if (tid != 0) return;
+#if MIM_REFINE_TIMING
+    {  // wall clock at 100 MHz: 10 ns ticks
+        const unsigned long long tot = wall_clock64() - rt_start;
+        if (tot > 20000)
+            printf("[refine-timing] p=%d ng=%d inl=%d iters=%d total=%llu mask=%llu refit=%llu norm0=%llu "
+                   "solve=%llu cost=%llu norm=%llu (us x100)\n", p, ng, sh.n_inl, rt_iters, tot, t_mask, t_refit,
+                   t_norm0, t_solve, t_cost, t_norm);
+    }
+#endif
     res.n_inl = ok ? sh.n_inl : 0;
     if (!ok) {
         // the RNG stream ran out before the loop ended: the host grows it and re-runs the batch

@@ -2902,7 +2902,8 @@ __global__ __launch_bounds__(64) void ransac_settle_kernel(const RansacState* __
                                                            const int2* __restrict__ bounds,
                                                            const int* __restrict__ cand, const int* __restrict__ ncand,
                                                            int* __restrict__ cex, double* __restrict__ cH,
-                                                           int* __restrict__ decided, int L, int cap) {
+                                                           int* __restrict__ decided, int L, int cap,
+                                                           int winner_h) {
     const int p = blockIdx.x, lane = threadIdx.x;
     const RansacState S = st[p];
     if (!S.active || S.done) return;
@@ -2929,6 +2930,20 @@ __global__ __launch_bounds__(64) void ransac_settle_kernel(const RansacState* __
             cH[(lb + k) * 9 + 8] = 0.0;
         }
         bar = max(bar, __shfl(incl, 63));
+    }
+    if (winner_h && bar > max(S.max_good, 3)) {
+        // the first listed decided candidate holding the largest decided count is the chunk's likely
+        // bestModel: send it through the exact pass too (same count), so its fp64 H reaches best_h and
+        // the refine needs no runKernel of its own (MIM_WINNER_H=1; the count and the outcome are unchanged)
+        for (int base = 0; base < nl; base += 64) {
+            const int k = base + lane;
+            const bool hit = k < nl && decided[lb + k] == 1 && cex[lb + k] == bar;
+            const unsigned long long m = __ballot(hit);
+            if (m) {
+                if (lane == __builtin_ctzll(m)) decided[lb + k] = 0;
+                break;
+            }
+        }
     }
 }
 
@@ -3926,6 +3941,9 @@ void ransac_enqueue(const RansacParams& prm, int n_probs, const ProbDev* probs, 
     // settling irrelevant candidates after the prescreen (MIM_SETTLE=0: off)
     const char* se = getenv("MIM_SETTLE");
     const int settle = (se && se[0] == '0') ? 0 : 1;
+    // the chunk's largest decided candidate through the exact pass as well (MIM_WINNER_H=1, off by default)
+    const char* we = getenv("MIM_WINNER_H");
+    const int winner_h = (we && we[0] == '1') ? 1 : 0;
     while (c0 < max_iters) {
         const int c1 = (int)std::min<long long>((long long)c0 + chunk, max_iters);
         // attempt outcomes for a window of ~28 draws per wanted iteration (pass rate ~1/5), the walk
@@ -4025,7 +4043,7 @@ void ransac_enqueue(const RansacParams& prm, int n_probs, const ProbDev* probs, 
                                                                           b.decided, thr2, L, cap);
                 if (settle)
                     ransac_settle_kernel<<<n_probs, 64, 0, s>>>(b.state, probs, b.bounds, b.cand, b.ncand, b.cex, b.cH,
-                                                                b.decided, L, cap);
+                                                                b.decided, L, cap, winner_h);
             }
             mark(mark_ctx, "cand", s);
             if (prescreen && getenv("MIM_CHECK_PRESCREEN")) {  // debug: decided candidates recounted exactly

@@ -2897,6 +2897,8 @@ __global__ __launch_bounds__(64) void ransac_prescreen_kernel(const RansacState*
 // a new best wherever the running best stands (it is at least that bar), so it is settled as
 // irrelevant (decided = 2, count 0: the replay's `count > best` test skips it) without the eigensolve.
 // Earlier candidates past the final niters only precede later ones that are past it as well.
+constexpr int kWinnerHMaxN = 256;
+
 __global__ __launch_bounds__(64) void ransac_settle_kernel(const RansacState* __restrict__ st,
                                                            const ProbDev* __restrict__ probs,
                                                            const int2* __restrict__ bounds,
@@ -2931,7 +2933,9 @@ __global__ __launch_bounds__(64) void ransac_settle_kernel(const RansacState* __
         }
         bar = max(bar, __shfl(incl, 63));
     }
-    if (winner_h && bar > max(S.max_good, 3)) {
+    // winner_h: 1 every problem, 2 problems of fewer than kWinnerHMaxN good matches (where the refine's
+    // own runKernel is a large share of its chain: real SIFT views), 0 none
+    if ((winner_h == 1 || (winner_h == 2 && S.n < kWinnerHMaxN)) && bar > max(S.max_good, 3)) {
         // the first listed decided candidate holding the largest decided count is the chunk's likely
         // bestModel: send it through the exact pass too (same count), so its fp64 H reaches best_h and
         // the refine needs no runKernel of its own (MIM_WINNER_H=1; the count and the outcome are unchanged)
@@ -3941,9 +3945,10 @@ void ransac_enqueue(const RansacParams& prm, int n_probs, const ProbDev* probs, 
     // settling irrelevant candidates after the prescreen (MIM_SETTLE=0: off)
     const char* se = getenv("MIM_SETTLE");
     const int settle = (se && se[0] == '0') ? 0 : 1;
-    // the chunk's largest decided candidate through the exact pass as well (MIM_WINNER_H=1, off by default)
+    // the chunk's largest decided candidate through the exact pass as well: by default for problems of
+    // fewer than kWinnerHMaxN good matches (MIM_WINNER_H=1: every problem, 0: none)
     const char* we = getenv("MIM_WINNER_H");
-    const int winner_h = (we && we[0] == '1') ? 1 : 0;
+    const int winner_h = !we ? 2 : we[0] == '1' ? 1 : we[0] == '0' ? 0 : 2;
     while (c0 < max_iters) {
         const int c1 = (int)std::min<long long>((long long)c0 + chunk, max_iters);
         // attempt outcomes for a window of ~28 draws per wanted iteration (pass rate ~1/5), the walk

@@ -460,7 +460,8 @@ def test_attempt_redraw_list_overflow_equals_walker(oracle):
 def test_candidate_prescreen_equals_exact_paths(capfd):
     """The prescreen (closed-form disc test in fp64, MIM_PRESCREEN=1, default) decides a part of the
     candidates without the eigensolve and the settle pass drops those that cannot beat the decided counts
-    before them: records and masks identical to the prescreen off, the settle pass off and to the all-exact
+    before them: records and masks identical to the prescreen off, the settle pass off, the largest decided
+    candidate sent through the exact pass on every problem (MIM_WINNER_H=1) and to the all-exact
     mode on C4's regime (8 % planted inliers of 2,000 good matches, 50,000 iterations),
     and the debug counts show candidates actually decided."""
     import os
@@ -469,7 +470,7 @@ def test_candidate_prescreen_equals_exact_paths(capfd):
     ds = make_dataset(1, 6, 3000, 3000, 2000, inlier_frac=0.08, seed=4242)
     outs = []
     for env in ({"MIM_PRESCREEN": "1", "MIM_DEBUG_NCAND": "1"}, {"MIM_PRESCREEN": "0"}, {"MIM_SETTLE": "0"},
-                {"MIM_RANSAC_EXACT": "1"}):
+                {"MIM_WINNER_H": "1"}, {"MIM_RANSAC_EXACT": "1"}):
         os.environ.update(env)
         m = Matcher(0)
         try:

@@ -58,8 +58,9 @@ mim::ModelViews to_views(const ObjectModel& m) {
 }
 
 // the converted models, kept across scenes (the models are loaded once, main.cpp:22).  Keyed by the
-// ObjectModel's address AND its descriptor matrices' data pointers and sizes, so a different model
-// that happens to reuse a freed address is converted anew.
+// ObjectModel's address AND the data pointers and sizes of its descriptor matrices and keypoint
+// vectors, so a different model that happens to reuse a freed address, or a model whose keypoints were
+// replaced while its descriptor Mats kept their buffers, is converted anew.
 const mim::ModelViews& views_of(const ObjectModel& m) {
     struct Entry {
         std::vector<std::pair<const void*, size_t>> key;
@@ -67,8 +68,9 @@ const mim::ModelViews& views_of(const ObjectModel& m) {
     };
     static std::unordered_map<const ObjectModel*, Entry> cache;
     std::vector<std::pair<const void*, size_t>> key;
-    key.reserve(m.descriptors.size());
+    key.reserve(m.descriptors.size() + m.keypoints.size());
     for (const cv::Mat& d : m.descriptors) key.emplace_back(static_cast<const void*>(d.data), d.total());
+    for (const std::vector<cv::KeyPoint>& k : m.keypoints) key.emplace_back(static_cast<const void*>(k.data()), k.size());
     auto it = cache.find(&m);
     if (it == cache.end() || it->second.key != key) it = cache.insert_or_assign(&m, Entry{key, to_views(m)}).first;
     return it->second.views;

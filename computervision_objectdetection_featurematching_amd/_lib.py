@@ -21,6 +21,9 @@ EXPORTS = [
     "mim_batch_results_dev", "mim_batch_results_copy", "mim_batch_problem_detail", "mim_batch_inlier_points", "mim_knn2_sets_dev", "mim_last_kernel_ms",
     "mim_set_timing", "mim_sift_detect_compute", "mim_sift_detect_compute_scales", "mim_sift_scales_sets",
     "mim_resize_linear_u8", "mim_default_box_params", "mim_detect_boxes",
+    "mim_group_shard", "mim_group_create", "mim_group_destroy", "mim_group_size", "mim_group_uses_rccl",
+    "mim_group_ctx", "mim_group_last_error", "mim_group_set_create", "mim_group_scene_batch_run",
+    "mim_group_results",
 ]
 
 
@@ -52,6 +55,10 @@ class Rect(C.Structure):
 
 class Problem(C.Structure):
     _fields_ = [("query_set", C.c_int32), ("train_set", C.c_int32)]
+
+
+class HostSet(C.Structure):  # mim_host_set
+    _fields_ = [("desc", C.c_void_p), ("kp_xy", C.c_void_p), ("n", C.c_int32)]
 
 
 RESULT_DTYPE = np.dtype([("n_good", np.int32), ("n_inl", np.int32), ("status", np.int32),
@@ -113,6 +120,21 @@ def load():
     L.mim_resize_linear_u8.argtypes = [vp, u8p, i32, i32, C.c_int64, u8p, i32, i32, C.c_double, C.c_double]
     L.mim_default_box_params.argtypes = [C.POINTER(BoxParams)]
     L.mim_detect_boxes.argtypes = [f32p, i32, C.POINTER(BoxParams), C.POINTER(Rect), i32, C.POINTER(C.c_int32)]
+    L.mim_group_shard.argtypes = [i32, i32, i32, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
+    L.mim_group_create.argtypes = [i32p, i32, C.POINTER(vp)]
+    L.mim_group_destroy.argtypes = [vp]
+    L.mim_group_size.argtypes = [vp]
+    L.mim_group_uses_rccl.argtypes = [vp]
+    L.mim_group_ctx.argtypes = [vp, i32]
+    L.mim_group_ctx.restype = vp
+    L.mim_group_last_error.argtypes = [vp]
+    L.mim_group_last_error.restype = C.c_char_p
+    L.mim_group_set_create.argtypes = [vp, f32p, f32p, i32, i32, C.POINTER(C.c_int32)]
+    L.mim_group_scene_batch_run.argtypes = [vp, i32, i32, C.POINTER(HostSet), i32, C.POINTER(Problem), C.POINTER(Params)]
+    L.mim_group_results.argtypes = [vp, vp]
+    for name in ("mim_group_shard", "mim_group_create", "mim_group_size", "mim_group_uses_rccl", "mim_group_set_create",
+                 "mim_group_scene_batch_run", "mim_group_results"):
+        getattr(L, name).restype = C.c_int32
     for name in ("mim_ctx_create", "mim_ctx_set_stream", "mim_synchronize", "mim_set_create", "mim_sets_create", "mim_sets_clear",
                  "mim_sets_truncate", "mim_knn2_l2", "mim_ratio_filter", "mim_find_homography", "mim_batch_run", "mim_batch_results",
                  "mim_batch_problem_detail", "mim_batch_inlier_points", "mim_knn2_sets_dev", "mim_set_timing", "mim_ctx_set_sampler_stream",

@@ -9,7 +9,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIBDIR = os.path.join(HERE, "lib")
 SO = os.path.join(LIBDIR, "libmim.so")
-SOURCES = ["knn.hip", "ransac.hip", "sift.hip", "api.cpp"]
+SOURCES = ["knn.hip", "ransac.hip", "sift.hip", "api.cpp", "group.cpp"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 # -ffp-contract=off: the RANSAC/DLT arithmetic must not be FMA-contracted (OpenCV's calib3d
 # x86-64 build has no FMA), see DESIGN.md "Floating-point contract".
@@ -58,7 +58,9 @@ def build(force: bool = False, verbose: bool = False) -> str:
         objs.append(obj)
     os.makedirs(os.path.dirname(os.path.abspath(SO)), exist_ok=True)
     tmp = f"{SO}.tmp{os.getpid()}"
-    cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", tmp, *objs]
+    # librccl: the several-GPU group's all-gather (group.cpp)
+    cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", tmp, *objs, "-L/opt/rocm/lib", "-lrccl",
+           "-Wl,-rpath,/opt/rocm/lib"]
     subprocess.check_call(cmd)
     os.replace(tmp, SO)
     for o in objs:

@@ -347,8 +347,9 @@ double mim_last_kernel_ms(mim_ctx* c, const char* name) {
     return it == c->last_ms.end() ? -1 : it->second;
 }
 
+// sync: wait for the copies of host rows before returning (false: the caller waits once for several)
 static mim_status set_create_locked(mim_ctx* c, const float* desc, const float* kp, int32_t n, int32_t dim,
-                                    int32_t on_device, int32_t* set_id) {
+                                    int32_t on_device, int32_t* set_id, bool sync = true) {
     if (!set_id || n < 0 || (n > 0 && (!desc || !kp))) return fail(c, MIM_EINVAL, "set_create: bad arguments");
     if (dim != kDim) return fail(c, MIM_EINVAL, "set_create: dim must be %d (got %d)", kDim, dim);
     HIPCHK(c, hipSetDevice(c->device));
@@ -376,7 +377,7 @@ static mim_status set_create_locked(mim_ctx* c, const float* desc, const float* 
     r.d.f32 = f32;
     r.d.kp = (const float2*)kpd;
     r.d.flags = nullptr;  // assigned when the prep is flushed
-    if (!on_device) HIPCHK(c, hipStreamSynchronize(c->stream));  // host buffers may go away
+    if (!on_device && sync) HIPCHK(c, hipStreamSynchronize(c->stream));  // host buffers may go away
     *set_id = (int32_t)c->sets.size();
     c->pend.push_back(PrepJob{f32, (int8_t*)frag, (int*)norm, nullptr, n, 0});
     c->pend_set.push_back(*set_id);
@@ -430,13 +431,24 @@ mim_status mim_sets_create(mim_ctx* c, int32_t count, const float* const* desc, 
         return fail(c, MIM_EINVAL, "sets_create: bad arguments");
     std::lock_guard<std::mutex> lk(c->mu);
     const int n0 = (int)c->sets.size();
+    const Arena::Mark m0 = c->arena.pos();
+    // all or nothing: the sets of this call go, and so does the storage a set that failed part-way
+    // took (it is not in `sets` yet, so only the arena mark of the call's start covers it)
+    auto undo = [&](mim_status st) {
+        if (!on_device) (void)hipStreamSynchronize(c->stream);  // copies already enqueued read the host rows
+        if ((int)c->sets.size() > n0) sets_truncate_locked(c, n0);
+        c->arena.seek(m0);
+        return st;
+    };
     for (int i = 0; i < count; ++i) {
         int32_t id = -1;
-        const mim_status st = set_create_locked(c, desc[i], kp[i], rows[i], dim, on_device, &id);
-        if (st != MIM_OK) {
-            if ((int)c->sets.size() > n0) sets_truncate_locked(c, n0);  // all or nothing
-            return st;
-        }
+        const mim_status st = set_create_locked(c, desc[i], kp[i], rows[i], dim, on_device, &id, false);
+        if (st != MIM_OK) return undo(st);
+    }
+    // host rows: every copy enqueued, one wait for all of them (the host buffers may go away after)
+    if (!on_device && count > 0) {
+        const hipError_t e = hipStreamSynchronize(c->stream);
+        if (e != hipSuccess) return undo(fail(c, MIM_EDEVICE, "sets_create: hipStreamSynchronize: %s", hipGetErrorString(e)));
     }
     *first_id = n0;
     return MIM_OK;

@@ -182,6 +182,19 @@ constexpr int kEarlyTiles = MIM_KNN_EARLY;
 #ifndef MIM_KNN_LATE_UNROLL
 #define MIM_KNN_LATE_UNROLL 1
 #endif
+// timing probes (diagnostic builds only, results wrong): 1 late tiles without the insertion events,
+// 2 without the min filter too, 3 and with zero accumulator seeds (no seed LDS reads)
+#ifndef MIM_KNN_PROBE
+#define MIM_KNN_PROBE 0
+#endif
+// parity word of a late half tile waited for with the seeds, before the MFMAs (1) or after them (0)
+#ifndef MIM_KNN_PW_EARLY
+#define MIM_KNN_PW_EARLY 0
+#endif
+// s_setprio 1 for waves 4-7 (the younger half of each SIMD's pair)
+#ifndef MIM_KNN_PRIO
+#define MIM_KNN_PRIO 0
+#endif
 
 
 // Threshold on R of a lane in the late tiles.  Lanes l, l ^ 32 hold the same query over disjoint
@@ -294,6 +307,7 @@ __global__ __launch_bounds__(kThreads, MIM_KNN_OCC) void knn2_i8_kernel(  // OCC
     // seeds read as a struct type the waitcnt pass could not tell them from the DMA's target and
     // waited for the next stage's DMA before each tile.)
     const int wv = __builtin_amdgcn_readfirstlane(wave);
+    if (MIM_KNN_PRIO && wv >= 4) __builtin_amdgcn_s_setprio(1);
     auto stage_dma = [&](int t0, int buf, bool keys) {
         unsigned char* base = smem + buf * kStage * kLdsTile;
 #pragma unroll
@@ -335,7 +349,7 @@ __global__ __launch_bounds__(kThreads, MIM_KNN_OCC) void knn2_i8_kernel(  // OCC
         const int* tnu = reinterpret_cast<const int*>(tb + kTileBytes) + 32 * u2 + 4 * h;
 #pragma unroll
         for (int gg = 0; gg < 4; ++gg) {
-            const i32x4 n = *reinterpret_cast<const i32x4*>(tnu + 8 * gg);
+            const i32x4 n = MIM_KNN_PROBE >= 3 ? i32x4{0, 0, 0, 0} : *reinterpret_cast<const i32x4*>(tnu + 8 * gg);
             acc[0][4 * gg + 0] = n.x; acc[0][4 * gg + 1] = n.y; acc[0][4 * gg + 2] = n.z; acc[0][4 * gg + 3] = n.w;
         }
 #pragma unroll
@@ -396,10 +410,16 @@ __global__ __launch_bounds__(kThreads, MIM_KNN_OCC) void knn2_i8_kernel(  // OCC
             const int row0 = tile * 64 + 32 * u2;
             const unsigned pw = (unsigned)tn[64 + u2] >> (4 * h);  // bit 8j + k: n2 & 1 of the lane's row
             i32x16 acc[QT];
+            if (MIM_KNN_PW_EARLY) asm volatile("" ::"v"(pw));
             block_mfma(tb, u2, acc);
             // the parity word is read with the seeds (its LDS latency hidden behind the MFMAs), not
             // inside the rare insertion path where the compiler would sink it: one LDS round trip per event
-            asm volatile("" ::"v"(pw));
+            if (!MIM_KNN_PW_EARLY) asm volatile("" ::"v"(pw));
+            if (MIM_KNN_PROBE >= 2) {
+#pragma unroll
+                for (int u = 0; u < QT; ++u) asm volatile("" ::"v"(acc[u]));
+                continue;
+            }
             // a lane's 16 R as two row groups (g 0-7, 8-15): the group minima cost one v_min more
             // than a single min chain and let an event compare the rows of the hit groups only
             int mn[QT], gmn[QT][2];
@@ -420,7 +440,8 @@ __global__ __launch_bounds__(kThreads, MIM_KNN_OCC) void knn2_i8_kernel(  // OCC
             }
             // the masks are tested on the scalar unit (re-evaluating the compare as a ballot made the
             // compiler rebuild each one with a v_cndmask + v_cmp pair per event)
-            if (__builtin_expect(any != 0, 0)) {  // ~1 insertion per wave and half tile
+            if (MIM_KNN_PROBE == 1) asm volatile("" ::"s"(any));
+            if (MIM_KNN_PROBE != 1 && __builtin_expect(any != 0, 0)) {  // ~1 insertion per wave and half tile
 #pragma unroll
                 for (int u = 0; u < QT; ++u) {
                     if (bm[u] != 0) {

@@ -106,17 +106,18 @@ def forget_models(matcher: Matcher) -> None:
 class SceneRun:
     """detect_objects' intermediate products (for tests and benches)."""
     scene_kp: list      # per scale: KEYPOINT_DTYPE
-    _scene_desc: list   # per scale: (n, 128) float32, copied out of the device sets the batch used
+    scene_desc: list | None  # per scale: (n, 128) float32 copied out of the device sets the batch
+    #                          used; None unless detect_objects(..., keep_descriptors=True)
     results: np.ndarray  # RESULT_DTYPE per problem, problems in (model, scale, view) order
     points: list        # per model: allUnfilteredScenePts (n, 2) float32
     detections: list    # [((x, y, w, h), name)]
 
-    @property
-    def scene_desc(self) -> list:
-        if self._scene_desc is None:
-            raise ValueError("SceneRun.scene_desc: detect_objects(..., keep=True) ran without "
+    def descriptors(self) -> list:
+        """scene_desc, or ValueError when the run did not keep them."""
+        if self.scene_desc is None:
+            raise ValueError("SceneRun.descriptors: detect_objects(..., keep=True) ran without "
                              "keep_descriptors=True (the scene's descriptors stay on the device)")
-        return self._scene_desc
+        return self.scene_desc
 
 
 def detect_objects(matcher: Matcher, scene_gray, models: list[ObjectModel], scales=SCALES, params=None,

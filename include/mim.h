@@ -263,6 +263,53 @@ void mim_default_box_params(mim_box_params* p);
 mim_status mim_detect_boxes(const float* pts_xy, int32_t n, const mim_box_params* bp, mim_rect* boxes, int32_t cap,
                             int32_t* n_boxes);
 
+/* ---- several GPUs of one node: scene-batch data parallelism ------------------
+ * Replaces the reference's one-GPU-less loop over the test scenes (processAllTestImages,
+ * Output.cpp:23-57, each scene into detectObjects, TestsDetector.cpp:58-95) for one process that owns
+ * every GPU of the node.  A group = one ctx per device + an RCCL communicator over them
+ * (ncclCommInitAll).  Query (model view) sets are replicated: mim_group_set_create registers the same
+ * host set on every device, with the same id.  A scene batch is split into contiguous scene ranges
+ * (mim_group_shard: sizes differ by at most one); each device uploads only its own scenes' sets and
+ * runs its problems as one mim_batch_run on its ctx; then ONE ncclAllGather over xGMI puts every
+ * device's mim_result records (padded to the largest range) on every device.  No descriptor crosses
+ * devices.  A device list that repeats a device (two ctxs on one GPU, for tests on a one-GPU machine)
+ * gathers with device-to-device copies instead of RCCL (mim_group_uses_rccl() == 0). */
+typedef struct mim_group mim_group;
+/* One scene set in host memory (n x 128 float32 descriptors, n x 2 float32 keypoint positions). */
+typedef struct {
+    const float* desc;
+    const float* kp_xy;
+    int32_t n;
+} mim_host_set;
+
+/* ≙ shard.shard_range: rank's contiguous share [*first, *first + *count) of n_items.  No device. */
+mim_status mim_group_shard(int32_t n_items, int32_t world, int32_t rank, int32_t* first, int32_t* count);
+mim_status mim_group_create(const int32_t* devices, int32_t n_devices, mim_group** out);
+void mim_group_destroy(mim_group* g);
+int32_t mim_group_size(const mim_group* g);
+int32_t mim_group_uses_rccl(const mim_group* g);
+/* The ctx of rank r (its device's), for per-device calls (timing, streams); owned by the group. */
+struct mim_ctx* mim_group_ctx(mim_group* g, int32_t rank);
+const char* mim_group_last_error(const mim_group* g);
+/* ObjectModel view registered on every device (host buffers, copied); same id on every ctx.  Drops
+ * the scene sets of the last batch.  All or nothing. */
+mim_status mim_group_set_create(mim_group* g, const float* desc, const float* kp_xy, int32_t n, int32_t dim,
+                                int32_t* set_id);
+/* Enqueues a batch of n_scenes scenes.  Scene s owns scene_sets[s * sets_per_scene ..
+ * (s + 1) * sets_per_scene) (its scales, host memory, read before the call returns).  Every scene runs
+ * the same problem template tmpl[0 .. n_tmpl): query_set = a replicated set id, train_set = an index
+ * 0 .. sets_per_scene - 1 into the scene's own sets (the reference's per-scene (model, scale, view)
+ * loop: TestsDetector.cpp:38,100,58).  Records: n_scenes * n_tmpl, scene-major, template order within
+ * a scene — exactly the records mim_batch_run gives for the same problems on one device.  Returns once
+ * every device's batch and the all-gather are enqueued. */
+mim_status mim_group_scene_batch_run(mim_group* g, int32_t n_scenes, int32_t sets_per_scene,
+                                     const mim_host_set* scene_sets, int32_t n_tmpl, const mim_problem* tmpl,
+                                     const mim_params* params);
+/* Waits for the batch and its gather; copies the n_scenes * n_tmpl records (from device 0's gathered
+ * buffer) to `out` (NULL: wait only).  A device whose problems ran out of RNG draws grows its stream
+ * and re-runs its share first, as mim_batch_results. */
+mim_status mim_group_results(mim_group* g, mim_result* out);
+
 /* ---- introspection for benches / profiles ----------------------------------------------------- */
 /* Per-kernel device time (ms) summed over the batches since the last result fetch, measured with
  * HIP events on the stream each kernel ran on.  names: "knn", "ratio", "attempt", "chain",

@@ -46,6 +46,8 @@ def test_scene_run_descriptors_only_when_kept():
     from computervision_objectdetection_featurematching_amd.pipeline import SceneRun
     run = SceneRun([], None, np.zeros(0), [], [])
     with pytest.raises(ValueError, match="keep_descriptors"):
-        _ = run.scene_desc
+        run.descriptors()
+    assert run.scene_desc is None
     d = [np.zeros((2, 128), np.float32)]
-    assert SceneRun([], d, np.zeros(0), [], []).scene_desc is d
+    assert SceneRun([], d, np.zeros(0), [], []).descriptors() is d
+    assert SceneRun(scene_kp=[], scene_desc=d, results=np.zeros(0), points=[], detections=[]).scene_desc is d

@@ -158,7 +158,7 @@ struct PinnedStage {
 namespace mim {
 // RANSAC workspace (definition shared with ransac.hip through this layout)
 struct RansacWs {
-    DevBuf state, samples, hyp, counts, bounds, flags, irr, irr_cnt, pass_bits, chains, best_h, cand, ncand, cex, cH, decided, stream,
+    DevBuf state, samples, hyp, counts, bounds, flags, irr_bits, irr, irr_cnt, pass_bits, chains, best_h, cand, ncand, cex, cH, decided, stream,
         scratch, inl, tiles, err;
     long long stream_len = 0;
 };
@@ -304,7 +304,7 @@ void mim_ctx_destroy(mim_ctx* c) {
     c->arena.release();
     for (DevBuf* b : {&c->probs, &c->works, &c->parts, &c->good_q, &c->good_t, &c->pts, &c->n_good,
                       &c->results, &c->masks, &c->knn_idx, &c->knn_dist, &c->inl_tab, &c->inl_out, &c->knn_ctr, &c->rws.state, &c->rws.samples,
-                      &c->rws.hyp, &c->rws.counts, &c->rws.bounds, &c->rws.flags, &c->rws.irr, &c->rws.irr_cnt, &c->rws.pass_bits, &c->rws.chains, &c->rws.best_h, &c->rws.cand, &c->rws.ncand, &c->rws.cex, &c->rws.cH, &c->rws.decided, &c->rws.stream, &c->rws.scratch, &c->rws.inl, &c->rws.tiles, &c->rws.err, &c->prep_jobs})
+                      &c->rws.hyp, &c->rws.counts, &c->rws.bounds, &c->rws.flags, &c->rws.irr_bits, &c->rws.irr, &c->rws.irr_cnt, &c->rws.pass_bits, &c->rws.chains, &c->rws.best_h, &c->rws.cand, &c->rws.ncand, &c->rws.cex, &c->rws.cH, &c->rws.decided, &c->rws.stream, &c->rws.scratch, &c->rws.inl, &c->rws.tiles, &c->rws.err, &c->prep_jobs})
         b->release();
     if (c->own) (void)hipStreamDestroy(c->own);
     delete c;
@@ -995,6 +995,8 @@ mim_status mim_sift_detect_compute_scales(mim_ctx* c, const uint8_t* gray, int32
 // mim_sift_scales_sets' registration of the scales as sets (lock held); total = keypoints of all scales
 static mim_status scales_sets_register(mim_ctx* c, const mim::SiftDevOut* out, int n_scales, int32_t* set_ids,
                                        int32_t* n_kp, long long& total) {
+    std::vector<float*> ddesc(n_scales, nullptr);
+    std::vector<float2*> dkp(n_scales, nullptr);
     for (int i = 0; i < n_scales; ++i) {
         const int n = out[i].n;
         n_kp[i] = n;
@@ -1010,11 +1012,9 @@ static mim_status scales_sets_register(mim_ctx* c, const mim::SiftDevOut* out, i
         if (n > 0) {
             HIPCHK(c, c->arena.alloc((size_t)n * kDim * sizeof(float), &df));
             HIPCHK(c, c->arena.alloc((size_t)n * 2 * sizeof(float), &dk));
-            HIPCHK(c, hipMemcpyAsync(df, out[i].desc, (size_t)n * kDim * sizeof(float), hipMemcpyDeviceToDevice, c->stream));
-            // KeyPoint::pt of each mim_keypoint (x, y are its first two floats): a strided 2D copy
-            HIPCHK(c, hipMemcpy2DAsync(dk, 2 * sizeof(float), out[i].kp, sizeof(mim_keypoint), 2 * sizeof(float), n,
-                                       hipMemcpyDeviceToDevice, c->stream));
         }
+        ddesc[i] = (float*)df;
+        dkp[i] = (float2*)dk;
         rec.d.frag = (const int8_t*)frag;
         rec.d.norm = (const int*)norm;
         rec.d.f32 = (const float*)df;
@@ -1025,6 +1025,9 @@ static mim_status scales_sets_register(mim_ctx* c, const mim::SiftDevOut* out, i
         c->pend_set.push_back(set_ids[i]);
         c->sets.push_back(rec);
     }
+    // every scale's rows and KeyPoint::pt (the first two floats of each mim_keypoint) in one launch
+    if (mim::sift_copy_sets(out, n_scales, ddesc.data(), dkp.data(), c->stream) != 0)
+        return fail(c, MIM_EDEVICE, "sift_scales_sets: set copy launch failed");
     return MIM_OK;
 }
 
@@ -1181,6 +1184,7 @@ static mim_status ransac_prepare(mim_ctx* c, int n, const mim_params* prm, Ransa
     flag_per = (chunk_max * 28 + 4096 + 63) & ~63LL;
     const long long flag_cap = (long long)std::max(n, 1) * flag_per;
     HIPCHK(c, c->rws.flags.ensure((size_t)flag_cap));
+    HIPCHK(c, c->rws.irr_bits.ensure((size_t)flag_cap / 8));
     const int irr_blocks = (int)((flag_per + kIrrBlock - 1) / kIrrBlock);
     HIPCHK(c, c->rws.irr.ensure(sizeof(int) * (size_t)std::max(n, 1) * irr_blocks * kIrrCap));
     HIPCHK(c, c->rws.irr_cnt.ensure(sizeof(int) * (size_t)std::max(n, 1) * irr_blocks));
@@ -1207,6 +1211,7 @@ static mim_status ransac_prepare(mim_ctx* c, int n, const mim_params* prm, Ransa
     b.counts = c->rws.counts.as<int>();
     b.bounds = c->rws.bounds.as<int2>();
     b.flags = c->rws.flags.as<uint8_t>();
+    b.irr_bits = c->rws.irr_bits.as<uint8_t>();
     b.best_h = c->rws.best_h.as<double>();
     b.cand = c->rws.cand.as<int>();
     b.ncand = c->rws.ncand.as<int>();
@@ -1258,6 +1263,7 @@ static mim_status ransac_enqueue_range(mim_ctx* c, int p0, int np, const RansacB
     RansacBufs g = b;
     g.state += p0;
     g.flags += (long long)p0 * flag_per;
+    g.irr_bits += (long long)p0 * flag_per / 8;
     g.flag_cap = (long long)np * flag_per;
     g.irr += (long long)p0 * b.irr_blocks * kIrrCap;
     g.irr_cnt += (long long)p0 * b.irr_blocks;

@@ -216,6 +216,25 @@ __device__ __forceinline__ unsigned med3_u32(unsigned a, unsigned b, unsigned c)
     return r;
 }
 
+__device__ __forceinline__ int med3_i32(int a, int b, int c) {
+    int r;
+    asm("v_med3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
+// insertion events of the late tiles: 0 a ballot per row of a hit row group and an out-of-line push per
+// hit row; 1 the group's two smallest (R, row) keys branch-free, the first pushed in every lane, the
+// second only when some lane can still take it, the rest of the group by rows after that (rare)
+#ifndef MIM_KNN_EVENT
+#define MIM_KNN_EVENT 0
+#endif
+// waves 4-7 (the second wave of each SIMD's pair in a block) defer the filter and events of each
+// stage's last half tile past the stage barrier, so a SIMD's two waves of one block do not filter at
+// the same time (MI355X_MICROARCH.md, "try a stagger")
+#ifndef MIM_KNN_STAGGER
+#define MIM_KNN_STAGGER 0
+#endif
+
 // ------------------------------------------------------------------------------------------------
 // Exact distance kernel.  Block = kKnnWaves waves = kKnnBlockQ queries (each wave: kKnnQT 32-query
 // MFMA column tiles, their q' fragments held in VGPRs for the whole sweep).  Train rows stream
@@ -402,8 +421,97 @@ __global__ __launch_bounds__(kThreads, MIM_KNN_OCC) void knn2_i8_kernel(  // OCC
         }
     };
     // late tiles: one min over a lane's 16 R per column tile against its threshold, the exact
-    // insertion only in groups some lane hits
-    auto tile_late = [&](const unsigned char* tb, int tile) {
+    // insertion only in groups some lane hits.  half_filter: the 32-row half tile starting at row0
+    // (accumulators acc, parity word pw); keyed: keys (R << 3 | g) cannot overflow (no padded row)
+    auto half_filter = [&](const i32x16 (&acc)[QT], unsigned pw, int row0, bool keyed) {
+        // a lane's 16 R as two row groups (g 0-7, 8-15): the group minima cost one v_min more
+        // than a single min chain and let an event compare the rows of the hit groups only
+        int mn[QT], gmn[QT][2];
+        unsigned long long bm[QT], any = 0;  // wave masks of the lanes with a candidate (SGPR pairs)
+#pragma unroll
+        for (int u = 0; u < QT; ++u) {
+            const i32x16& p = acc[u];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                int a = min(min(p[8 * i], p[8 * i + 1]), p[8 * i + 2]);
+                a = min(min(a, p[8 * i + 3]), p[8 * i + 4]);
+                a = min(min(a, p[8 * i + 5]), p[8 * i + 6]);
+                gmn[u][i] = min(a, p[8 * i + 7]);
+            }
+            mn[u] = min(gmn[u][0], gmn[u][1]);
+            bm[u] = __ballot(mn[u] <= T[u]);
+            any |= bm[u];
+        }
+        // the masks are tested on the scalar unit (re-evaluating the compare as a ballot made the
+        // compiler rebuild each one with a v_cndmask + v_cmp pair per event)
+        if (MIM_KNN_PROBE == 1) asm volatile("" ::"s"(any));
+        if (MIM_KNN_PROBE != 1 && __builtin_expect(any != 0, 0)) {  // ~1 insertion per wave and half tile
+#pragma unroll
+            for (int u = 0; u < QT; ++u) {
+                if (bm[u] != 0) {
+                    // per row of a hit group: one compare (the ballot) and, if some lane has the row
+                    // under its threshold, an unconditional insertion in every lane (the lane lists
+                    // stay the exact top-2 of the rows pushed, a superset of the filtered ones); the
+                    // row ballots of a group first (independent compares into SGPR pairs), then a
+                    // not-taken scalar test per row: the insertion code sits out of line
+                    unsigned long long gb[2];
+#pragma unroll
+                    for (int i = 0; i < 2; ++i) gb[i] = __ballot(gmn[u][i] <= T[u]);
+#pragma unroll
+                    for (int i = 0; i < 2; ++i) {
+                        if (gb[i] != 0) {
+                            // rows of group i in this lane: pos = (g & 3) + 8 (g >> 2) + 16 i (without 4h),
+                            // ascending with g; the parity of the row is bit pos of pw
+                            int k2 = INT_MAX;
+                            if (MIM_KNN_EVENT == 1 && keyed) {
+                                // the group's two smallest (R, row) keys: every lane pushes its own
+                                // smallest row (pushing rows beyond the filter keeps a lane list the
+                                // exact top-2 of the rows pushed into it); the second only if some lane
+                                // can still take it once the first is in; further rows by row ballots
+                                int k1 = INT_MAX;
+#pragma unroll
+                                for (int g = 0; g < 8; ++g) {
+                                    const int key = (acc[u][8 * i + g] << 3) | g;
+                                    k2 = med3_i32(k1, k2, key);
+                                    k1 = min(k1, key);
+                                }
+                                const int pos1 = (k1 & 3) + 8 * ((k1 >> 2) & 1) + 16 * i;
+                                sel_push(st[u], dval(k1 >> 3, (pw >> pos1) & 1), row0 + pos1);
+                                T[u] = late_threshold(st[u], o1c[u], o2c[u]);
+                                if (__builtin_expect(__ballot((k2 >> 3) <= T[u]) == 0, 1)) continue;
+                                const int pos2 = (k2 & 3) + 8 * ((k2 >> 2) & 1) + 16 * i;
+                                sel_push(st[u], dval(k2 >> 3, (pw >> pos2) & 1), row0 + pos2);
+                                T[u] = late_threshold(st[u], o1c[u], o2c[u]);
+                            }
+                            // rows in index order (keyed: only those after the second key, all of which
+                            // have a larger D than the two pushed rows' or an equal D and a larger row)
+                            unsigned long long hm[8];
+#pragma unroll
+                            for (int g = 0; g < 8; ++g)
+                                hm[g] = __ballot(acc[u][8 * i + g] <= T[u] &&
+                                                 (MIM_KNN_EVENT != 1 || !keyed || ((acc[u][8 * i + g] << 3) | g) > k2));
+#pragma unroll
+                            for (int g = 8 * i; g < 8 * i + 8; ++g) {
+                                if (__builtin_expect(hm[g - 8 * i] != 0, 0))
+                                    sel_push(st[u], dval(acc[u][g], (pw >> ((g & 3) + 8 * (g >> 2))) & 1),
+                                             row0 + (g & 3) + 8 * (g >> 2));
+                            }
+                        }
+                    }
+                    T[u] = late_threshold(st[u], o1c[u], o2c[u]);
+                }
+            }
+        }
+    };
+    // deferred half tile (MIM_KNN_STAGGER, waves 4-7): its accumulators, parity word and first row
+    i32x16 dacc[QT];
+    unsigned dpw = 0;
+    int drow0 = -1;
+    bool dkeyed = false;
+    const bool stagger = MIM_KNN_STAGGER && wv >= 4;
+    // the last set tile holds padded rows (R ~ 2^30): no keyed events there
+    const int pad_tile = (P->t.n & 63) ? P->t.n_tiles - 1 : INT_MAX;
+    auto tile_late = [&](const unsigned char* tb, int tile, bool defer) {
         const int* tn = reinterpret_cast<const int*>(tb + kTileBytes);
 #pragma unroll
         for (int u2 = 0; u2 < 2; ++u2) {
@@ -420,57 +528,21 @@ __global__ __launch_bounds__(kThreads, MIM_KNN_OCC) void knn2_i8_kernel(  // OCC
                 for (int u = 0; u < QT; ++u) asm volatile("" ::"v"(acc[u]));
                 continue;
             }
-            // a lane's 16 R as two row groups (g 0-7, 8-15): the group minima cost one v_min more
-            // than a single min chain and let an event compare the rows of the hit groups only
-            int mn[QT], gmn[QT][2];
-            unsigned long long bm[QT], any = 0;  // wave masks of the lanes with a candidate (SGPR pairs)
+            if (defer && u2 == 1) {
 #pragma unroll
-            for (int u = 0; u < QT; ++u) {
-                const i32x16& p = acc[u];
-#pragma unroll
-                for (int i = 0; i < 2; ++i) {
-                    int a = min(min(p[8 * i], p[8 * i + 1]), p[8 * i + 2]);
-                    a = min(min(a, p[8 * i + 3]), p[8 * i + 4]);
-                    a = min(min(a, p[8 * i + 5]), p[8 * i + 6]);
-                    gmn[u][i] = min(a, p[8 * i + 7]);
-                }
-                mn[u] = min(gmn[u][0], gmn[u][1]);
-                bm[u] = __ballot(mn[u] <= T[u]);
-                any |= bm[u];
+                for (int u = 0; u < QT; ++u) dacc[u] = acc[u];
+                dpw = pw;
+                drow0 = row0;
+                dkeyed = tile != pad_tile;
+                continue;
             }
-            // the masks are tested on the scalar unit (re-evaluating the compare as a ballot made the
-            // compiler rebuild each one with a v_cndmask + v_cmp pair per event)
-            if (MIM_KNN_PROBE == 1) asm volatile("" ::"s"(any));
-            if (MIM_KNN_PROBE != 1 && __builtin_expect(any != 0, 0)) {  // ~1 insertion per wave and half tile
-#pragma unroll
-                for (int u = 0; u < QT; ++u) {
-                    if (bm[u] != 0) {
-                        // per row of a hit group: one compare (the ballot) and, if some lane has the row
-                        // under its threshold, an unconditional insertion in every lane (the lane lists
-                        // stay the exact top-2 of the rows pushed, a superset of the filtered ones); the
-                        // row ballots of a group first (independent compares into SGPR pairs), then a
-                        // not-taken scalar test per row: the insertion code sits out of line
-                        unsigned long long gb[2];
-#pragma unroll
-                        for (int i = 0; i < 2; ++i) gb[i] = __ballot(gmn[u][i] <= T[u]);
-#pragma unroll
-                        for (int i = 0; i < 2; ++i) {
-                            if (gb[i] != 0) {
-                                unsigned long long hm[8];
-#pragma unroll
-                                for (int g = 0; g < 8; ++g) hm[g] = __ballot(acc[u][8 * i + g] <= T[u]);
-#pragma unroll
-                                for (int g = 8 * i; g < 8 * i + 8; ++g) {
-                                    if (__builtin_expect(hm[g - 8 * i] != 0, 0))
-                                        sel_push(st[u], dval(acc[u][g], (pw >> ((g & 3) + 8 * (g >> 2))) & 1),
-                                                 row0 + (g & 3) + 8 * (g >> 2));
-                                }
-                            }
-                        }
-                        T[u] = late_threshold(st[u], o1c[u], o2c[u]);
-                    }
-                }
-            }
+            half_filter(acc, pw, row0, tile != pad_tile);
+        }
+    };
+    auto flush_deferred = [&]() {
+        if (stagger && drow0 >= 0) {
+            half_filter(dacc, dpw, drow0, dkeyed);
+            drow0 = -1;
         }
     };
 
@@ -491,6 +563,7 @@ __global__ __launch_bounds__(kThreads, MIM_KNN_OCC) void knn2_i8_kernel(  // OCC
         const bool more = stage + kStage < w.tile1;
         if (more) stage_dma(stage + kStage, buf ^ 1, false);
         const unsigned char* sb = smem + buf * kStage * kLdsTile;
+        flush_deferred();  // the previous stage's last half tile (waves 4-7 with MIM_KNN_STAGGER)
         auto refresh = [&]() {  // thresholds from the partner lane's current m1, m2 (every tile: slower, r03bd)
 #pragma unroll
             for (int u = 0; u < QT; ++u) {
@@ -505,10 +578,12 @@ __global__ __launch_bounds__(kThreads, MIM_KNN_OCC) void knn2_i8_kernel(  // OCC
         // rolled by default (unrolling measured no faster; the late tile is ~3 KiB of code)
 #pragma unroll MIM_KNN_LATE_UNROLL
         for (int ts = 0; ts < kStage; ++ts)
-            if (kStage == 1 || stage + ts < w.tile1) tile_late(sb + ts * kLdsTile, stage + ts);
+            if (kStage == 1 || stage + ts < w.tile1)
+                tile_late(sb + ts * kLdsTile, stage + ts, stagger && (ts == kStage - 1 || stage + ts + 1 == w.tile1));
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA into the next buffer landed
         __syncthreads();
     }
+    flush_deferred();
 
     // ---- merge the two lane halves (disjoint train rows of the same query), keys ----
 #pragma unroll

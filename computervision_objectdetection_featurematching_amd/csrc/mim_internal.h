@@ -131,7 +131,10 @@ struct RansacBufs {
     int* cex;                 // [problem][list][kCandPerProblem] their exact inlier counts
     double* cH;               // [problem][list][kCandPerProblem][9] their exact models
     int* decided;             // [problem][list][kCandPerProblem] 1: the prescreen decided the listed candidate
-    uint8_t* flags;           // [problem][window] getSubset attempt outcomes ahead of stream_pos
+    uint8_t* flags;           // [problem][window] getSubset attempt outcomes ahead of stream_pos (written and
+                              // valid only where irr_bits is set: the repeated-index and serial attempts)
+    uint8_t* irr_bits;        // [problem][window / 8] bit per attempt position: irregular (its flag byte is
+                              // written); a clear bit means kPassUnknown (4 draws, checkSubset not evaluated)
     long long flag_cap;       // bytes of `flags`
     int* irr;                 // [problem][block][kIrrCap] positions of irregular attempts (chain sampler)
     int* irr_cnt;             // [problem][block] their count (-1: more than kIrrCap)
@@ -178,4 +181,6 @@ struct SiftDevOut {
 };
 int sift_scales_device(std::vector<SiftWs*>& ws, hipStream_t st, const uint8_t* img, int rows, int cols,
                        long long step, int n_scales, const float* scales, SiftDevOut* out, std::string& err);
+// out[j]'s n rows and keypoint positions into ddesc[j] / dkp[j], j < n <= 8, one launch (0, -1 HIP error)
+int sift_copy_sets(const SiftDevOut* out, int n, float* const* ddesc, float2* const* dkp, hipStream_t st);
 }  // namespace mim

@@ -959,8 +959,8 @@ __device__ __forceinline__ void sampler_slice_block(int n_probs, int bpp, int& p
 
 __global__ __launch_bounds__(256) void ransac_attempt_kernel(const RansacState* __restrict__ st,
                                                              const uint32_t* __restrict__ stream, long long slen,
-                                                             uint8_t* __restrict__ flags, int wcap, int bpp, int c1,
-                                                             int rep_cap, int n_probs) {
+                                                             uint8_t* __restrict__ flags, uint8_t* __restrict__ ibits,
+                                                             int wcap, int bpp, int c1, int rep_cap, int n_probs) {
     constexpr int D = kAttemptPerThread + 3;  // the first 4 draws of the thread's 8 attempts
     constexpr int kStageVecs = kAttemptSpan / 4 + 4;  // 16-byte vectors: the span, its 3 extra draws, alignment
     __shared__ __attribute__((aligned(16))) unsigned sdraw[4 * kStageVecs];
@@ -975,6 +975,7 @@ __global__ __launch_bounds__(256) void ransac_attempt_kernel(const RansacState* 
                     "[attempt] p=%d c1=%d wlen=%d bpp=%d produced=%d stream_pos=%lld n=%d\n", p, c1, wlen, bpp, S.produced,
                     (long long)S.stream_pos, S.n);
     uint8_t* __restrict__ F = flags + (long long)p * wcap;
+    uint8_t* __restrict__ IB = ibits + (long long)p * (wcap >> 3);
     const unsigned N = (unsigned)S.n, mB = 0xFFFFFFFFu / N;
     const bool big = N > 256 && N < (1u << 24);  // q and n both fit 24 bits
     if (threadIdx.x == 0) n_rep = 0;
@@ -1024,14 +1025,19 @@ __global__ __launch_bounds__(256) void ransac_attempt_kernel(const RansacState* 
     for (int k = 0; k < D - 2; ++k) d2[k] = u[k] == u[k + 2];
 #pragma unroll
     for (int k = 0; k < D - 3; ++k) d3[k] = u[k] == u[k + 3];
-    unsigned long long w = 0;  // the 8 flag bytes (one 64-bit word: indexed by a runtime j below)
-    unsigned repm = 0;
+    // one irregular bit per position (a byte per thread's 8 positions); flag bytes only for the irregular
+    // positions (~0.3 % at n = 2000): a regular position's outcome is kPassUnknown, implied by its clear bit
+    unsigned repm = 0, tailm = 0;
 #pragma unroll
     for (int j = 0; j < kAttemptPerThread; ++j) {
         const bool rep = d1[j] | d1[j + 1] | d1[j + 2] | d2[j] | d2[j + 1] | d3[j];
         const bool tail = q0 + j + 4 > (int)slen;
         repm |= (unsigned)(rep && !tail) << j;
-        w |= (unsigned long long)(tail ? kAttemptSerial : kPassUnknown) << (8 * j);
+        tailm |= (unsigned)tail << j;
+    }
+    IB[off >> 3] = (uint8_t)(repm | tailm);
+    if (tailm) {  // the stream's end: resolved by the walker
+        for (unsigned m = tailm; m; m &= m - 1) F[off + __builtin_ctz(m)] = (uint8_t)kAttemptSerial;
     }
     if (repm) {  // rare: list them (a full list: resolved here, from the stream)
         const int sl = atomicAdd(&n_rep, __popc(repm));
@@ -1043,12 +1049,10 @@ __global__ __launch_bounds__(256) void ransac_attempt_kernel(const RansacState* 
             } else {
                 int idx[4];
                 const int len = resolve_at(q0 + j, stream, slen, N, S.modM, idx);
-                const unsigned long long f = (len == 0 || len > 67) ? kAttemptSerial : (((len - 4) << 1) | kPassUnknown);
-                w = (w & ~(0xFFull << (8 * j))) | (f << (8 * j));
+                F[off + j] = (uint8_t)((len == 0 || len > 67) ? kAttemptSerial : (((len - 4) << 1) | kPassUnknown));
             }
         }
     }
-    *reinterpret_cast<uint2*>(F + off) = make_uint2((uint32_t)w, (uint32_t)(w >> 32));
     }
     }
     // the listed positions' redraw lengths, one per thread, over the flag bytes just written (same block)
@@ -1111,7 +1115,7 @@ __device__ __forceinline__ int mbcnt64(unsigned long long m) {
 // attempt-by-attempt walker (ransac_sample_kernel), which resumes from the state it stores.
 // ------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void ransac_irr_kernel(const RansacState* __restrict__ st,
-                                                         const uint8_t* __restrict__ flags, int wcap, int bpp,
+                                                         const uint8_t* __restrict__ ibits, int wcap, int bpp,
                                                          int c1, int* __restrict__ irr, int* __restrict__ irr_cnt,
                                                          int irr_blocks) {
     __shared__ int wsum[4];
@@ -1122,22 +1126,10 @@ __global__ __launch_bounds__(256) void ransac_irr_kernel(const RansacState* __re
     for (int b = blockIdx.x % bpp; b * kIrrBlock < wlen; b += bpp) {
     __syncthreads();  // wsum of the previous round read
     const int b0 = b * kIrrBlock;
-    const uint8_t* F = flags + (long long)p * wcap;
-    const int r0 = b0 + tid * 64;  // 64 positions per thread
-    uint32_t wd[16];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        uint4 v = make_uint4(0, 0, 0, 0);
-        if (r0 + 16 * k + 16 <= wlen) v = *reinterpret_cast<const uint4*>(F + r0 + 16 * k);
-        wd[4 * k] = v.x; wd[4 * k + 1] = v.y; wd[4 * k + 2] = v.z; wd[4 * k + 3] = v.w;
-    }
-    // irregular: a repeated-index redraw (len > 4) or resolved by the walker (0xFF); positions past
-    // wlen (a partial last vector) read as regular: the chain kernels never walk past wlen
-    uint64_t irrm = 0;
-#pragma unroll
-    for (int k = 0; k < 16; ++k)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) irrm |= (uint64_t)((((wd[k] >> (8 * j)) & 0x7F)) >= 2) << (4 * k + j);
+    const int r0 = b0 + tid * 64;  // 64 positions per thread: one 8-byte word of irregular bits
+    // positions past wlen read as regular (wlen is a multiple of 64: a thread's word is all in or all
+    // out); the chain kernels never walk past wlen
+    uint64_t irrm = r0 + 64 <= wlen ? *reinterpret_cast<const uint64_t*>(ibits + (long long)p * (wcap >> 3) + (r0 >> 3)) : 0ull;
     const int c = __popcll(irrm);
     int incl = c;
 #pragma unroll
@@ -2027,7 +2019,7 @@ __global__ __launch_bounds__(64) void ransac_sample_kernel(RansacState* __restri
                                                            const uint32_t* __restrict__ stream, long long slen,
                                                            int4* __restrict__ samples, int c1,
                                                            int* __restrict__ err, const uint8_t* __restrict__ flags,
-                                                           int wcap, int after_chain) {
+                                                           const uint8_t* __restrict__ ibits, int wcap, int after_chain) {
     __shared__ __attribute__((aligned(16))) uint8_t win[kFlagWin];
     constexpr int BIG = 1 << 30;
     const int p = blockIdx.x, lane = threadIdx.x;
@@ -2039,6 +2031,7 @@ __global__ __launch_bounds__(64) void ransac_sample_kernel(RansacState* __restri
     const long long wbase = after_chain ? S.win_base : S.stream_pos;
     const int wlen = after_chain ? S.win_len : window_len(S, c1, wcap);
     const uint8_t* F = flags + (long long)p * wcap;
+    const uint8_t* IB = ibits + (long long)p * (wcap >> 3);
     const unsigned N = (unsigned)S.n;
     const unsigned long long M = S.modM;
     const float4* P = pts + probs[p].good_off;
@@ -2056,7 +2049,23 @@ __global__ __launch_bounds__(64) void ransac_sample_kernel(RansacState* __restri
             const long long r0 = lb + 16LL * (lane + 64 * j);
             uint4 v;
             if (r0 + 16 <= wlen) {
-                v = *reinterpret_cast<const uint4*>(F + r0);
+                // the flag bytes of the irregular positions, kPassUnknown for the others (their bytes
+                // are not written: ransac_attempt_kernel)
+                const unsigned ib = *reinterpret_cast<const uint16_t*>(IB + (r0 >> 3));
+                if (ib == 0) {
+                    v = make_uint4(0x80808080u, 0x80808080u, 0x80808080u, 0x80808080u);
+                } else {
+                    uint32_t w4[4];
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        uint32_t w = 0;
+#pragma unroll
+                        for (int b = 0; b < 4; ++b)
+                            w |= (uint32_t)((ib >> (4 * k + b)) & 1 ? F[r0 + 4 * k + b] : kPassUnknown) << (8 * b);
+                        w4[k] = w;
+                    }
+                    v = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+                }
             } else {
                 // past the precomputed window: the redraw lengths computed here (pass bits unknown)
                 uint32_t w4[4];
@@ -2065,7 +2074,9 @@ __global__ __launch_bounds__(64) void ransac_sample_kernel(RansacState* __restri
                     uint32_t w = 0;
                     for (int b = 0; b < 4; ++b) {
                         const long long r = r0 + 4 * k + b;
-                        w |= (uint32_t)(r < wlen ? F[r] : length_flag(wbase + r, stream, slen, N, M)) << (8 * b);
+                        const int fr = r < wlen ? (((IB[r >> 3] >> (r & 7)) & 1) ? F[r] : kPassUnknown)
+                                                : length_flag(wbase + r, stream, slen, N, M);
+                        w |= (uint32_t)fr << (8 * b);
                     }
                     w4[k] = w;
                 }
@@ -2396,6 +2407,10 @@ constexpr double kOutScale = 0x1p30;
 #ifndef MIM_BOUND_CHUNK
 #define MIM_BOUND_CHUNK 8
 #endif
+#ifndef MIM_BOUND_WAVES
+#define MIM_BOUND_WAVES 4
+#endif
+constexpr int kBoundThreads = 64 * MIM_BOUND_WAVES;  // iterations per MFMA bound block (64 per wave)
 constexpr int kTileChunk = MIM_BOUND_CHUNK;  // 32-point tiles per LDS stage of the MFMA bound kernel (2 x 16 KiB)
 
 // clamp to [0, 1]: folds into the producing instruction's clamp bit (no NaN reaches it here)
@@ -2519,7 +2534,7 @@ __global__ __launch_bounds__(256) void ransac_tiles_kernel(RansacState* __restri
 // the float sum's rounding.  The lower bound adds clamp(C_lo |W'| - K E_lo - (|X'| + |Y'|)), positive
 // only where the point is surely in, so lo = ceil(sum - slack) never exceeds the exact count.
 template <bool kLo>
-__global__ __launch_bounds__(256) void ransac_bound_mfma_kernel(const RansacState* __restrict__ st,
+__global__ __launch_bounds__(kBoundThreads) void ransac_bound_mfma_kernel(const RansacState* __restrict__ st,
                                                                 const ProbDev* __restrict__ probs,
                                                                 const float4* __restrict__ pts,
                                                                 const int4* __restrict__ samples,
@@ -2535,10 +2550,10 @@ __global__ __launch_bounds__(256) void ransac_bound_mfma_kernel(const RansacStat
     const int p = xcd + 8 * (j / bpp), kb = j % bpp;
     if (p >= n_probs) return;
     const int tid = threadIdx.x, lane = tid & 63;
-    const int it = c0 + kb * 256 + tid;
+    const int it = c0 + kb * kBoundThreads + tid;
     const RansacState S = st[p];
     if (!S.active || S.done) return;  // uniform over the block
-    if (c0 + kb * 256 >= min(c1, S.produced)) return;  // whole block idle
+    if (c0 + kb * kBoundThreads >= min(c1, S.produced)) return;  // whole block idle
     const bool act = it < c1 && it < S.produced;
     const long long o = probs[p].it_off + it;
     const long long go = probs[p].good_off;
@@ -2645,7 +2660,7 @@ __global__ __launch_bounds__(256) void ransac_bound_mfma_kernel(const RansacStat
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     auto stage = [&](int t0, int buf) {
         const int tc = min(kTileChunk, nt - t0);
-        for (int i0 = wv * 64; i0 < tc * 128; i0 += 256)
+        for (int i0 = wv * 64; i0 < tc * 128; i0 += kBoundThreads)
             __builtin_amdgcn_global_load_lds((const void*)(T + (long long)t0 * 128 + i0 + lane),
                                              (__attribute__((address_space(3))) void*)(lt[buf] + i0), 16, 0, 0);
     };
@@ -2689,18 +2704,23 @@ __global__ __launch_bounds__(256) void ransac_bound_mfma_kernel(const RansacStat
         __syncthreads();
     }
     // rows (points) of a column are split over lanes l and l ^ 32.  Rounding of the float counts: a
-    // lane adds m = 16 nt values in [0, 1], each add off by <= 2^-24 m, plus the add of the two lanes:
-    // |error| <= 2^-24 (2 m^2 + 2 m) <= 2^-24 (32 nt)^2 = slack (0.24 at 2,000 points); an exact
-    // integer count (no value in the band) is unchanged by floor(+ slack) while slack < 1.
+    // lane adds m = 16 nt values in [0, 1] in order, then the two lanes' sums are added: m additions
+    // on the longest chain, so the computed sum s' is within gamma_m s of the exact sum s of the values
+    // (recursive summation of nonnegative terms, gamma_m = m 2^-24 / (1 - m 2^-24)), and s <= s' + that,
+    // so |error| <= 1.25 m 2^-24 (s' + 1) for m 2^-24 < 0.1 (slack: 0.0007 for a random hypothesis at
+    // 2,000 points; it grows with the count, not with n^2: tight brackets at any n); an exact integer
+    // count (no value in the band) is unchanged by floor(+ slack) while slack < 1.
     // Zero-padded rows (ex = ey = W = 0) add exactly 1 to the upper count (K E + 1 >= 1) and 0 to the
     // lower one (-K E_lo < 0).
     const float k0 = keep0 + __shfl_xor(keep0, 32), k1 = keep1 + __shfl_xor(keep1, 32);
-    const double slack = 0x1p-24 * (double)(32 * nt) * (double)(32 * nt);
-    const int hi = min(n, max(0, (int)floor((double)(lowh ? k0 : k1) + slack) - (32 * nt - n)));
+    const double m2 = 0x1p-24 * 1.25 * (double)(16 * nt + 2);
+    const double kk = (double)(lowh ? k0 : k1);
+    const int hi = min(n, max(0, (int)floor(kk + m2 * (kk + 1.0)) - (32 * nt - n)));
     int lo = 0;
     if (kLo) {
         const float i0 = in0 + __shfl_xor(in0, 32), i1 = in1 + __shfl_xor(in1, 32);
-        lo = min(hi, max(0, (int)ceil((double)(lowh ? i0 : i1) - slack)));
+        const double ii = (double)(lowh ? i0 : i1);
+        lo = min(hi, max(0, (int)ceil(ii - m2 * (ii + 1.0))));
     }
     if (act) bounds[o] = invalid ? make_int2(-1, -1) : (uncertain ? make_int2(0, n) : make_int2(lo, hi));
 }
@@ -2898,6 +2918,7 @@ __global__ __launch_bounds__(64) void ransac_prescreen_kernel(const RansacState*
 // irrelevant (decided = 2, count 0: the replay's `count > best` test skips it) without the eigensolve.
 // Earlier candidates past the final niters only precede later ones that are past it as well.
 constexpr int kWinnerHMaxN = 256;
+constexpr int kDecidedForceH = 3;  // decided flag: for the exact pass, with runKernel even when lo == hi
 
 __global__ __launch_bounds__(64) void ransac_settle_kernel(const RansacState* __restrict__ st,
                                                            const ProbDev* __restrict__ probs,
@@ -2938,13 +2959,15 @@ __global__ __launch_bounds__(64) void ransac_settle_kernel(const RansacState* __
     if ((winner_h == 1 || (winner_h == 2 && S.n < kWinnerHMaxN)) && bar > max(S.max_good, 3)) {
         // the first listed decided candidate holding the largest decided count is the chunk's likely
         // bestModel: send it through the exact pass too (same count), so its fp64 H reaches best_h and
-        // the refine needs no runKernel of its own (MIM_WINNER_H=1; the count and the outcome are unchanged)
+        // the refine needs no runKernel of its own (MIM_WINNER_H=1; the count and the outcome are unchanged).
+        // decided = 3: undecided with its H forced, so a candidate the bound kernel pinned (lo == hi) runs
+        // runKernel in the exact pass instead of taking the tight shortcut (which stores no H)
         for (int base = 0; base < nl; base += 64) {
             const int k = base + lane;
             const bool hit = k < nl && decided[lb + k] == 1 && cex[lb + k] == bar;
             const unsigned long long m = __ballot(hit);
             if (m) {
-                if (lane == __builtin_ctzll(m)) decided[lb + k] = 0;
+                if (lane == __builtin_ctzll(m)) decided[lb + k] = kDecidedForceH;
                 break;
             }
         }
@@ -2956,7 +2979,8 @@ __device__ __forceinline__ int undecided_position(const int* __restrict__ decide
     const int lane = threadIdx.x & 63;
     int seen = 0;
     for (int base = 0; base < nl; base += 64) {
-        const bool u = base + lane < nl && decided[lb + base + lane] == 0;
+        const int dv = base + lane < nl ? decided[lb + base + lane] : 1;
+        const bool u = dv == 0 || dv == kDecidedForceH;
         const unsigned long long m = __ballot(u);
         const int c = __popcll(m);
         if (r < seen + c) {  // the (r - seen)-th set bit of m
@@ -3117,7 +3141,8 @@ __global__ __launch_bounds__(64, MIM_EXACT_OCC) void ransac_exact_kernel(const R
     const int t = cand[lb + k];
     const long long o = lb + k;
     const int2 bd = bounds[probs[p].it_off + t];
-    const bool tight = bd.x == bd.y;  // lo == hi pins the exact count: no eigensolve needed
+    // lo == hi pins the exact count: no eigensolve needed, unless the settle pass wants the H
+    const bool tight = bd.x == bd.y && !(prescreen && decided[o] == kDecidedForceH);
     double H[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
     int ok = 0;
     const float4* __restrict__ P = pts + probs[p].good_off;
@@ -3964,13 +3989,13 @@ void ransac_enqueue(const RansacParams& prm, int n_probs, const ProbDev* probs, 
                                    std::min(bppw_cap, (kSamplerMinBlocks + n_probs - 1) / n_probs)) + 7) / 8 * 8;
         // (MIM_ATTEMPT_REP_CAP < kAttemptRepCap: test knob forcing the in-place redraw resolution)
         const int rep_cap = prm.rep_cap > 0 ? std::min(prm.rep_cap, kAttemptRepCap) : kAttemptRepCap;
-        ransac_attempt_kernel<<<n_probs * bppw, 256, 0, ss>>>(b.state, b.stream, b.stream_len, b.flags, wcap, bppw, c1,
-                                                             rep_cap, n_probs);
+        ransac_attempt_kernel<<<n_probs * bppw, 256, 0, ss>>>(b.state, b.stream, b.stream_len, b.flags, b.irr_bits, wcap,
+                                                             bppw, c1, rep_cap, n_probs);
         mark(mark_ctx, "attempt", ss);
         if (use_chain) {
             ChainSegs* chains = reinterpret_cast<ChainSegs*>(b.chains);
             const int bpp_irr = (west + kIrrBlock - 1) / kIrrBlock;
-            ransac_irr_kernel<<<n_probs * bpp_irr, 256, 0, ss>>>(b.state, b.flags, wcap, bpp_irr, c1, b.irr,
+            ransac_irr_kernel<<<n_probs * bpp_irr, 256, 0, ss>>>(b.state, b.irr_bits, wcap, bpp_irr, c1, b.irr,
                                                                b.irr_cnt, b.irr_blocks);
             ransac_walk_kernel<<<n_probs, kWalkThreads, 0, ss>>>(b.state, b.flags, wcap, c1, b.irr, b.irr_cnt,
                                                                  b.irr_blocks, chains);
@@ -3988,7 +4013,7 @@ void ransac_enqueue(const RansacParams& prm, int n_probs, const ProbDev* probs, 
         ransac_small_kernel<<<n_probs, kSmallThreads, 0, ss>>>(b.state, probs, pts, b.stream, b.stream_len, b.samples,
                                                               c1, b.err);
         ransac_sample_kernel<<<n_probs, 64, 0, ss>>>(b.state, probs, pts, b.stream, b.stream_len, b.samples, c1, b.err,
-                                                    b.flags, wcap, use_chain);
+                                                    b.flags, b.irr_bits, wcap, use_chain);
         mark(mark_ctx, "sample", ss);
         if (split) {  // this chunk's selection waits for its samples; the next chunk's sampler does not
             (void)hipEventRecord(b.ev_samp[ci & 1], ss);
@@ -3997,6 +4022,7 @@ void ransac_enqueue(const RansacParams& prm, int n_probs, const ProbDev* probs, 
         }
         ++ci;
         const int bpp256 = (c1 - c0 + 255) / 256;
+        const int bppb = (c1 - c0 + kBoundThreads - 1) / kBoundThreads;
         if (exact_all) {  // reference mode: every hypothesis through runKernel + computeError
             const int bpp64 = (c1 - c0 + 63) / 64;
             ransac_hypo_kernel<<<n_probs * bpp64, 64, 0, s>>>(b.state, probs, pts, b.samples, b.stream, b.hyp, b.counts, c0, c1,
@@ -4018,11 +4044,11 @@ void ransac_enqueue(const RansacParams& prm, int n_probs, const ProbDev* probs, 
             }
         } else {
             if (c0 == 0)
-                ransac_bound_mfma_kernel<true><<<8 * ((n_probs + 7) / 8) * bpp256, 256, 0, s>>>(
-                    b.state, probs, pts, b.samples, b.stream, b.tiles, b.bounds, c0, c1, bpp256, thr2, n_probs);
+                ransac_bound_mfma_kernel<true><<<8 * ((n_probs + 7) / 8) * bppb, kBoundThreads, 0, s>>>(
+                    b.state, probs, pts, b.samples, b.stream, b.tiles, b.bounds, c0, c1, bppb, thr2, n_probs);
             else
-                ransac_bound_mfma_kernel<false><<<8 * ((n_probs + 7) / 8) * bpp256, 256, 0, s>>>(
-                    b.state, probs, pts, b.samples, b.stream, b.tiles, b.bounds, c0, c1, bpp256, thr2, n_probs);
+                ransac_bound_mfma_kernel<false><<<8 * ((n_probs + 7) / 8) * bppb, kBoundThreads, 0, s>>>(
+                    b.state, probs, pts, b.samples, b.stream, b.tiles, b.bounds, c0, c1, bppb, thr2, n_probs);
             mark(mark_ctx, "score", s);
             if (getenv("MIM_CHECK_BOUNDS")) {  // debug: every bracket against the exact count
                 unsigned long long* dst = nullptr;
@@ -4094,6 +4120,17 @@ void ransac_enqueue(const RansacParams& prm, int n_probs, const ProbDev* probs, 
         if (c0 == 0) c1_first = c1;
         c0 = c1;
         chunk = 1 << 30;  // one chunk after the first: every chunk costs a latency-bound exact pass
+    }
+    if (getenv("MIM_CHECK_BESTH")) {  // debug: problems whose bestModel the refine must recompute itself
+        std::vector<double> bh((size_t)n_probs * 9);
+        std::vector<RansacState> hs(n_probs);
+        (void)hipMemcpyAsync(bh.data(), b.best_h, sizeof(double) * bh.size(), hipMemcpyDeviceToHost, s);
+        (void)hipMemcpyAsync(hs.data(), b.state, sizeof(RansacState) * n_probs, hipMemcpyDeviceToHost, s);
+        (void)hipStreamSynchronize(s);
+        int with = 0, without = 0;
+        for (int i = 0; i < n_probs; ++i)
+            if (hs[i].active && hs[i].best_iter >= 0 && hs[i].n >= kSmallMaxN) (bh[9 * i + 8] != 0.0 ? with : without)++;
+        fprintf(stderr, "[mim] best_h: %d problems with the exact pass's fp64 bestModel, %d without\n", with, without);
     }
     ransac_refine_kernel<<<(n_probs + kRW - 1) / kRW, kRT, 0, s>>>(b.state, probs, pts, n_good, b.samples, b.stream, b.inl,
                                                                   masks, results, prm, raw, b.best_h, exact_all, n_probs);

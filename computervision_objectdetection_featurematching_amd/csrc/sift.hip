@@ -664,8 +664,16 @@ __device__ __forceinline__ int ctz64(unsigned long long m) { return __builtin_ct
 #ifndef MIM_DESCR_GRID
 #define MIM_DESCR_GRID 4096  // descriptor blocks of a batch launch (at least 1024 per image)
 #endif
-constexpr int kDescrT = 256, kDescrWords = kDescrT / 64;
+constexpr int kDescrT = 256;        // threads of a descriptor block: pixels per batch of a patch
+constexpr int kDescrTBig = 1024;    // the same for the large patches (4x fewer batches in the chain)
 constexpr int kDescrRowsMax = 512;
+// patch width W = 2 radius + 1 above which a keypoint's descriptor is computed by a kDescrTBig block: a
+// patch is ~W^2 / 2 pixels after the window compaction, one block's dependent chain of batches (pixel
+// loads, the sort's barriers) per kDescrT pixels, so the largest patches (W ~ 250, ~120 batches) set
+// the launch's length (~1 ms per scene, r06b) while most keypoints take a handful of batches
+#ifndef MIM_DESCR_BIG_W
+#define MIM_DESCR_BIG_W 64
+#endif
 
 // columns j of one patch row with a j + b in (-2.5, 2.5) (c_rot or r_rot of the window test, rbin /
 // cbin in (-1, kDW)), intersected into [lo, hi]: conservative (value margin 1e-3, one pixel each side)
@@ -682,7 +690,6 @@ __device__ __forceinline__ void window_cols(double a, double b, int& lo, int& hi
     lo = max(lo, (int)floor(j0));
     hi = min(hi, (int)ceil(j1));
 }
-static_assert(kHistLen <= 2 * kDescrT, "two bins per thread");
 struct DescB {
     const Pyr* pyr[kMaxImg];
     const mim_keypoint* kp[kMaxImg];
@@ -691,19 +698,26 @@ struct DescB {
     float* desc[kMaxImg];
 };
 
-__global__ __launch_bounds__(kDescrT) void descr_kernel(DescB A) {  // blockIdx.y = image
+// T threads per block (kDescrT or kDescrTBig); cls: which keypoints the launch describes by patch width W
+// (0: W <= MIM_DESCR_BIG_W, 1: W > MIM_DESCR_BIG_W, -1: all).  The result does not depend on T: a bin's
+// values are summed in pixel order across the batches whatever their size.
+template <int T>
+__global__ __launch_bounds__(T) void descr_kernel(DescB A, int cls) {  // blockIdx.y = image
+    constexpr int kWords = T / 64;                          // mask words per bin (one per wave)
+    constexpr int kBinsPer = (kHistLen + T - 1) / T;        // bins owned per thread
+    constexpr int kRowsPer = (kDescrRowsMax + T - 1) / T;   // compacted patch rows per thread
     const Pyr* __restrict__ pyr = A.pyr[blockIdx.y];
     const mim_keypoint* __restrict__ kp = A.kp[blockIdx.y];
     float* __restrict__ desc = A.desc[blockIdx.y];
     __shared__ float hist[kHistLen];
-    __shared__ unsigned long long bm[kHistLen][kDescrWords];  // per bin: the batch's pixels that hit it
-    __shared__ unsigned short pre[kHistLen][kDescrWords];      // per bin and word: pixels in earlier words
-    __shared__ int seg[kHistLen];                              // per bin: its segment of `sorted`
-    __shared__ int wsum[kDescrWords];
-    __shared__ float sorted[kDescrT * 8];                      // the batch's values grouped by bin
+    __shared__ unsigned long long bm[kHistLen][kWords];  // per bin: the batch's pixels that hit it
+    __shared__ unsigned short pre[kHistLen][kWords];      // per bin and word: pixels in earlier words
+    __shared__ int seg[kHistLen];                         // per bin: its segment of `sorted`
+    __shared__ int wsum[kWords];
+    __shared__ float sorted[T * 8];                       // the batch's values grouped by bin
     __shared__ int row_off[kDescrRowsMax + 1], row_lo[kDescrRowsMax];  // the compacted patch's rows
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    for (int e = tid; e < kHistLen * kDescrWords; e += kDescrT) (&bm[0][0])[e] = 0ull;
+    for (int e = tid; e < kHistLen * kWords; e += T) (&bm[0][0])[e] = 0ull;
     __syncthreads();
   const int n = min(*A.n[blockIdx.y], A.n_cap[blockIdx.y]);
   for (int t = blockIdx.x; t < n; t += gridDim.x) {  // fixed grid, block-uniform loop
@@ -727,13 +741,15 @@ __global__ __launch_bounds__(kDescrT) void descr_kernel(DescB A) {  // blockIdx.
     cos_t /= hist_width;
     sin_t /= hist_width;
     const int W = 2 * radius + 1;
+    if (cls >= 0 && (W > MIM_DESCR_BIG_W) != (cls == 1)) continue;  // the other launch's keypoint (block-uniform)
     const bool compact = W <= kDescrRowsMax;
     int P = W * W;
     if (compact) {  // per row: the first column and the count of the conservative range, then offsets
-        int len[2] = {0, 0};
+        int len[kRowsPer];
 #pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            const int rr = 2 * tid + k;
+        for (int k = 0; k < kRowsPer; ++k) {
+            len[k] = 0;
+            const int rr = kRowsPer * tid + k;
             if (rr < W) {
                 const int i = rr - radius, r = py + i;
                 int lo = max(-radius, 1 - px), hi = min(radius, im.cols - 2 - px);
@@ -744,7 +760,9 @@ __global__ __launch_bounds__(kDescrT) void descr_kernel(DescB A) {  // blockIdx.
                 row_lo[rr] = lo;
             }
         }
-        const int mine = len[0] + len[1];
+        int mine = 0;
+#pragma unroll
+        for (int k = 0; k < kRowsPer; ++k) mine += len[k];
         int incl = mine;
 #pragma unroll
         for (int d = 1; d < 64; d <<= 1) {
@@ -755,16 +773,19 @@ __global__ __launch_bounds__(kDescrT) void descr_kernel(DescB A) {  // blockIdx.
         __syncthreads();
         int excl = incl - mine;
 #pragma unroll
-        for (int w = 0; w < kDescrWords; ++w) excl += w < wv ? wsum[w] : 0;
-        if (2 * tid < W) row_off[2 * tid] = excl;
-        if (2 * tid + 1 < W) row_off[2 * tid + 1] = excl + len[0];
-        if (tid == kDescrT - 1) row_off[W] = excl + mine;  // the last thread's inclusive sum: the total
+        for (int w = 0; w < kWords; ++w) excl += w < wv ? wsum[w] : 0;
+#pragma unroll
+        for (int k = 0, o = excl; k < kRowsPer; o += len[k], ++k)
+            if (kRowsPer * tid + k < W) row_off[kRowsPer * tid + k] = o;
+        if (tid == T - 1) row_off[W] = excl + mine;  // the last thread's inclusive sum: the total
         __syncthreads();
         P = row_off[W];
         __syncthreads();  // wsum reused by the batches' scans
     }
-    float h0 = 0.f, h1 = 0.f;  // bins tid, tid + 256
-    for (int base = 0; base < P; base += kDescrT) {
+    float hb[kBinsPer];  // bins tid + T s2
+#pragma unroll
+    for (int s2 = 0; s2 < kBinsPer; ++s2) hb[s2] = 0.f;
+    for (int base = 0; base < P; base += T) {
         // ---- A: pixel base + tid ----
         int idx = -1;
         float vals[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -816,7 +837,7 @@ __global__ __launch_bounds__(kDescrT) void descr_kernel(DescB A) {  // blockIdx.
             }
         }
 #if MIM_PROBE_DESCR == 2  // timing probe only: phase A alone
-        h0 += vals[0] + vals[1] + vals[2] + vals[3] + vals[4] + vals[5] + vals[6] + vals[7] + (float)idx;
+        hb[0] += vals[0] + vals[1] + vals[2] + vals[3] + vals[4] + vals[5] + vals[6] + vals[7] + (float)idx;
         continue;
 #endif
         // ---- B: stable counting sort of the batch's contributions by bin, then sequential sums ----
@@ -829,14 +850,15 @@ __global__ __launch_bounds__(kDescrT) void descr_kernel(DescB A) {  // blockIdx.
         }
         __syncthreads();
         // owned bins: per mask word the count of earlier pixels, and the bin's total
-        int tot[2] = {0, 0};
+        int tot[kBinsPer];
 #pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-            const int bin = tid + kDescrT * s2;
+        for (int s2 = 0; s2 < kBinsPer; ++s2) {
+            tot[s2] = 0;
+            const int bin = tid + T * s2;
             if (bin < kHistLen) {
                 int run = 0;
 #pragma unroll
-                for (int w = 0; w < kDescrWords; ++w) {
+                for (int w = 0; w < kWords; ++w) {
                     pre[bin][w] = (unsigned short)run;
                     run += __popcll(bm[bin][w]);
                 }
@@ -844,7 +866,9 @@ __global__ __launch_bounds__(kDescrT) void descr_kernel(DescB A) {  // blockIdx.
             }
         }
         // segment starts: exclusive scan of the owners' totals over the block
-        const int mine = tot[0] + tot[1];
+        int mine = 0;
+#pragma unroll
+        for (int s2 = 0; s2 < kBinsPer; ++s2) mine += tot[s2];
         int incl = mine;
 #pragma unroll
         for (int d = 1; d < 64; d <<= 1) {
@@ -855,9 +879,13 @@ __global__ __launch_bounds__(kDescrT) void descr_kernel(DescB A) {  // blockIdx.
         __syncthreads();
         int excl = incl - mine;
 #pragma unroll
-        for (int w = 0; w < kDescrWords; ++w) excl += w < wv ? wsum[w] : 0;
-        if (tid < kHistLen) seg[tid] = excl;
-        if (tid + kDescrT < kHistLen) seg[tid + kDescrT] = excl + tot[0];
+        for (int w = 0; w < kWords; ++w) excl += w < wv ? wsum[w] : 0;
+        int st0[kBinsPer];  // the owned bins' segment starts (bins tid + T s2 are consecutive in `sorted`)
+#pragma unroll
+        for (int s2 = 0, o = excl; s2 < kBinsPer; o += tot[s2], ++s2) {
+            st0[s2] = o;
+            if (tid + T * s2 < kHistLen) seg[tid + T * s2] = o;
+        }
         __syncthreads();
         // scatter: the pixel's value for bin b goes to b's segment at its rank among the batch's pixels
         // hitting b (the earlier pixels of its own mask word and the words before)
@@ -872,22 +900,22 @@ __global__ __launch_bounds__(kDescrT) void descr_kernel(DescB A) {  // blockIdx.
         __syncthreads();
         // owners: the bin's values in pixel order (independent LDS reads, one add chain)
 #pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-            const int bin = tid + kDescrT * s2;
+        for (int s2 = 0; s2 < kBinsPer; ++s2) {
+            const int bin = tid + T * s2;
             if (bin < kHistLen) {
-                const int st0 = s2 ? excl + tot[0] : excl;
-                float acc = s2 ? h1 : h0;
+                float acc = hb[s2];
 #pragma unroll 4
-                for (int i = 0; i < tot[s2]; ++i) acc += sorted[st0 + i];
-                if (s2) h1 = acc; else h0 = acc;
+                for (int i = 0; i < tot[s2]; ++i) acc += sorted[st0[s2] + i];
+                hb[s2] = acc;
 #pragma unroll
-                for (int w = 0; w < kDescrWords; ++w) bm[bin][w] = 0ull;  // cleared for the next batch
+                for (int w = 0; w < kWords; ++w) bm[bin][w] = 0ull;  // cleared for the next batch
             }
         }
         __syncthreads();
     }
-    hist[tid] = h0;
-    if (tid + kDescrT < kHistLen) hist[tid + kDescrT] = h1;
+#pragma unroll
+    for (int s2 = 0; s2 < kBinsPer; ++s2)
+        if (tid + T * s2 < kHistLen) hist[tid + T * s2] = hb[s2];
     __syncthreads();
     // the orientation wrap (cells independent: one thread each)
     if (tid < kDW * kDW) {
@@ -1310,7 +1338,7 @@ static int sift_describe_host(SiftJob& J, hipStream_t st, std::string& err) {
     D.n[0] = J.d_cnt + 3;
     D.n_cap[0] = n;
     D.desc[0] = (float*)J.w->desc;
-    descr_kernel<<<dim3(4096, 1), kDescrT, 0, st>>>(D);
+    descr_kernel<kDescrT><<<dim3(4096, 1), kDescrT, 0, st>>>(D, -1);
     SCHK(hipGetLastError());
     SCHK(hipStreamSynchronize(st));  // `n` and `k` are host locals of this call
     return 0;
@@ -1522,10 +1550,12 @@ static int sift_batch(std::vector<SiftJob>& jobs, SiftWs* bw, hipStream_t st, st
             D1.n[0] = Ds.n[k];
             D1.n_cap[0] = Ds.n_cap[k];
             D1.desc[0] = Ds.desc[k];
-            descr_kernel<<<dim3(MIM_DESCR_GRID, 1), kDescrT, 0, st>>>(D1);
+            descr_kernel<kDescrT><<<dim3(MIM_DESCR_GRID, 1), kDescrT, 0, st>>>(D1, -1);
         }
 #else
-        descr_kernel<<<dim3(std::max(MIM_DESCR_GRID / nl, 1024), nl), kDescrT, 0, st>>>(Ds);
+        // the large patches first, by 1024-thread blocks (few keypoints: a small grid), then the rest
+        descr_kernel<kDescrTBig><<<dim3(64, nl), kDescrTBig, 0, st>>>(Ds, 1);
+        descr_kernel<kDescrT><<<dim3(std::max(MIM_DESCR_GRID / nl, 1024), nl), kDescrT, 0, st>>>(Ds, 0);
 #endif
         SCHK(hipGetLastError());
     }
@@ -1672,6 +1702,45 @@ int sift_scales_device(std::vector<SiftWs*>& ws, hipStream_t st, const uint8_t* 
     if (int r = sift_batch(jobs, ws[n_scales], st, err)) return r;
     for (int i = 0; i < n_scales; ++i) out[i] = SiftDevOut{jobs[i].out_kp, (const float*)jobs[i].w->desc, jobs[i].n};
     return 0;
+}
+
+// The scales' rows and keypoint positions copied into their sets' storage in one launch (was two copies
+// per scale, each a blit launch and ~30 us of host enqueue): thread e copies float4 e % 32 of row e / 32
+// of the scale holding it, and the row's KeyPoint::pt with its first float4
+struct SetCopyB {
+    const float* desc[kMaxImg];
+    const mim_keypoint* kp[kMaxImg];
+    float* ddesc[kMaxImg];
+    float2* dkp[kMaxImg];
+    long long off[kMaxImg + 1];  // first float4 of each scale
+    int m;
+};
+
+__global__ __launch_bounds__(256) void set_copy_kernel(SetCopyB A) {
+    for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < A.off[A.m]; e += (long long)gridDim.x * 256) {
+        int j = 0;
+        while (j + 1 < A.m && A.off[j + 1] <= e) ++j;
+        const long long v = e - A.off[j], row = v >> 5;
+        reinterpret_cast<float4*>(A.ddesc[j])[v] = reinterpret_cast<const float4*>(A.desc[j])[v];
+        if ((v & 31) == 0) A.dkp[j][row] = make_float2(A.kp[j][row].x, A.kp[j][row].y);
+    }
+}
+
+int sift_copy_sets(const SiftDevOut* out, int n, float* const* ddesc, float2* const* dkp, hipStream_t st) {
+    if (n <= 0 || n > kMaxImg) return n == 0 ? 0 : -3;
+    SetCopyB A{};
+    A.m = n;
+    for (int j = 0; j < n; ++j) {
+        A.desc[j] = out[j].desc;
+        A.kp[j] = out[j].kp;
+        A.ddesc[j] = ddesc[j];
+        A.dkp[j] = dkp[j];
+        A.off[j + 1] = A.off[j] + (long long)out[j].n * (kDim / 4);
+    }
+    if (A.off[n] == 0) return 0;
+    const long long nb = std::min<long long>((A.off[n] + 255) / 256, 4096);
+    set_copy_kernel<<<(int)nb, 256, 0, st>>>(A);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 int sift_resize_u8(SiftWs* w, hipStream_t st, const uint8_t* src, int rows, int cols, long long step, uint8_t* dst,

@@ -409,11 +409,18 @@ class Matcher:
             raise ValueError(f"batch_inlier_points: {sc.shape} scales for {n} problems")
         scp = None if sc is None else sc.ctypes.data_as(C.POINTER(C.c_float))
         op = offs.ctypes.data_as(C.POINTER(C.c_int64))
-        self._check(self.L.mim_batch_inlier_points(self._ctx, scp, None, 0, op))
-        pts = np.zeros((max(int(offs[n]), 1), 2), np.float32)
-        self._check(self.L.mim_batch_inlier_points(self._ctx, scp, pts.ctypes.data_as(C.POINTER(C.c_float)),
-                                                   int(offs[n]), op))
-        return offs, pts[:int(offs[n])]
+        # one call into a kept buffer (one wait, one gather); a larger total comes back as MIM_ERANGE with
+        # the offsets set, and the call is made again with room for all
+        buf = getattr(self, "_inl_buf", None)
+        if buf is None:
+            buf = self._inl_buf = np.zeros((1 << 16, 2), np.float32)
+        st = self.L.mim_batch_inlier_points(self._ctx, scp, buf.ctypes.data_as(C.POINTER(C.c_float)), buf.shape[0], op)
+        total = int(offs[n])
+        if st == _lib.MIM_ERANGE and total > buf.shape[0]:
+            buf = self._inl_buf = np.zeros((2 * total, 2), np.float32)
+            st = self.L.mim_batch_inlier_points(self._ctx, scp, buf.ctypes.data_as(C.POINTER(C.c_float)), buf.shape[0], op)
+        self._check(st)
+        return offs, buf[:total].copy()
 
     def match_batch(self, problems, params: Params | None = None) -> np.ndarray:
         n = self.match_batch_async(problems, params)

@@ -388,6 +388,70 @@ def test_bound_brackets_exact_counts(capfd):
         assert (lo_v, hi_v, vm) == ("0", "0", "0"), err + cap.out
 
 
+def test_bound_brackets_tight_at_large_n(capfd):
+    """Thousands of good matches (n ~ 7,000): the bound kernel's float counts are summed over 32 nt
+    values, and a rounding slack that grew with n^2 (round 5: 2.9 counts here) would leave no bracket
+    tight (lo == hi) in chunk 1, sending every candidate to the prescreen or the eigensolve.  The slack
+    now follows the count itself: the brackets still hold every exact count, and most of chunk 1's are
+    tight."""
+    import os
+    import re
+    from computervision_objectdetection_featurematching_amd import Matcher, default_params
+    ds = make_dataset(1, 1, 8000, 9000, 7000, inlier_frac=0.08, seed=123)
+    os.environ["MIM_CHECK_BOUNDS"] = "1"
+    m = Matcher(0)
+    try:
+        q = m.add_set(ds.model_desc[0], ds.model_kp[0])
+        t = m.add_set(ds.scene_desc[0], ds.scene_kp[0])
+        res = m.match_batch([(q, t)], default_params(max_iters=1500))
+    finally:
+        m.close()
+        os.environ.pop("MIM_CHECK_BOUNDS", None)
+    assert int(res[0]["n_good"]) > 4096
+    err = capfd.readouterr().err
+    lines = re.findall(r"chunk \[(\d+),\d+\): checked (\d+) lo_viol (\d+) hi_viol (\d+) valid_mismatch (\d+) "
+                       r"mean_width \S+ tight (\d+)", err)
+    assert lines, err
+    for c0, c, lo_v, hi_v, vm, tight in lines:
+        assert (lo_v, hi_v, vm) == ("0", "0", "0"), err
+        if c0 == "0":
+            assert int(tight) > 0.1 * int(c), err  # ~20 % at n ~ 7,000 (points between the two diamonds); 0 before
+
+
+def test_winner_h_reaches_refine(capfd):
+    """MIM_WINNER_H=1: the settle pass sends each chunk's largest decided candidate through the exact
+    pass, so the refine starts from that candidate's fp64 H.  A candidate the bound kernel pinned
+    (lo == hi) used to take the exact kernel's shortcut, which stores no H; it is now
+    flagged to run runKernel.  Every problem of the bound path reaches the refine with its bestModel
+    (MIM_CHECK_BESTH report), and the records equal MIM_WINNER_H=0's."""
+    import os
+    import re
+    from computervision_objectdetection_featurematching_amd import Matcher, default_params
+    ds = make_dataset(2, 4, 1200, 2000, 400, inlier_frac=0.1, seed=31337)
+    out = {}
+    os.environ["MIM_CHECK_BESTH"] = "1"
+    try:
+        for wh in ("0", "1"):
+            os.environ["MIM_WINNER_H"] = wh
+            m = Matcher(0)
+            try:
+                q = [m.add_set(d, k) for d, k in zip(ds.model_desc, ds.model_kp)]
+                t = [m.add_set(d, k) for d, k in zip(ds.scene_desc, ds.scene_kp)]
+                res = m.match_batch([(q[a], t[b]) for a, b in ds.problems], default_params(max_iters=20000))
+            finally:
+                m.close()
+            err = capfd.readouterr().err
+            rep = re.findall(r"best_h: (\d+) problems with the exact pass's fp64 bestModel, (\d+) without", err)
+            assert rep, err
+            out[wh] = (res.tobytes(), rep[-1])
+    finally:
+        os.environ.pop("MIM_CHECK_BESTH", None)
+        os.environ.pop("MIM_WINNER_H", None)
+    assert out["0"][0] == out["1"][0]
+    with_h, without = map(int, out["1"][1])
+    assert with_h > 0 and without == 0, out
+
+
 @pytest.mark.parametrize("mode", ["0", "1"])
 def test_sampler_stream_identical(mode):
     """The next chunk's getSubset replay on its own stream (MIM_SAMPLER_STREAM=1, concurrent with

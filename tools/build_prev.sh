@@ -7,7 +7,7 @@ set -e
 REV=${1:-HEAD}
 OUT=${2:-variants/libmim_prev.so}
 shift $(( $# > 2 ? 2 : $# ))
-FILES=${*:-"knn.hip ransac.hip sift.hip api.cpp mim_internal.h mim_debug.h"}
+FILES=${*:-"knn.hip ransac.hip sift.hip api.cpp group.cpp mim_internal.h mim_debug.h"}
 D=computervision_objectdetection_featurematching_amd
 TMP=$D/csrc_variant
 rm -rf $TMP && cp -r $D/csrc $TMP && mkdir -p "$(dirname "$OUT")"
@@ -23,7 +23,7 @@ for f in B.SOURCES:
     o = os.path.join(od, f + '.o')
     subprocess.check_call([B.HIPCC, *B.FLAGS, *B.SRC_FLAGS.get(f, []), '-c', f'{src}/{f}', '-o', o], stderr=subprocess.DEVNULL)
     objs.append(o)
-subprocess.check_call([B.HIPCC, '--offload-arch=gfx950', '-shared', '-fPIC', '-o', out, *objs])
+subprocess.check_call([B.HIPCC, '--offload-arch=gfx950', '-shared', '-fPIC', '-o', out, *objs, '-L/opt/rocm/lib', '-lrccl', '-Wl,-rpath,/opt/rocm/lib'])
 PY
 rm -rf $TMP
 echo "$OUT"

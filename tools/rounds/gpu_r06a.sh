@@ -31,4 +31,5 @@ GRBM_GUI_ACTIVE SQ_VALU_MFMA_COEXEC_CYCLES SQ_INST_LEVEL_VMEM SQ_ACTIVE_INST_FLA
 PASSES
 python3 tools/pmc_summary.py $O/pmc > $O/pmc_summary.txt
 timeout -k 10 300 python3 -u -m pytest tests/test_group.py -m gpu -x -v --timeout 240 --timeout-method thread > $O/pytest_group.log 2>&1 || echo "group test failed"
+timeout -k 10 600 python3 -u -m pytest tests/test_ransac_gpu.py tests/test_small_sampler_gpu.py -m gpu -x -v --timeout 240 --timeout-method thread > $O/pytest_ransac.log 2>&1 || echo "ransac tests failed"
 echo done

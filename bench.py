@@ -416,12 +416,13 @@ def run_c1img(args, rank, world, local):
     # alone on one context, no keypoints copied out, no per-kernel events; median of the calls
     m.set_sampler_stream(True)
     m.set_timing(False)
-    lat = []
+    lat, stages = [], {}
     for _ in range(max(args.iso_steps, 5)):
         t1 = time.perf_counter()
-        detect_objects(m, scene, [model])
+        detect_objects(m, scene, [model], stage_ms=stages)
         lat.append(time.perf_counter() - t1)
     scene_ms = 1e3 * statistics.median(lat)
+    stages = {k: round(v / len(lat), 3) for k, v in stages.items()}
     # isolated pass (not part of `value`): one scene at a time on one context, kernel timing on — the
     # kernel breakdown and the distance kernel's launch duration
     m.set_timing(True)
@@ -459,6 +460,7 @@ def run_c1img(args, rank, world, local):
                "single_scene_ms": round(scene_ms, 3),
                "single_scene_ms_range": [round(1e3 * min(lat), 3), round(1e3 * max(lat), 3)],
                "single_scene_ms_with_kernel_events": round(scene_ms_events, 3),
+               "single_scene_stage_ms": stages,
                "roofline": {"kernel": "knn2_i8_kernel (145 ragged problems of one scene, 1 launch per scene)",
                             "bound": "mfma", "unit": "TFLOP/s", "peak": PEAK_I8_TOPS,
                             "achieved": round(knn_ops / (iso["knn"] * 1e-3) / 1e12, 2),

@@ -665,14 +665,18 @@ __device__ __forceinline__ int ctz64(unsigned long long m) { return __builtin_ct
 #define MIM_DESCR_GRID 4096  // descriptor blocks of a batch launch (at least 1024 per image)
 #endif
 constexpr int kDescrT = 256;        // threads of a descriptor block: pixels per batch of a patch
-constexpr int kDescrTBig = 1024;    // the same for the large patches (4x fewer batches in the chain)
+constexpr int kDescrTBig = 1024;    // MIM_DESCR_BIG_SPLIT: the large patches by 1024-thread blocks
 constexpr int kDescrRowsMax = 512;
-// patch width W = 2 radius + 1 above which a keypoint's descriptor is computed by a kDescrTBig block: a
-// patch is ~W^2 / 2 pixels after the window compaction, one block's dependent chain of batches (pixel
-// loads, the sort's barriers) per kDescrT pixels, so the largest patches (W ~ 250, ~120 batches) set
-// the launch's length (~1 ms per scene, r06b) while most keypoints take a handful of batches
+// MIM_DESCR_BIG_SPLIT (off; measured slower, r06c): patches wider than MIM_DESCR_BIG_W described by
+// kDescrTBig blocks in a launch of their own (4x fewer batches in their chains).  The launch is bound by
+// the blocks resident per CU (4 at 108 VGPRs) times each block's chain of batches, so the split only
+// lengthened it; a software prefetch of the next batch's gradient loads and a 5-block register cap were
+// even (r06d)
 #ifndef MIM_DESCR_BIG_W
 #define MIM_DESCR_BIG_W 64
+#endif
+#ifndef MIM_DESCR_BIG_SPLIT
+#define MIM_DESCR_BIG_SPLIT 0
 #endif
 
 // columns j of one patch row with a j + b in (-2.5, 2.5) (c_rot or r_rot of the window test, rbin /
@@ -1553,9 +1557,12 @@ static int sift_batch(std::vector<SiftJob>& jobs, SiftWs* bw, hipStream_t st, st
             descr_kernel<kDescrT><<<dim3(MIM_DESCR_GRID, 1), kDescrT, 0, st>>>(D1, -1);
         }
 #else
-        // the large patches first, by 1024-thread blocks (few keypoints: a small grid), then the rest
+#if MIM_DESCR_BIG_SPLIT  // measured slower (r06c: 1.42 + 0.76 ms against 0.99 ms for one launch per scene)
         descr_kernel<kDescrTBig><<<dim3(64, nl), kDescrTBig, 0, st>>>(Ds, 1);
         descr_kernel<kDescrT><<<dim3(std::max(MIM_DESCR_GRID / nl, 1024), nl), kDescrT, 0, st>>>(Ds, 0);
+#else
+        descr_kernel<kDescrT><<<dim3(std::max(MIM_DESCR_GRID / nl, 1024), nl), kDescrT, 0, st>>>(Ds, -1);
+#endif
 #endif
         SCHK(hipGetLastError());
     }

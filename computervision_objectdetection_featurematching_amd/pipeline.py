@@ -121,19 +121,34 @@ class SceneRun:
 
 
 def detect_objects(matcher: Matcher, scene_gray, models: list[ObjectModel], scales=SCALES, params=None,
-                   box_params: BoxParams | None = None, keep: bool = False, keep_descriptors: bool = False):
+                   box_params: BoxParams | None = None, keep: bool = False, keep_descriptors: bool = False,
+                   stage_ms: dict | None = None):
     """detectObjects(scene, models, detector) (TestsDetector.cpp:32-251) on a grayscale scene.
 
     Returns [((x, y, w, h), name)], or the SceneRun when keep=True (its scene_desc only with
     keep_descriptors: the scene's descriptors never leave the device on the detection path; for the
-    caller they are copied out of the very sets the batch matched against, mim_set_rows)."""
+    caller they are copied out of the very sets the batch matched against, mim_set_rows).
+    stage_ms (diagnostic): host wall time of each stage added to it (ms): "sift" (resize + SIFT of every
+    scale, sets registered), "match" (the batch enqueued and its records), "gather" (inlier points),
+    "boxes"; each stage waits for the device work it needs, so together they are the call's latency."""
+    import time as _time
+    t_last = [_time.perf_counter()]
+
+    def _mark(name):
+        if stage_ms is not None:
+            t = _time.perf_counter()
+            stage_ms[name] = stage_ms.get(name, 0.0) + 1e3 * (t - t_last[0])
+            t_last[0] = t
+
     params = params or default_params()
     view_ids = _model_sets(matcher, models)
     # :99-107, all scales in one call, the scene's descriptors registered as sets on the device
     scene_ids, _, scene_kp = matcher.sift_scales_to_sets(scene_gray, scales, keypoints=keep)
     scene_desc = [matcher.set_rows(i)[0] for i in scene_ids] if keep_descriptors else None
+    _mark("sift")
     tags = [(mi, si, vi) for mi in range(len(models)) for si in range(len(scales)) for vi in range(len(view_ids[mi]))]
     res = matcher.match_batch([(view_ids[mi][vi], scene_ids[si]) for mi, si, vi in tags], params)
+    _mark("match")
     # :87-94 inlier scene points of the accepted problems (:74, :79, :81, :84), /scale when scale != 1,
     # gathered on the device in batch order; a model's problems are contiguous (model-major tags)
     offs, allpts = matcher.batch_inlier_points(len(tags), np.array([scales[si] for _, si, _ in tags], np.float32))
@@ -142,9 +157,11 @@ def detect_objects(matcher: Matcher, scene_gray, models: list[ObjectModel], scal
         i1 = i0 + len(scales) * len(view_ids[mi])
         points.append(allpts[offs[i0]:offs[i1]].copy())
         i0 = i1
+    _mark("gather")
     dets = []
     for mi, m in enumerate(models):  # :111-248, model order
         dets += [(b, m.name) for b in detect_boxes(points[mi], box_params)]
+    _mark("boxes")
     if keep:
         return SceneRun(scene_kp, scene_desc, res, points, dets)
     return dets

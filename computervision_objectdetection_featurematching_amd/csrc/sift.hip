@@ -29,8 +29,11 @@
 #include <limits.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <cmath>
 #include <cstdlib>
+#include <cstring>
 #include <string>
 #include <vector>
 
@@ -180,6 +183,8 @@ struct BlurB {
     Flat f;
     const float* src[kMaxImg];
     float* dst[kMaxImg];
+    float* dog[kMaxImg];       // dst - src (the DoG plane of layers src, dst), or null: fused so the
+                               // large octaves need no separate DoG pass over two Gaussian planes
     int rows[kMaxImg], cols[kMaxImg];
 };
 
@@ -190,6 +195,7 @@ __global__ __launch_bounds__(256) void blur_kernel(BlurB A, Taps t) {
     const int j = flat_job(A.f, blockIdx.x, bx, by);
     const float* __restrict__ src = A.src[j];
     float* __restrict__ dst = A.dst[j];
+    float* __restrict__ dog = A.dog[j];
     const int rows = A.rows[j], cols = A.cols[j];
     const int a = t.n / 2, W = kBlurTW + 2 * a, H = kBlurTH + 2 * a;
     float* in = lds;             // H x W
@@ -229,6 +235,95 @@ __global__ __launch_bounds__(256) void blur_kernel(BlurB A, Taps t) {
         float acc = tk[a] * M[0] + 0.f;
         for (int i = 1; i <= a; ++i) acc += tk[a + i] * (M[i * kBlurTW] + M[-i * kBlurTW]);
         dst[(size_t)y * cols + x] = acc;
+        if (dog) dog[(size_t)y * cols + x] = acc - in[(r + a) * W + c + a];
+    }
+}
+
+// blur_kernel with the half-width A a compile-time constant (the SIFT taps are fixed: A = 5, 5, 6, 8, 10,
+// 13), register-blocked.  The taps are kernel-argument SGPRs (the unrolled loops index them by
+// constants), the row pass computes 4 adjacent outputs per work item from one window read as float4s
+// (4 + 2A LDS values for 4 outputs instead of 2 (2A + 1) per output: source and tap), and the column pass
+// one column strip of kColR outputs per thread from kColR + 2A values held in registers.  The float
+// operations and their order per output are blur_kernel's (row: k0 s0 + k1 s1 + ...; column: k_A m +
+// sum of k_{A+i} (m_+i + m_-i)), so the planes are identical.  Tile kBlurTW x TH.
+#ifndef MIM_BLUR_TH
+#define MIM_BLUR_TH 32
+#endif
+template <int A, int TH>
+__global__ __launch_bounds__(256) void blur_reg_kernel(BlurB B, Taps t) {
+    constexpr int N = 2 * A + 1, H = TH + 2 * A;
+    constexpr int WS = (kBlurTW + 2 * A + 3) / 4 * 4 + 4;  // in row stride: float4-aligned, 4 floats of slack
+    constexpr int kColR = TH / 4;                           // output rows per thread in the column pass
+    constexpr int kWin = (4 + 2 * A + 3) / 4;               // float4s of a row-pass window
+    __shared__ __attribute__((aligned(16))) float in[H * WS];
+    __shared__ __attribute__((aligned(16))) float mid[H * kBlurTW];
+    int bx, by;
+    const int j = flat_job(B.f, blockIdx.x, bx, by);
+    const float* __restrict__ src = B.src[j];
+    float* __restrict__ dst = B.dst[j];
+    float* __restrict__ dog = B.dog[j];
+    const int rows = B.rows[j], cols = B.cols[j];
+    const int x0 = bx * kBlurTW, y0 = by * TH, tid = threadIdx.x;
+    constexpr int W = kBlurTW + 2 * A, NE = H * W;
+    for (int e0 = tid; e0 < NE; e0 += 256 * 8) {
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int e = e0 + 256 * u;
+            if (e < NE) {
+                const int r = e / W, c = e - r * W;
+                v[u] = src[(size_t)reflect101(y0 - A + r, rows) * cols + reflect101(x0 - A + c, cols)];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int e = e0 + 256 * u;
+            if (e < NE) {
+                const int r = e / W, c = e - r * W;
+                in[r * WS + c] = v[u];
+            }
+        }
+    }
+    __syncthreads();
+    // row pass: item = (row r of H, group g of 4 output columns)
+    for (int item = tid; item < H * (kBlurTW / 4); item += 256) {
+        const int r = item >> 4, g = item & 15;
+        float w[4 * kWin];
+        const float4* S = (const float4*)(in + r * WS + 4 * g);
+#pragma unroll
+        for (int q = 0; q < kWin; ++q) {
+            const float4 f = S[q];
+            w[4 * q] = f.x;
+            w[4 * q + 1] = f.y;
+            w[4 * q + 2] = f.z;
+            w[4 * q + 3] = f.w;
+        }
+        float o[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            float acc = t.k[0] * w[c];
+#pragma unroll
+            for (int i = 1; i < N; ++i) acc += t.k[i] * w[c + i];
+            o[c] = acc;
+        }
+        *(float4*)(mid + r * kBlurTW + 4 * g) = make_float4(o[0], o[1], o[2], o[3]);
+    }
+    __syncthreads();
+    // column pass: column c, rows r0 .. r0 + kColR - 1 of the tile
+    const int c = tid & 63, r0 = (tid >> 6) * kColR, x = x0 + c;
+    float m[kColR + 2 * A];
+#pragma unroll
+    for (int i = 0; i < kColR + 2 * A; ++i) m[i] = mid[(r0 + i) * kBlurTW + c];
+#pragma unroll
+    for (int q = 0; q < kColR; ++q) {
+        const int y = y0 + r0 + q;
+        float acc = t.k[A] * m[q + A] + 0.f;
+#pragma unroll
+        for (int i = 1; i <= A; ++i) acc += t.k[A + i] * (m[q + A + i] + m[q + A - i]);
+        if (y < rows && x < cols) {
+            dst[(size_t)y * cols + x] = acc;
+            if (dog) dog[(size_t)y * cols + x] = acc - in[(r0 + q + A) * WS + c + A];
+        }
     }
 }
 
@@ -341,23 +436,6 @@ __global__ void down2_kernel(DownB A) {
 }
 
 // the 5 DoG layers of one octave (blockIdx.y = layer): dog[i] = gauss[i + 1] - gauss[i]
-struct DogB {
-    Flat f;
-    const float* g[kMaxImg];
-    float* d[kMaxImg];
-    long long plane[kMaxImg];
-};
-
-__global__ void dog_kernel(DogB A) {
-    int bx, by;
-    const int j = flat_job(A.f, blockIdx.x, bx, by);
-    const size_t plane = (size_t)A.plane[j];
-    const size_t p = (size_t)bx * blockDim.x + threadIdx.x;
-    const int i = blockIdx.y;
-    if (p >= plane) return;
-    A.d[j][i * plane + p] = A.g[j][(i + 1) * plane + p] - A.g[j][i * plane + p];
-}
-
 struct Cand {
     int o, layer, r, c;
 };
@@ -373,38 +451,73 @@ struct ExtB {
     int octave, threshold, cap;
 };
 
-__global__ void extrema_kernel(ExtB A) {
+// One block per kExtTW x kExtTH tile of one layer: the tile of the three DoG planes (one-pixel halo) staged
+// in LDS with coalesced loads, the 26-neighbour test per pixel from LDS, the block's extrema gathered in an
+// LDS list and appended with ONE global atomic per block.  Round 5's one-thread-per-pixel form (26 global
+// loads per pixel over the threshold, one returning atomic per wave with an extremum on the single
+// counter) took 259 us on octave 0 of a 640x480 scene (profiles/r06d_c1img_timeline_rank.txt).
+constexpr int kExtTW = 64, kExtTH = 16, kExtW = kExtTW + 2, kExtH = kExtTH + 2;
+
+__global__ __launch_bounds__(256) void extrema_kernel(ExtB A) {
+    __shared__ float t[3][kExtH][kExtW];
+    __shared__ Cand list[kExtTW * kExtTH];
+    __shared__ int n_list, base;
     int bx, by;
     const int j = flat_job(A.f, blockIdx.x, bx, by);
     const float* __restrict__ dog = A.dog[j];
     const int rows = A.rows[j], cols = A.cols[j], octave = A.octave, threshold = A.threshold, cap = A.cap;
-    Cand* __restrict__ cand = A.cand[j];
-    int* __restrict__ n_cand = A.n_cand[j];
-    const int c = bx * blockDim.x + threadIdx.x + kBorder, r = by + kBorder, layer = blockIdx.z + 1;
-    if (c >= cols - kBorder || r >= rows - kBorder) return;
+    const int layer = blockIdx.z + 1, tid = threadIdx.x;
+    const int r0 = kBorder + by * kExtTH, c0 = kBorder + bx * kExtTW;  // first pixel of the tile
     const size_t plane = (size_t)rows * cols;
-    const float* cur = dog + layer * plane;
-    const float val = cur[(size_t)r * cols + c];
-    if (!(fabsf(val) > (float)threshold)) return;
-    // all 26 neighbours loaded at once (independent, L1/L2 hits) and tested branch-free: the same
-    // predicate as OpenCV's early-exit comparisons, without a dependent load per comparison
-    const bool pos = val > 0;
-    bool ext = true;
+    if (tid == 0) n_list = 0;
+    // the halo rows/cols past the last tested pixel are clamped into the image: only pixels outside the
+    // tested range [kBorder, rows|cols - kBorder) ever read them
+    constexpr int kN = 3 * kExtH * kExtW;
+    for (int e0 = tid; e0 < kN; e0 += 256 * 8) {
+        float v[8];
 #pragma unroll
-    for (int dz = -1; dz <= 1; ++dz) {
-        const float* L = cur + dz * (long long)plane;
-#pragma unroll
-        for (int dy = -1; dy <= 1; ++dy)
-#pragma unroll
-            for (int dx = -1; dx <= 1; ++dx) {
-                if (dz == 0 && dy == 0 && dx == 0) continue;
-                const float nb = L[(size_t)(r + dy) * cols + c + dx];
-                ext &= pos ? (val >= nb) : (val <= nb);
+        for (int u = 0; u < 8; ++u) {
+            const int e = e0 + 256 * u;
+            if (e < kN) {
+                const int z = e / (kExtH * kExtW), rc = e - z * (kExtH * kExtW), r = rc / kExtW, c = rc - r * kExtW;
+                const int y = min(r0 - 1 + r, rows - 1), x = min(c0 - 1 + c, cols - 1);
+                v[u] = dog[(layer - 1 + z) * plane + (size_t)y * cols + x];
             }
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (e0 + 256 * u < kN) (&t[0][0][0])[e0 + 256 * u] = v[u];
     }
-    if (!ext) return;
-    const int k = atomicAdd(n_cand, 1);
-    if (k < cap) cand[k] = Cand{octave, layer, r, c};
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < kExtTW * kExtTH / 256; ++u) {
+        const int e = tid + 256 * u, lr = e / kExtTW, lc = e - lr * kExtTW, r = r0 + lr, c = c0 + lc;
+        if (r >= rows - kBorder || c >= cols - kBorder) continue;
+        const float val = t[1][lr + 1][lc + 1];
+        if (!(fabsf(val) > (float)threshold)) continue;
+        // the same predicate as OpenCV's early-exit comparisons, evaluated branch-free
+        const bool pos = val > 0;
+        bool ext = true;
+#pragma unroll
+        for (int dz = 0; dz < 3; ++dz)
+#pragma unroll
+            for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+                for (int dx = 0; dx < 3; ++dx) {
+                    if (dz == 1 && dy == 1 && dx == 1) continue;
+                    const float nb = t[dz][lr + dy][lc + dx];
+                    ext &= pos ? (val >= nb) : (val <= nb);
+                }
+        if (ext) list[atomicAdd(&n_list, 1)] = Cand{octave, layer, r, c};
+    }
+    __syncthreads();
+    const int n = n_list;
+    if (n == 0) return;
+    if (tid == 0) base = atomicAdd(A.n_cand[j], n);
+    __syncthreads();
+    Cand* __restrict__ cand = A.cand[j];
+    for (int i = tid; i < n; i += 256)
+        if (base + i < cap) cand[base + i] = list[i];
 }
 
 #define AT(L, r, c) ((L).p[(size_t)(r) * (L).cols + (c)])
@@ -546,6 +659,10 @@ struct OriB {
     int surv_cap, kp_cap;
 };
 
+#ifndef MIM_PROBE_ORIENT
+#define MIM_PROBE_ORIENT 0  // timing probes (wrong output): 1 slot = survivor (no counter), 2 no ordered
+                            // sums, 3 gradients without loads, 4 float exp
+#endif
 __global__ __launch_bounds__(64) void orient_kernel(OriB A) {  // blockIdx.y = image
     __shared__ int rb[64];
     __shared__ float rv[64];
@@ -576,9 +693,17 @@ __global__ __launch_bounds__(64) void orient_kernel(OriB A) {  // blockIdx.y = i
             const int ii = q / W - radius, j = q % W - radius;
             const int y = sv.r + ii, x = sv.c + j;
             if (y > 0 && y < g.rows - 1 && x > 0 && x < g.cols - 1) {
+#if MIM_PROBE_ORIENT == 3
+                const float dx = (float)((ii * 7 + j * 3) % 13) - 6.f, dy = (float)((ii * 5 + j * 11) % 17) - 8.f;
+#else
                 const float dx = AT(g, y, x + 1) - AT(g, y, x - 1);
                 const float dy = AT(g, y - 1, x) - AT(g, y + 1, x);
+#endif
+#if MIM_PROBE_ORIENT == 4
+                const float w = __expf((float)(ii * ii + j * j) * expf_scale);
+#else
                 const float w = (float)exp((double)((float)(ii * ii + j * j) * expf_scale));
+#endif
                 const float ori = fast_atan2(dy, dx);
                 const float mag = sqrtf(dx * dx + dy * dy);
                 bin = cv_round((kOriBins / 360.f) * ori);
@@ -593,12 +718,16 @@ __global__ __launch_bounds__(64) void orient_kernel(OriB A) {  // blockIdx.y = i
         const int m = min(64, P - base);
         // unrolled: the batch's (bin, value) reads are broadcast LDS loads independent of the sums, so
         // 16 issue back to back instead of one dependent round trip per pixel (the adds stay in order)
+#if MIM_PROBE_ORIENT == 2
+        acc += rb[lane] == lane ? rv[lane] : 0.f + (float)m;
+#else
 #pragma unroll 16
         for (int i = 0; i < m; ++i) {
             const int bi = rb[i];
             const float vi = rv[i], sum = acc + vi;
             acc = bi == lane ? sum : acc;
         }
+#endif
         __syncthreads();
     }
     if (lane < kOriBins) th[lane + 2] = acc;
@@ -622,7 +751,12 @@ __global__ __launch_bounds__(64) void orient_kernel(OriB A) {  // blockIdx.y = i
             bin = bin < 0 ? kOriBins + bin : (bin >= kOriBins ? bin - kOriBins : bin);
             k.angle = 360.f - (float)((360.f / kOriBins) * bin);
             if (fabsf(k.angle - 360.f) < FLT_EPSILON) k.angle = 0.f;
+#if MIM_PROBE_ORIENT == 1
+            const int slot = t;
+            if (t == 0) atomicAdd(n_kp, n_s);
+#else
             const int slot = atomicAdd(n_kp, 1);
+#endif
             if (slot < kp_cap) kp[slot] = k;
         }
     }
@@ -665,7 +799,7 @@ __device__ __forceinline__ int ctz64(unsigned long long m) { return __builtin_ct
 #define MIM_DESCR_GRID 4096  // descriptor blocks of a batch launch (at least 1024 per image)
 #endif
 constexpr int kDescrT = 256;        // threads of a descriptor block: pixels per batch of a patch
-constexpr int kDescrTBig = 1024;    // MIM_DESCR_BIG_SPLIT: the large patches by 1024-thread blocks
+[[maybe_unused]] constexpr int kDescrTBig = 1024;    // MIM_DESCR_BIG_SPLIT: the large patches by 1024-thread blocks
 constexpr int kDescrRowsMax = 512;
 // MIM_DESCR_BIG_SPLIT (off; measured slower, r06c): patches wider than MIM_DESCR_BIG_W described by
 // kDescrTBig blocks in a launch of their own (4x fewer batches in their chains).  The launch is bound by
@@ -1147,6 +1281,12 @@ struct SiftWs {
     void* batch = nullptr; size_t batch_cap = 0;  // a call's Pyr tables and counters (batch owner only)
     Pyr* h_pyr = nullptr;  // pinned staging of the Pyr tables
     int* h_cnt = nullptr;  // pinned copy of the counters
+    // pinned staging of the caller's 8-bit planes (0: image, 1: mask), see stage_h2d
+    struct Stage {
+        uint8_t* p = nullptr;
+        size_t cap = 0;
+        hipEvent_t ev = nullptr;  // recorded after the copy out of p
+    } stage[2];
 };
 
 static hipError_t grow(void*& p, size_t& cap, size_t need) {
@@ -1171,6 +1311,10 @@ void sift_ws_destroy(SiftWs* w) {
         if (p) (void)hipFree(p);
     if (w->h_pyr) (void)hipHostFree(w->h_pyr);
     if (w->h_cnt) (void)hipHostFree(w->h_cnt);
+    for (auto& S : w->stage) {
+        if (S.ev) (void)hipEventSynchronize(S.ev), (void)hipEventDestroy(S.ev);
+        if (S.p) (void)hipHostFree(S.p);
+    }
     delete w;
 }
 
@@ -1182,6 +1326,32 @@ void sift_ws_destroy(SiftWs* w) {
             return -1;                                       \
         }                                                    \
     } while (0)
+
+// rows x cols bytes of a caller's plane (row step `step`) to the device: copied on the host into the
+// workspace's pinned stage, then one asynchronous copy.  hipMemcpy2DAsync straight from the caller's
+// pageable rows took 11-27 ms per 640x480 image in some processes against ~25 us in others
+// (profiles/r06g_sift_phases.txt).  The stage is reused only after its previous copy has completed.
+static int stage_h2d(SiftWs* w, int slot, void* dst, const uint8_t* src, long long step, int cols, int rows,
+                     hipStream_t st, std::string& err) {
+    SiftWs::Stage& S = w->stage[slot];
+    const size_t bytes = (size_t)rows * cols;
+    if (bytes == 0) return 0;
+    if (S.ev) SCHK(hipEventSynchronize(S.ev));
+    else SCHK(hipEventCreateWithFlags(&S.ev, hipEventDisableTiming));
+    if (bytes > S.cap) {
+        if (S.p) SCHK(hipHostFree(S.p));
+        S.p = nullptr;
+        S.cap = 0;
+        SCHK(hipHostMalloc((void**)&S.p, bytes + bytes / 4, hipHostMallocDefault));
+        S.cap = bytes + bytes / 4;
+    }
+    if (step == cols) memcpy(S.p, src, bytes);
+    else
+        for (int r = 0; r < rows; ++r) memcpy(S.p + (size_t)r * cols, src + (size_t)r * step, cols);
+    SCHK(hipMemcpyAsync(dst, S.p, bytes, hipMemcpyHostToDevice, st));
+    SCHK(hipEventRecord(S.ev, st));
+    return 0;
+}
 
 // One image of a SIFT call: its workspace (the 8-bit image already in w->img, rows x cols packed),
 // its mask (host, optional), where its keypoints / descriptors go and their capacity.
@@ -1389,7 +1559,8 @@ static int sift_batch(std::vector<SiftJob>& jobs, SiftWs* bw, hipStream_t st, st
         J.d_cnt = d_cnt + 4 * j;
         bw->h_pyr[j] = J.h_pyr;
         if (J.n_oct > 0) live.push_back(j);
-        if (J.d_mask) SCHK(hipMemcpy2DAsync(J.d_mask, J.cols, J.mask, J.mstep, J.cols, J.rows, hipMemcpyHostToDevice, st));
+        if (J.d_mask)
+            if (int r = stage_h2d(J.w, 1, J.d_mask, J.mask, J.mstep, J.cols, J.rows, st, err)) return r;
     }
     SCHK(hipMemcpyAsync(d_pyr, bw->h_pyr, pyr_bytes, hipMemcpyHostToDevice, st));
     SCHK(hipMemsetAsync(d_cnt, 0, sizeof(int) * 4 * nj, st));
@@ -1421,17 +1592,36 @@ static int sift_batch(std::vector<SiftJob>& jobs, SiftWs* bw, hipStream_t st, st
                 const size_t plane = (size_t)J.orows[o] * J.ocols[o];
                 A.src[k] = init ? J.T0 : J.P + J.goff[o] + (layer - 1) * plane;
                 A.dst[k] = J.P + J.goff[o] + layer * plane;
+                A.dog[k] = init ? nullptr : J.P + J.doff[o] + (layer - 1) * plane;
                 A.rows[k] = J.orows[o];
                 A.cols[k] = J.ocols[o];
             }
             const int a = t.n / 2;
+            auto reg = [&](auto kern) {
+                // the register-blocked kernel's tiles are MIM_BLUR_TH rows: its own grid
+                const int nb2 = flatten(A.f, imgs, [&](int j, int& gx, int& gy) {
+                    gx = (jobs[j].ocols[o] + kBlurTW - 1) / kBlurTW;
+                    gy = (jobs[j].orows[o] + MIM_BLUR_TH - 1) / MIM_BLUR_TH;
+                });
+                kern<<<nb2, 256, 0, st>>>(A, t);
+                return true;
+            };
+            switch (a) {
+            case 5: return reg(blur_reg_kernel<5, MIM_BLUR_TH>);
+            case 6: return reg(blur_reg_kernel<6, MIM_BLUR_TH>);
+            case 8: return reg(blur_reg_kernel<8, MIM_BLUR_TH>);
+            case 10: return reg(blur_reg_kernel<10, MIM_BLUR_TH>);
+            case 13: return reg(blur_reg_kernel<13, MIM_BLUR_TH>);
+            default: break;
+            }
             const size_t lds = sizeof(float) * (size_t)(kBlurTH + 2 * a) * (kBlurTW + 2 * a + kBlurTW);
             if (lds > 64 * 1024) return false;
             blur_kernel<<<nb, 256, lds, st>>>(A, t);
             return true;
         };
         if (!blur(live, 0, 0, true, t0)) { err = "kernel size"; return -4; }
-        // buildGaussianPyramid + DoG of the large octaves, all images with octave o at once
+        // buildGaussianPyramid + DoG of the large octaves, all images with octave o at once (each blur
+        // after the first writes the DoG plane of its source and destination layers too)
         int o_max = 0;
         for (int j : live) o_max = std::max(o_max, jobs[j].o_small);
         for (int o = 0; o < o_max; ++o) {
@@ -1455,18 +1645,6 @@ static int sift_batch(std::vector<SiftJob>& jobs, SiftWs* bw, hipStream_t st, st
             }
             for (int i = 1; i < kNOL + 3; ++i)
                 if (!blur(imgs, o, i, false, tl[i - 1])) { err = "kernel size"; return -4; }
-            DogB A{};
-            const int nb = flatten(A.f, imgs, [&](int j, int& gx, int& gy) {
-                gx = (int)(((size_t)jobs[j].orows[o] * jobs[j].ocols[o] + 255) / 256);
-                gy = 1;
-            });
-            for (int k = 0; k < A.f.n; ++k) {
-                const SiftJob& J = jobs[imgs[k]];
-                A.g[k] = J.P + J.goff[o];
-                A.d[k] = J.P + J.doff[o];
-                A.plane[k] = (long long)J.orows[o] * J.ocols[o];
-            }
-            dog_kernel<<<dim3(nb, kNOL + 2), 256, 0, st>>>(A);
         }
         {  // the small octaves: one block per image
             SmallB A{};
@@ -1491,8 +1669,8 @@ static int sift_batch(std::vector<SiftJob>& jobs, SiftWs* bw, hipStream_t st, st
             if (imgs.empty()) continue;
             ExtB A{};
             const int nb = flatten(A.f, imgs, [&](int j, int& gx, int& gy) {
-                gx = (jobs[j].ocols[o] - 2 * kBorder + 127) / 128;
-                gy = jobs[j].orows[o] - 2 * kBorder;
+                gx = (jobs[j].ocols[o] - 2 * kBorder + kExtTW - 1) / kExtTW;
+                gy = (jobs[j].orows[o] - 2 * kBorder + kExtTH - 1) / kExtTH;
             });
             for (int k = 0; k < A.f.n; ++k) {
                 const SiftJob& J = jobs[imgs[k]];
@@ -1505,7 +1683,7 @@ static int sift_batch(std::vector<SiftJob>& jobs, SiftWs* bw, hipStream_t st, st
             A.octave = o;
             A.threshold = threshold;
             A.cap = cand_limit();
-            extrema_kernel<<<dim3(nb, 1, kNOL), 128, 0, st>>>(A);
+            extrema_kernel<<<dim3(nb, 1, kNOL), 256, 0, st>>>(A);
         }
         // adjustLocalExtrema, orientations, keypoint post-processing, descriptors: grids of (X, images)
         RefB Rf{};
@@ -1605,8 +1783,13 @@ int sift_detect_compute(SiftWs* w, hipStream_t st, const uint8_t* img, int rows,
                         const uint8_t* mask, long long mstep, int max_kp, mim_keypoint* kps, float* desc, int* n_out,
                         std::string& err) {
     *n_out = 0;
+    // MIM_SIFT_TRACE=1: host times of the call's phases on stderr (diagnostic)
+    static const bool trace = getenv("MIM_SIFT_TRACE") != nullptr;
+    auto now = [] { return std::chrono::steady_clock::now(); };
+    const auto t0 = now();
     SCHK(grow(w->img, w->img_cap, (size_t)rows * cols));
-    SCHK(hipMemcpy2DAsync(w->img, cols, img, step, cols, rows, hipMemcpyHostToDevice, st));
+    if (int r = stage_h2d(w, 0, w->img, img, step, cols, rows, st, err)) return r;
+    const auto t1 = now();
     std::vector<SiftJob> jobs(1);
     SiftJob& J = jobs[0];
     J.w = w;
@@ -1618,7 +1801,14 @@ int sift_detect_compute(SiftWs* w, hipStream_t st, const uint8_t* img, int rows,
     J.kps = kps;
     J.desc = desc;
     int r = sift_batch(jobs, w, st, err);
+    const auto t2 = now();
     if (!r) r = sift_fetch(jobs, st, err);
+    if (trace) {
+        const auto t3 = now();
+        auto us = [](auto a, auto b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
+        fprintf(stderr, "[mim] sift %dx%d: image copy %.0f us, batch %.0f us, fetch %.0f us\n", rows, cols, us(t0, t1),
+                us(t1, t2), us(t2, t3));
+    }
     *n_out = J.n;
     return r;
 }
@@ -1634,7 +1824,7 @@ static int sift_scale_images(std::vector<SiftWs*>& ws, hipStream_t st, const uin
     while ((int)ws.size() < n_scales + 1) ws.push_back(sift_ws_create());
     SiftWs* src = ws[n_scales];  // the scene itself, and the batch buffer
     SCHK(grow(src->img, src->img_cap, (size_t)rows * cols));
-    SCHK(hipMemcpy2DAsync(src->img, cols, img, step, cols, rows, hipMemcpyHostToDevice, st));
+    if (int r = stage_h2d(src, 0, src->img, img, step, cols, rows, st, err)) return r;
     jobs.assign(n_scales, SiftJob{});
     ResizeB A{};
     A.src = (const uint8_t*)src->img;
@@ -1756,7 +1946,7 @@ int sift_resize_u8(SiftWs* w, hipStream_t st, const uint8_t* src, int rows, int 
     SCHK(grow(w->img, w->img_cap, sb + db));
     uint8_t* ds = (uint8_t*)w->img;
     uint8_t* dd = ds + sb;
-    SCHK(hipMemcpy2DAsync(ds, cols, src, step, cols, rows, hipMemcpyHostToDevice, st));
+    if (int r = stage_h2d(w, 0, ds, src, step, cols, rows, st, err)) return r;
     ResizeB A{};
     A.src = ds;
     A.rows = rows;

@@ -1,0 +1,31 @@
+# r06h: (1) SIFT / pipeline GPU tests on the current tree (register-blocked blurs with the taps as
+# constants, pinned staging of the caller's image); (2) time_sift + c1img lines: prev (HEAD sift.hip),
+# cur (blur tile 32 rows), th16 (16 rows); (3) kernel traces of time_sift for cur and the orientation
+# probes ori1-4 (timing only: the orient_kernel durations are read from the traces).
+set -e
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+O=gpurun_out/r06h
+mkdir -p $O
+V=$PWD/computervision_objectdetection_featurematching_amd/lib/variants
+CUR=$PWD/computervision_objectdetection_featurematching_amd/lib/libmim.so
+rc=0
+timeout -k 10 600 python3 -u -m pytest tests/test_sift_gpu.py tests/test_golden_gpu.py tests/test_pipeline_gpu.py tests/test_sift_limits_gpu.py -q --timeout 300 --timeout-method thread > $O/pytest_sift.log 2>&1 || rc=$?
+tail -3 $O/pytest_sift.log
+case $rc in 0) ;; *) echo "pytest rc $rc: stopping"; exit 1;; esac
+for i in 1 2; do
+  for v in prev cur th16; do
+    L=$V/libmim_$v.so; [ $v = cur ] && L=$CUR
+    MIM_LIB=$L timeout -k 10 120 python3 -u tools/time_sift.py --reps 10 > $O/time_sift_${v}_$i.log 2>&1
+    MIM_LIB=$L timeout -k 10 300 python3 -u bench.py --config c1img --cpu-sample 0 > $O/bench_c1img_${v}_$i.log 2>&1
+  done
+done
+for v in cur th16 ori1 ori2 ori3 ori4; do
+  L=$V/libmim_$v.so; [ $v = cur ] && L=$CUR
+  MIM_LIB=$L timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/tr_$v -o run -- \
+    python3 tools/time_sift.py --reps 3 > $O/trace_$v.log 2>&1 < /dev/null
+done
+timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/c1img -o run -- \
+  python3 bench.py --config c1img --inflight 1 --steps 3 --warmup 1 --iso-steps 3 --cpu-sample 0 > $O/c1img_trace_bench.log 2>&1 < /dev/null
+python3 tools/scene_timeline.py $O/c1img/run_kernel_trace.csv 4 > $O/c1img_timeline.txt
+echo done

@@ -659,24 +659,40 @@ struct OriB {
     int surv_cap, kp_cap;
 };
 
-#ifndef MIM_PROBE_ORIENT
-#define MIM_PROBE_ORIENT 0  // timing probes (wrong output): 1 slot = survivor (no counter), 2 no ordered
-                            // sums, 3 gradients without loads, 4 float exp
-#endif
-__global__ __launch_bounds__(64) void orient_kernel(OriB A) {  // blockIdx.y = image
-    __shared__ int rb[64];
-    __shared__ float rv[64];
-    __shared__ float th[kOriBins + 4];
-    const int lane = threadIdx.x, j = blockIdx.y;
+// Four survivors per 256-thread block, one per wave: the waves synchronise among their own lanes only
+// (their patches differ in size), and the block appends all its keypoints with ONE counter atomic.
+// Round 5's one-survivor blocks did one returning atomic per keypoint on the image's single counter:
+// 11.4 ns each serialised (profiles/r06e_atomic_probe.txt), ~60 us of a 5-scale scene's 234 us
+// (r06h: the kernel without the counter, profiles/r06h_sift_ab.txt).
+constexpr int kOriWaves = 4;
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+__global__ __launch_bounds__(64 * kOriWaves) void orient_kernel(OriB A) {  // blockIdx.y = image
+    __shared__ int rb_[kOriWaves][64];
+    __shared__ float rv_[kOriWaves][64];
+    __shared__ float th_[kOriWaves][kOriBins + 4];
+    __shared__ float pang[kOriWaves][kOriBins];  // the angles of each wave's keypoints, in peak order
+    __shared__ int npk[kOriWaves], base;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, j = blockIdx.y;
+    int* rb = rb_[wv];
+    float* rv = rv_[wv];
+    float* th = th_[wv];
     const Pyr* __restrict__ pyr = A.pyr[j];
     const Surv* __restrict__ surv = A.surv[j];
     mim_keypoint* __restrict__ kp = A.kp[j];
     int* __restrict__ n_kp = A.n_kp[j];
     const int kp_cap = A.kp_cap;
   const int n_s = min(*A.n_surv[j], A.surv_cap);
-  for (int t = blockIdx.x; t < n_s; t += gridDim.x) {  // fixed grid, block-uniform loop
+  for (int t0 = blockIdx.x * kOriWaves; t0 < n_s; t0 += gridDim.x * kOriWaves) {  // block-uniform loop
+    const int t = t0 + wv;
+    mim_keypoint k{};
+    if (lane == 0) npk[wv] = 0;
+    if (t < n_s) {
     const Surv sv = surv[t];
-    mim_keypoint k = sv.k;
+    k = sv.k;
     const int octv = k.octave & 255;
     const Layer g = pyr->gauss[octv][sv.layer];
     const float scl_octv = k.size * 0.5f / (1 << octv);
@@ -693,17 +709,9 @@ __global__ __launch_bounds__(64) void orient_kernel(OriB A) {  // blockIdx.y = i
             const int ii = q / W - radius, j = q % W - radius;
             const int y = sv.r + ii, x = sv.c + j;
             if (y > 0 && y < g.rows - 1 && x > 0 && x < g.cols - 1) {
-#if MIM_PROBE_ORIENT == 3
-                const float dx = (float)((ii * 7 + j * 3) % 13) - 6.f, dy = (float)((ii * 5 + j * 11) % 17) - 8.f;
-#else
                 const float dx = AT(g, y, x + 1) - AT(g, y, x - 1);
                 const float dy = AT(g, y - 1, x) - AT(g, y + 1, x);
-#endif
-#if MIM_PROBE_ORIENT == 4
-                const float w = __expf((float)(ii * ii + j * j) * expf_scale);
-#else
                 const float w = (float)exp((double)((float)(ii * ii + j * j) * expf_scale));
-#endif
                 const float ori = fast_atan2(dy, dx);
                 const float mag = sqrtf(dx * dx + dy * dy);
                 bin = cv_round((kOriBins / 360.f) * ori);
@@ -714,24 +722,20 @@ __global__ __launch_bounds__(64) void orient_kernel(OriB A) {  // blockIdx.y = i
         }
         rb[lane] = bin;
         rv[lane] = val;
-        __syncthreads();
+        wave_sync();
         const int m = min(64, P - base);
         // unrolled: the batch's (bin, value) reads are broadcast LDS loads independent of the sums, so
         // 16 issue back to back instead of one dependent round trip per pixel (the adds stay in order)
-#if MIM_PROBE_ORIENT == 2
-        acc += rb[lane] == lane ? rv[lane] : 0.f + (float)m;
-#else
 #pragma unroll 16
         for (int i = 0; i < m; ++i) {
             const int bi = rb[i];
             const float vi = rv[i], sum = acc + vi;
             acc = bi == lane ? sum : acc;
         }
-#endif
-        __syncthreads();
+        wave_sync();
     }
     if (lane < kOriBins) th[lane + 2] = acc;
-    __syncthreads();
+    wave_sync();
     if (lane == 0) {
     th[1] = th[kOriBins + 1];
     th[0] = th[kOriBins];
@@ -744,24 +748,36 @@ __global__ __launch_bounds__(64) void orient_kernel(OriB A) {  // blockIdx.y = i
         mx = b == 0 ? hist[0] : fmaxf(mx, hist[b]);
     }
     const float mag_thr = mx * 0.8f;
+    int np = 0;
     for (int j = 0; j < kOriBins; j++) {
         const int l = j > 0 ? j - 1 : kOriBins - 1, r2 = j < kOriBins - 1 ? j + 1 : 0;
         if (hist[j] > hist[l] && hist[j] > hist[r2] && hist[j] >= mag_thr) {
             float bin = j + 0.5f * (hist[l] - hist[r2]) / (hist[l] - 2 * hist[j] + hist[r2]);
             bin = bin < 0 ? kOriBins + bin : (bin >= kOriBins ? bin - kOriBins : bin);
-            k.angle = 360.f - (float)((360.f / kOriBins) * bin);
-            if (fabsf(k.angle - 360.f) < FLT_EPSILON) k.angle = 0.f;
-#if MIM_PROBE_ORIENT == 1
-            const int slot = t;
-            if (t == 0) atomicAdd(n_kp, n_s);
-#else
-            const int slot = atomicAdd(n_kp, 1);
-#endif
-            if (slot < kp_cap) kp[slot] = k;
+            float angle = 360.f - (float)((360.f / kOriBins) * bin);
+            if (fabsf(angle - 360.f) < FLT_EPSILON) angle = 0.f;
+            pang[wv][np++] = angle;
         }
     }
+    npk[wv] = np;
     }
-    __syncthreads();  // th, rb, rv reused by the block's next survivor
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int tot = 0;
+#pragma unroll
+        for (int w = 0; w < kOriWaves; ++w) tot += npk[w];
+        base = tot ? atomicAdd(n_kp, tot) : 0;
+    }
+    __syncthreads();
+    int off = base;
+    for (int w = 0; w < wv; ++w) off += npk[w];
+    if (lane < npk[wv]) {
+        const int slot = off + lane;
+        k.angle = pang[wv][lane];
+        if (slot < kp_cap) kp[slot] = k;
+    }
+    __syncthreads();  // rb, rv, th, pang, npk, base reused by the block's next survivors
   }
 }
 
@@ -1042,8 +1058,12 @@ __global__ __launch_bounds__(T) void descr_kernel(DescB A, int cls) {  // blockI
             const int bin = tid + T * s2;
             if (bin < kHistLen) {
                 float acc = hb[s2];
+#if MIM_PROBE_DESCR == 3  // timing probe only: no ordered sums
+                acc += tot[s2] ? sorted[st0[s2]] : 0.f;
+#else
 #pragma unroll 4
                 for (int i = 0; i < tot[s2]; ++i) acc += sorted[st0[s2] + i];
+#endif
                 hb[s2] = acc;
 #pragma unroll
                 for (int w = 0; w < kWords; ++w) bm[bin][w] = 0ull;  // cleared for the next batch
@@ -1162,32 +1182,45 @@ __global__ __launch_bounds__(1024) void kp_post_kernel(KpB A) {  // blockIdx.y =
     // before(a, b): a precedes b in KeypointGreater order (padding never precedes)
     auto before = [&](int a, int b) { return a >= 0 && (b < 0 || kp_greater_d(kp[a], kp[b])); };
     if (P <= kKeySortCap) {
-        // bitonic sort of (key, index) pairs in LDS: KeypointGreater compares x, then y first, so the
-        // key decides every pair with different (x, y); equal keys (duplicate positions) fall back to
-        // the full comparison of the keypoints.  Was: every comparison read two keypoints from L2
-        // (~150 us per call for ~5k keypoints).
-        auto before_k = [&](int a, unsigned long long ka, int b, unsigned long long kb) {
-            if (a < 0) return false;
-            if (b < 0) return true;
-            return ka != kb ? ka > kb : kp_greater_d(kp[a], kp[b]);
-        };
+        // bitonic sort of (key, index) pairs in LDS by the key alone, then the runs of equal keys
+        // (duplicate positions: a keypoint's extra orientations) put in KeypointGreater order by the full
+        // comparison.  KeypointGreater compares x, then y first, so the key decides every pair with
+        // different (x, y).  Was (to round 6): the full comparison inside the network on equal keys, a
+        // dependent L2 read in most of its ~90 barrier-separated stages (~300 us per 5-scale scene).
+        // One compare-exchange per thread and pair, the pairs enumerated directly (no idle half).
         for (int k = 2; k <= P; k <<= 1)
             for (int j = k >> 1; j > 0; j >>= 1) {
-                for (int i = tid; i < P; i += 1024) {
-                    const int l = i ^ j;
-                    if (l > i) {
+                for (int q = tid; q < P / 2; q += 1024) {
+                    const int i = ((q & ~(j - 1)) << 1) | (q & (j - 1)), l = i | j;
+                    const unsigned long long ka = skey[i], kb = skey[l];
+                    if ((i & k) == 0 ? kb > ka : ka > kb) {
                         const int a = idx[i], b = idx[l];
-                        const unsigned long long ka = skey[i], kb = skey[l];
-                        if ((i & k) == 0 ? before_k(b, kb, a, ka) : before_k(a, ka, b, kb)) {
-                            idx[i] = b;
-                            idx[l] = a;
-                            skey[i] = kb;
-                            skey[l] = ka;
-                        }
+                        idx[i] = b;
+                        idx[l] = a;
+                        skey[i] = kb;
+                        skey[l] = ka;
                     }
                 }
                 __syncthreads();
             }
+        // runs of equal keys (padding, key 0, is never part of one: it sorts after every keypoint)
+        for (int i = tid; i < n; i += 1024) {
+            const unsigned long long ki = skey[i];
+            if ((i > 0 && skey[i - 1] == ki) || i + 1 >= n || skey[i + 1] != ki) continue;
+            int e = i + 2;
+            while (e < n && skey[e] == ki) ++e;
+            for (int u = i + 1; u < e; ++u) {  // insertion sort of idx[i, e) (a stable order for ties)
+                const int v = idx[u];
+                const mim_keypoint kv = kp[v];
+                int w = u;
+                while (w > i && kp_greater_d(kv, kp[idx[w - 1]])) {
+                    idx[w] = idx[w - 1];
+                    --w;
+                }
+                idx[w] = v;
+            }
+        }
+        __syncthreads();
     } else {
         for (int k = 2; k <= P; k <<= 1)
             for (int j = k >> 1; j > 0; j >>= 1) {
@@ -1722,7 +1755,7 @@ static int sift_batch(std::vector<SiftJob>& jobs, SiftWs* bw, hipStream_t st, st
         Kp.kp_cap = kKpCap;
         Kp.sort_cap = sort_limit();
         refine_kernel<<<dim3(std::max(1024 / nl, 128), nl), 128, 0, st>>>(Rf);
-        orient_kernel<<<dim3(std::max(4096 / nl, 512), nl), 64, 0, st>>>(Or);
+        orient_kernel<<<dim3(std::max(1024 / nl, 128), nl), 64 * kOriWaves, 0, st>>>(Or);
         kp_post_kernel<<<dim3(1, nl), 1024, 0, st>>>(Kp);
 #if MIM_DESCR_SPLIT
         for (int k = 0; k < nl; ++k) {  // one launch per image, in order

@@ -3882,8 +3882,9 @@ __global__ __launch_bounds__(kRT) void ransac_refine_kernel(const RansacState* _
         const unsigned long long tot = wall_clock64() - rt_start;
         if (tot > 20000)
             printf("[refine-timing] p=%d ng=%d inl=%d iters=%d total=%llu mask=%llu refit=%llu norm0=%llu "
-                   "solve=%llu cost=%llu norm=%llu (us x100)\n", p, ng, sh.n_inl, rt_iters, tot, t_mask, t_refit,
-                   t_norm0, t_solve, t_cost, t_norm);
+                   "solve=%llu cost=%llu norm=%llu (us x100) niters=%d produced=%d done=%d small=%d\n", p, ng,
+                   sh.n_inl, rt_iters, tot, t_mask, t_refit, t_norm0, t_solve, t_cost, t_norm, S.niters, S.produced,
+                   S.done, (int)(S.n < kSmallMaxN));
     }
 #endif
     res.n_inl = ok ? sh.n_inl : 0;

@@ -459,6 +459,7 @@ struct ExtB {
 constexpr int kExtTW = 64, kExtTH = 16, kExtW = kExtTW + 2, kExtH = kExtTH + 2;
 
 __global__ __launch_bounds__(256) void extrema_kernel(ExtB A) {
+    static_assert(kExtTW == 64 && kExtW - 64 <= 64, "one tile row per wave, lane = column");
     __shared__ float t[3][kExtH][kExtW];
     __shared__ Cand list[kExtTW * kExtTH];
     __shared__ int n_list, base;
@@ -466,49 +467,59 @@ __global__ __launch_bounds__(256) void extrema_kernel(ExtB A) {
     const int j = flat_job(A.f, blockIdx.x, bx, by);
     const float* __restrict__ dog = A.dog[j];
     const int rows = A.rows[j], cols = A.cols[j], octave = A.octave, threshold = A.threshold, cap = A.cap;
-    const int layer = blockIdx.z + 1, tid = threadIdx.x;
+    const int layer = blockIdx.z + 1, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int r0 = kBorder + by * kExtTH, c0 = kBorder + bx * kExtTW;  // first pixel of the tile
     const size_t plane = (size_t)rows * cols;
     if (tid == 0) n_list = 0;
-    // the halo rows/cols past the last tested pixel are clamped into the image: only pixels outside the
-    // tested range [kBorder, rows|cols - kBorder) ever read them
-    constexpr int kN = 3 * kExtH * kExtW;
-    for (int e0 = tid; e0 < kN; e0 += 256 * 8) {
-        float v[8];
+    // staging: wave w loads tile rows w, w + 4, ... of the three planes (lane = column; the two halo
+    // columns past 64 by lanes 0, 1), every load in flight before the LDS writes.  Rows/columns past
+    // the last tested pixel are clamped into the image: only pixels outside the tested range
+    // [kBorder, rows|cols - kBorder) ever read them.
+    constexpr int kRows = 3 * kExtH, kRPW = (kRows + 3) / 4;
+    const int xa = min(c0 - 1 + lane, cols - 1), xb = min(c0 + 63 + lane, cols - 1);
+    float va[kRPW], vb[kRPW];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const int e = e0 + 256 * u;
-            if (e < kN) {
-                const int z = e / (kExtH * kExtW), rc = e - z * (kExtH * kExtW), r = rc / kExtW, c = rc - r * kExtW;
-                const int y = min(r0 - 1 + r, rows - 1), x = min(c0 - 1 + c, cols - 1);
-                v[u] = dog[(layer - 1 + z) * plane + (size_t)y * cols + x];
-            }
+    for (int i = 0; i < kRPW; ++i) {
+        const int row = wv + 4 * i;
+        if (row < kRows) {
+            const int z = row / kExtH, r = row - z * kExtH;
+            const float* bp = dog + (layer - 1 + z) * plane + (size_t)min(r0 - 1 + r, rows - 1) * cols;
+            va[i] = bp[xa];
+            if (lane < kExtW - 64) vb[i] = bp[xb];
         }
+    }
 #pragma unroll
-        for (int u = 0; u < 8; ++u)
-            if (e0 + 256 * u < kN) (&t[0][0][0])[e0 + 256 * u] = v[u];
+    for (int i = 0; i < kRPW; ++i) {
+        const int row = wv + 4 * i;
+        if (row < kRows) {
+            float* tr = &t[0][0][0] + row * kExtW;
+            tr[lane] = va[i];
+            if (lane < kExtW - 64) tr[64 + lane] = vb[i];
+        }
     }
     __syncthreads();
+    // wave w tests tile rows w, w + 4, w + 8, w + 12 (lane = column).  OpenCV's predicate (val >= every
+    // neighbour for val > 0, val <= every neighbour otherwise) as one comparison against the max / min
+    // of the 26 neighbours (finite values: the same outcome)
 #pragma unroll
-    for (int u = 0; u < kExtTW * kExtTH / 256; ++u) {
-        const int e = tid + 256 * u, lr = e / kExtTW, lc = e - lr * kExtTW, r = r0 + lr, c = c0 + lc;
+    for (int u = 0; u < kExtTH / 4; ++u) {
+        const int lr = wv + 4 * u, lc = lane, r = r0 + lr, c = c0 + lc;
         if (r >= rows - kBorder || c >= cols - kBorder) continue;
         const float val = t[1][lr + 1][lc + 1];
         if (!(fabsf(val) > (float)threshold)) continue;
-        // the same predicate as OpenCV's early-exit comparisons, evaluated branch-free
-        const bool pos = val > 0;
-        bool ext = true;
+        float mx = t[0][lr][lc], mn = mx;
 #pragma unroll
         for (int dz = 0; dz < 3; ++dz)
 #pragma unroll
             for (int dy = 0; dy < 3; ++dy)
 #pragma unroll
                 for (int dx = 0; dx < 3; ++dx) {
-                    if (dz == 1 && dy == 1 && dx == 1) continue;
+                    if ((dz == 1 && dy == 1 && dx == 1) || (dz == 0 && dy == 0 && dx == 0)) continue;
                     const float nb = t[dz][lr + dy][lc + dx];
-                    ext &= pos ? (val >= nb) : (val <= nb);
+                    mx = fmaxf(mx, nb);
+                    mn = fminf(mn, nb);
                 }
-        if (ext) list[atomicAdd(&n_list, 1)] = Cand{octave, layer, r, c};
+        if (val > 0 ? val >= mx : val <= mn) list[atomicAdd(&n_list, 1)] = Cand{octave, layer, r, c};
     }
     __syncthreads();
     const int n = n_list;
@@ -701,7 +712,26 @@ __global__ __launch_bounds__(64 * kOriWaves) void orient_kernel(OriB A) {  // bl
     const float expf_scale = -1.f / (2.f * sigma * sigma);
     const int W = 2 * radius + 1, P = W * W;
     float acc = 0.f;  // th[lane + 2] for lane < 36
+    // the four gradient reads of a batch's pixel are issued one batch ahead (software pipelined): a
+    // batch's loads are in flight while the previous batch's sums run
+    auto fetch = [&](int b, float& xr, float& xl, float& yu, float& yd) {
+        const int q = b + lane;
+        if (q < P) {
+            const int ii = q / W - radius, j = q % W - radius;
+            const int y = sv.r + ii, x = sv.c + j;
+            if (y > 0 && y < g.rows - 1 && x > 0 && x < g.cols - 1) {
+                xr = AT(g, y, x + 1);
+                xl = AT(g, y, x - 1);
+                yu = AT(g, y - 1, x);
+                yd = AT(g, y + 1, x);
+            }
+        }
+    };
+    float nxr = 0.f, nxl = 0.f, nyu = 0.f, nyd = 0.f;
+    fetch(0, nxr, nxl, nyu, nyd);
     for (int base = 0; base < P; base += 64) {
+        const float cxr = nxr, cxl = nxl, cyu = nyu, cyd = nyd;
+        if (base + 64 < P) fetch(base + 64, nxr, nxl, nyu, nyd);
         const int q = base + lane;
         int bin = -1;
         float val = 0.f;
@@ -709,8 +739,8 @@ __global__ __launch_bounds__(64 * kOriWaves) void orient_kernel(OriB A) {  // bl
             const int ii = q / W - radius, j = q % W - radius;
             const int y = sv.r + ii, x = sv.c + j;
             if (y > 0 && y < g.rows - 1 && x > 0 && x < g.cols - 1) {
-                const float dx = AT(g, y, x + 1) - AT(g, y, x - 1);
-                const float dy = AT(g, y - 1, x) - AT(g, y + 1, x);
+                const float dx = cxr - cxl;
+                const float dy = cyu - cyd;
                 const float w = (float)exp((double)((float)(ii * ii + j * j) * expf_scale));
                 const float ori = fast_atan2(dy, dx);
                 const float mag = sqrtf(dx * dx + dy * dy);

@@ -373,9 +373,12 @@ class Matcher:
     # ---- fused batch ----------------------------------------------------------------------
     def match_batch_async(self, problems, params: Params | None = None):
         params = params or default_params()
-        arr = (Problem * len(problems))(*[Problem(int(a), int(b)) for a, b in problems])
-        self._check(self.L.mim_batch_run(self._ctx, arr, len(problems), C.byref(params)))
-        return len(problems)
+        # an (n, 2) int32 array is mim_problem[n] as it is (no per-problem ctypes objects: ~1 us each)
+        arr = problems if isinstance(problems, np.ndarray) else np.asarray(list(problems), np.int32)
+        arr = np.ascontiguousarray(arr, np.int32).reshape(-1, 2)
+        self._check(self.L.mim_batch_run(self._ctx, arr.ctypes.data_as(C.POINTER(Problem)), len(arr),
+                                         C.byref(params)))
+        return len(arr)
 
     def batch_results(self, n: int) -> np.ndarray:
         """Waits for the last batch and returns its n records (n must be the batch's problem count;

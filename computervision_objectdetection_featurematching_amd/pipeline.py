@@ -146,12 +146,19 @@ def detect_objects(matcher: Matcher, scene_gray, models: list[ObjectModel], scal
     scene_ids, _, scene_kp = matcher.sift_scales_to_sets(scene_gray, scales, keypoints=keep)
     scene_desc = [matcher.set_rows(i)[0] for i in scene_ids] if keep_descriptors else None
     _mark("sift")
-    tags = [(mi, si, vi) for mi in range(len(models)) for si in range(len(scales)) for vi in range(len(view_ids[mi]))]
-    res = matcher.match_batch([(view_ids[mi][vi], scene_ids[si]) for mi, si, vi in tags], params)
+    # problems in (model, scale, view) order, built as arrays (145 per c1img scene)
+    ns = len(scales)
+    sid = np.asarray(scene_ids, np.int32)
+    probs = np.concatenate([np.stack([np.tile(np.asarray(view_ids[mi], np.int32), ns),
+                                      np.repeat(sid, len(view_ids[mi]))], axis=1)
+                            for mi in range(len(models))]) if models else np.zeros((0, 2), np.int32)
+    prob_scale = np.concatenate([np.repeat(np.asarray(scales, np.float32), len(view_ids[mi]))
+                                 for mi in range(len(models))]) if models else np.zeros(0, np.float32)
+    res = matcher.match_batch(probs, params)
     _mark("match")
     # :87-94 inlier scene points of the accepted problems (:74, :79, :81, :84), /scale when scale != 1,
-    # gathered on the device in batch order; a model's problems are contiguous (model-major tags)
-    offs, allpts = matcher.batch_inlier_points(len(tags), np.array([scales[si] for _, si, _ in tags], np.float32))
+    # gathered on the device in batch order; a model's problems are contiguous (model-major order)
+    offs, allpts = matcher.batch_inlier_points(len(probs), prob_scale)
     points, i0 = [], 0
     for mi in range(len(models)):
         i1 = i0 + len(scales) * len(view_ids[mi])

@@ -48,8 +48,11 @@ __device__ __forceinline__ double d_hypot(double a, double b) {
 }
 
 // packed upper-triangle index of (i, j), i < j, for an n x n symmetric matrix
+// (the masks are exact for 0 <= i < n <= 16 and let the product select the full-rate 24-bit multiply;
+// __umul24 compiled to the quarter-rate v_mul_lo_u32 in the Jacobi rotation)
 template <int n> __device__ __forceinline__ int pk(int i, int j) {
-    return (int)(__umul24((unsigned)i, (unsigned)(2 * n - i - 1)) >> 1) + (j - i - 1);
+    static_assert(n <= 16, "packed index masks");
+    return (int)(((unsigned)(i & 15) * (unsigned)((2 * n - 1 - i) & 31)) >> 1) + (j - i - 1);
 }
 
 template <int n> __device__ __forceinline__ int pk_any(int a, int b) {  // (min, max) of two distinct indices
@@ -365,8 +368,10 @@ __device__ __forceinline__ void row_max_nn(double (&v)[R]) {
 
 // First maximum of |A(idx, i)| over the slots' candidate indices (slots 9..15 carry the rotated
 // values, in increasing index order) plus, optionally, a zero entry at index `zi` (-1: none), for the
-// four caches of rows/columns k and l at once.  The index of the first maximal slot j is recomputed
-// from j (the (j-9)-th index outside {k, l}) instead of being fetched from that lane: no LDS round trip.
+// four caches of rows/columns k and l at once.  The first maximal slot's index is the smallest index
+// among the slots holding the maximum: each slot's own index (the (slot-9)-th index outside {k, l},
+// increasing with the slot) min-reduced over the row, the four reductions interleaved step by step
+// (round 5: a ballot and find-first-set per cache, four dependent chains one after another).
 template <int n>
 __device__ __forceinline__ void refresh_argmax4(const double (&val)[4], const bool (&cand)[4], int k, int l,
                                                 const int (&zi)[4], int (&first)[4]) {
@@ -374,15 +379,21 @@ __device__ __forceinline__ void refresh_argmax4(const double (&val)[4], const bo
 #pragma unroll
     for (int j = 0; j < 4; ++j) mx[j] = cand[j] ? val[j] : -1.0;
     row_max_nn<4>(mx);
+    int im = (int)(threadIdx.x & 15) - n;
+    im += im >= k;
+    im += im >= l;
+    int f[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) f[j] = (cand[j] && val[j] == mx[j]) ? im : INT_MAX;
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) f[j] = min(f[j], dpp_row(f[j], c));
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-        const unsigned m = group_bits(__ballot(cand[j] & (val[j] == mx[j])));
-        int im = __ffs(m) - 1 - n;  // branch-free: m == 0 is selected away below
-        im += im >= k;
-        im += im >= l;
-        int f = m ? im : INT_MAX;
-        if (zi[j] >= 0 && !(mx[j] > 0.0)) f = min(f, zi[j]);
-        first[j] = f;
+        int fj = f[j];
+        if (zi[j] >= 0 && !(mx[j] > 0.0)) fj = min(fj, zi[j]);
+        first[j] = fj;
     }
 }
 
@@ -446,12 +457,15 @@ __device__ __forceinline__ void jacobi_group(double* __restrict__ A, double* __r
         const int k = kc & 255, l = (kc >> 8) & 255;  // k < l
         // ---- the pair of this slot ----
         int im = slot - n;  // slots 9..15: the (slot-9)-th index outside {k, l}
-        if (im >= k) ++im;
-        if (im >= l) ++im;
+        im += im >= k;
+        im += im >= l;
         const bool vslot = slot < n;
         const bool idle = slot >= 2 * n - 2;  // n = 8: slots 14, 15
-        const int ia = vslot ? k * n + slot : (idle ? 0 : pk_any<n>(im, k));
-        const int ib = vslot ? l * n + slot : (idle ? 0 : pk_any<n>(im, l));
+        // both forms computed and selected (no divergent branch around the packed indices); im < k <
+        // l is the common case of the min/max
+        const int pak = pk<n>(min(im, k), max(im, k)), pal = pk<n>(min(im, l), max(im, l));
+        const int ia = vslot ? k * n + slot : (idle ? 0 : pak);
+        const int ib = vslot ? l * n + slot : (idle ? 0 : pal);
         double* base = vslot ? V : A;
         const double a0 = base[ia], b0 = base[ib];
         const double wk = W[k], wl = W[l];

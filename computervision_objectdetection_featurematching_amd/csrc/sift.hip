@@ -249,6 +249,9 @@ __global__ __launch_bounds__(256) void blur_kernel(BlurB A, Taps t) {
 #ifndef MIM_BLUR_TH
 #define MIM_BLUR_TH 32
 #endif
+#ifndef MIM_BLUR_TH_BIG
+#define MIM_BLUR_TH_BIG 32  // tile rows for A >= 10 (fewer halo rows per output row in the row pass)
+#endif
 template <int A, int TH>
 __global__ __launch_bounds__(256) void blur_reg_kernel(BlurB B, Taps t) {
     constexpr int N = 2 * A + 1, H = TH + 2 * A;
@@ -1660,21 +1663,21 @@ static int sift_batch(std::vector<SiftJob>& jobs, SiftWs* bw, hipStream_t st, st
                 A.cols[k] = J.ocols[o];
             }
             const int a = t.n / 2;
-            auto reg = [&](auto kern) {
-                // the register-blocked kernel's tiles are MIM_BLUR_TH rows: its own grid
+            auto reg = [&](auto kern, int th) {
+                // the register-blocked kernel's tiles are th rows: its own grid
                 const int nb2 = flatten(A.f, imgs, [&](int j, int& gx, int& gy) {
                     gx = (jobs[j].ocols[o] + kBlurTW - 1) / kBlurTW;
-                    gy = (jobs[j].orows[o] + MIM_BLUR_TH - 1) / MIM_BLUR_TH;
+                    gy = (jobs[j].orows[o] + th - 1) / th;
                 });
                 kern<<<nb2, 256, 0, st>>>(A, t);
                 return true;
             };
             switch (a) {
-            case 5: return reg(blur_reg_kernel<5, MIM_BLUR_TH>);
-            case 6: return reg(blur_reg_kernel<6, MIM_BLUR_TH>);
-            case 8: return reg(blur_reg_kernel<8, MIM_BLUR_TH>);
-            case 10: return reg(blur_reg_kernel<10, MIM_BLUR_TH>);
-            case 13: return reg(blur_reg_kernel<13, MIM_BLUR_TH>);
+            case 5: return reg(blur_reg_kernel<5, MIM_BLUR_TH>, MIM_BLUR_TH);
+            case 6: return reg(blur_reg_kernel<6, MIM_BLUR_TH>, MIM_BLUR_TH);
+            case 8: return reg(blur_reg_kernel<8, MIM_BLUR_TH>, MIM_BLUR_TH);
+            case 10: return reg(blur_reg_kernel<10, MIM_BLUR_TH_BIG>, MIM_BLUR_TH_BIG);
+            case 13: return reg(blur_reg_kernel<13, MIM_BLUR_TH_BIG>, MIM_BLUR_TH_BIG);
             default: break;
             }
             const size_t lds = sizeof(float) * (size_t)(kBlurTH + 2 * a) * (kBlurTW + 2 * a + kBlurTW);

@@ -3989,6 +3989,9 @@ void ransac_enqueue(const RansacParams& prm, int n_probs, const ProbDev* probs, 
     // fewer than kWinnerHMaxN good matches (MIM_WINNER_H=1: every problem, 0: none)
     const char* we = getenv("MIM_WINNER_H");
     const int winner_h = !we ? 2 : we[0] == '1' ? 1 : we[0] == '0' ? 0 : 2;
+    // the sampler grids' floor (MIM_SAMPLER_MIN_BLOCKS: blocks in all; 0 = only what the window needs)
+    int min_blocks = kSamplerMinBlocks;
+    if (const char* mb = getenv("MIM_SAMPLER_MIN_BLOCKS")) min_blocks = std::max(0, atoi(mb));
     while (c0 < max_iters) {
         const int c1 = (int)std::min<long long>((long long)c0 + chunk, max_iters);
         // attempt outcomes for a window of ~28 draws per wanted iteration (pass rate ~1/5), the walk
@@ -4001,7 +4004,7 @@ void ransac_enqueue(const RansacParams& prm, int n_probs, const ProbDev* probs, 
         // first chunk would otherwise leave most of the GPU idle), a multiple of 8 per problem (placement)
         const int bppw_cap = std::max(1, wcap / kAttemptSpan);
         const int bppw = (std::max((west + kAttemptSpan - 1) / kAttemptSpan,
-                                   std::min(bppw_cap, (kSamplerMinBlocks + n_probs - 1) / n_probs)) + 7) / 8 * 8;
+                                   std::min(bppw_cap, (min_blocks + n_probs - 1) / n_probs)) + 7) / 8 * 8;
         // (MIM_ATTEMPT_REP_CAP < kAttemptRepCap: test knob forcing the in-place redraw resolution)
         const int rep_cap = prm.rep_cap > 0 ? std::min(prm.rep_cap, kAttemptRepCap) : kAttemptRepCap;
         ransac_attempt_kernel<<<n_probs * bppw, 256, 0, ss>>>(b.state, b.stream, b.stream_len, b.flags, b.irr_bits, wcap,
@@ -4017,7 +4020,7 @@ void ransac_enqueue(const RansacParams& prm, int n_probs, const ProbDev* probs, 
             mark(mark_ctx, "chain", ss);
             constexpr int kChkSpan = kCheckBlock * kCheckPer;
             const int bpp_chk = std::max((west / 4 + kChkSpan) / kChkSpan,  // T ~ wlen / 4
-                                         std::min(std::max(1, wcap / 4 / kChkSpan), (kSamplerMinBlocks + n_probs - 1) / n_probs));
+                                         std::min(std::max(1, wcap / 4 / kChkSpan), (min_blocks + n_probs - 1) / n_probs));
             ransac_check_kernel<<<8 * ((n_probs + 7) / 8) * bpp_chk, kCheckBlock, 0, ss>>>(
                 chains, probs, pts, b.state, b.stream, b.stream_len, b.pass_bits, wcap, bpp_chk, n_probs);
             mark(mark_ctx, "check", ss);

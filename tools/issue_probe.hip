@@ -7,6 +7,7 @@
 //   hipcc --offload-arch=gfx950 -O3 -o /tmp/issue_probe tools/issue_probe.hip
 #include <hip/hip_runtime.h>
 #include <cstdio>
+#include <cstdlib>
 
 #define R16(OP) OP(0) OP(1) OP(2) OP(3) OP(4) OP(5) OP(6) OP(7) OP(8) OP(9) OP(10) OP(11) OP(12) OP(13) OP(14) OP(15)
 #define OUTS                                                                                          \
@@ -77,6 +78,27 @@ KERNEL(bfe, BFE)
 KERNEL(med3i, MED3I)
 KERNEL(mini, MINI)
 KERNEL(min3i, MIN3I)
+// round 6: mixed-precision forms for the bound kernel's count (f32 test, f16 clamp result, f32 dot2 sum)
+#define MIXLO(n) "v_fma_mixlo_f16 %" #n ", -|%" #n "|, %16, %17 op_sel_hi:[0,0,0] clamp\n"
+#define MIXHI(n) "v_fma_mixhi_f16 %" #n ", -|%" #n "|, %16, %17 op_sel_hi:[0,0,0] clamp\n"
+#define MIXF32(n) "v_fma_mix_f32 %" #n ", -|%" #n "|, %16, %17 op_sel_hi:[0,0,0]\n"
+#define DOT2(n) "v_dot2_f32_f16 %" #n ", %16, %17, %" #n "\n"
+#define DOT2C(n) "v_dot2c_f32_f16_e32 %" #n ", %16, %17\n"
+#define PKADDH(n) "v_pk_add_f16 %" #n ", %" #n ", %16\n"
+#define PKFMAH(n) "v_pk_fma_f16 %" #n ", %" #n ", %16, %17\n"
+#define CVTPK(n) "v_cvt_pkrtz_f16_f32 %" #n ", %" #n ", %16\n"
+#define ADDH(n) "v_add_f16_e32 %" #n ", %" #n ", %16\n"
+#define SUBCL_FMA(n) "v_fma_f32 %" #n ", %16, |%" #n "|, -|%17|\n"
+KERNEL(mixlo, MIXLO)
+KERNEL(mixhi, MIXHI)
+KERNEL(mixf32, MIXF32)
+KERNEL(dot2, DOT2)
+KERNEL(dot2c, DOT2C)
+KERNEL(pkaddh, PKADDH)
+KERNEL(pkfmah, PKFMAH)
+KERNEL(cvtpk, CVTPK)
+KERNEL(addh, ADDH)
+KERNEL(fma_negabs, SUBCL_FMA)
 // v_cndmask with the mask set once before the loop (VCC or an SGPR pair): does the form matter
 #define KERNEL_CND(NAME, OP, SETUP)                                                            \
     __global__ __launch_bounds__(256) void k_##NAME(float* out, int iters) {                  \
@@ -293,7 +315,11 @@ int main() {
         {"v_med3_i32", k_med3i},           {"v_min_i32_e32", k_mini},        {"v_min3_i32", k_min3i},
         {"v_cndmask_b32_e32 (vcc set)", k_cnd_e32}, {"v_cndmask_b32_e64 (sgpr)", k_cnd_e64},
         {"cmp_e32 vcc + cndmask_e32 (pair)", k_cs_e32}, {"cmp_e64 sgpr + cndmask_e64 (pair)", k_cs_e64},
-        {"cmp_e64 vcc + cndmask_e64 (pair)", k_cs_e64v}};
+        {"cmp_e64 vcc + cndmask_e64 (pair)", k_cs_e64v},
+        {"v_fma_mixlo_f16 clamp", k_mixlo}, {"v_fma_mixhi_f16 clamp", k_mixhi}, {"v_fma_mix_f32", k_mixf32},
+        {"v_dot2_f32_f16", k_dot2}, {"v_dot2c_f32_f16", k_dot2c}, {"v_pk_add_f16", k_pkaddh},
+        {"v_pk_fma_f16", k_pkfmah}, {"v_cvt_pkrtz_f16_f32", k_cvtpk}, {"v_add_f16", k_addh},
+        {"v_fma_f32 c,|a|,-|b|", k_fma_negabs}};
     // packed forms: 8 instructions per asm block, each doing 2 lanes' worth (reported per instruction)
     const Entry pk[] = {{"v_pk_add_f32", k_pk_add}, {"v_pk_fma_f32", k_pk_fma}, {"v_pk_mul_f32", k_pk_mul},
                         {"v_pk_mov_b32", k_pk_mov}};
@@ -304,6 +330,7 @@ int main() {
     hipMalloc(&out, (size_t)ncu * 16 * 256 * sizeof(float));
     hipEventCreate(&e0);
     hipEventCreate(&e1);
+    const bool only_a = getenv("PROBE_ONLY_A") != nullptr;
     printf("A. %d CUs, %d iterations x 16 instructions per wave, 8 waves per SIMD\n", ncu, iters);
     double ref = 0;
     for (const Entry& k : ks) {
@@ -317,6 +344,7 @@ int main() {
         const double ns = ms * 1e6 / ((double)8 * iters * 8);
         printf("  %-26s %8.3f ns  %5.2f x fma (per instruction = 2 fp32 results)\n", k.name, ns, ns / ref);
     }
+    if (only_a) return 0;
     printf("B. per loop iteration and SIMD: 2 v_mfma_f32_32x32x16_f16 (2 accumulators) + NV v_fma_f32 per wave\n");
     printf("  %-22s %10s %10s %10s\n", "variant", "1 w/SIMD", "2 w/SIMD", "4 w/SIMD");
     struct CE {

@@ -75,7 +75,7 @@ H_TOL = 1e-4                  # SURVEY.md 8(c) contract item 4 (the GPU tests ho
 
 def pmc_traffic(kernel, config):
     """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC pass (or None)."""
-    for name in (f"r05_pmc_traffic_{config}.json", f"r04_pmc_traffic_{config}.json"):  # newest first
+    for name in (f"r06_pmc_traffic_{config}.json", f"r05_pmc_traffic_{config}.json"):  # newest first
         try:
             with open(os.path.join(ROOT, "profiles", name)) as f:
                 d = json.load(f)

@@ -158,7 +158,7 @@ struct PinnedStage {
 namespace mim {
 // RANSAC workspace (definition shared with ransac.hip through this layout)
 struct RansacWs {
-    DevBuf state, samples, hyp, counts, bounds, flags, irr_bits, irr, irr_cnt, pass_bits, chains, best_h, cand, ncand, cex, cH, decided, stream,
+    DevBuf state, samples, hyp, counts, bounds, flags, irr_bits, irr, irr_cnt, pass_bits, defer, defer_n, chains, best_h, cand, ncand, cex, cH, decided, stream,
         scratch, inl, tiles, err;
     long long stream_len = 0;
 };
@@ -304,7 +304,7 @@ void mim_ctx_destroy(mim_ctx* c) {
     c->arena.release();
     for (DevBuf* b : {&c->probs, &c->works, &c->parts, &c->good_q, &c->good_t, &c->pts, &c->n_good,
                       &c->results, &c->masks, &c->knn_idx, &c->knn_dist, &c->inl_tab, &c->inl_out, &c->knn_ctr, &c->rws.state, &c->rws.samples,
-                      &c->rws.hyp, &c->rws.counts, &c->rws.bounds, &c->rws.flags, &c->rws.irr_bits, &c->rws.irr, &c->rws.irr_cnt, &c->rws.pass_bits, &c->rws.chains, &c->rws.best_h, &c->rws.cand, &c->rws.ncand, &c->rws.cex, &c->rws.cH, &c->rws.decided, &c->rws.stream, &c->rws.scratch, &c->rws.inl, &c->rws.tiles, &c->rws.err, &c->prep_jobs})
+                      &c->rws.hyp, &c->rws.counts, &c->rws.bounds, &c->rws.flags, &c->rws.irr_bits, &c->rws.irr, &c->rws.irr_cnt, &c->rws.pass_bits, &c->rws.defer, &c->rws.defer_n, &c->rws.chains, &c->rws.best_h, &c->rws.cand, &c->rws.ncand, &c->rws.cex, &c->rws.cH, &c->rws.decided, &c->rws.stream, &c->rws.scratch, &c->rws.inl, &c->rws.tiles, &c->rws.err, &c->prep_jobs})
         b->release();
     if (c->own) (void)hipStreamDestroy(c->own);
     delete c;
@@ -1189,6 +1189,10 @@ static mim_status ransac_prepare(mim_ctx* c, int n, const mim_params* prm, Ransa
     HIPCHK(c, c->rws.irr.ensure(sizeof(int) * (size_t)std::max(n, 1) * irr_blocks * kIrrCap));
     HIPCHK(c, c->rws.irr_cnt.ensure(sizeof(int) * (size_t)std::max(n, 1) * irr_blocks));
     HIPCHK(c, c->rws.pass_bits.ensure((size_t)flag_cap / 8));
+    // deferred-attempt lists of the check rounds: a chain holds at most ~window / 4 attempts
+    const int def_rounds = (int)((flag_per / 4 + 2 * kRansacDefRoundAttempts) / kRansacDefRoundAttempts);
+    HIPCHK(c, c->rws.defer.ensure(sizeof(int2) * kRansacDefSlots * (size_t)std::max(n, 1) * def_rounds));
+    HIPCHK(c, c->rws.defer_n.ensure(sizeof(int) * (size_t)std::max(n, 1) * def_rounds));
     HIPCHK(c, c->rws.chains.ensure(ransac_chain_bytes() * (size_t)std::max(n, 1)));
     HIPCHK(c, c->rws.best_h.ensure(sizeof(double) * 9 * std::max(n, 1)));
     // two candidate lists per problem: chunk 1's (kept when its exact pass is deferred) and chunk 2's
@@ -1222,6 +1226,11 @@ static mim_status ransac_prepare(mim_ctx* c, int n, const mim_params* prm, Ransa
     b.irr = c->rws.irr.as<int>();
     b.irr_cnt = c->rws.irr_cnt.as<int>();
     b.pass_bits = c->rws.pass_bits.as<uint32_t>();
+    b.defer = c->rws.defer.as<int2>();
+    b.defer_n = c->rws.defer_n.as<int>();
+    // MIM_CHECK_DEFER=0: every deferred attempt decided inside the check kernel (test knob)
+    const char* cde = getenv("MIM_CHECK_DEFER");
+    b.def_rounds = (cde && cde[0] == '0') ? 0 : def_rounds;
     b.irr_blocks = irr_blocks;
     b.chains = c->rws.chains.p;
     b.stream = c->rws.stream.as<uint32_t>();
@@ -1268,6 +1277,8 @@ static mim_status ransac_enqueue_range(mim_ctx* c, int p0, int np, const RansacB
     g.irr += (long long)p0 * b.irr_blocks * kIrrCap;
     g.irr_cnt += (long long)p0 * b.irr_blocks;
     g.pass_bits += (long long)p0 * flag_per / 32;
+    g.defer += (long long)p0 * b.def_rounds * kRansacDefSlots;
+    g.defer_n += (long long)p0 * b.def_rounds;
     g.chains = static_cast<char*>(b.chains) + (size_t)p0 * ransac_chain_bytes();
     g.best_h += 9LL * p0;
     g.cand += (long long)p0 * 2 * kCandPerProblem;

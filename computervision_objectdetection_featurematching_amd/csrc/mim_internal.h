@@ -116,6 +116,11 @@ struct RansacParams {
 namespace mim {
 constexpr int kCandPerProblem = 1024;  // listed exact-evaluation candidates per problem and chunk
 constexpr int kIrrBlock = 16384;       // attempt positions per irregular-list block
+constexpr int kRansacDefSlots = 16;             // deferred attempts listed per check round (ransac.hip)
+#ifndef MIM_CHECK_PER
+#define MIM_CHECK_PER 4  // chain attempts per thread and check round (ransac.hip kCheckPer)
+#endif
+constexpr int kRansacDefRoundAttempts = 256 * MIM_CHECK_PER;  // chain attempts per check round (kCheckBlock x kCheckPer)
 constexpr int kIrrCap = 4096;          // listed irregular attempts per block (25 %: n >= ~25 points fit)
 
 // Device buffers of one RANSAC batch (owned by the ctx in api.cpp).
@@ -140,6 +145,9 @@ struct RansacBufs {
     int* irr_cnt;             // [problem][block] their count (-1: more than kIrrCap)
     uint32_t* pass_bits;      // [problem][window / 32] bit per chain attempt: checkSubset passes
     void* chains;             // [problem] ChainSegs (ransac.hip): the walked chain of the chunk
+    int2* defer;              // [problem][check round][kDefSlots] deferred attempts (attempt index, position)
+    int* defer_n;             // [problem][check round] how many are listed
+    int def_rounds;           // check rounds per problem with a list (0: every deferred attempt in place)
     int irr_blocks;           // list blocks per problem
     const uint32_t* stream;   // raw cv::RNG((uint64)-1).next() stream shared by every problem
     long long stream_len;

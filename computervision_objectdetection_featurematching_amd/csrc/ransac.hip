@@ -1405,20 +1405,57 @@ __device__ __forceinline__ int chain_seg(const ChainSegs* G, int t) {
 
 // Each thread checks kCheckPer attempts (block-strided, so every round is one ballot word pair per
 // wave): their stream draws and point gathers are all in flight at once.
-constexpr int kCheckPer = 4;
+constexpr int kCheckPer = MIM_CHECK_PER;
 constexpr int kCheckSegs = 8;  // segments preloaded per block (a block spans ~4 on average)
+#ifndef MIM_PROBE_CHECK
+#define MIM_PROBE_CHECK 0  // timing probe only (wrong samples): 1 = no deferred pass, 2 = and no fp32 checks,
+                           // 3 = no deferred pass, every point gathered, a 16-add stand-in for the fp32 check
+#endif
+// Deferred attempts listed per check round (ransac_check_defer_kernel); a round with more decides the
+// rest in place.  C4: ~4 per round of 1,024 attempts.
+constexpr int kDefSlots = kRansacDefSlots;
+#ifndef MIM_CHECK_LDS
+#define MIM_CHECK_LDS 0  // 1: the check blocks gather the points of problems with n <= 2,048 from LDS
+#endif
+constexpr int kCheckLdsPts = MIM_CHECK_LDS ? 2048 : 1;
+static_assert(kCheckBlock * kCheckPer == kRansacDefRoundAttempts, "check round size shared with api.cpp");
 
-__global__ __launch_bounds__(kCheckBlock) void ransac_check_kernel(const ChainSegs* __restrict__ chains,
+// checkSubset (fp64) of a deferred attempt: qe = its first draw's stream position, or -position - 1 for
+// a redraw attempt.  Out of line: inlined, its fp64 sample and redraw buffer raised the check kernel's
+// register count (102 against 71 without it, i.e. 5 instead of 7 waves per SIMD to hide the gathers).
+__device__ __attribute__((noinline)) bool check_deferred(int qe, const uint32_t* __restrict__ stream, long long slen,
+                                                         unsigned N, unsigned long long modM,
+                                                         const float4* __restrict__ P) {
+    const long long qq = qe < 0 ? -(long long)qe - 1 : qe;
+    int ix[4];
+    if (qe < 0) {
+        resolve_at(qq, stream, slen, N, modM, ix);  // the walk only listed resolvable ones
+    } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) ix[k] = (int)fastmod(stream[qq + k], modM, N);
+    }
+    const float4 a = P[ix[0]], bp = P[ix[1]], c = P[ix[2]], d = P[ix[3]];
+    const float s4[8] = {a.x, a.y, bp.x, bp.y, c.x, c.y, d.x, d.y};
+    const float t4[8] = {a.z, a.w, bp.z, bp.w, c.z, c.w, d.z, d.w};
+    return check_subset(s4, t4);
+}
+
+#ifndef MIM_CHECK_OCC
+#define MIM_CHECK_OCC 1  // minimum waves per SIMD the check kernel's register budget is fitted to (build knob)
+#endif
+__global__ __launch_bounds__(kCheckBlock, MIM_CHECK_OCC) void ransac_check_kernel(const ChainSegs* __restrict__ chains,
                                                                    const ProbDev* __restrict__ probs,
                                                                    const float4* __restrict__ pts,
                                                                    const RansacState* __restrict__ st,
                                                                    const uint32_t* __restrict__ stream, long long slen,
                                                                    uint32_t* __restrict__ pass_bits, int wcap, int bpp,
-                                                                   int n_probs) {
+                                                                   int2* __restrict__ defer, int* __restrict__ defer_n,
+                                                                   int def_rounds, int n_probs) {
     __shared__ uint32_t words[kCheckBlock * kCheckPer / 32];  // the round's pass bits
-    __shared__ int def_t[kCheckBlock * kCheckPer], def_q[kCheckBlock * kCheckPer];
+    __shared__ int def_t[kCheckBlock * kCheckPer], def_q[kCheckBlock * kCheckPer];  // the round's deferred attempts
     __shared__ int4 seg_tab[kCheckSegs];
     __shared__ int n_def;
+    __shared__ float4 spts[kCheckLdsPts];  // the problem's points (MIM_CHECK_LDS, n <= kCheckLdsPts)
     // placement (speed only): problem p on XCD p mod 8 (its points stay in one L2), and an XCD's
     // problems in dispatch order for each chain slice kb (the slice's stream draws read from that L2 by
     // all of them); grid 8 ceil(n_probs / 8) bpp, blocks past n_probs idle
@@ -1429,6 +1466,12 @@ __global__ __launch_bounds__(kCheckBlock) void ransac_check_kernel(const ChainSe
     const int T = G->T;
     if (T <= 0) return;  // nothing this chunk
     const RansacState S = st[p];
+    const float4* P = pts + probs[p].good_off;
+    const bool lds = MIM_CHECK_LDS && S.n <= kCheckLdsPts;  // uniform over the block
+    if (lds) {
+        for (int i = threadIdx.x; i < S.n; i += kCheckBlock) spts[i] = P[i];
+        // (the first round's barriers order these stores before the gathers)
+    }
     for (int b = kb0; b * kCheckBlock * kCheckPer < T; b += bpp) {
     const int base = b * kCheckBlock * kCheckPer;
     // segment data of the block's first kCheckSegs segments in one round of (uniform, scalar) loads
@@ -1484,22 +1527,32 @@ __global__ __launch_bounds__(kCheckBlock) void ransac_check_kernel(const ChainSe
     for (int r = 0; r < kCheckPer; ++r)
 #pragma unroll
         for (int k = 0; k < 4; ++k) idx[r][k] = valid[r] ? (int)fastmod(raw[r][k], S.modM, N) : 0;
-    const float4* P = pts + probs[p].good_off;
     float4 g[kCheckPer][4];
+    __syncthreads();  // n_def reset (and the staged points)
+    if (lds) {
 #pragma unroll
-    for (int r = 0; r < kCheckPer; ++r)
+        for (int r = 0; r < kCheckPer; ++r)
 #pragma unroll
-        for (int k = 0; k < 4; ++k) g[r][k] = P[idx[r][k]];
-    __syncthreads();  // n_def reset
+            for (int k = 0; k < 4; ++k) g[r][k] = spts[idx[r][k]];
+    } else {
+#pragma unroll
+        for (int r = 0; r < kCheckPer; ++r)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) g[r][k] = P[idx[r][k]];
+    }
+    const bool listed = b < def_rounds;
 #pragma unroll
     for (int r = 0; r < kCheckPer; ++r) {
         const float s4[8] = {g[r][0].x, g[r][0].y, g[r][1].x, g[r][1].y, g[r][2].x, g[r][2].y, g[r][3].x, g[r][3].y};
         const float t4[8] = {g[r][0].z, g[r][0].w, g[r][1].z, g[r][1].w, g[r][2].z, g[r][2].w, g[r][3].z, g[r][3].w};
-        bool clear;
-        const bool pass32 = check_subset_fp32(s4, t4, clear);
-        // deferred to the block's second pass: the redraw attempts (their indices need the walk over the
-        // stream) and the samples fp32 cannot decide; in place they made most waves run both slow paths
-        const bool defer = valid[r] && (irr[r] || !clear);
+        bool clear = true;
+        const bool pass32 = MIM_PROBE_CHECK == 3 ? (s4[0] + s4[1] + s4[2] + s4[3] + s4[4] + s4[5] + s4[6] + s4[7] +
+                                                    t4[0] + t4[1] + t4[2] + t4[3] + t4[4] + t4[5] + t4[6] + t4[7]) > 4000.f
+                          : MIM_PROBE_CHECK == 2 ? s4[0] != t4[1] : check_subset_fp32(s4, t4, clear);
+        // deferred: the redraw attempts (their indices need the walk over the stream) and the samples
+        // fp32 cannot decide, decided by ransac_check_defer_kernel (in place they made most waves run
+        // both slow paths)
+        const bool defer = MIM_PROBE_CHECK == 0 && valid[r] && (irr[r] || !clear);
         const unsigned long long m = __ballot(valid[r] && !defer && pass32);
         const int wl = (r * kCheckBlock + (threadIdx.x & ~63)) >> 5;  // the wave's 2 words of the block's
         if (lane == 0) words[wl] = (uint32_t)m;
@@ -1513,27 +1566,52 @@ __global__ __launch_bounds__(kCheckBlock) void ransac_check_kernel(const ChainSe
     __syncthreads();
     MIM_DEBUG_PRINT(threadIdx.x == 0 && (p == 0 || p == 100), "[check] p=%d b=%d bpp=%d T=%d nseg=%d n_def=%d wlen=%d\n",
                     p, b, bpp, T, nseg, n_def, G->wlen);
-    for (int e = threadIdx.x; e < n_def; e += kCheckBlock) {  // one deferred attempt per thread
-        const int tl = def_t[e], qe = def_q[e];
-        const long long qq = qe < 0 ? -(long long)qe - 1 : qe;
-        int ix[4];
-        if (qe < 0) {
-            resolve_at(qq, stream, slen, N, S.modM, ix);  // the walk only listed resolvable ones
-        } else {
-#pragma unroll
-            for (int k = 0; k < 4; ++k) ix[k] = (int)fastmod(stream[qq + k], S.modM, N);
+    // the round's first kDefSlots deferred attempts go to ransac_check_defer_kernel's list (their pass
+    // bits are set there, after this kernel), so the block does not wait on their draws and gathers;
+    // any further ones (rare) are decided here
+    const int nl = listed ? min(n_def, kDefSlots) : 0;
+    if (listed && threadIdx.x == 0) defer_n[(long long)p * def_rounds + b] = nl;
+    if (threadIdx.x < nl)
+        defer[((long long)p * def_rounds + b) * kDefSlots + threadIdx.x] =
+            make_int2(base + def_t[threadIdx.x], def_q[threadIdx.x]);
+    if (n_def > nl) {
+        for (int e = nl + threadIdx.x; e < n_def; e += kCheckBlock) {  // one deferred attempt per thread
+            const int tl = def_t[e];
+            if (check_deferred(def_q[e], stream, slen, N, S.modM, P)) atomicOr(&words[tl >> 5], 1u << (tl & 31));
         }
-        const float4 a = P[ix[0]], bp = P[ix[1]], c = P[ix[2]], d = P[ix[3]];
-        const float s4[8] = {a.x, a.y, bp.x, bp.y, c.x, c.y, d.x, d.y};
-        const float t4[8] = {a.z, a.w, bp.z, bp.w, c.z, c.w, d.z, d.w};
-        if (check_subset(s4, t4)) atomicOr(&words[tl >> 5], 1u << (tl & 31));
+        __syncthreads();
     }
-    __syncthreads();
     uint32_t* PB = pass_bits + (long long)p * (wcap / 32);
     if (threadIdx.x < kCheckBlock * kCheckPer / 32 && (base + 32 * (int)threadIdx.x) < T)
         PB[(base >> 5) + threadIdx.x] = words[threadIdx.x];
     __syncthreads();  // words / n_def reused by the next round
     }
+}
+
+// The check rounds' listed deferred attempts (redraw attempts, samples fp32 could not decide): one
+// thread each, fp64 checkSubset as in the check kernel's second pass, the pass bit OR-ed into the
+// round's word the check kernel stored.  Grid n_probs x nblk, thread j of problem p: round j / kDefSlots,
+// slot j % kDefSlots; rounds past the chain's attempts hold stale counts and are skipped.
+__global__ __launch_bounds__(256) void ransac_check_defer_kernel(const ChainSegs* __restrict__ chains,
+                                                                 const ProbDev* __restrict__ probs,
+                                                                 const float4* __restrict__ pts,
+                                                                 const RansacState* __restrict__ st,
+                                                                 const uint32_t* __restrict__ stream, long long slen,
+                                                                 uint32_t* __restrict__ pass_bits, int wcap,
+                                                                 const int2* __restrict__ defer,
+                                                                 const int* __restrict__ defer_n, int def_rounds,
+                                                                 int nblk, int n_probs) {
+    const int p = blockIdx.x / nblk;
+    const int j = (blockIdx.x % nblk) * 256 + threadIdx.x, round = j / kDefSlots, e = j % kDefSlots;
+    if (p >= n_probs || round >= def_rounds) return;
+    const int T = chains[p].T;
+    if (round * (kCheckBlock * kCheckPer) >= T) return;
+    const long long rr = (long long)p * def_rounds + round;
+    if (e >= defer_n[rr]) return;
+    const int2 en = defer[rr * kDefSlots + e];
+    const int t = en.x, qe = en.y;
+    if (check_deferred(qe, stream, slen, (unsigned)st[p].n, st[p].modM, pts + probs[p].good_off))
+        atomicOr(pass_bits + (long long)p * (wcap / 32) + (t >> 5), 1u << (t & 31));
 }
 
 // ---- count: ranks of the passing attempts, getSubset's failure rule, samples, state ----
@@ -4022,7 +4100,14 @@ void ransac_enqueue(const RansacParams& prm, int n_probs, const ProbDev* probs, 
             const int bpp_chk = std::max((west / 4 + kChkSpan) / kChkSpan,  // T ~ wlen / 4
                                          std::min(std::max(1, wcap / 4 / kChkSpan), (min_blocks + n_probs - 1) / n_probs));
             ransac_check_kernel<<<8 * ((n_probs + 7) / 8) * bpp_chk, kCheckBlock, 0, ss>>>(
-                chains, probs, pts, b.state, b.stream, b.stream_len, b.pass_bits, wcap, bpp_chk, n_probs);
+                chains, probs, pts, b.state, b.stream, b.stream_len, b.pass_bits, wcap, bpp_chk, b.defer, b.defer_n,
+                b.def_rounds, n_probs);
+            if (b.def_rounds > 0) {
+                const int nblk = (b.def_rounds * kDefSlots + 255) / 256;
+                ransac_check_defer_kernel<<<n_probs * nblk, 256, 0, ss>>>(chains, probs, pts, b.state, b.stream,
+                                                                        b.stream_len, b.pass_bits, wcap, b.defer,
+                                                                        b.defer_n, b.def_rounds, nblk, n_probs);
+            }
             mark(mark_ctx, "check", ss);
             ransac_count_kernel<<<n_probs, kChainThreads, 0, ss>>>(b.state, probs, chains, b.pass_bits, b.flags, wcap,
                                                                   b.samples, c1);

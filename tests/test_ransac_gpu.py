@@ -559,3 +559,31 @@ def test_candidate_prescreen_equals_exact_paths(capfd):
         assert r0.tobytes() == r1.tobytes()
         for a, b in zip(m0, m1):
             np.testing.assert_array_equal(a, b)
+
+
+def test_check_defer_list_equals_in_place():
+    """The check rounds' deferred attempts (redraw attempts, samples fp32 cannot decide) decided by
+    ransac_check_defer_kernel from the rounds' lists give the same pass bits, hence the same samples and
+    records, as deciding them inside the check kernel (MIM_CHECK_DEFER=0), on a C4-shaped batch at
+    50,000 iterations and on the adversarial sets; both equal the walker (MIM_SAMPLER_WALK=1)."""
+    import os
+    from computervision_objectdetection_featurematching_amd import Matcher, default_params
+    ds = make_dataset(1, 12, 2500, 10000, 2000, inlier_frac=0.08, seed=4242)
+    sets = _adversarial_sets()
+    outs = []
+    for env in ({}, {"MIM_CHECK_DEFER": "0"}, {"MIM_SAMPLER_WALK": "1"}):
+        os.environ.update(env)
+        m = Matcher(0)
+        try:
+            q = [m.add_set(d, k) for d, k in zip(ds.model_desc, ds.model_kp)]
+            t = [m.add_set(d, k) for d, k in zip(ds.scene_desc, ds.scene_kp)]
+            res = m.match_batch([(q[a], t[b]) for a, b in ds.problems], default_params(max_iters=50000))
+            fh = [m.find_homography(s_, d_, 5.0, 20000)[1].tobytes() + m.batch_results(1).tobytes()
+                  for s_, d_ in sets]
+        finally:
+            m.close()
+            for k in env:
+                os.environ.pop(k, None)
+        outs.append((res.tobytes(), fh))
+    assert outs[0] == outs[1]
+    assert outs[0] == outs[2]

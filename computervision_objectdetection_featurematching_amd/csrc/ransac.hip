@@ -688,68 +688,56 @@ __device__ __forceinline__ bool check_subset(const float* s, const float* d) {
     return !(negative != 0 && negative != 4);
 }
 
-// checkSubset decided in fp32 where fp32 cannot disagree with the fp64 reference, else fp64.
-// Collinearity: dx, dy are floats (the reference subtracts in float), so the fp64 cross product is
-// X (1 + d), |d| <= 2^-53, X = dx2 dy1 - dy2 dx1 exact; c = fma(dx2, dy1, -rn(dy2 dx1)) is within
-// 2^-24 (|c| + |rn(dy2 dx1)|) of X, and the fp64 right side is at most 2^-23 S (1 + 2^-51), S =
-// |dx1| + |dy1| + |dx2| + |dy2| <= 4 M, M >= every |delta| of the pair (here: the largest |delta| of
-// the set's three).  |c| > 2^-21 M (M + 4) (the bound evaluated in fp32: two roundings) gives
-// |X| >= |c| (1 - 2^-24) - 2^-24 M^2 (1 + 2^-24) > 2^-19 M (1 - 2^-22), four times the fp64 right
-// side (<= 2^-21 M (1 + 2^-51)): the pair is "clearly not collinear".
-// Orientation: |det| of a point triple in fp32 (three fma, three roundings fewer than the plain
-// form: within 17 2^-24 M^2) and in fp64 are both within 22 2^-24 M^2 of the exact value (M >= the
-// triple's largest |coordinate|; here the set's largest); with |det32| > 2^-18 M^2 = (2^-9 M)^2 (the
-// same fp32 value: power-of-two scaling commutes with rounding) the fp64 determinant has the same
-// sign, so dA dB < 0 is decided by the signs.  Anything not clear (near-collinear samples, tiny
-// triangles, duplicated points) runs the fp64 check: same result as check_subset always.  (One M
-// per set instead of per pair or triple: 4 of the 4-point sample's bounds instead of 14, and "not
-// clear" stays ~0.3 % of the attempts, profiles/r04_sampler_probe.txt.)
-__device__ __forceinline__ bool collinear4_clear(const float* xy) {
+// checkSubset decided in fp32 where fp32 cannot disagree with the fp64 reference, else fp64 (round 6
+// form: the orientation determinants reuse the collinearity test's cross products).
+// Per point set, with the deltas d_j = p_j - p_3 in float (as haveCollinearPoints subtracts) and
+// m >= every |delta| component:
+// Collinearity: c_kj = fma(dx_k, dy_j, -rn(dy_k dx_j)) is the fp64 test's cross product X' = dx_k dy_j -
+//   dy_k dx_j within 2^-24 (|c| + m^2); the fp64 right side is at most 2^-23 S (1 + 2^-51), S <= 4 m; so
+//   |c| > 2^-21 m (m + 4) (the round-5 bound, proof there) gives "clearly not collinear".
+// Orientation: the same c_kj is orient(p_k, p_j, p_3) of the exact points within 5 2^-24 m^2 + 2^-24 |c|
+//   (the deltas' roundings, 2 2^-24 relative on each product, plus the two roundings above), and
+//   orient(p_0, p_1, p_2) = c_21 - c_20 + c_10 (the 4-point identity [012] = [123] - [023] + [013], two
+//   float additions) within 25 2^-24 m^2 + 2^-24 |c_012|.  The fp64 reference det3xy (float inputs,
+//   no FMA) is within ~60 2^-53 A^2 < 2^-44 A^2 of the exact value, A = max(|x_3|, |y_3|) + m >= every
+//   coordinate.  So |c| > 2^-20 m (m + 4) + 2^-44 A^2 (the three triples with p_3) and |c_012| > 2^-18 m^2
+//   + 2^-44 A^2 give the fp64 signs (each bound above the error with a factor >= 2.5 for the roundings
+//   of the bounds themselves); a floor of 2^-100 keeps products out of the subnormal range, where the
+//   relative error model fails.  "Not clear" (near-collinear or tiny sets, duplicated points) runs the
+//   fp64 check_subset: same result as check_subset always.
+__device__ __forceinline__ bool set_orient_fp32(const float* xy, float (&o)[4]) {
     float dx[3], dy[3];
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
         dx[j] = xy[2 * j] - xy[6];
         dy[j] = xy[2 * j + 1] - xy[7];
     }
-    const float m = fmaxf(fmaxf(fmaxf(fabsf(dx[0]), fabsf(dy[0])), fmaxf(fabsf(dx[1]), fabsf(dy[1]))),
-                          fmaxf(fabsf(dx[2]), fabsf(dy[2])));
-    const float bound = m * 0x1p-21f * (m + 4.f);
-    bool clear = true;
-#pragma unroll
-    for (int j = 0; j < 3; ++j)
-#pragma unroll
-        for (int k = 0; k < j; ++k) clear &= fabsf(fmaf(dx[k], dy[j], -(dy[k] * dx[j]))) > bound;
-    return clear;
-}
-
-// x0 (y1 - y2) - y0 (x1 - x2) + (x1 y2 - x2 y1), the fp32 decision's form (fma: fewer roundings)
-__device__ __forceinline__ float det3xy_f(float x0, float y0, float x1, float y1, float x2, float y2) {
-    return fmaf(-y0, x1 - x2, fmaf(x0, y1 - y2, fmaf(x1, y2, -(x2 * y1))));
-}
-
-__device__ __forceinline__ float max_abs8(const float* v) {
-    return fmaxf(fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))),
-                 fmaxf(fmaxf(fabsf(v[4]), fabsf(v[5])), fmaxf(fabsf(v[6]), fabsf(v[7]))));
+    const float m = fmaxf(fmaxf(fmaxf(fabsf(dx[0]), fabsf(dx[1])), fabsf(dx[2])),
+                          fmaxf(fmaxf(fabsf(dy[0]), fabsf(dy[1])), fabsf(dy[2])));
+    const float A = fmaxf(fabsf(xy[6]), fabsf(xy[7])) + m;
+    const float a2 = (A * A) * 0x1p-44f;
+    const float c10 = fmaf(dx[0], dy[1], -(dy[0] * dx[1]));  // orient(p0, p1, p3): triple 3
+    const float c20 = fmaf(dx[0], dy[2], -(dy[0] * dx[2]));  // orient(p0, p2, p3): triple 2
+    const float c21 = fmaf(dx[1], dy[2], -(dy[1] * dx[2]));  // orient(p1, p2, p3): triple 1
+    const float c012 = (c21 - c20) + c10;                     // orient(p0, p1, p2): triple 0
+    const float thr = fmaxf(fmaf(m * (m + 4.f), 0x1p-20f, a2), 0x1p-100f);
+    const float thr0 = fmaxf(fmaf(m * m, 0x1p-18f, a2), 0x1p-100f);
+    o[0] = c012; o[1] = c21; o[2] = c20; o[3] = c10;
+    return fminf(fminf(fabsf(c10), fabsf(c20)), fabsf(c21)) > thr && fabsf(c012) > thr0;
 }
 
 // the fp32 decision and whether it is the fp64 one (clear); !clear: check_subset decides
 __device__ __forceinline__ bool check_subset_fp32(const float* s, const float* d, bool& clear_out) {
-    bool clear = (int)collinear4_clear(s) & (int)collinear4_clear(d);  // both evaluated: no branch
-    const float ms = max_abs8(s) * 0x1p-9f, md = max_abs8(d) * 0x1p-9f;
-    const float ts = ms * ms, td = md * md;
-    const int tt[4][3] = {{0, 1, 2}, {1, 2, 3}, {0, 2, 3}, {0, 1, 3}};
-    int negative = 0;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int a = tt[i][0], b = tt[i][1], c = tt[i][2];
-        const float dA = det3xy_f(s[2 * a], s[2 * a + 1], s[2 * b], s[2 * b + 1], s[2 * c], s[2 * c + 1]);
-        const float dB = det3xy_f(d[2 * a], d[2 * a + 1], d[2 * b], d[2 * b + 1], d[2 * c], d[2 * c + 1]);
-        clear &= fabsf(dA) > ts;
-        clear &= fabsf(dB) > td;
-        negative += (dA < 0.f) != (dB < 0.f);
-    }
-    clear_out = clear;
-    return !(negative != 0 && negative != 4);
+    float os[4], od[4];
+    const bool cs = set_orient_fp32(s, os), cd = set_orient_fp32(d, od);
+    clear_out = cs && cd;
+    // checkSubset's count of triples whose orientations differ, 0 or 4 to pass: the four sign bits of
+    // os ^ od all equal
+    const unsigned x0 = __float_as_uint(os[0]) ^ __float_as_uint(od[0]);
+    const unsigned x1 = __float_as_uint(os[1]) ^ __float_as_uint(od[1]);
+    const unsigned x2 = __float_as_uint(os[2]) ^ __float_as_uint(od[2]);
+    const unsigned x3 = __float_as_uint(os[3]) ^ __float_as_uint(od[3]);
+    return (int)((x0 ^ x1) | (x0 ^ x2) | (x0 ^ x3)) >= 0;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1549,6 +1537,9 @@ __global__ __launch_bounds__(kCheckBlock, MIM_CHECK_OCC) void ransac_check_kerne
         const bool pass32 = MIM_PROBE_CHECK == 3 ? (s4[0] + s4[1] + s4[2] + s4[3] + s4[4] + s4[5] + s4[6] + s4[7] +
                                                     t4[0] + t4[1] + t4[2] + t4[3] + t4[4] + t4[5] + t4[6] + t4[7]) > 4000.f
                           : MIM_PROBE_CHECK == 2 ? s4[0] != t4[1] : check_subset_fp32(s4, t4, clear);
+        MIM_DEBUG_CHECK(!valid[r] || !clear || pass32 == check_subset(s4, t4),
+                        "[check] fp32 checkSubset %d differs from fp64 (p=%d t=%d)\n", (int)pass32, p,
+                        base + r * kCheckBlock + (int)threadIdx.x);
         // deferred: the redraw attempts (their indices need the walk over the stream) and the samples
         // fp32 cannot decide, decided by ransac_check_defer_kernel (in place they made most waves run
         // both slow paths)

@@ -770,6 +770,7 @@ __device__ __forceinline__ unsigned fastmod(unsigned a, unsigned long long M, un
     return min(r, r - d);
 }
 
+
 // getSubset's draw loop for one attempt starting at stream position q: redraw while an index
 // repeats.  Returns the number of draws consumed (0 if the stream ends first).
 __device__ __forceinline__ int resolve_at(long long q, const uint32_t* __restrict__ stream, long long slen,
@@ -925,7 +926,14 @@ __device__ __forceinline__ int length_flag(long long q, const uint32_t* __restri
 template <bool kNgt256>
 __device__ __forceinline__ unsigned mod_barrett(unsigned a, unsigned m, unsigned n) {
     const unsigned q = __umulhi(a, m);
-    const unsigned r = a - (kNgt256 ? __umul24(q, n) : q * n);
+    // the 24-bit product as the full-rate v_mul_u32_u24 (written out: __umul24 and masked operands both
+    // compiled to a mask and the quarter-rate v_mul_lo_u32 here, the range of n coming from a branch)
+    unsigned qn;
+    if (kNgt256)
+        asm("v_mul_u32_u24 %0, %1, %2" : "=v"(qn) : "v"(q), "v"(n));
+    else
+        qn = q * n;
+    const unsigned r = a - qn;
     return min(r, r - n);
 }
 

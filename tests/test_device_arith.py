@@ -108,3 +108,4 @@ def test_early_key_padded_row_is_uint_max():
     R = np.array([(1 << 30) - 1])
     K = 255
     assert ((int(R[0]) << 8) + K) & 0xFFFFFFFF == 0xFFFFFFFF
+

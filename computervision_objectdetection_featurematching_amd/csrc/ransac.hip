@@ -938,6 +938,9 @@ __device__ __forceinline__ unsigned mod_barrett(unsigned a, unsigned m, unsigned
 }
 
 constexpr int kAttemptPerThread = 8;  // window positions per thread (11 draws reduced for 8 attempts)
+#ifndef MIM_ATTEMPT_PREFETCH
+#define MIM_ATTEMPT_PREFETCH 0
+#endif
 
 // The block's 2048 + 3 draws are staged through LDS with coalesced 16-byte loads (a lane's own 11
 // draws at a 32-byte lane stride would touch 12 cache lines per load instruction, 11 times over).
@@ -989,31 +992,36 @@ __global__ __launch_bounds__(256) void ransac_attempt_kernel(const RansacState* 
     const unsigned N = (unsigned)S.n, mB = 0xFFFFFFFFu / N;
     const bool big = N > 256 && N < (1u << 24);  // q and n both fit 24 bits
     if (threadIdx.x == 0) n_rep = 0;
+    // stream positions fit 32 bits (the stream is capped at 2^28 draws; 64 zero draws pad its end);
+    // the stage starts at the 16-byte vector holding qb: draw qb + e is sdraw[shift + e]
+    const int nvec = ((int)slen + 64) >> 2;  // 16-byte vectors in the padded stream buffer
+    const uint4* __restrict__ sv = reinterpret_cast<const uint4*>(stream);
+    uint4* sd4 = reinterpret_cast<uint4*>(sdraw);
+    constexpr int NV = (kStageVecs + 255) / 256;
+    // every load of a stage in flight before the first LDS write (unconditional, clamped loads; three
+    // named registers: an array carried across the loop went to scratch)
+    static_assert(NV == 3, "stage vectors per thread");
+#define MIM_ATTEMPT_LOAD_STAGE(bo)                                                   \
+    {                                                                                \
+        const int qv = ((int)S.stream_pos + (bo)) >> 2;                              \
+        v0 = sv[min(qv + min((int)threadIdx.x, kStageVecs - 1), nvec - 1)];          \
+        v1 = sv[min(qv + min((int)threadIdx.x + 256, kStageVecs - 1), nvec - 1)];    \
+        v2 = sv[min(qv + min((int)threadIdx.x + 512, kStageVecs - 1), nvec - 1)];    \
+    }
+    uint4 v0, v1, v2;
+    if (MIM_ATTEMPT_PREFETCH) MIM_ATTEMPT_LOAD_STAGE(kb * kAttemptSpan);
     // the grid covers the window a typical draw rate implies (kAttemptRateEst), not its capacity; a
     // longer window (low checkSubset pass rate) is covered by the same blocks looping
     for (int boff = kb * kAttemptSpan; boff < wlen; boff += bpp * kAttemptSpan) {
     __syncthreads();  // the previous round's reads of sdraw are done (and n_rep's reset seen)
-    // stream positions fit 32 bits (the stream is capped at 2^28 draws; 64 zero draws pad its end);
-    // the stage starts at the 16-byte vector holding qb: draw qb + e is sdraw[shift + e]
     const int qb = (int)S.stream_pos + boff;
     const int shift = qb & 3;
-    const int nvec = ((int)slen + 64) >> 2;  // 16-byte vectors in the padded stream buffer
-    const uint4* __restrict__ sv = reinterpret_cast<const uint4*>(stream);
-    uint4* sd4 = reinterpret_cast<uint4*>(sdraw);
-    {
-        uint4 v[(kStageVecs + 255) / 256];  // every load in flight before the first LDS write
-#pragma unroll
-        for (int k = 0; k < (kStageVecs + 255) / 256; ++k) {  // unconditional (clamped) loads
-            const int i = min((int)threadIdx.x + 256 * k, kStageVecs - 1);
-            v[k] = sv[min((qb >> 2) + i, nvec - 1)];
-        }
-#pragma unroll
-        for (int k = 0; k < (kStageVecs + 255) / 256; ++k) {
-            const int i = threadIdx.x + 256 * k;
-            if (i < kStageVecs) sd4[i] = v[k];
-        }
-    }
+    if (!MIM_ATTEMPT_PREFETCH) MIM_ATTEMPT_LOAD_STAGE(boff);
+    sd4[threadIdx.x] = v0;
+    sd4[threadIdx.x + 256] = v1;
+    if (threadIdx.x + 512 < kStageVecs) sd4[threadIdx.x + 512] = v2;
     __syncthreads();
+    if (MIM_ATTEMPT_PREFETCH && boff + bpp * kAttemptSpan < wlen) MIM_ATTEMPT_LOAD_STAGE(boff + bpp * kAttemptSpan);
     const int off = boff + threadIdx.x * kAttemptPerThread;
     if (off < wlen) {
     const int q0 = qb + threadIdx.x * kAttemptPerThread;
